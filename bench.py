@@ -1,0 +1,189 @@
+#!/usr/bin/env python
+"""Headline benchmark: scene-flow pairs/sec, fwd+bwd, N=8192 (BASELINE.json `metric`).
+
+One step = one training iteration of PointConvBidirection on B synthetic
+FlyingThings3D-shaped pairs per GPU (BASELINE.json configs[2]: B=8, N=8192): forward,
+multiScaleLoss, backward, Adam step (`--mode kd` adds the frozen teacher forward and the
+biDirection_loss_ht KD objective of configs[3]).  With N GPUs: one process per GPU, DDP over
+RCCL, per-GPU batch fixed (weak scaling), no data-path collective beyond DDP's gradient
+all-reduce.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line.  `roofline` is measured live over the timed region: every
+launch of the chosen kernel is bracketed by HIP events on its stream, and its algorithmic
+bytes (or flops) per launch are summed by the op wrapper.  `cpu_baseline` is the oracle's
+pure-PyTorch CPU restatement of the reference path (square_distance+topk kNN,
+torch.gather indexing, FPS replaced by a random subsample) on a bounded sample, rank 0 only.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "kd-pointcloud_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_MFMA_PEAK_TF = 157.3  # dense f32 MFMA / vector peak
+FP32_VALU_PEAK_TF = 157.3
+
+# kernel -> (bound, unit, peak)
+ROOFLINE = {
+    "kdpc_group_rows": ("hbm", "GB/s", HBM_PEAK_GBS),
+    "kdpc_group_rows_grad_csr": ("hbm", "GB/s", HBM_PEAK_GBS),
+    "kdpc_group_points": ("hbm", "GB/s", HBM_PEAK_GBS),
+    "kdpc_knn_point": ("valu", "TFLOP/s", FP32_VALU_PEAK_TF),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=8, help="pairs per GPU")
+    ap.add_argument("--npoints", type=int, default=8192)
+    ap.add_argument("--mode", choices=["train", "kd"], default="train")
+    ap.add_argument("--roofline-kernel", default="kdpc_group_rows")
+    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(args):
+    """Oracle CPU path on a bounded sample: B=1 pair, N=npoints, fwd+bwd+Adam."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch_model as M
+    import synthetic
+    torch.manual_seed(0)
+    M.FPS_MODE["mode"] = "random"
+    M.FPS_MODE["generator"] = torch.Generator().manual_seed(0)
+    model = M.PointConvBidirection().train()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-4)
+    p1, p2, fl = (torch.from_numpy(a) for a in synthetic.ft3d_batch(1, args.npoints, seed=99))
+
+    def step():
+        out = model(p1, p2, p1, p2)
+        loss = M.multiScaleLoss(out[0], fl, out[1])
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+
+    step()  # warm-up
+    times = []
+    for _ in range(args.cpu_steps):
+        t0 = time.perf_counter()
+        step()
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    return {"value": round(1.0 / med, 4), "unit": "pairs/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"1 pair x N={args.npoints}, fwd+bwd+Adam, median of {args.cpu_steps} "
+                      f"steps after 1 warm-up ({med:.2f} s/step); oracle/torch_model.py "
+                      f"(square_distance+topk kNN, torch.gather, FPS->randperm); "
+                      f"host os.cpu_count()={os.cpu_count()}"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import kdpc_native
+    import synthetic
+    from distill import FlowTrainStep, KDTrainStep, make_optimizer, wrap_ddp
+    from models_bid_pointconv import PointConvBidirection
+
+    torch.manual_seed(0)
+    student = PointConvBidirection().to(dev)
+    model = wrap_ddp(student, dev)
+    opt = make_optimizer(model)
+    if args.mode == "kd":
+        torch.manual_seed(1)
+        teacher = PointConvBidirection().to(dev)
+        step = KDTrainStep(teacher, model, opt)
+    else:
+        step = FlowTrainStep(model, opt)
+
+    # inputs resident in HBM before timing; a few distinct batches per rank, cycled
+    nb = 4
+    batches = []
+    for i in range(nb):
+        p1, p2, fl = synthetic.ft3d_batch(args.batch, args.npoints, seed=1000 + rank,
+                                          first_pair=i * args.batch)
+        batches.append(tuple(torch.from_numpy(a).to(dev) for a in (p1, p2, fl)))
+
+    for i in range(args.warmup):
+        step(*batches[i % nb])
+    timer = kdpc_native.LaunchTimer([args.roofline_kernel])
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kdpc_native.set_launch_timer(timer)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(*batches[i % nb])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    kdpc_native.set_launch_timer(None)
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    summ = timer.summary().get(args.roofline_kernel)
+    roof = None
+    if summ and summ["ms"] > 0:
+        bound, unit, peak = ROOFLINE.get(args.roofline_kernel, ("hbm", "GB/s", HBM_PEAK_GBS))
+        per_launch_ms = summ["ms"] / summ["launches"]
+        if unit == "GB/s":
+            achieved = summ["bytes"] / (summ["ms"] * 1e-3) / 1e9
+        else:
+            achieved = summ["flops"] / (summ["ms"] * 1e-3) / 1e12
+        roof = {"bound": bound, "kernel": args.roofline_kernel, "achieved": round(achieved, 2),
+                "peak": peak, "unit": unit, "frac": round(achieved / peak, 4), "traffic": None,
+                "launches": summ["launches"], "avg_launch_us": round(per_launch_ms * 1e3, 2),
+                "algorithmic_bytes_per_launch": round(summ["bytes"] / summ["launches"])}
+
+    pairs = world * args.batch * args.steps
+    line = {
+        "metric": "scene-flow pairs/sec fwd+bwd @ N=8192; EPE3D vs ref; 1/2/4/8 MI355X",
+        "value": round(pairs / dt, 3), "unit": "pairs/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic FlyingThings3D-shaped pairs (kd-pointcloud_amd/synthetic.py), "
+                "random-init weights",
+        "config": {"workload": "PointConvBidirection fwd+bwd+Adam (BASELINE configs[2])"
+                   if args.mode == "train" else
+                   "KD step: teacher fwd + student fwd+bwd + biDirection_loss_ht (configs[3])",
+                   "model": "models_bid_pointconv.PointConvBidirection",
+                   "batch_per_gpu": args.batch, "global_batch": world * args.batch,
+                   "npoints": args.npoints, "parallelism": f"ddp{world}"},
+        "roofline": roof,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,135 @@
+/*
+ * kdpc.h — C ABI of kd-pointcloud_amd's MI355X (gfx950) point-cloud kernels.
+ *
+ * Drop-in boundary for the reference's native extension `pointnet2_cuda`
+ * (yunminjin2/KD-PointCloud pointnet2/src/pointnet2_api.cpp:10-24) and for the
+ * torch-side kNN of pointconv_util.py.  Plain pointers and sizes only:
+ *   - every pointer is DEVICE memory (hipMalloc / a torch-ROCm tensor's data_ptr());
+ *   - float = f32, int = int32; layouts are the reference's (contiguous, row-major);
+ *   - `stream` is a hipStream_t (NULL = default stream); every call is asynchronous on it,
+ *     never synchronises the host, and allocates nothing (except the reference-shaped
+ *     *_grad entry points, see below);
+ *   - return value is a hipError_t code (0 = hipSuccess).  Invalid sizes/pointers return
+ *     hipErrorInvalidValue (1) without launching.  The reference instead printed and
+ *     called exit(-1) on launch failure (e.g. sampling_gpu.cu:39-43).
+ *
+ * Outputs follow the reference's in-place contract (caller allocates), with these
+ * documented strengthenings: ball_query writes every slot (the reference relied on the
+ * caller's .zero_()), and every *_grad overwrites grad_points (the reference accumulated
+ * into a caller-zeroed buffer with atomicAdd) with a deterministic sum.
+ */
+#ifndef KDPC_H_
+#define KDPC_H_
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- sampling -------------------------------------------------------------------------- */
+
+/* Replaces furthest_point_sampling_wrapper(b, n, m, points, temp, idx)
+ * (pointnet2/src/sampling.cpp:38-49; kernel sampling_gpu.cu:93-209).
+ * points (B,N,3), temp (B,N) scratch pre-filled by the caller (reference: 1e10) and left
+ * holding the final min-distances, idx (B,M) out.  Bit-exact indices incl. tie-break.
+ * Requires N < 2^22. */
+int kdpc_furthest_point_sampling(int b, int n, int m, const float *points, float *temp, int *idx,
+                                 void *stream);
+
+/* The reference's block-size rule opt_n_threads (pointnet2/src/cuda_utils.h:10-14). */
+int kdpc_opt_n_threads(int n);
+
+/* Replaces gather_points_wrapper(b, c, n, npoints, points, idx, out)
+ * (sampling.cpp:11-22; kernel sampling_gpu.cu:8-24).  points (B,C,N), idx (B,M), out (B,C,M). */
+int kdpc_gather_points(int b, int c, int n, int npoints, const float *points, const int *idx,
+                       float *out, void *stream);
+
+/* Replaces gather_points_grad_wrapper(b, c, n, npoints, grad_out, idx, grad_points)
+ * (sampling.cpp:25-35; kernel sampling_gpu.cu:46-63).  Overwrites grad_points (B,C,N). */
+int kdpc_gather_points_grad(int b, int c, int n, int npoints, const float *grad_out,
+                            const int *idx, float *grad_points, void *stream);
+
+/* ---- grouping -------------------------------------------------------------------------- */
+
+/* Replaces ball_query_wrapper(b, n, m, radius, nsample, new_xyz, xyz, idx)
+ * (ball_query.cpp:16-28; kernel ball_query_gpu.cu:9-45).  new_xyz (B,M,3), xyz (B,N,3),
+ * idx (B,M,nsample) out.  Bit-exact. */
+int kdpc_ball_query(int b, int n, int m, float radius, int nsample, const float *new_xyz,
+                    const float *xyz, int *idx, void *stream);
+
+/* Replaces group_points_wrapper(b, c, n, npoints, nsample, points, idx, out)
+ * (group_points.cpp:27-38; kernel group_points_gpu.cu:47-66).
+ * points (B,C,N), idx (B,npoints,nsample), out (B,C,npoints,nsample). */
+int kdpc_group_points(int b, int c, int n, int npoints, int nsample, const float *points,
+                      const int *idx, float *out, void *stream);
+
+/* Replaces group_points_grad_wrapper(b, c, n, npoints, nsample, grad_out, idx, grad_points)
+ * (group_points.cpp:11-24; kernel group_points_gpu.cu:8-25).  Overwrites grad_points (B,C,N).
+ * Uses a library-owned workspace grown with hipMalloc on first use (not capture-safe on
+ * that first call); the *_csr entry points below take caller-owned buffers instead. */
+int kdpc_group_points_grad(int b, int c, int n, int npoints, int nsample, const float *grad_out,
+                           const int *idx, float *grad_points, void *stream);
+
+/* ---- interpolation --------------------------------------------------------------------- */
+
+/* Replaces three_nn_wrapper(b, n, m, unknown, known, dist2, idx)
+ * (interpolate.cpp:14-24; kernel interpolate_gpu.cu:9-52).  unknown (B,N,3), known (B,M,3),
+ * dist2 (B,N,3) squared distances, idx (B,N,3). */
+int kdpc_three_nn(int b, int n, int m, const float *unknown, const float *known, float *dist2,
+                  int *idx, void *stream);
+
+/* Replaces three_interpolate_wrapper(b, c, m, n, points, idx, weight, out)
+ * (interpolate.cpp:27-41; kernel interpolate_gpu.cu:77-97).  points (B,C,M), idx/weight
+ * (B,N,3), out (B,C,N). */
+int kdpc_three_interpolate(int b, int c, int m, int n, const float *points, const int *idx,
+                           const float *weight, float *out, void *stream);
+
+/* Replaces three_interpolate_grad_wrapper(b, c, n, m, grad_out, idx, weight, grad_points)
+ * (interpolate.cpp:43-57; kernel interpolate_gpu.cu:120-142).  Overwrites grad_points (B,C,M). */
+int kdpc_three_interpolate_grad(int b, int c, int n, int m, const float *grad_out,
+                                const int *idx, const float *weight, float *grad_points,
+                                void *stream);
+
+/* ---- kNN (pointconv_util.py:73-107) ---------------------------------------------------- */
+
+/* Replaces knn_point(nsample, xyz, new_xyz) = square_distance + topk(largest=False).
+ * xyz (B,N,3) refs, new_xyz (B,S,3) queries, idx (B,S,K) int32 out ascending by
+ * (distance, index), dist (B,S,K) optional (NULL to skip).  1 <= K <= min(N, 64). */
+int kdpc_knn_point(int b, int n, int s, int k, const float *xyz, const float *new_xyz, int *idx,
+                   float *dist, void *stream);
+
+/* ---- point-major grouping + deterministic scatter (no reference counterpart: these
+ *      replace index_points_group's permute/grouping_operation/permute chain,
+ *      pointconv_util.py:122-133, and its atomicAdd backward) ------------------------- */
+
+/* out[b,p,:] = points[b, idx[b,p], :] ; points (B,N,C), idx (B,P), out (B,P,C). */
+int kdpc_group_rows(int b, int n, int c, int p, const float *points, const int *idx, float *out,
+                    void *stream);
+
+/* Inverted index of idx (B,P) with values in [0,N): offsets (B*N+1) and perm (B*P) (flat
+ * positions sorted by key b*N+idx, ascending position within a key).  workspace must hold
+ * kdpc_csr_workspace_bytes(b, n, p) bytes (query returns 0 on invalid sizes). */
+size_t kdpc_csr_workspace_bytes(int b, int n, int p);
+int kdpc_csr_build(int b, int n, int p, const int *idx, void *workspace, size_t workspace_bytes,
+                   int *offsets, int *perm, void *stream);
+
+/* grad_points[b,n,:] = sum of grad_out rows (B,P,C) that idx sent to n, ascending position. */
+int kdpc_group_rows_grad_csr(int b, int n, int c, const float *grad_out, const int *offsets,
+                             const int *perm, float *grad_points, void *stream);
+
+/* dst[b,c,n] = sum of src[b,c,p] over the positions p that idx sent to n (src (B,C,P),
+ * dst (B,C,N)): group_points_grad / gather_points_grad with a caller-built CSR. */
+int kdpc_csr_sum_channels(int b, int c, int n, int p, const float *src, const int *offsets,
+                          const int *perm, float *dst, void *stream);
+
+/* three_interpolate_grad with a caller-built CSR over idx (B,N,3) (key space M). */
+int kdpc_three_interpolate_grad_csr(int b, int c, int n, int m, const float *grad_out,
+                                    const float *weight, const int *offsets, const int *perm,
+                                    float *grad_points, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KDPC_H_ */

@@ -1,0 +1,82 @@
+// Shared device helpers for the gfx950 kernels of kd-pointcloud_amd.
+// Wave64 only: every cross-lane helper below assumes 64 lanes (CDNA4).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kdpc.h"  // C ABI declarations (include/kdpc.h): definitions must match
+
+#define KDPC_API extern "C" __attribute__((visibility("default")))
+
+namespace kdpc {
+
+constexpr int kWave = 64;
+
+__host__ __device__ inline int divup(int a, int b) { return (a + b - 1) / b; }
+__host__ __device__ inline long long divupll(long long a, long long b) { return (a + b - 1) / b; }
+
+// nvcc -O2 (fmad=true) contraction of (x2-x1)^2 + (y2-y1)^2 + (z2-z1)^2, as used by the
+// reference kernels (sampling_gpu.cu:130, ball_query_gpu.cu:33, interpolate_gpu.cu:36).
+// Written with explicit fmas so the compiler cannot re-contract or SLP-pack it.
+__device__ __forceinline__ float dist3(float x1, float y1, float z1, float x2, float y2,
+                                       float z2) {
+  const float dx = x2 - x1, dy = y2 - y1, dz = z2 - z1;
+  return __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __fmul_rn(dx, dx)));
+}
+
+// pointconv_util.py:73-94 square_distance, expanded form, exactly as torch evaluates it:
+//   dot = fma(z,z', fma(y,y', x*x'));  d = -2*dot;  d += |q|^2;  d += |r|^2
+// with |p|^2 = (x*x + y*y) + z*z separately rounded.
+__device__ __forceinline__ float sqnorm3(float x, float y, float z) {
+  return __fadd_rn(__fadd_rn(__fmul_rn(x, x), __fmul_rn(y, y)), __fmul_rn(z, z));
+}
+__device__ __forceinline__ float sqdist_expanded(float qx, float qy, float qz, float sq, float rx,
+                                                 float ry, float rz, float sr) {
+  const float dot = __builtin_fmaf(qz, rz, __builtin_fmaf(qy, ry, __fmul_rn(qx, rx)));
+  return __fadd_rn(__fadd_rn(-2.0f * dot, sq), sr);
+}
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
+
+// Full-wave butterfly reductions (every lane ends with the result).
+__device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    unsigned w = __shfl_xor(v, o, kWave);
+    v = w > v ? w : v;
+  }
+  return v;
+}
+__device__ __forceinline__ unsigned wave_min_u32(unsigned v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    unsigned w = __shfl_xor(v, o, kWave);
+    v = w < v ? w : v;
+  }
+  return v;
+}
+
+// lane l receives lane l-1's value; lane 0 receives `fill` (DPP wave_shr:1, gfx9).
+__device__ __forceinline__ float wave_shr1(float v, float fill) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(fill), __float_as_int(v),
+                                                    0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ int wave_shr1(int v, int fill) {
+  return __builtin_amdgcn_update_dpp(fill, v, 0x138, 0xf, 0xf, false);
+}
+
+__device__ __forceinline__ unsigned long long lanemask_lt() {
+  const int l = lane_id();
+  return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+
+}  // namespace kdpc
+
+// Argument validation shared by every C entry point: a bad size is an error code,
+// never a launch (reference launchers printed and exit(-1)ed on failure).
+#define KDPC_CHECK_ARG(cond)                       \
+  do {                                             \
+    if (!(cond)) return (int)hipErrorInvalidValue; \
+  } while (0)
+
+#define KDPC_RETURN_LAUNCH() return (int)hipGetLastError()

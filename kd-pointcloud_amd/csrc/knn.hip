@@ -1,0 +1,176 @@
+// Streaming k-nearest-neighbour selection: the MI355X replacement for the reference's
+// knn_point (pointconv_util.py:96-107) = square_distance (:73-94, a materialised (B,S,N)
+// matrix) + torch.topk(largest=False, sorted=False).
+//
+// Semantics: for each query, the K refs with the smallest expanded-form squared distance
+//   d = (-2 * fma(z,z',fma(y,y',x*x')) + |q|^2) + |r|^2
+// (bit-identical to torch's square_distance, see kdpc_common.h), ordered ascending by
+// (d, index).  topk(sorted=False) leaves order and exact-tie choice unspecified; we fix
+// them (ascending, lower index wins a tie), which the oracle (oracle_knn) restates.
+//
+// Design (no S x N matrix is ever written):
+//   * a workgroup = 4 waves; each wave owns QW queries; the workgroup streams the refs of
+//     its cloud through LDS in tiles of float4 {x, y, z, |r|^2} (|r|^2 computed once at
+//     staging), read by ds_read_b128 lane-contiguous (conflict-free);
+//   * each query's current best-64 list lives in the wave's registers, rank r in lane r
+//     ({d, idx} = 2 VGPRs per query); the K-th entry is the rejection threshold;
+//   * per 64-ref chunk a query costs 4 VALU + one compare whose VCC mask is the ballot;
+//     a chunk with no candidate (the common case once the list is warm) is skipped by
+//     a scalar branch;
+//   * few candidates: serial insertion with a DPP wave_shr:1 shift (~10 instr each);
+//     many candidates (the first chunks): 64-lane bitonic sort of the chunk + bitonic
+//     merge with the list.
+#include "kdpc_common.h"
+
+using namespace kdpc;
+
+namespace {
+
+constexpr int kTile = 2048;      // refs per LDS tile (32 KiB of float4)
+constexpr int kSerialMax = 8;    // candidates per chunk inserted one by one
+
+__device__ __forceinline__ bool kv_less(float ad, int ai, float bd, int bi) {
+  return ad < bd || (ad == bd && ai < bi);
+}
+
+// bitonic compare-exchange step across lanes l and l^jj
+__device__ __forceinline__ void bitonic_step(float& d, int& i, int jj, bool up) {
+  const float od = __shfl_xor(d, jj, kWave);
+  const int oi = __shfl_xor(i, jj, kWave);
+  const bool lower = (lane_id() & jj) == 0;
+  const bool o_less = kv_less(od, oi, d, i);
+  const bool take = (lower == up) ? o_less : !o_less && !(od == d && oi == i);
+  d = take ? od : d;
+  i = take ? oi : i;
+}
+
+__device__ __forceinline__ void bitonic_sort64(float& d, int& i) {
+#pragma unroll
+  for (int kk = 2; kk <= 64; kk <<= 1) {
+    const bool up = (lane_id() & kk) == 0 || kk == 64;
+#pragma unroll
+    for (int jj = kk >> 1; jj > 0; jj >>= 1) bitonic_step(d, i, jj, up);
+  }
+}
+
+__device__ __forceinline__ void bitonic_merge64(float& d, int& i) {
+#pragma unroll
+  for (int jj = 32; jj > 0; jj >>= 1) bitonic_step(d, i, jj, true);
+}
+
+// Merge the chunk's candidates (cand lanes carry {d, gi}) into the sorted list {ld, li}.
+__device__ __forceinline__ void insert_candidates(unsigned long long mask, bool cand, float d,
+                                                  int gi, float& ld, int& li) {
+  if (__popcll(mask) > kSerialMax) {
+    float cd = cand ? d : INFINITY;
+    int ci = cand ? gi : 0x7fffffff;
+    bitonic_sort64(cd, ci);
+    const int src = 63 - lane_id();
+    const float rd = __shfl(cd, src, kWave);
+    const int ri = __shfl(ci, src, kWave);
+    const bool take = kv_less(rd, ri, ld, li);
+    ld = take ? rd : ld;
+    li = take ? ri : li;
+    bitonic_merge64(ld, li);
+  } else {
+    // candidates arrive in ascending index order and every list entry has a smaller
+    // index, so an equal distance keeps the existing entry first (strict >).
+    while (mask) {
+      const int j = __ffsll((long long)mask) - 1;
+      mask &= mask - 1;
+      const float cd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), j));
+      const int ci = __builtin_amdgcn_readlane(gi, j);
+      const bool gt = ld > cd;
+      const float pd = wave_shr1(ld, -INFINITY);
+      const int pi = wave_shr1(li, 0);
+      const bool pgt = pd > cd;
+      const float nd = gt ? (pgt ? pd : cd) : ld;
+      const int ni = gt ? (pgt ? pi : ci) : li;
+      ld = nd;
+      li = ni;
+    }
+  }
+}
+
+template <int QW>
+__global__ __launch_bounds__(256) void knn_kernel(int n, int s, int k,
+                                                  const float* __restrict__ xyz,
+                                                  const float* __restrict__ new_xyz,
+                                                  int* __restrict__ idx,
+                                                  float* __restrict__ dist) {
+  __shared__ float4 tile[kTile];
+  const int b = blockIdx.y;
+  const int wave = threadIdx.x >> 6;
+  const int lane = lane_id();
+  const int qbase = (blockIdx.x * 4 + wave) * QW;
+  const float* xb = xyz + (long long)b * n * 3;
+
+  float qx[QW], qy[QW], qz[QW], qs[QW], thr[QW], ld[QW];
+  int li[QW];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) {
+    const int qi = min(qbase + q, s - 1);
+    const float* qp = new_xyz + ((long long)b * s + qi) * 3;
+    qx[q] = qp[0];
+    qy[q] = qp[1];
+    qz[q] = qp[2];
+    qs[q] = sqnorm3(qx[q], qy[q], qz[q]);
+    thr[q] = INFINITY;
+    ld[q] = INFINITY;
+    li[q] = 0x7fffffff;
+  }
+
+  for (int t0 = 0; t0 < n; t0 += kTile) {
+    const int tn = min(kTile, n - t0);
+    __syncthreads();
+    for (int e = threadIdx.x; e < tn; e += blockDim.x) {
+      const float* r = xb + (long long)(t0 + e) * 3;
+      const float x = r[0], y = r[1], z = r[2];
+      tile[e] = make_float4(x, y, z, sqnorm3(x, y, z));
+    }
+    __syncthreads();
+    for (int c0 = 0; c0 < tn; c0 += kWave) {
+      const int j = c0 + lane;
+      const bool valid = j < tn;
+      const float4 r = tile[valid ? j : 0];
+      const int gi = t0 + j;
+#pragma unroll
+      for (int q = 0; q < QW; ++q) {
+        if (qbase + q >= s) continue;  // wave-uniform
+        const float d = sqdist_expanded(qx[q], qy[q], qz[q], qs[q], r.x, r.y, r.z, r.w);
+        const bool cand = valid && d < thr[q];
+        const unsigned long long mask = __ballot(cand);
+        if (mask == 0ull) continue;
+        insert_candidates(mask, cand, d, gi, ld[q], li[q]);
+        thr[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ld[q]), k - 1));
+      }
+    }
+  }
+
+#pragma unroll
+  for (int q = 0; q < QW; ++q) {
+    const int qi = qbase + q;
+    if (qi < s && lane < k) {
+      const long long o = ((long long)b * s + qi) * k + lane;
+      idx[o] = li[q];
+      if (dist) dist[o] = ld[q];
+    }
+  }
+}
+
+}  // namespace
+
+// knn_point(nsample=k, xyz (B,N,3) refs, new_xyz (B,S,3) queries) -> idx (B,S,K) int32,
+// optional dist (B,S,K) f32 (expanded-form squared distances).  Requires 1 <= K <= min(N,64).
+// Replaces pointconv_util.py:96-107 (which returns int64 from topk).
+KDPC_API int kdpc_knn_point(int b, int n, int s, int k, const float* xyz, const float* new_xyz,
+                            int* idx, float* dist, void* stream) {
+  KDPC_CHECK_ARG(b >= 0 && n > 0 && s >= 0 && k >= 1 && k <= 64 && k <= n && b <= 65535);
+  if ((long long)b * s == 0) return (int)hipSuccess;
+  KDPC_CHECK_ARG(xyz && new_xyz && idx);
+  constexpr int QW = 4;
+  const int per_block = 4 * QW;
+  hipLaunchKernelGGL(knn_kernel<QW>, dim3(divup(s, per_block), b), dim3(256), 0,
+                     (hipStream_t)stream, n, s, k, xyz, new_xyz, idx, dist);
+  KDPC_RETURN_LAUNCH();
+}

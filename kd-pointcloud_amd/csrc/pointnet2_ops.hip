@@ -1,0 +1,254 @@
+// Forward kernels behind the reference's pointnet2_cuda API (channel-major (B,C,N)
+// features, point-major (B,N,3) xyz, int32 indices).  Backward kernels live in
+// scatter.hip (deterministic CSR reductions instead of the reference's float atomics).
+#include "kdpc_common.h"
+
+using namespace kdpc;
+
+namespace {
+
+// ---------------------------------------------------------------------------------------
+// gather_points: out[b,c,m] = points[b,c,idx[b,m]]        (reference sampling_gpu.cu:8-24)
+// One thread per output element, m fastest: coalesced idx reads and stores.
+__global__ __launch_bounds__(256) void gather_points_kernel(int b, int c, int n, int m,
+                                                            const float* __restrict__ points,
+                                                            const int* __restrict__ idx,
+                                                            float* __restrict__ out) {
+  const long long total = (long long)b * c * m;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int p = (int)(e % m);
+    const long long bc = e / m;
+    const int bi = (int)(bc / c);
+    out[e] = points[bc * n + idx[(long long)bi * m + p]];
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// group_points: out[b,c,s,k] = points[b,c,idx[b,s,k]]   (reference group_points_gpu.cu:47-66)
+// A thread owns 4 consecutive (s,k) positions (one int4 idx load reused for CG channels,
+// one float4 store per channel); blockIdx.y walks channel groups.  The index tile is read
+// once per channel group instead of once per channel.
+constexpr int kGroupCG = 8;
+
+__global__ __launch_bounds__(256) void group_points_kernel(int c, int n, int p_total,
+                                                           const float* __restrict__ points,
+                                                           const int* __restrict__ idx,
+                                                           float* __restrict__ out) {
+  const int bi = blockIdx.z;
+  const int c0 = blockIdx.y * kGroupCG;
+  const int p4 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (p4 >= p_total) return;
+  const int* ib = idx + (long long)bi * p_total;
+  const float* pb = points + ((long long)bi * c + c0) * n;
+  float* ob = out + ((long long)bi * c + c0) * p_total;
+  const int cg = min(kGroupCG, c - c0);
+  if (p4 + 3 < p_total && (p_total & 3) == 0) {
+    const int4 q = *reinterpret_cast<const int4*>(ib + p4);
+    for (int cc = 0; cc < cg; ++cc) {
+      const float* row = pb + (long long)cc * n;
+      float4 v;
+      v.x = row[q.x];
+      v.y = row[q.y];
+      v.z = row[q.z];
+      v.w = row[q.w];
+      *reinterpret_cast<float4*>(ob + (long long)cc * p_total + p4) = v;
+    }
+  } else {
+    for (int t = 0; t < 4 && p4 + t < p_total; ++t) {
+      const int q = ib[p4 + t];
+      for (int cc = 0; cc < cg; ++cc) ob[(long long)cc * p_total + p4 + t] = pb[(long long)cc * n + q];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// ball_query (reference ball_query_gpu.cu:9-45): the first nsample k (ascending) with
+// d2 < r^2; if any hit, the remaining slots repeat the first hit; no hit -> zeros.
+// One wave per query: lanes test 64 consecutive candidates, ballot + popcount give each
+// hit its slot in ascending-k order, and the wave stops as soon as nsample hits exist —
+// identical output to the reference's serial scan.
+__global__ __launch_bounds__(256) void ball_query_kernel(int b, int n, int m, float radius2,
+                                                         int nsample,
+                                                         const float* __restrict__ new_xyz,
+                                                         const float* __restrict__ xyz,
+                                                         int* __restrict__ idx) {
+  const int wave_global = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = lane_id();
+  if (wave_global >= b * m) return;
+  const int bi = wave_global / m;
+  const float* q = new_xyz + (long long)wave_global * 3;
+  const float qx = q[0], qy = q[1], qz = q[2];
+  const float* xb = xyz + (long long)bi * n * 3;
+  int* out = idx + (long long)wave_global * nsample;
+  int cnt = 0;
+  int first = 0;
+  for (int base = 0; base < n && cnt < nsample; base += kWave) {
+    const int k = base + lane;
+    bool hit = false;
+    if (k < n) {
+      const float d2 = dist3(xb[k * 3 + 0], xb[k * 3 + 1], xb[k * 3 + 2], qx, qy, qz);
+      hit = d2 < radius2;
+    }
+    const unsigned long long mask = __ballot(hit);
+    if (mask == 0ull) continue;
+    if (cnt == 0) first = base + __ffsll((long long)mask) - 1;
+    const int slot = cnt + __popcll(mask & lanemask_lt());
+    if (hit && slot < nsample) out[slot] = k;
+    cnt += __popcll(mask);
+  }
+  // slots past the hit count: first hit (reference fill loop, :36-39) or zero
+  for (int s = cnt + lane; s < nsample; s += kWave) out[s] = cnt > 0 ? first : 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// three_nn (reference interpolate_gpu.cu:9-52): 3 smallest d2 per unknown point, strict <
+// so the earlier known index wins ties (the reference's double running bests compare the
+// same float values).  One thread per unknown point; known points staged through LDS in
+// tiles and read as broadcasts.
+constexpr int kNNTile = 1024;
+
+__global__ __launch_bounds__(256) void three_nn_kernel(int b, int n, int m,
+                                                       const float* __restrict__ unknown,
+                                                       const float* __restrict__ known,
+                                                       float* __restrict__ dist2,
+                                                       int* __restrict__ idx) {
+  __shared__ float sk[kNNTile * 3];
+  const int bi = blockIdx.y;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = p < n;
+  float ux = 0.f, uy = 0.f, uz = 0.f;
+  if (active) {
+    const float* u = unknown + ((long long)bi * n + p) * 3;
+    ux = u[0]; uy = u[1]; uz = u[2];
+  }
+  const float* kb = known + (long long)bi * m * 3;
+  float b1 = INFINITY, b2 = INFINITY, b3 = INFINITY;
+  int i1 = 0, i2 = 0, i3 = 0;
+  for (int t0 = 0; t0 < m; t0 += kNNTile) {
+    const int tn = min(kNNTile, m - t0);
+    __syncthreads();
+    for (int e = threadIdx.x; e < tn * 3; e += blockDim.x) sk[e] = kb[(long long)t0 * 3 + e];
+    __syncthreads();
+    if (active) {
+      for (int j = 0; j < tn; ++j) {
+        const float d = dist3(sk[j * 3 + 0], sk[j * 3 + 1], sk[j * 3 + 2], ux, uy, uz);
+        const int k = t0 + j;
+        if (d < b1) {
+          b3 = b2; i3 = i2; b2 = b1; i2 = i1; b1 = d; i1 = k;
+        } else if (d < b2) {
+          b3 = b2; i3 = i2; b2 = d; i2 = k;
+        } else if (d < b3) {
+          b3 = d; i3 = k;
+        }
+      }
+    }
+  }
+  if (active) {
+    float* o = dist2 + ((long long)bi * n + p) * 3;
+    int* oi = idx + ((long long)bi * n + p) * 3;
+    // reference initial best is 1e40 in double, stored as (float)1e40 == +inf
+    o[0] = b1; o[1] = b2; o[2] = b3;
+    oi[0] = i1; oi[1] = i2; oi[2] = i3;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// three_interpolate (reference interpolate_gpu.cu:77-97), n fastest.
+__global__ __launch_bounds__(256) void three_interpolate_kernel(int b, int c, int m, int n,
+                                                                const float* __restrict__ points,
+                                                                const int* __restrict__ idx,
+                                                                const float* __restrict__ weight,
+                                                                float* __restrict__ out) {
+  const long long total = (long long)b * c * n;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int p = (int)(e % n);
+    const long long bc = e / n;
+    const int bi = (int)(bc / c);
+    const float* row = points + bc * m;
+    const long long o3 = ((long long)bi * n + p) * 3;
+    const float w0 = weight[o3 + 0], w1 = weight[o3 + 1], w2 = weight[o3 + 2];
+    const float v0 = row[idx[o3 + 0]], v1 = row[idx[o3 + 1]], v2 = row[idx[o3 + 2]];
+    out[e] = __builtin_fmaf(w2, v2, __builtin_fmaf(w1, v1, __fmul_rn(w0, v0)));
+  }
+}
+
+inline int grid_for(long long total, int block) {
+  long long g = divupll(total, block);
+  if (g > 65536) g = 65536;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+// Reference: gather_points_wrapper(b, c, n, npoints, points, idx, out)  (sampling.cpp:11-22)
+KDPC_API int kdpc_gather_points(int b, int c, int n, int npoints, const float* points,
+                                const int* idx, float* out, void* stream) {
+  KDPC_CHECK_ARG(b >= 0 && c >= 0 && n > 0 && npoints >= 0);
+  const long long total = (long long)b * c * npoints;
+  if (total == 0) return (int)hipSuccess;
+  KDPC_CHECK_ARG(points && idx && out);
+  hipLaunchKernelGGL(gather_points_kernel, dim3(grid_for(total, 256)), dim3(256), 0,
+                     (hipStream_t)stream, b, c, n, npoints, points, idx, out);
+  KDPC_RETURN_LAUNCH();
+}
+
+// Reference: group_points_wrapper(b, c, n, npoints, nsample, points, idx, out)
+// (group_points.cpp:27-38)
+KDPC_API int kdpc_group_points(int b, int c, int n, int npoints, int nsample, const float* points,
+                               const int* idx, float* out, void* stream) {
+  KDPC_CHECK_ARG(b >= 0 && c >= 0 && n > 0 && npoints >= 0 && nsample >= 0);
+  const long long p_total = (long long)npoints * nsample;
+  if ((long long)b * c * p_total == 0) return (int)hipSuccess;
+  KDPC_CHECK_ARG(points && idx && out && p_total < (1ll << 31));
+  KDPC_CHECK_ARG(b <= 65535);
+  dim3 grid(divup((int)divupll(p_total, 4), 256), divup(c, kGroupCG), b);
+  KDPC_CHECK_ARG(grid.y <= 65535);
+  hipLaunchKernelGGL(group_points_kernel, grid, dim3(256), 0, (hipStream_t)stream, c, n,
+                     (int)p_total, points, idx, out);
+  KDPC_RETURN_LAUNCH();
+}
+
+// Reference: ball_query_wrapper(b, n, m, radius, nsample, new_xyz, xyz, idx)
+// (ball_query.cpp:16-28).  idx is fully written (zeros where the reference relied on the
+// caller's .zero_()).
+KDPC_API int kdpc_ball_query(int b, int n, int m, float radius, int nsample, const float* new_xyz,
+                             const float* xyz, int* idx, void* stream) {
+  KDPC_CHECK_ARG(b >= 0 && n >= 0 && m >= 0 && nsample >= 0);
+  if ((long long)b * m * nsample == 0) return (int)hipSuccess;
+  KDPC_CHECK_ARG(new_xyz && idx && (n == 0 || xyz));
+  const long long waves = (long long)b * m;
+  KDPC_CHECK_ARG(waves * kWave < (1ll << 31));
+  const float r2 = radius * radius;
+  hipLaunchKernelGGL(ball_query_kernel, dim3((int)divupll(waves * kWave, 256)), dim3(256), 0,
+                     (hipStream_t)stream, b, n, m, r2, nsample, new_xyz, xyz, idx);
+  KDPC_RETURN_LAUNCH();
+}
+
+// Reference: three_nn_wrapper(b, n, m, unknown, known, dist2, idx)  (interpolate.cpp:14-24).
+// dist2 holds squared distances (the Python wrapper takes the sqrt).
+KDPC_API int kdpc_three_nn(int b, int n, int m, const float* unknown, const float* known,
+                           float* dist2, int* idx, void* stream) {
+  KDPC_CHECK_ARG(b >= 0 && n >= 0 && m >= 0 && b <= 65535);
+  if ((long long)b * n == 0) return (int)hipSuccess;
+  KDPC_CHECK_ARG(unknown && dist2 && idx && (m == 0 || known));
+  hipLaunchKernelGGL(three_nn_kernel, dim3(divup(n, 256), b), dim3(256), 0, (hipStream_t)stream,
+                     b, n, m, unknown, known, dist2, idx);
+  KDPC_RETURN_LAUNCH();
+}
+
+// Reference: three_interpolate_wrapper(b, c, m, n, points, idx, weight, out)
+// (interpolate.cpp:27-41)
+KDPC_API int kdpc_three_interpolate(int b, int c, int m, int n, const float* points,
+                                    const int* idx, const float* weight, float* out,
+                                    void* stream) {
+  KDPC_CHECK_ARG(b >= 0 && c >= 0 && m > 0 && n >= 0);
+  const long long total = (long long)b * c * n;
+  if (total == 0) return (int)hipSuccess;
+  KDPC_CHECK_ARG(points && idx && weight && out);
+  hipLaunchKernelGGL(three_interpolate_kernel, dim3(grid_for(total, 256)), dim3(256), 0,
+                     (hipStream_t)stream, b, c, m, n, points, idx, weight, out);
+  KDPC_RETURN_LAUNCH();
+}

@@ -1,0 +1,101 @@
+"""Training and knowledge-distillation steps, single GPU or DDP over RCCL.
+
+Restates the per-step body of distilTrain.py:156-185 (and the flow-network step of
+train_bid_pointconv.py) MI355X-first:
+  * one process per GPU, torch DDP (backend "nccl" = RCCL over xGMI) instead of the
+    reference's single-process nn.DataParallel (distilTrain.py:108-117).  DDP's bucketed
+    gradient all-reduce runs on RCCL's own stream, overlapped with the backward;
+  * the frozen teacher is replicated per rank outside DDP (no communication);
+  * BatchNorm statistics stay per replica (the DataParallel semantics, no SyncBN);
+    broadcast_buffers keeps rank 0's running stats authoritative, as DataParallel's
+    device-0 module was;
+  * the 80 parameters that never receive a gradient (the cost volumes' unused
+    bias1/bias2, WeightNet's unused BN modules) are handled by static_graph;
+  * no per-step host sync: the loss stays on the device (the reference called
+    loss.cpu() twice per step, distilTrain.py:179,184).
+The step is model-agnostic (any module returning the reference's 8-tuple), which lets the
+multi-process path be tested on CPU with gloo.
+"""
+import torch
+import torch.distributed as dist
+
+import loss_functions
+
+
+def is_dist():
+    return dist.is_available() and dist.is_initialized()
+
+
+def wrap_ddp(model, device=None):
+    """Wrap the trained model for DDP when a process group is up (no-op otherwise)."""
+    if not is_dist() or dist.get_world_size() == 1:
+        return model
+    kw = dict(broadcast_buffers=True, static_graph=True, gradient_as_bucket_view=True)
+    if device is not None and device.type == "cuda":
+        kw["device_ids"] = [device.index]
+    return torch.nn.parallel.DistributedDataParallel(model, **kw)
+
+
+def make_optimizer(model, lr=1e-3, weight_decay=1e-4):
+    """Adam as configured by config_train_kd_pointconv.yaml:15-24 / distilTrain.py:134-135."""
+    return torch.optim.Adam(model.parameters(), lr=lr, betas=(0.9, 0.999), eps=1e-08,
+                            weight_decay=weight_decay)
+
+
+class FlowTrainStep:
+    """fwd -> multiScaleLoss -> bwd -> optimizer step (one scene-flow training iteration)."""
+
+    def __init__(self, model, optimizer, loss_fn=None):
+        self.model = model
+        self.opt = optimizer
+        self.loss_fn = loss_fn or loss_functions.multiScaleLoss
+
+    def __call__(self, pos1, pos2, flow, color1=None, color2=None):
+        color1 = pos1 if color1 is None else color1
+        color2 = pos2 if color2 is None else color2
+        self.model.train()
+        flows, fps1, _, _, _, _, _, _ = self.model(pos1, pos2, color1, color2)
+        loss = self.loss_fn(flows, flow, fps1)
+        loss.backward()
+        self.opt.step()
+        self.opt.zero_grad(set_to_none=True)
+        return loss.detach()
+
+
+class KDTrainStep:
+    """distilTrain.py:164-182: teacher fwd (eval, no_grad) + student fwd (train) + KD loss +
+    bwd + step.  The loss is biDirection_loss_ht(gamma=0.3, beta=0.8, layer=3): the shipped
+    cross_biDirection_loss_ht cannot run on this teacher/student pair."""
+
+    def __init__(self, teacher, student, optimizer, gamma=0.3, beta=0.8, layer=3, loss_fn=None):
+        self.loss_fn = loss_fn or loss_functions.biDirection_loss_ht
+        self.teacher = teacher
+        self.student = student
+        self.opt = optimizer
+        self.gamma, self.beta, self.layer = gamma, beta, layer
+        for p in self.teacher.parameters():
+            p.requires_grad_(False)
+
+    def __call__(self, pos1, pos2, flow, color1=None, color2=None):
+        color1 = pos1 if color1 is None else color1
+        color2 = pos2 if color2 is None else color2
+        self.teacher.eval()
+        with torch.no_grad():
+            t_flows, t_fps1, t_fps2, _, _, t_feat1s, t_feat2s, _ = self.teacher(pos1, pos2, color1, color2)
+        self.student.train()
+        flows, fps1, fps2, _, _, feat1s, feat2s, _ = self.student(pos1, pos2, color1, color2)
+        loss = self.loss_fn(
+            flows, feat1s, feat2s, fps1, fps2, flow, t_flows, t_feat1s, t_feat2s, t_fps1, t_fps2,
+            self.gamma, self.beta, layer=self.layer)
+        loss.backward()
+        self.opt.step()
+        self.opt.zero_grad(set_to_none=True)
+        return loss.detach()
+
+
+@torch.no_grad()
+def epe3d(model, pos1, pos2, flow):
+    """EPE3D as distilTrain.py:229 / evaluation_utils.py:23-24: mean ||flow0^T - gt||."""
+    model.eval()
+    flows = model(pos1, pos2, pos1, pos2)[0]
+    return torch.norm(flows[0].permute(0, 2, 1) - flow, dim=2).mean()

@@ -1,0 +1,290 @@
+"""ctypes binding of libkdpc_hip.so (the C ABI in include/kdpc.h) for torch-ROCm tensors.
+
+Every op here runs the gfx950 HIP kernels on the tensors' device and the current torch
+stream.  There is no CPU path: a missing library, a CPU tensor or a wrong dtype raises.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libkdpc_hip.so")
+
+_c_int, _c_float, _c_size, _vp = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
+
+# name -> argtypes (all return int hipError_t, except where noted)
+_SIGNATURES = {
+    "kdpc_furthest_point_sampling": [_c_int, _c_int, _c_int, _vp, _vp, _vp, _vp],
+    "kdpc_opt_n_threads": [_c_int],
+    "kdpc_gather_points": [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp],
+    "kdpc_gather_points_grad": [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp],
+    "kdpc_ball_query": [_c_int, _c_int, _c_int, _c_float, _c_int, _vp, _vp, _vp, _vp],
+    "kdpc_group_points": [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp],
+    "kdpc_group_points_grad": [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp],
+    "kdpc_three_nn": [_c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
+    "kdpc_three_interpolate": [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
+    "kdpc_three_interpolate_grad": [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
+    "kdpc_knn_point": [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
+    "kdpc_group_rows": [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp],
+    "kdpc_csr_workspace_bytes": [_c_int, _c_int, _c_int],
+    "kdpc_csr_build": [_c_int, _c_int, _c_int, _vp, _vp, _c_size, _vp, _vp, _vp],
+    "kdpc_group_rows_grad_csr": [_c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
+    "kdpc_csr_sum_channels": [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
+    "kdpc_three_interpolate_grad_csr": [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp,
+                                        _vp, _vp],
+}
+_RESTYPES = {"kdpc_csr_workspace_bytes": _c_size}
+
+EXPORTED = tuple(_SIGNATURES)
+
+_lib = None
+
+
+class KdpcError(RuntimeError):
+    pass
+
+
+def load_library(path=LIB_PATH):
+    """Load and type the HIP library (works without a GPU: symbols only)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise KdpcError(
+            f"kd-pointcloud_amd HIP library not found at {path}; build it with "
+            "`python kd-pointcloud_amd/build_native.py` (there is no CPU fallback)")
+    lib = ctypes.CDLL(path)
+    for name, args in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = _RESTYPES.get(name, _c_int)
+    _lib = lib
+    return lib
+
+
+def _check(status, name):
+    if status != 0:
+        raise KdpcError(f"{name} failed with hipError_t {status}")
+
+
+def _stream(t):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _dev(t, dtype, name):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a tensor")
+    if not t.is_cuda:
+        raise KdpcError(f"{name} must be a GPU (HIP) tensor: kd-pointcloud_amd has no CPU path")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    return t.data_ptr()
+
+
+class LaunchTimer:
+    """Brackets every launch of the named C entry points with HIP events on the current
+    torch stream (the stream the kernel runs on) and accumulates per-launch algorithmic
+    bytes/flops supplied by the op wrappers.  Used by bench.py for the live roofline."""
+
+    def __init__(self, names):
+        self.names = set(names)
+        self.records = []  # (name, start_event, end_event, bytes, flops)
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for name, e0, e1, nbytes, flops in self.records:
+            d = out.setdefault(name, {"launches": 0, "ms": 0.0, "bytes": 0.0, "flops": 0.0})
+            d["launches"] += 1
+            d["ms"] += e0.elapsed_time(e1)
+            d["bytes"] += nbytes
+            d["flops"] += flops
+        return out
+
+
+_timer = None
+
+
+def set_launch_timer(timer):
+    global _timer
+    _timer = timer
+
+
+def _call(name, *args, work=None):
+    """Invoke a C entry point; `work` = (algorithmic bytes, flops) for the launch timer."""
+    lib = load_library()
+    t = _timer
+    if t is not None and name in t.names:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        _check(getattr(lib, name)(*args), name)
+        e1.record()
+        nb, fl = work if work is not None else (0.0, 0.0)
+        t.records.append((name, e0, e1, float(nb), float(fl)))
+        return
+    _check(getattr(lib, name)(*args), name)
+
+
+# ------------------------------------------------------------------------------ ops
+def furthest_point_sampling(xyz, npoint, temp=None):
+    """xyz (B,N,3) f32 -> idx (B,npoint) i32.  temp: optional (B,N) scratch (1e10-filled)."""
+    B, N, _ = xyz.shape
+    idx = torch.empty((B, npoint), dtype=torch.int32, device=xyz.device)
+    if temp is None:
+        temp = torch.full((B, N), 1e10, dtype=torch.float32, device=xyz.device)
+    _call("kdpc_furthest_point_sampling", B, N, npoint, _dev(xyz, torch.float32, "xyz"),
+          _dev(temp, torch.float32, "temp"), _dev(idx, torch.int32, "idx"), _stream(xyz),
+          work=(B * (12 * N + 8 * N + 4 * npoint), B * N * npoint * 8))
+    return idx
+
+
+def gather_points(points, idx):
+    """points (B,C,N), idx (B,M) i32 -> (B,C,M)."""
+    B, C, N = points.shape
+    M = idx.shape[1]
+    out = torch.empty((B, C, M), dtype=torch.float32, device=points.device)
+    _call("kdpc_gather_points", B, C, N, M, _dev(points, torch.float32, "points"),
+          _dev(idx, torch.int32, "idx"), _dev(out, torch.float32, "out"), _stream(points))
+    return out
+
+
+def ball_query(radius, nsample, xyz, new_xyz):
+    B, N, _ = xyz.shape
+    M = new_xyz.shape[1]
+    idx = torch.empty((B, M, nsample), dtype=torch.int32, device=xyz.device)
+    _call("kdpc_ball_query", B, N, M, float(radius), int(nsample),
+          _dev(new_xyz, torch.float32, "new_xyz"), _dev(xyz, torch.float32, "xyz"),
+          _dev(idx, torch.int32, "idx"), _stream(xyz))
+    return idx
+
+
+def group_points(points, idx):
+    """points (B,C,N), idx (B,S,K) i32 -> (B,C,S,K)."""
+    B, C, N = points.shape
+    _, S, K = idx.shape
+    out = torch.empty((B, C, S, K), dtype=torch.float32, device=points.device)
+    # SURVEY §8d algorithmic bytes: B*(4CN + 4SK + 4CSK)
+    _call("kdpc_group_points", B, C, N, S, K, _dev(points, torch.float32, "points"),
+          _dev(idx, torch.int32, "idx"), _dev(out, torch.float32, "out"), _stream(points),
+          work=(B * (4 * C * N + 4 * S * K + 4 * C * S * K), 0))
+    return out
+
+
+def three_nn(unknown, known):
+    """-> (dist2 (B,N,3) squared, idx (B,N,3) i32)."""
+    B, N, _ = unknown.shape
+    M = known.shape[1]
+    dist2 = torch.empty((B, N, 3), dtype=torch.float32, device=unknown.device)
+    idx = torch.empty((B, N, 3), dtype=torch.int32, device=unknown.device)
+    _call("kdpc_three_nn", B, N, M, _dev(unknown, torch.float32, "unknown"),
+          _dev(known, torch.float32, "known"), _dev(dist2, torch.float32, "dist2"),
+          _dev(idx, torch.int32, "idx"), _stream(unknown))
+    return dist2, idx
+
+
+def three_interpolate(points, idx, weight):
+    B, C, M = points.shape
+    N = idx.shape[1]
+    out = torch.empty((B, C, N), dtype=torch.float32, device=points.device)
+    _call("kdpc_three_interpolate", B, C, M, N, _dev(points, torch.float32, "points"),
+          _dev(idx, torch.int32, "idx"), _dev(weight, torch.float32, "weight"),
+          _dev(out, torch.float32, "out"), _stream(points))
+    return out
+
+
+def knn_point(nsample, xyz, new_xyz, return_dist=False):
+    """xyz (B,N,3) refs, new_xyz (B,S,3) queries -> idx (B,S,K) i32 ascending (dist, idx)."""
+    B, N, _ = xyz.shape
+    S = new_xyz.shape[1]
+    if nsample > N:
+        raise ValueError(f"knn_point: nsample={nsample} > number of points {N}")
+    idx = torch.empty((B, S, nsample), dtype=torch.int32, device=xyz.device)
+    dist = torch.empty((B, S, nsample), dtype=torch.float32, device=xyz.device) if return_dist else None
+    _call("kdpc_knn_point", B, N, S, int(nsample), _dev(xyz, torch.float32, "xyz"),
+          _dev(new_xyz, torch.float32, "new_xyz"), _dev(idx, torch.int32, "idx"),
+          _dev(dist, torch.float32, "dist") if dist is not None else None, _stream(xyz),
+          work=(B * (12 * N + 12 * S + 4 * S * nsample * (2 if return_dist else 1)),
+                B * S * N * 8))
+    return (idx, dist) if return_dist else idx
+
+
+def group_rows(points, idx):
+    """points (B,N,C), idx (B,P) i32 -> (B,P,C) (point-major row gather)."""
+    B, N, C = points.shape
+    P = idx.shape[1]
+    out = torch.empty((B, P, C), dtype=torch.float32, device=points.device)
+    # algorithmic bytes: idx read + gathered rows read + rows written (B*(4P + 8PC))
+    _call("kdpc_group_rows", B, N, C, P, _dev(points, torch.float32, "points"),
+          _dev(idx, torch.int32, "idx"), _dev(out, torch.float32, "out"), _stream(points),
+          work=(B * (4 * P + 8 * P * C), 0))
+    return out
+
+
+class Csr:
+    """Inverted index of an int32 index tensor (B,P) over a key space of n values."""
+    __slots__ = ("offsets", "perm", "n", "p")
+
+    def __init__(self, idx2d, n):
+        B, P = idx2d.shape
+        lib = load_library()
+        ws_bytes = lib.kdpc_csr_workspace_bytes(B, n, P)
+        if ws_bytes == 0:
+            raise KdpcError("kdpc_csr_workspace_bytes returned 0 (invalid sizes?)")
+        dev = idx2d.device
+        ws = torch.empty((ws_bytes,), dtype=torch.uint8, device=dev)
+        self.offsets = torch.empty((B * n + 1,), dtype=torch.int32, device=dev)
+        self.perm = torch.empty((B * P,), dtype=torch.int32, device=dev)
+        self.n, self.p = n, P
+        _call("kdpc_csr_build", B, n, P, _dev(idx2d, torch.int32, "idx"), ws.data_ptr(), ws_bytes,
+              self.offsets.data_ptr(), self.perm.data_ptr(), _stream(idx2d))
+
+
+def csr_of(idx, n):
+    """CSR for idx (B,...) flattened to (B,P), cached on the index tensor object."""
+    cache = getattr(idx, "_kdpc_csr", None)
+    if cache is not None and cache.n == n:
+        return cache
+    csr = Csr(idx.reshape(idx.shape[0], -1), n)
+    try:
+        idx._kdpc_csr = csr
+    except AttributeError:
+        pass
+    return csr
+
+
+def group_rows_grad(grad_out, csr, B, N, C):
+    """grad_out (B,P,C) -> (B,N,C) deterministic scatter-add through csr."""
+    grad_out = grad_out.contiguous()
+    out = torch.empty((B, N, C), dtype=torch.float32, device=grad_out.device)
+    P = grad_out.shape[1]
+    _call("kdpc_group_rows_grad_csr", B, N, C, _dev(grad_out, torch.float32, "grad_out"),
+          csr.offsets.data_ptr(), csr.perm.data_ptr(), _dev(out, torch.float32, "grad_points"),
+          _stream(grad_out), work=(B * (4 * P * C + 4 * P + 4 * N + 4 * N * C), 0))
+    return out
+
+
+def csr_sum_channels(src, csr, B, C, N):
+    """src (B,C,P) -> (B,C,N): the backward of gather_points/group_points."""
+    src = src.contiguous()
+    P = src.numel() // max(1, B * C)
+    out = torch.empty((B, C, N), dtype=torch.float32, device=src.device)
+    _call("kdpc_csr_sum_channels", B, C, N, P, _dev(src, torch.float32, "src"),
+          csr.offsets.data_ptr(), csr.perm.data_ptr(), _dev(out, torch.float32, "dst"),
+          _stream(src))
+    return out
+
+
+def three_interpolate_grad(grad_out, idx, weight, m):
+    """grad_out (B,C,N) -> (B,C,M) deterministic."""
+    grad_out = grad_out.contiguous()
+    B, C, N = grad_out.shape
+    csr = csr_of(idx, m)
+    out = torch.empty((B, C, m), dtype=torch.float32, device=grad_out.device)
+    _call("kdpc_three_interpolate_grad_csr", B, C, N, m, _dev(grad_out, torch.float32, "grad_out"),
+          _dev(weight, torch.float32, "weight"), csr.offsets.data_ptr(), csr.perm.data_ptr(),
+          _dev(out, torch.float32, "grad_points"), _stream(grad_out))
+    return out

@@ -1,0 +1,130 @@
+"""Scene-flow and knowledge-distillation losses (drop-in for the reference's loss_functions.py).
+
+Same names, arguments and arithmetic as the reference (loss_functions.py:6-235); the only
+change is that accumulators are created on the inputs' device instead of via
+`torch.zeros(1).cuda()`, and the GT pyramid is gathered with the HIP row gather.
+The iterative/bridge variants (att_*, bridge_*) belong to models outside this build's scope.
+"""
+import torch
+
+from pointconv_util import index_points_gather as index_points
+
+scale = 1.0
+
+
+def _zero(ref):
+    return torch.zeros(1, device=ref.device, dtype=ref.dtype)
+
+
+def _gt_pyramid(gt_flow, fps_idxs):
+    gt_flows = [gt_flow]
+    for fps_idx in fps_idxs:
+        gt_flows.append(index_points(gt_flows[-1], fps_idx) / scale)
+    return gt_flows
+
+
+def multiScaleLoss(pred_flows, gt_flow, fps_idxs, alpha=[0.02, 0.04, 0.08, 0.16]):
+    """Reference: loss_functions.py:6-25.
+    sum_i alpha_i * mean_b sum_n ||pred_i^T - gt_i||_2 over a GT pyramid gathered with the
+    FPS indices; pred_flows[i] is (B,3,N_i), gt_flow (B,N,3)."""
+    num_scale = len(pred_flows)
+    offset = len(fps_idxs) - num_scale + 1
+    gt_flows = _gt_pyramid(gt_flow, fps_idxs)
+    total_loss = _zero(gt_flow)
+    for i in range(num_scale):
+        diff_flow = pred_flows[i].permute(0, 2, 1) - gt_flows[i + offset]
+        total_loss += alpha[i] * torch.norm(diff_flow, dim=2).sum(dim=1).mean()
+    return total_loss
+
+
+def loss_fn_kd_2(outputs, fps_idxs, gt_flow, teacher_outputs, teacher_fps_idxs, gamma,
+                 alpha=[0.02, 0.04, 0.08, 0.16]):
+    """Reference: loss_functions.py:27-36."""
+    t0 = teacher_outputs[0].permute(0, 2, 1)
+    loss1 = multiScaleLoss(outputs, t0, fps_idxs)
+    loss2 = multiScaleLoss(outputs, gt_flow, fps_idxs)
+    return _zero(gt_flow) + (gamma * loss1 + (1 - gamma) * loss2)
+
+
+def attentiveImitationLoss(outputs, fps_idxs, gt_flow, teacher_outputs, teacher_fps_idxs,
+                           t_history, gamma, alpha=[0.02, 0.04, 0.08, 0.16]):
+    """Reference: loss_functions.py:38-51."""
+    t0 = teacher_outputs[0].permute(0, 2, 1)
+    loss_ST = multiScaleLoss(outputs, t0, fps_idxs)
+    loss_SG = multiScaleLoss(outputs, gt_flow, fps_idxs)
+    loss_TG = multiScaleLoss(teacher_outputs, gt_flow, teacher_fps_idxs)
+    sigma = 1 - ((loss_TG) / (max(t_history) - min(t_history)))
+    return _zero(gt_flow) + (gamma * loss_SG + (1 - gamma) * sigma * loss_ST)
+
+
+def biDirectionLoss(outputs, fps_idxs1, fps_idxs2, gt_flow, teacher_outputs, teacher_fps_idxs,
+                    gamma1, gamma2, beta, alpha=[0.02, 0.04, 0.08, 0.16]):
+    """Reference: loss_functions.py:53-66."""
+    t0 = teacher_outputs[0].permute(0, 2, 1)
+    g_loss1 = multiScaleLoss(outputs, gt_flow, fps_idxs1)
+    g_loss2 = multiScaleLoss(outputs, gt_flow, fps_idxs2)
+    k_loss1 = multiScaleLoss(outputs, t0, fps_idxs1)
+    k_loss2 = multiScaleLoss(outputs, t0, fps_idxs2)
+    return _zero(gt_flow) + (beta * (gamma1 * k_loss1 + (1 - gamma1) * g_loss1)
+                             + (1 - beta) * (gamma2 * k_loss2 + (1 - gamma2) * g_loss2))
+
+
+def loss_fn_ht(outputs, feat1s, fps_idxs1, fps_idxs2, gt_flow, teacher_outputs, t_feat1s,
+               teacher_fps_idxs, gamma, layer=0, alpha=[0.02, 0.04, 0.08, 0.16]):
+    """Reference: loss_functions.py:69-81 (hint normalised by feat1s[0].nelement())."""
+    t0 = teacher_outputs[0].permute(0, 2, 1)
+    loss1 = multiScaleLoss(outputs, t0, fps_idxs1)
+    loss2 = multiScaleLoss(outputs, gt_flow, fps_idxs1)
+    hint = ((feat1s[layer] - t_feat1s[layer]) ** 2) / 2
+    return _zero(gt_flow) + (gamma * loss1 + (1 - gamma) * loss2
+                             + hint.sum() / (feat1s[0].nelement()))
+
+
+def biDirection_loss_ht(outputs, feat1s, feat2s, fps_idxs1, fps_idxs2, gt_flow, teacher_outputs,
+                        t_feat1s, t_feat2s, t_fps_idxs1, t_fps_idxs2, gamma, beta, layer=0,
+                        alpha=[0.02, 0.04, 0.08, 0.16]):
+    """Reference: loss_functions.py:83-96 — the runnable KD objective:
+    beta*(gamma*MSL(s, teacher flow0) + (1-gamma)*MSL(s, gt))
+      + (1-beta)*(0.5*sum((f1-t_f1)^2/2) + 0.5*sum((f2-t_f2)^2/2)) at `layer`."""
+    t0 = teacher_outputs[0].permute(0, 2, 1)
+    loss1 = multiScaleLoss(outputs, t0, fps_idxs1)
+    loss2 = multiScaleLoss(outputs, gt_flow, fps_idxs1)
+    src_hint_loss = ((feat1s[layer] - t_feat1s[layer]) ** 2) / 2
+    target_hint_loss = ((feat2s[layer] - t_feat2s[layer]) ** 2) / 2
+    return _zero(gt_flow) + (beta * (gamma * loss1 + (1 - gamma) * loss2)
+                             + (1 - beta) * (0.5 * src_hint_loss.sum()
+                                             + 0.5 * target_hint_loss.sum()))
+
+
+# flow_loss_ht (reference loss_functions.py:98-121) reads the undefined names `fps_idxs`
+# and `loss1` and raises NameError on every call; it is not reproduced.
+
+
+def cross_biDirection_loss_ht(outputs, feat1s, feat2s, fps_idxs1, fps_idxs2, gt_flow,
+                              teacher_outputs, t_feat1s, t_feat2s, t_fps_idxs1, t_fps_idxs2,
+                              gamma, beta, layer=0, alpha=[0.02, 0.04, 0.08, 0.16]):
+    """Reference: loss_functions.py:201-219, the loss distilTrain.py:174 calls.  It compares
+    student feat1s[l] (C channels) with cat(teacher feat1s[l], feat2s[l]) (2C channels); for
+    the shipped teacher/student pair (equal widths) the reference raises a size-mismatch
+    RuntimeError, and so does this (same arithmetic)."""
+    t0 = teacher_outputs[0].permute(0, 2, 1)
+    loss1 = multiScaleLoss(outputs, t0, fps_idxs1)
+    loss2 = multiScaleLoss(outputs, gt_flow, fps_idxs1)
+    src_hint_loss = _zero(gt_flow)
+    for each in layer:
+        t_feats = torch.cat([t_feat1s[each], t_feat2s[each]], dim=1)
+        src_hint_loss += ((feat1s[each] - t_feats) ** 2).sum() / 2
+    return _zero(gt_flow) + (beta * (gamma * loss1 + (1 - gamma) * loss2)
+                             + (1 - beta) * src_hint_loss)
+
+
+def cross_loss(outputs, crosses, fps_idxs1, fps_idxs2, gt_flow, teacher_outputs, t_crosses,
+               t_fps_idxs1, t_fps_idxs2, gamma, beta, alpha=[0.02, 0.04, 0.08, 0.16]):
+    """Reference: loss_functions.py:222-235 (cost-volume hint, normalised per layer)."""
+    t0 = teacher_outputs[0].permute(0, 2, 1)
+    loss1 = multiScaleLoss(outputs, t0, fps_idxs1)
+    loss2 = multiScaleLoss(outputs, gt_flow, fps_idxs1)
+    closs = 0
+    for layer in range(len(crosses)):
+        closs += ((((crosses[layer] - t_crosses[layer]) ** 2) / 2).sum()) / crosses[layer].nelement()
+    return _zero(gt_flow) + (beta * (gamma * loss1 + (1 - gamma) * loss2) + (1 - beta) * closs)

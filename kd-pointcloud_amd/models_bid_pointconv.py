@@ -1,0 +1,130 @@
+"""Bidirectional PointConv scene-flow network (teacher) — drop-in for the reference's
+models_bid_pointconv.PointConvBidirection (models_bid_pointconv.py:14-207).
+
+Same submodules, attribute names (=> the same 438 state_dict keys), inputs and 8-tuple
+output.  MI355X-first restructuring of the forward, with identical per-sample arithmetic:
+
+  * pc1 and pc2 share every encoder module and every cost-volume direction, and none of
+    those layers has batch statistics, so both clouds run as ONE batch of 2B through the
+    encoder (conv, FPS, kNN, PointConvD) and the decoder's feature upsampling: half the
+    launches, twice the work per launch (FPS: 2B workgroups instead of B);
+  * only the pc1-side layers (cost volume refinement, scene-flow estimators whose train-mode
+    BatchNorm sees pc1 only, warping) run at batch B.
+"""
+import torch
+import torch.nn as nn
+
+from pointconv_util import (PointConvD, PointWarping, UpsampleFlow, CrossLayerLight as CrossLayer,
+                            SceneFlowEstimatorResidual, Conv1d)
+from pointconv_util import index_points_gather as index_points, index_points_group, square_distance  # noqa: F401
+from loss_functions import multiScaleLoss  # noqa: F401  (the reference defines it here too)
+
+scale = 1.0
+
+
+class PointConvBidirection(nn.Module):
+    def __init__(self, weightnet=16):
+        super().__init__()
+        flow_nei = 32
+        feat_nei = 16
+        self.scale = scale
+        # l0: 8192
+        self.level0 = Conv1d(3, 32)
+        self.level0_1 = Conv1d(32, 32)
+        self.cross0 = CrossLayer(flow_nei, 32 + 32, [32, 32], [32, 32])
+        self.flow0 = SceneFlowEstimatorResidual(32 + 64, 32, weightnet=weightnet)
+        self.level0_2 = Conv1d(32, 64)
+        # l1: 2048
+        self.level1 = PointConvD(2048, feat_nei, 64 + 3, 64, weightnet=weightnet)
+        self.cross1 = CrossLayer(flow_nei, 64 + 32, [64, 64], [64, 64])
+        self.flow1 = SceneFlowEstimatorResidual(64 + 64, 64, weightnet=weightnet)
+        self.level1_0 = Conv1d(64, 64)
+        self.level1_1 = Conv1d(64, 128)
+        # l2: 512
+        self.level2 = PointConvD(512, feat_nei, 128 + 3, 128, weightnet=weightnet)
+        self.cross2 = CrossLayer(flow_nei, 128 + 64, [128, 128], [128, 128])
+        self.flow2 = SceneFlowEstimatorResidual(128 + 64, 128, weightnet=weightnet)
+        self.level2_0 = Conv1d(128, 128)
+        self.level2_1 = Conv1d(128, 256)
+        # l3: 256
+        self.level3 = PointConvD(256, feat_nei, 256 + 3, 256, weightnet=weightnet)
+        self.cross3 = CrossLayer(flow_nei, 256 + 64, [256, 256], [256, 256])
+        self.flow3 = SceneFlowEstimatorResidual(256, 256, weightnet=weightnet)
+        self.level3_0 = Conv1d(256, 256)
+        self.level3_1 = Conv1d(256, 512)
+        # l4: 64
+        self.level4 = PointConvD(64, feat_nei, 512 + 3, 256, weightnet=weightnet)
+        # deconv
+        self.deconv4_3 = Conv1d(256, 64)
+        self.deconv3_2 = Conv1d(256, 64)
+        self.deconv2_1 = Conv1d(128, 32)
+        self.deconv1_0 = Conv1d(64, 32)
+        self.warping = PointWarping()
+        self.upsample = UpsampleFlow()
+
+    # ---------------------------------------------------------------------------------
+    def _encode(self, pc, color):
+        """Shared encoder on the pair batch (2B).  Returns per-level xyz, features, fps idx."""
+        feat_l0 = self.level0_1(self.level0(color))
+        feat_l0_1 = self.level0_2(feat_l0)
+        levels = [(self.level1, self.level1_0, self.level1_1),
+                  (self.level2, self.level2_0, self.level2_1),
+                  (self.level3, self.level3_0, self.level3_1)]
+        pcs, feats, feats_out, fps = [pc], [feat_l0], [feat_l0_1], []
+        x, f = pc, feat_l0_1
+        for down, mix, widen in levels:
+            x, f, idx = down(x, f)
+            f = mix(f)
+            pcs.append(x)
+            feats.append(f)
+            fps.append(idx)
+            f = widen(f)
+            feats_out.append(f)
+        pc_l4, feat_l4, _ = self.level4(x, f)
+        feat_l4_3 = self.deconv4_3(self.upsample(x, pc_l4, feat_l4))
+        return pcs, feats, feats_out, fps, feat_l4_3
+
+    def forward(self, xyz1, xyz2, color1, color2):
+        """xyz*, color*: (B,N,3).  Returns (flows, fps_pc1_idxs, fps_pc2_idxs, pc1, pc2,
+        feat1s, feat2s, crosses) exactly as the reference (models_bid_pointconv.py:198-207)."""
+        B = xyz1.shape[0]
+        pc = torch.cat([xyz1, xyz2], 0).permute(0, 2, 1)
+        color = torch.cat([color1, color2], 0).permute(0, 2, 1)
+        pcs, feats, feats_out, fps, feat_l4_3 = self._encode(pc, color)
+        one = lambda t: t[:B]  # noqa: E731
+        two = lambda t: t[B:]  # noqa: E731
+
+        # ---- level 3 (coarsest): no prior flow
+        c_feat_l3 = torch.cat([feats[3], feat_l4_3], dim=1)
+        f1n, f2n, cross3 = self.cross3(one(pcs[3]), two(pcs[3]), one(c_feat_l3), two(c_feat_l3))
+        feat_est, flow = self.flow3(one(pcs[3]), one(feats[3]), cross3)
+        flows, crosses, up_feats = [flow], [cross3], []
+
+        decoders = [(2, self.cross2, self.flow2, self.deconv3_2),
+                    (1, self.cross1, self.flow1, self.deconv2_1),
+                    (0, self.cross0, self.flow0, self.deconv1_0)]
+        for lv, cross, flow_est, deconv in decoders:
+            # bidirectional features of the coarser level, upsampled for both clouds at once
+            f_up = deconv(self.upsample(pcs[lv], pcs[lv + 1], torch.cat([f1n, f2n], 0)))
+            up_feats.append(f_up)
+            c_feat = torch.cat([feats[lv], f_up], dim=1)
+            pc1_lv, pc2_lv = one(pcs[lv]), two(pcs[lv])
+            up_flow = self.upsample(pc1_lv, one(pcs[lv + 1]), self.scale * flow)
+            pc2_warp = self.warping(pc1_lv, pc2_lv, up_flow)
+            out = cross(pc1_lv, pc2_warp, one(c_feat), two(c_feat))
+            f1n, f2n, cost = out
+            feat_up = self.upsample(pc1_lv, one(pcs[lv + 1]), feat_est)
+            new_feat1 = torch.cat([one(feats[lv]), feat_up], dim=1)
+            feat_est, flow = flow_est(pc1_lv, new_feat1, cost, up_flow)
+            flows.insert(0, flow)
+            crosses.insert(0, cost)
+
+        pc1 = [one(p) for p in pcs]
+        pc2 = [two(p) for p in pcs]
+        fps_pc1_idxs = [one(i) for i in fps]
+        fps_pc2_idxs = [two(i) for i in fps]
+        # feat{1,2}s = [l0_1, l1_2, l2_3, l3_4, l3_2, l2_1, l1_0] (reference :203-204)
+        enc = feats_out[:4]
+        feat1s = [one(t) for t in enc] + [one(t) for t in up_feats]
+        feat2s = [two(t) for t in enc] + [two(t) for t in up_feats]
+        return flows, fps_pc1_idxs, fps_pc2_idxs, pc1, pc2, feat1s, feat2s, crosses

@@ -1,0 +1,238 @@
+"""Generate tests/golden/*.npz by running the REFERENCE Python itself (CPU, this container).
+
+    python oracle/make_fixtures.py            # needs /root/reference (not on the GPU box)
+
+Recipe (no reference file is modified or copied):
+  1. sys.path.insert(0, /root/reference);
+  2. stub modules: `pointnet2_cuda` (FPS -> the C restatement in oracle/pointnet2_oracle.c,
+     gather/group -> plain torch indexing, an implementation independent of the oracle),
+     `thop`, `cv2`;
+  3. torch.cuda.{Float,Int}Tensor -> CPU allocators, Tensor.cuda -> identity, so the
+     reference's own pointnet2_utils.py wrappers (allocation/init semantics) run on CPU;
+  4. pointconv_util.BottleNeck injected (models_bid_pointconv.py:7 imports a class the
+     current pointconv_util.py lacks).
+Only inputs/outputs are written; weights are regenerated from key names (oracle/weights.py).
+"""
+import importlib.util
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+REF = os.environ.get("KDPC_REFERENCE", "/root/reference")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+sys.path.insert(0, HERE)
+import pointnet2_oracle as C  # noqa: E402
+from weights import synthetic_state_dict  # noqa: E402
+
+_spec = importlib.util.spec_from_file_location(
+    "kdpc_synthetic", os.path.join(ROOT, "kd-pointcloud_amd", "synthetic.py"))
+synthetic = importlib.util.module_from_spec(_spec)
+_spec.loader.exec_module(synthetic)
+
+
+# ------------------------------------------------------------------------- stubs
+def _stub_pointnet2_cuda():
+    m = types.ModuleType("pointnet2_cuda")
+
+    def furthest_point_sampling_wrapper(b, n, npoint, points, temp, idx):
+        out, tmp = C.furthest_point_sample(points.numpy(), npoint)
+        idx.copy_(torch.from_numpy(out))
+        temp.copy_(torch.from_numpy(tmp))
+        return 1
+
+    def gather_points_wrapper(b, c, n, npoint, points, idx, out):
+        out.copy_(torch.gather(points, 2, idx.long().unsqueeze(1).expand(-1, c, -1)))
+        return 1
+
+    def gather_points_grad_wrapper(b, c, n, npoint, grad_out, idx, grad_points):
+        grad_points.scatter_add_(2, idx.long().unsqueeze(1).expand(-1, c, -1), grad_out)
+        return 1
+
+    def group_points_wrapper(b, c, n, npoints, nsample, points, idx, out):
+        flat = idx.long().view(b, 1, npoints * nsample).expand(-1, c, -1)
+        out.copy_(torch.gather(points, 2, flat).view(b, c, npoints, nsample))
+        return 1
+
+    def group_points_grad_wrapper(b, c, n, npoints, nsample, grad_out, idx, grad_points):
+        flat = idx.long().view(b, 1, npoints * nsample).expand(-1, c, -1)
+        grad_points.scatter_add_(2, flat, grad_out.reshape(b, c, -1))
+        return 1
+
+    for f in (furthest_point_sampling_wrapper, gather_points_wrapper, gather_points_grad_wrapper,
+              group_points_wrapper, group_points_grad_wrapper):
+        setattr(m, f.__name__, f)
+    return m
+
+
+def setup_reference():
+    if not os.path.isdir(REF):
+        raise SystemExit(f"reference not found at {REF}")
+    sys.modules["pointnet2_cuda"] = _stub_pointnet2_cuda()
+    thop = types.ModuleType("thop")
+    thop.profile = lambda *a, **k: (0, 0)
+    thop.clever_format = lambda *a, **k: a
+    sys.modules["thop"] = thop
+    cv2 = types.ModuleType("cv2")
+    cv2.kmeans = lambda *a, **k: None
+    sys.modules["cv2"] = cv2
+    torch.cuda.FloatTensor = lambda *s: torch.empty(*s, dtype=torch.float32)
+    torch.cuda.IntTensor = lambda *s: torch.empty(*s, dtype=torch.int32)
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    torch.nn.Module.cuda = lambda self, *a, **k: self
+    sys.path.insert(0, REF)
+    import pointconv_util
+    if not hasattr(pointconv_util, "BottleNeck"):
+        class BottleNeck(nn.Module):  # placeholder: only unused student classes need it
+            pass
+        pointconv_util.BottleNeck = BottleNeck
+    import pointconv_util2  # noqa: F401
+    import models_bid_pointconv
+    import models_bid_lighttoken_res
+    import loss_functions
+    return types.SimpleNamespace(pcu=pointconv_util, teacher=models_bid_pointconv,
+                                 student=models_bid_lighttoken_res, loss=loss_functions)
+
+
+def _synth(module, seed):
+    module.load_state_dict(synthetic_state_dict(module.state_dict(), seed))
+    return module
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+# ------------------------------------------------------------------------- fixtures
+def make_knn(R):
+    cases = {}
+    specs = [("self1024_k9", 1024, None, 9), ("q512_r2048_k32", 2048, 512, 32),
+             ("q300_r512_k16", 512, 300, 16), ("q4096_r1024_k3", 1024, 4096, 3)]
+    for i, (name, n, s, k) in enumerate(specs):
+        p1, p2, _ = synthetic.ft3d_pair(max(n, s or 0), seed=11, pair=i)
+        xyz = torch.from_numpy(p2[:n][None])
+        new_xyz = xyz if s is None else torch.from_numpy(p1[:s][None])
+        idx = R.pcu.knn_point(k, xyz, new_xyz)
+        dist = R.pcu.square_distance(new_xyz, xyz)
+        kth = torch.sort(torch.gather(dist, 2, idx), dim=-1)[0]
+        cases[name + "_xyz"] = _np(xyz)
+        cases[name + "_new_xyz"] = _np(new_xyz)
+        cases[name + "_idx_sorted"] = np.sort(_np(idx), axis=-1).astype(np.int32)
+        cases[name + "_dist_sorted"] = _np(kth)
+    np.savez_compressed(os.path.join(GOLDEN, "knn_ref.npz"), **cases)
+
+
+def make_losses(R):
+    rng = np.random.default_rng(5)
+    B, N = 2, 2048
+    sizes = [2048, 512, 128, 64]
+    preds = [torch.from_numpy((rng.normal(size=(B, 3, s)) * 0.1).astype(np.float32)) for s in sizes]
+    fps = []
+    for a, b in zip(sizes[:-1], sizes[1:]):
+        fps.append(torch.from_numpy(np.stack([np.sort(rng.choice(a, b, replace=False))
+                                              for _ in range(B)]).astype(np.int32)))
+    gt = torch.from_numpy((rng.normal(size=(B, N, 3)) * 0.5).astype(np.float32))
+    loss = R.loss.multiScaleLoss(preds, gt, fps)
+    out = {f"pred{i}": _np(p) for i, p in enumerate(preds)}
+    out.update({f"fps{i}": _np(f) for i, f in enumerate(fps)})
+    out["gt"] = _np(gt)
+    out["loss"] = _np(loss)
+    np.savez_compressed(os.path.join(GOLDEN, "multiscale_loss_ref.npz"), **out)
+
+
+def make_layers(R):
+    torch.manual_seed(0)
+    out = {}
+    n1, n2 = 1024, 1024
+    p1, p2, fl = synthetic.ft3d_pair(n1, seed=21, pair=0)
+    # (B,3,N) views of (B,N,3) storage, as the models pass them: the reference FPS wrapper
+    # asserts that xyz.permute(0,2,1) is contiguous (pointnet2_utils.py:22)
+    x1 = torch.from_numpy(p1[None]).permute(0, 2, 1)
+    x2 = torch.from_numpy(p2[None]).permute(0, 2, 1)
+    rng = np.random.default_rng(3)
+    f32 = lambda *s: torch.from_numpy(rng.normal(size=s).astype(np.float32))  # noqa: E731
+    out["x1"], out["x2"] = _np(x1), _np(x2)
+    # PointConvD
+    layer = _synth(R.pcu.PointConvD(256, 16, 32 + 3, 64), seed=31)
+    feat = f32(1, 32, n1)
+    nx, nf, fidx = layer(x1, feat)
+    out.update(pcd_feat=_np(feat), pcd_new_xyz=_np(nx), pcd_out=_np(nf), pcd_fps=_np(fidx))
+    # CrossLayerLight (K=32)
+    layer = _synth(R.pcu.CrossLayerLight(32, 64, [32, 32], [32, 32]), seed=32)
+    fa, fb = f32(1, 64, n1), f32(1, 64, n2)
+    a, b, c = layer(x1, x2, fa, fb)
+    out.update(cl_f1=_np(fa), cl_f2=_np(fb), cl_out1=_np(a), cl_out2=_np(b), cl_out3=_np(c))
+    # UpsampleFlow 1024 <- 256
+    sparse = torch.from_numpy(np.ascontiguousarray(p1[None, :256])).permute(0, 2, 1)
+    sflow = f32(1, 3, 256)
+    out.update(up_sparse_flow=_np(sflow), up_out=_np(R.pcu.UpsampleFlow()(x1, sparse, sflow)))
+    # PointWarping
+    flow1 = torch.from_numpy(fl[None]).permute(0, 2, 1).contiguous()
+    out.update(warp_flow=_np(flow1), warp_out=_np(R.pcu.PointWarping()(x1, x2, flow1)))
+    # SceneFlowEstimatorResidual (train-mode BN)
+    est = _synth(R.pcu.SceneFlowEstimatorResidual(32 + 32, 32), seed=33)
+    est.train()
+    fe, cv = f32(1, 64, n1), f32(1, 32, n1)
+    feats_o, flow_o = est(x1, fe, cv, flow1)
+    out.update(est_feats=_np(fe), est_cost=_np(cv), est_out_feats=_np(feats_o),
+               est_out_flow=_np(flow_o))
+    np.savez_compressed(os.path.join(GOLDEN, "layers_ref.npz"), **out)
+
+
+def make_model(R, n=4096):
+    """Teacher (eval) + student (train) at B=1, N=n; MSL and KD losses and grad summaries."""
+    p1, p2, fl = synthetic.ft3d_pair(n, seed=7, pair=0)
+    pos1, pos2, flow = (torch.from_numpy(a[None]) for a in (p1, p2, fl))
+    teacher = _synth(R.teacher.PointConvBidirection(), seed=1).eval()
+    student = _synth(R.student.PointConvBidirection(), seed=2).train()
+    with torch.no_grad():
+        t_out = teacher(pos1, pos2, pos1, pos2)
+    s_out = student(pos1, pos2, pos1, pos2)
+    flows, f1i, f2i, _, _, feat1s, feat2s, crosses = s_out
+    msl = R.loss.multiScaleLoss(flows, flow, f1i)
+    kd = R.loss.biDirection_loss_ht(flows, feat1s, feat2s, f1i, f2i, flow, t_out[0], t_out[5],
+                                    t_out[6], t_out[1], t_out[2], 0.3, 0.8, layer=3)
+    kd.backward()
+    out = dict(pos1=p1[None], pos2=p2[None], flow=fl[None], msl=_np(msl), kd=_np(kd))
+    for tag, o in (("t", t_out), ("s", s_out)):
+        for i, f in enumerate(o[0]):
+            out[f"{tag}_flow{i}"] = _np(f)
+        for i, f in enumerate(o[1]):
+            out[f"{tag}_fps1_{i}"] = _np(f)
+        for i, f in enumerate(o[2]):
+            out[f"{tag}_fps2_{i}"] = _np(f)
+        out[f"{tag}_feat1_3"] = _np(o[5][3])
+        out[f"{tag}_cross0"] = _np(o[7][0])
+    out["s_epe3d"] = _np(torch.norm(flows[0].permute(0, 2, 1) - flow, dim=2).mean())
+    out["t_epe3d"] = _np(torch.norm(t_out[0][0].permute(0, 2, 1) - flow, dim=2).mean())
+    names = [k for k, p in student.named_parameters()]
+    out["grad_names"] = np.array(names)
+    out["grad_sum"] = np.array([float(p.grad.sum()) if p.grad is not None else 0.0
+                                for _, p in student.named_parameters()], dtype=np.float64)
+    out["grad_abs"] = np.array([float(p.grad.abs().sum()) if p.grad is not None else 0.0
+                                for _, p in student.named_parameters()], dtype=np.float64)
+    out["grad_none"] = np.array([p.grad is None for _, p in student.named_parameters()])
+    out["n_params"] = np.array(sum(p.numel() for p in student.parameters()))
+    out["state_keys"] = np.array(list(student.state_dict().keys()))
+    np.savez_compressed(os.path.join(GOLDEN, f"model_ref_n{n}.npz"), **out)
+
+
+def main():
+    os.makedirs(GOLDEN, exist_ok=True)
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    R = setup_reference()
+    make_knn(R)
+    make_losses(R)
+    make_layers(R)
+    make_model(R)
+    print("fixtures written to", GOLDEN)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,371 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY (never imported by kd-pointcloud_amd/).
+
+Pure-PyTorch CPU restatement of the reference's hot path, written op-for-op after the
+reference so CPU results are bitwise comparable with the reference run on CPU:
+  * square_distance + topk kNN               pointconv_util.py:73-107
+  * index_points via torch.gather            (reference: pointnet2 gather/group ext)
+  * FPS: the C restatement (oracle/pointnet2_oracle.c) or, for the CPU baseline the
+    north star names, a random subsample (the PointConvDRand pattern, pointconv_util.py:621)
+  * layers                                   pointconv_util.py:17-258,401-446,1791-1868,
+                                             2114-2256
+  * PointConvBidirection                     models_bid_pointconv.py:14-207 (two clouds
+                                             run separately, in reference order)
+  * multiScaleLoss, biDirection_loss_ht      loss_functions.py:6-25, 83-96
+Module/attribute names equal the reference's, so state_dicts are interchangeable with the
+product model (kd-pointcloud_amd) and with the reference itself.
+Parity: pinned against the reference Python (tests/golden/*, oracle/make_fixtures.py).
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import pointnet2_oracle as _c  # noqa: E402
+
+LEAKY = 0.1
+
+# "oracle": C restatement of the CUDA FPS; "random": randperm subsample (CPU baseline)
+FPS_MODE = {"mode": "oracle", "generator": None}
+
+
+def furthest_point_sample(xyz, npoint):
+    if FPS_MODE["mode"] == "random":
+        B, N, _ = xyz.shape
+        g = FPS_MODE["generator"]
+        return torch.stack([torch.randperm(N, generator=g)[:npoint] for _ in range(B)]).int()
+    idx, _ = _c.furthest_point_sample(xyz.detach().cpu().numpy(), npoint)
+    return torch.from_numpy(idx)
+
+
+def square_distance(src, dst):
+    B, N, _ = src.shape
+    M = dst.shape[1]
+    dist = -2 * torch.matmul(src, dst.permute(0, 2, 1))
+    dist += torch.sum(src ** 2, -1).view(B, N, 1)
+    dist += torch.sum(dst ** 2, -1).view(B, 1, M)
+    return dist
+
+
+def knn_point(nsample, xyz, new_xyz):
+    _, idx = torch.topk(square_distance(new_xyz, xyz), nsample, dim=-1, largest=False, sorted=False)
+    return idx
+
+
+def index_points_gather(points, idx):
+    """points (B,N,C), idx (B,S) -> (B,S,C)"""
+    idx = idx.long()
+    return torch.gather(points, 1, idx.unsqueeze(-1).expand(-1, -1, points.shape[-1]))
+
+
+def index_points_group(points, idx):
+    """points (B,N,C), idx (B,S,K) -> (B,S,K,C)"""
+    B, S, K = idx.shape
+    flat = index_points_gather(points, idx.reshape(B, S * K).long())
+    return flat.view(B, S, K, points.shape[-1])
+
+
+def _act(use_leaky=True):
+    return nn.LeakyReLU(LEAKY, inplace=True) if use_leaky else nn.ReLU(inplace=True)
+
+
+class Conv1d(nn.Module):
+    def __init__(self, cin, cout, kernel_size=1, stride=1, padding=0, use_leaky=True, bn=False):
+        super().__init__()
+        self.composed_module = nn.Sequential(
+            nn.Conv1d(cin, cout, kernel_size=kernel_size, stride=stride, padding=padding, bias=True),
+            nn.BatchNorm1d(cout) if bn else nn.Identity(), _act(use_leaky))
+
+    def forward(self, x):
+        return self.composed_module(x)
+
+
+class Conv2d(nn.Module):
+    def __init__(self, cin, cout, kernel_size=1, stride=1, padding=0, use_leaky=True, bn=False,
+                 bias=True):
+        super().__init__()
+        self.composed_module = nn.Sequential(
+            nn.Conv2d(cin, cout, kernel_size=kernel_size, stride=stride, padding=padding, bias=bias),
+            nn.BatchNorm2d(cout) if bn else nn.Identity(), _act(use_leaky))
+
+    def forward(self, x):
+        return self.composed_module(x)
+
+
+class WeightNet(nn.Module):
+    def __init__(self, cin, cout, hidden=(8, 8)):
+        super().__init__()
+        widths = [cin] + list(hidden) + [cout]
+        self.mlp_convs = nn.ModuleList(nn.Conv2d(a, b, 1) for a, b in zip(widths[:-1], widths[1:]))
+        self.mlp_bns = nn.ModuleList(nn.BatchNorm2d(b) for b in widths[1:])
+
+    def forward(self, x):
+        for conv in self.mlp_convs:
+            x = F.relu(conv(x))
+        return x
+
+
+def _group(nsample, s_xyz, q_xyz, s_points):
+    """group / group_query: (new_points (B,S,K,3+D), grouped_xyz_norm (B,S,K,3))"""
+    B, S, C = q_xyz.shape
+    idx = knn_point(nsample, s_xyz, q_xyz)
+    norm = index_points_group(s_xyz, idx) - q_xyz.view(B, S, 1, C)
+    return torch.cat([norm, index_points_group(s_points, idx)], dim=-1), norm
+
+
+class _PConv(nn.Module):
+    def _conv(self, new_points, norm, B, S):
+        weights = self.weightnet(norm.permute(0, 3, 2, 1))
+        new_points = torch.matmul(input=new_points.permute(0, 1, 3, 2),
+                                  other=weights.permute(0, 3, 2, 1)).view(B, S, -1)
+        new_points = self.linear(new_points).permute(0, 2, 1)
+        if self.bn:
+            new_points = self.bn_linear(new_points)
+        return self.relu(new_points)
+
+
+class PointConv(_PConv):
+    def __init__(self, nsample, cin, cout, weightnet=16, bn=False, use_leaky=True):
+        super().__init__()
+        self.bn, self.nsample = bn, nsample
+        self.weightnet = WeightNet(3, weightnet)
+        self.linear = nn.Linear(weightnet * cin, cout)
+        if bn:
+            self.bn_linear = nn.BatchNorm1d(cout)
+        self.relu = _act(use_leaky)
+
+    def forward(self, xyz, points):
+        B, _, N = xyz.shape
+        xyz, points = xyz.permute(0, 2, 1), points.permute(0, 2, 1)
+        new_points, norm = _group(self.nsample, xyz, xyz, points)
+        return self._conv(new_points, norm, B, N)
+
+
+class PointConvD(_PConv):
+    def __init__(self, npoint, nsample, cin, cout, weightnet=16, bn=False, use_leaky=True):
+        super().__init__()
+        self.npoint, self.bn, self.nsample = npoint, bn, nsample
+        self.weightnet = WeightNet(3, weightnet)
+        self.linear = nn.Linear(weightnet * cin, cout)
+        if bn:
+            self.bn_linear = nn.BatchNorm1d(cout)
+        self.relu = _act(use_leaky)
+
+    def forward(self, xyz, points):
+        B = xyz.shape[0]
+        xyz, points = xyz.permute(0, 2, 1), points.permute(0, 2, 1)
+        fps_idx = furthest_point_sample(xyz.contiguous(), self.npoint)
+        new_xyz = index_points_gather(xyz, fps_idx)
+        new_points, norm = _group(self.nsample, xyz, new_xyz, points)
+        return new_xyz.permute(0, 2, 1), self._conv(new_points, norm, B, self.npoint), fps_idx
+
+
+class CrossLayerLight(nn.Module):
+    def __init__(self, nsample, cin, mlp1, mlp2, bn=False, use_leaky=True):
+        super().__init__()
+        self.nsample, self.bn = nsample, bn
+        self.pos1 = nn.Conv2d(3, mlp1[0], 1)
+        self.mlp1 = nn.ModuleList()
+        self.cross_t11 = nn.Conv1d(cin, mlp1[0], 1)
+        self.cross_t22 = nn.Conv1d(cin, mlp1[0], 1)
+        self.bias1 = nn.Parameter(torch.randn((1, mlp1[0], 1, 1)))
+        self.bn1 = nn.Identity()
+        for a, b in zip(mlp1[:-1], mlp1[1:]):
+            self.mlp1.append(Conv2d(a, b, use_leaky=use_leaky))
+        self.cross_t1 = nn.Conv1d(mlp1[-1], mlp2[0], 1)
+        self.cross_t2 = nn.Conv1d(mlp1[-1], mlp2[0], 1)
+        self.pos2 = nn.Conv2d(3, mlp2[0], 1)
+        self.bias2 = nn.Parameter(torch.randn((1, mlp2[0], 1, 1)))
+        self.bn2 = nn.Identity()
+        self.mlp2 = nn.ModuleList()
+        for a, b in zip(mlp2[:-1], mlp2[1:]):
+            self.mlp2.append(Conv2d(a, b, use_leaky=use_leaky))
+        self.relu = _act(use_leaky)
+
+    def cross(self, xyz1, xyz2, points1, points2, pos, mlp, bn):
+        B, C, N1 = xyz1.shape
+        D1 = points1.shape[1]
+        xyz1, xyz2 = xyz1.permute(0, 2, 1), xyz2.permute(0, 2, 1)
+        points1, points2 = points1.permute(0, 2, 1), points2.permute(0, 2, 1)
+        idx = knn_point(self.nsample, xyz2, xyz1)
+        direction = index_points_group(xyz2, idx) - xyz1.view(B, N1, 1, C)
+        g2 = index_points_group(points2, idx).permute(0, 3, 2, 1)
+        g1 = points1.view(B, N1, 1, D1).repeat(1, 1, self.nsample, 1).permute(0, 3, 2, 1)
+        h = self.relu(bn(g2 + g1 + pos(direction.permute(0, 3, 2, 1))))
+        for conv in mlp:
+            h = conv(h)
+        return F.max_pool2d(h, (h.size(2), 1)).squeeze(2)
+
+    def forward(self, pc1, pc2, feat1, feat2):
+        f1 = self.cross(pc1, pc2, self.cross_t11(feat1), self.cross_t22(feat2), self.pos1,
+                        self.mlp1, self.bn1)
+        f2 = self.cross(pc2, pc1, self.cross_t11(feat2), self.cross_t22(feat1), self.pos1,
+                        self.mlp1, self.bn1)
+        f1 = self.cross_t1(f1)
+        f2 = self.cross_t2(f2)
+        return f1, f2, self.cross(pc1, pc2, f1, f2, self.pos2, self.mlp2, self.bn2)
+
+
+def _idw(grouped_xyz_norm, grouped_vals, B, N):
+    dist = torch.norm(grouped_xyz_norm, dim=3).clamp(min=1e-10)
+    norm = torch.sum(1.0 / dist, dim=2, keepdim=True)
+    weight = (1.0 / dist) / norm
+    return torch.sum(weight.view(B, N, 3, 1) * grouped_vals, dim=2)
+
+
+class PointWarping(nn.Module):
+    def forward(self, xyz1, xyz2, flow1=None):
+        if flow1 is None:
+            return xyz2
+        B, C, _ = xyz1.shape
+        N2 = xyz2.shape[2]
+        x12 = (xyz1 + flow1).permute(0, 2, 1)
+        xyz2 = xyz2.permute(0, 2, 1)
+        flow1 = flow1.permute(0, 2, 1)
+        idx = knn_point(3, x12, xyz2)
+        g = index_points_group(x12, idx) - xyz2.view(B, N2, 1, C)
+        flow2 = _idw(g, index_points_group(flow1, idx), B, N2)
+        return (xyz2 - flow2).permute(0, 2, 1)
+
+
+class UpsampleFlow(nn.Module):
+    def forward(self, xyz, sparse_xyz, sparse_flow):
+        B, C, N = xyz.shape
+        xyz = xyz.permute(0, 2, 1)
+        sparse_xyz = sparse_xyz.permute(0, 2, 1)
+        sparse_flow = sparse_flow.permute(0, 2, 1)
+        idx = knn_point(3, sparse_xyz, xyz)
+        g = index_points_group(sparse_xyz, idx) - xyz.view(B, N, 1, C)
+        return _idw(g, index_points_group(sparse_flow, idx), B, N).permute(0, 2, 1)
+
+
+class SceneFlowEstimatorResidual(nn.Module):
+    def __init__(self, feat_ch, cost_ch, channels=(128, 128), mlp=(128, 64), neighbors=9,
+                 clamp=(-200, 200), weightnet=16):
+        super().__init__()
+        self.clamp = clamp
+        self.pointconv_list = nn.ModuleList()
+        last = feat_ch + cost_ch
+        for c in channels:
+            self.pointconv_list.append(PointConv(neighbors, last + 3, c, bn=True, weightnet=weightnet))
+            last = c
+        self.mlp_convs = nn.ModuleList()
+        for c in mlp:
+            self.mlp_convs.append(Conv1d(last, c))
+            last = c
+        self.fc = nn.Conv1d(last, 3, 1)
+
+    def forward(self, xyz, feats, cost_volume, flow=None):
+        x = torch.cat([feats, cost_volume], dim=1)
+        for pc in self.pointconv_list:
+            x = pc(xyz, x)
+        for conv in self.mlp_convs:
+            x = conv(x)
+        local = self.fc(x).clamp(self.clamp[0], self.clamp[1])
+        return x, local if flow is None else local + flow
+
+
+class PointConvBidirection(nn.Module):
+    """Restatement of models_bid_pointconv.PointConvBidirection (identical to the student)."""
+
+    def __init__(self, weightnet=16):
+        super().__init__()
+        fn, kn = 32, 16
+        self.scale = 1.0
+        self.level0 = Conv1d(3, 32)
+        self.level0_1 = Conv1d(32, 32)
+        self.cross0 = CrossLayerLight(fn, 64, [32, 32], [32, 32])
+        self.flow0 = SceneFlowEstimatorResidual(96, 32, weightnet=weightnet)
+        self.level0_2 = Conv1d(32, 64)
+        self.level1 = PointConvD(2048, kn, 67, 64, weightnet=weightnet)
+        self.cross1 = CrossLayerLight(fn, 96, [64, 64], [64, 64])
+        self.flow1 = SceneFlowEstimatorResidual(128, 64, weightnet=weightnet)
+        self.level1_0 = Conv1d(64, 64)
+        self.level1_1 = Conv1d(64, 128)
+        self.level2 = PointConvD(512, kn, 131, 128, weightnet=weightnet)
+        self.cross2 = CrossLayerLight(fn, 192, [128, 128], [128, 128])
+        self.flow2 = SceneFlowEstimatorResidual(192, 128, weightnet=weightnet)
+        self.level2_0 = Conv1d(128, 128)
+        self.level2_1 = Conv1d(128, 256)
+        self.level3 = PointConvD(256, kn, 259, 256, weightnet=weightnet)
+        self.cross3 = CrossLayerLight(fn, 320, [256, 256], [256, 256])
+        self.flow3 = SceneFlowEstimatorResidual(256, 256, weightnet=weightnet)
+        self.level3_0 = Conv1d(256, 256)
+        self.level3_1 = Conv1d(256, 512)
+        self.level4 = PointConvD(64, kn, 515, 256, weightnet=weightnet)
+        self.deconv4_3 = Conv1d(256, 64)
+        self.deconv3_2 = Conv1d(256, 64)
+        self.deconv2_1 = Conv1d(128, 32)
+        self.deconv1_0 = Conv1d(64, 32)
+        self.warping = PointWarping()
+        self.upsample = UpsampleFlow()
+
+    def _encoder(self, pc, color):
+        f0 = self.level0_1(self.level0(color))
+        f0_1 = self.level0_2(f0)
+        p1, f1, i1 = self.level1(pc, f0_1)
+        f1 = self.level1_0(f1)
+        f1_2 = self.level1_1(f1)
+        p2, f2, i2 = self.level2(p1, f1_2)
+        f2 = self.level2_0(f2)
+        f2_3 = self.level2_1(f2)
+        p3, f3, i3 = self.level3(p2, f2_3)
+        f3 = self.level3_0(f3)
+        f3_4 = self.level3_1(f3)
+        p4, f4, _ = self.level4(p3, f3_4)
+        f4_3 = self.deconv4_3(self.upsample(p3, p4, f4))
+        return dict(p=[pc, p1, p2, p3], f=[f0, f1, f2, f3], fo=[f0_1, f1_2, f2_3, f3_4],
+                    i=[i1, i2, i3], f4_3=f4_3)
+
+    def forward(self, xyz1, xyz2, color1, color2):
+        e1 = self._encoder(xyz1.permute(0, 2, 1), color1.permute(0, 2, 1))
+        e2 = self._encoder(xyz2.permute(0, 2, 1), color2.permute(0, 2, 1))
+        p1, p2, f1, f2 = e1["p"], e2["p"], e1["f"], e2["f"]
+        f1n, f2n, cross3 = self.cross3(p1[3], p2[3], torch.cat([f1[3], e1["f4_3"]], 1),
+                                       torch.cat([f2[3], e2["f4_3"]], 1))
+        feat, flow = self.flow3(p1[3], f1[3], cross3)
+        flows, crosses, ups1, ups2 = [flow], [cross3], [], []
+        stages = [(2, self.cross2, self.flow2, self.deconv3_2),
+                  (1, self.cross1, self.flow1, self.deconv2_1),
+                  (0, self.cross0, self.flow0, self.deconv1_0)]
+        for lv, cross, est, deconv in stages:
+            u1 = deconv(self.upsample(p1[lv], p1[lv + 1], f1n))
+            u2 = deconv(self.upsample(p2[lv], p2[lv + 1], f2n))
+            ups1.append(u1)
+            ups2.append(u2)
+            up_flow = self.upsample(p1[lv], p1[lv + 1], self.scale * flow)
+            warp = self.warping(p1[lv], p2[lv], up_flow)
+            f1n, f2n, cost = cross(p1[lv], warp, torch.cat([f1[lv], u1], 1),
+                                   torch.cat([f2[lv], u2], 1))
+            feat_up = self.upsample(p1[lv], p1[lv + 1], feat)
+            feat, flow = est(p1[lv], torch.cat([f1[lv], feat_up], 1), cost, up_flow)
+            flows.insert(0, flow)
+            crosses.insert(0, cost)
+        return (flows, e1["i"], e2["i"], p1, p2, e1["fo"] + ups1, e2["fo"] + ups2, crosses)
+
+
+def multiScaleLoss(pred_flows, gt_flow, fps_idxs, alpha=(0.02, 0.04, 0.08, 0.16)):
+    offset = len(fps_idxs) - len(pred_flows) + 1
+    gts = [gt_flow]
+    for idx in fps_idxs:
+        gts.append(index_points_gather(gts[-1], idx) / 1.0)
+    total = torch.zeros(1)
+    for i in range(len(pred_flows)):
+        diff = pred_flows[i].permute(0, 2, 1) - gts[i + offset]
+        total += alpha[i] * torch.norm(diff, dim=2).sum(dim=1).mean()
+    return total
+
+
+def biDirection_loss_ht(outputs, feat1s, feat2s, fps_idxs1, fps_idxs2, gt_flow, teacher_outputs,
+                        t_feat1s, t_feat2s, t_fps_idxs1, t_fps_idxs2, gamma, beta, layer=0):
+    t0 = teacher_outputs[0].permute(0, 2, 1)
+    loss1 = multiScaleLoss(outputs, t0, fps_idxs1)
+    loss2 = multiScaleLoss(outputs, gt_flow, fps_idxs1)
+    src = ((feat1s[layer] - t_feat1s[layer]) ** 2) / 2
+    tgt = ((feat2s[layer] - t_feat2s[layer]) ** 2) / 2
+    out = torch.zeros(1)
+    out += beta * (gamma * loss1 + (1 - gamma) * loss2) + (1 - beta) * (0.5 * src.sum() + 0.5 * tgt.sum())
+    return out
