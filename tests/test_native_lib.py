@@ -1,0 +1,54 @@
+"""CPU: the C-ABI library loads and exports exactly what include/kdpc.h declares, and
+rejects invalid sizes with hipErrorInvalidValue before touching a device."""
+import ctypes
+import os
+import re
+
+import pytest
+
+import kdpc_native
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "kdpc.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(kdpc_\w+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = kdpc_native.load_library()
+    declared = _declared()
+    assert len(declared) >= 17
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert sorted(kdpc_native.EXPORTED) == declared
+
+
+def test_exported_symbols_are_only_the_abi():
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", kdpc_native.LIB_PATH],
+                         capture_output=True, text=True).stdout
+    ours = sorted(set(re.findall(r"\b(kdpc_\w+)$", out, flags=re.M)))
+    assert ours == _declared()
+
+
+def test_invalid_sizes_rejected_without_launch():
+    lib = kdpc_native.load_library()
+    EINVAL = 1  # hipErrorInvalidValue
+    assert lib.kdpc_knn_point(1, 10, 5, 0, None, None, None, None, None) == EINVAL  # k=0
+    assert lib.kdpc_knn_point(1, 10, 5, 65, None, None, None, None, None) == EINVAL  # k>64
+    assert lib.kdpc_knn_point(1, 10, 5, 11, None, None, None, None, None) == EINVAL  # k>n
+    assert lib.kdpc_furthest_point_sampling(1, 0, 5, None, None, None, None) == EINVAL
+    assert lib.kdpc_group_points(-1, 1, 1, 1, 1, None, None, None, None) == EINVAL
+    assert lib.kdpc_csr_workspace_bytes(0, 10, 10) == 0
+    # empty work is a successful no-op
+    assert lib.kdpc_gather_points(0, 3, 10, 4, None, None, None, None) == 0
+
+
+def test_opt_n_threads_matches_reference_rule():
+    lib = kdpc_native.load_library()
+    import pointnet2_oracle as O
+    for n in (1, 2, 3, 63, 64, 100, 512, 1000, 1024, 4096, 8192, 100000):
+        assert lib.kdpc_opt_n_threads(n) == O.opt_n_threads(n)

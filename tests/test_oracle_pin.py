@@ -1,0 +1,201 @@
+"""CPU: pin the oracle against the reference's own outputs (tests/golden, produced by
+running the reference Python, oracle/make_fixtures.py) and against independent
+restatements; then the oracle is trusted as the checker for the GPU tests."""
+import numpy as np
+import pytest
+import torch
+
+import pointnet2_oracle as O
+import torch_model as M
+from weights import load_synthetic
+
+
+def test_square_distance_bitwise_equals_torch_formula():
+    rng = np.random.default_rng(0)
+    src = rng.uniform(-12, 35, (2, 300, 3)).astype(np.float32)
+    dst = rng.uniform(-12, 35, (2, 500, 3)).astype(np.float32)
+    ref = M.square_distance(torch.from_numpy(src), torch.from_numpy(dst)).numpy()
+    np.testing.assert_array_equal(O.square_distance(src, dst).view(np.int32), ref.view(np.int32))
+
+
+def test_knn_oracle_matches_reference_topk(golden):
+    g = golden("knn_ref.npz")
+    names = sorted({k.rsplit("_", 2)[0] for k in g.files if k.endswith("_idx_sorted")})
+    assert len(names) == 4
+    for name in names:
+        ref = g[name + "_idx_sorted"]
+        idx, dist = O.knn(ref.shape[-1], g[name + "_xyz"], g[name + "_new_xyz"])
+        np.testing.assert_array_equal(np.sort(idx, -1), ref, err_msg=name)
+        np.testing.assert_array_equal(dist, g[name + "_dist_sorted"], err_msg=name)
+
+
+def test_multiscale_loss_oracle_matches_reference(golden):
+    g = golden("multiscale_loss_ref.npz")
+    preds = [torch.from_numpy(g[f"pred{i}"]) for i in range(4)]
+    fps = [torch.from_numpy(g[f"fps{i}"]) for i in range(3)]
+    loss = M.multiScaleLoss(preds, torch.from_numpy(g["gt"]), fps)
+    np.testing.assert_array_equal(loss.numpy(), g["loss"])
+
+
+def test_layer_oracle_matches_reference(golden):
+    g = golden("layers_ref.npz")
+    x1 = torch.from_numpy(g["x1"].transpose(0, 2, 1).copy()).permute(0, 2, 1)
+    x2 = torch.from_numpy(g["x2"].transpose(0, 2, 1).copy()).permute(0, 2, 1)
+    layer = load_synthetic(M.PointConvD(256, 16, 35, 64), seed=31)
+    nx, nf, fidx = layer(x1, torch.from_numpy(g["pcd_feat"]))
+    np.testing.assert_array_equal(fidx.numpy(), g["pcd_fps"])
+    _close(nf, g["pcd_out"])
+    layer = load_synthetic(M.CrossLayerLight(32, 64, [32, 32], [32, 32]), seed=32)
+    a, b, c = layer(x1, x2, torch.from_numpy(g["cl_f1"]), torch.from_numpy(g["cl_f2"]))
+    for got, key in ((a, "cl_out1"), (b, "cl_out2"), (c, "cl_out3")):
+        _close(got, g[key])
+    flow = torch.from_numpy(g["warp_flow"])
+    _close(M.PointWarping()(x1, x2, flow), g["warp_out"])
+
+
+@pytest.fixture(scope="module")
+def oracle_model_run(golden):
+    g = golden("model_ref_n4096.npz")
+    pos1, pos2, flow = (torch.from_numpy(g[k]) for k in ("pos1", "pos2", "flow"))
+    teacher = load_synthetic(M.PointConvBidirection(), 1).eval()
+    student = load_synthetic(M.PointConvBidirection(), 2).train()
+    with torch.no_grad():
+        t_out = teacher(pos1, pos2, pos1, pos2)
+    s_out = student(pos1, pos2, pos1, pos2)
+    kd = M.biDirection_loss_ht(s_out[0], s_out[5], s_out[6], s_out[1], s_out[2], flow, t_out[0],
+                               t_out[5], t_out[6], t_out[1], t_out[2], 0.3, 0.8, layer=3)
+    kd.backward()
+    return g, student, t_out, s_out, kd, flow
+
+
+def _close(got, want, rtol=1e-5):
+    """Float outputs: the restatement is op-for-op the reference, so with the fixture's
+    thread count and CPU it is bitwise equal; CPU GEMM blocking varies with threads/ISA,
+    so the check is rtol=1e-5 of the tensor's scale (indices stay exact)."""
+    got = got.detach().numpy() if torch.is_tensor(got) else got
+    scale = max(float(np.abs(want).max()), 1e-6)
+    np.testing.assert_allclose(got, want, rtol=rtol, atol=rtol * scale)
+
+
+def test_model_oracle_forward_matches_reference(oracle_model_run):
+    g, student, t_out, s_out, kd, flow = oracle_model_run
+    assert list(student.state_dict().keys()) == list(g["state_keys"])
+    for tag, out in (("t", t_out), ("s", s_out)):
+        for i in range(4):
+            _close(out[0][i], g[f"{tag}_flow{i}"])
+        for i in range(3):
+            np.testing.assert_array_equal(out[1][i].numpy(), g[f"{tag}_fps1_{i}"])
+            np.testing.assert_array_equal(out[2][i].numpy(), g[f"{tag}_fps2_{i}"])
+    msl = M.multiScaleLoss(s_out[0], flow, s_out[1])
+    _close(msl, g["msl"])
+    _close(kd, g["kd"])
+
+
+def test_model_oracle_backward_matches_reference(oracle_model_run):
+    g, student, *_ = oracle_model_run
+    for (name, p), gs, ga in zip(student.named_parameters(), g["grad_sum"], g["grad_abs"]):
+        if p.grad is None:
+            continue
+        pre_bn = name.endswith("linear.bias") and "pointconv_list" in name
+        tol = 1e-5 if pre_bn else 1e-4 * ga + 1e-6
+        assert abs(float(p.grad.double().sum()) - gs) <= tol, name
+
+
+# ---------------------------------------------------------------- restatement self-checks
+def _fps_literal(xyz, m):
+    """Independent pure-Python restatement of sampling_gpu.cu:93-209 for tiny clouds."""
+    n = len(xyz)
+    T = O.opt_n_threads(n)
+    temp = [1e10] * n
+    out = [0]
+    old = 0
+    f32 = np.float32
+    for _ in range(1, m):
+        x1, y1, z1 = (f32(v) for v in xyz[old])
+        vals, ids = [], []
+        for t in range(T):
+            best, besti = f32(-1), 0
+            for k in range(t, n, T):
+                dx, dy, dz = f32(xyz[k][0] - x1), f32(xyz[k][1] - y1), f32(xyz[k][2] - z1)
+                # fmaf(dz,dz,fmaf(dy,dy,dx*dx)) evaluated exactly in float64 then rounded
+                inner = f32(np.float64(dy) * dy + np.float64(f32(dx * dx)))
+                d = f32(np.float64(dz) * dz + np.float64(inner))
+                d2 = min(d, f32(temp[k]))
+                temp[k] = d2
+                if d2 > best:
+                    best, besti = d2, k
+            vals.append(best)
+            ids.append(besti)
+        s = T // 2
+        while s >= 1:
+            for t in range(s):
+                if vals[t + s] > vals[t]:
+                    vals[t], ids[t] = vals[t + s], ids[t + s]
+            s //= 2
+        old = ids[0]
+        out.append(old)
+    return np.array(out, np.int32)
+
+
+@pytest.mark.parametrize("n,m", [(37, 20), (64, 40), (100, 60)])
+def test_fps_oracle_vs_literal_restatement(n, m):
+    rng = np.random.default_rng(n)
+    xyz = np.round(rng.uniform(-2, 2, (n, 3)), 1).astype(np.float32)  # many exact ties
+    idx, _ = O.furthest_point_sample(xyz[None], m)
+    np.testing.assert_array_equal(idx[0], _fps_literal(xyz, m))
+
+
+def test_fps_oracle_properties():
+    rng = np.random.default_rng(1)
+    xyz = rng.normal(size=(1, 500, 3)).astype(np.float32)
+    idx, temp = O.furthest_point_sample(xyz, 100)
+    assert idx[0, 0] == 0 and len(set(idx[0].tolist())) == 100
+    # temp holds the min distance to every sample except the last (updated before it is chosen)
+    d = ((xyz[0][:, None, :] - xyz[0][idx[0][:-1]][None]) ** 2).sum(-1).min(1)
+    np.testing.assert_allclose(temp[0], d, rtol=1e-5, atol=1e-6)
+    same = np.zeros((1, 50, 3), np.float32)
+    assert (O.furthest_point_sample(same, 10)[0] == 0).all()
+
+
+def test_ball_query_oracle_vs_numpy():
+    rng = np.random.default_rng(2)
+    xyz = rng.uniform(0, 4, (2, 800, 3)).astype(np.float32)
+    q = xyz[:, :50].copy()
+    q[:, :5] += 50
+    out = O.ball_query(0.5, 16, xyz, q)
+    d2 = ((q[:, :, None].astype(np.float64) - xyz[:, None]) ** 2).sum(-1)
+    for b in range(2):
+        for i in range(50):
+            hits = np.nonzero(d2[b, i] < 0.25 - 1e-6)[0]
+            near = np.abs(d2[b, i] - 0.25) < 1e-5
+            if near.any():
+                continue
+            exp = np.zeros(16, np.int32)
+            if len(hits):
+                h = hits[:16]
+                exp[:] = h[0]
+                exp[:len(h)] = h
+            np.testing.assert_array_equal(out[b, i], exp)
+
+
+def test_three_nn_and_grads_oracle_vs_numpy():
+    rng = np.random.default_rng(3)
+    known = rng.normal(size=(1, 60, 3)).astype(np.float32)
+    unknown = rng.normal(size=(1, 90, 3)).astype(np.float32)
+    d2, idx = O.three_nn(unknown, known)
+    ref = ((unknown[0][:, None].astype(np.float64) - known[0][None]) ** 2).sum(-1)
+    np.testing.assert_array_equal(idx[0], np.argsort(ref, axis=1, kind="stable")[:, :3])
+    feats = rng.normal(size=(1, 4, 60)).astype(np.float32)
+    w = rng.uniform(size=(1, 90, 3)).astype(np.float32)
+    out = O.three_interpolate(feats, idx, w)
+    np.testing.assert_allclose(out[0], (feats[0][:, idx[0]] * w[0][None]).sum(-1), rtol=1e-5, atol=1e-6)
+    g = rng.normal(size=(1, 4, 90)).astype(np.float32)
+    gp = O.three_interpolate_grad(g, idx, w, 60)
+    ref_gp = np.zeros((4, 60))
+    for n in range(90):
+        for j in range(3):
+            ref_gp[:, idx[0, n, j]] += g[0, :, n] * w[0, n, j]
+    np.testing.assert_allclose(gp[0], ref_gp, rtol=1e-5, atol=1e-6)
+    gg = O.group_points_grad(rng.normal(size=(1, 4, 30, 3)).astype(np.float32),
+                             idx[:, :30], 60)
+    assert gg.shape == (1, 4, 60)
