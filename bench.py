@@ -101,6 +101,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if os.environ.get("KDPC_BLAS"):
+        torch.backends.cuda.preferred_blas_library(os.environ["KDPC_BLAS"])
 
     import kdpc_native
     import synthetic

@@ -1,0 +1,117 @@
+"""Dense 1x1 layers (Linear / Conv1d / per-neighbour Conv2d) with split-K weight gradients.
+
+Every dense layer of the network is a GEMM over "rows" = points (x neighbours): up to
+B*N*K = 2.1M rows, with in/out widths of 3..2096.  The weight gradient dW = dY^T X is then a
+tiny output (out x in) reduced over millions of rows, which the BLAS heuristics run on a
+handful of workgroups (rocprofv3, profiles/round01: 38 % of the step in GEMMs with < 64
+workgroups).  Here dW is computed as a batched GEMM over row chunks (split-K) followed by a
+sum over the chunk axis, which spreads the reduction over the whole chip.  Forward and
+input-gradient GEMMs are unchanged (they are well shaped).  fp32 throughout.
+"""
+import torch
+from torch.autograd import Function
+
+_MIN_ROWS_PER_CHUNK = 2048
+_MAX_CHUNKS = 64
+
+
+def _chunks(rows, out_elems):
+    if rows < 2 * _MIN_ROWS_PER_CHUNK:
+        return 1
+    # enough chunks to keep ~64 workgroups busy even for tiny outputs, bounded by the
+    # extra traffic of the (chunks x out x in) partial sums
+    c = min(_MAX_CHUNKS, rows // _MIN_ROWS_PER_CHUNK)
+    while c > 1 and c * out_elems > (1 << 26):
+        c //= 2
+    return c
+
+
+def splitk_tn(a, b):
+    """a (R,O), b (R,I) -> a^T b (O,I) with the R reduction split over chunks."""
+    R, O = a.shape
+    I = b.shape[1]
+    c = _chunks(R, O * I)
+    if c == 1:
+        return a.t().mm(b)
+    rc = (R // c) * c
+    part = torch.bmm(a[:rc].reshape(c, rc // c, O).transpose(1, 2), b[:rc].reshape(c, rc // c, I))
+    out = part.sum(0)
+    if rc < R:
+        out.addmm_(a[rc:].t(), b[rc:])
+    return out
+
+
+class _Linear(Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])
+        y = torch.addmm(bias, x2, weight.t()) if bias is not None else x2.mm(weight.t())
+        ctx.save_for_backward(x2, weight)
+        ctx.has_bias = bias is not None
+        ctx.shape = shape
+        return y.view(*shape[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, weight = ctx.saved_tensors
+        g2 = gy.reshape(-1, weight.shape[0])
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = g2.mm(weight).view(ctx.shape)
+        if ctx.needs_input_grad[1]:
+            gw = splitk_tn(g2.contiguous(), x2)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = g2.sum(0)
+        return gx, gw, gb
+
+
+def linear(x, weight, bias=None):
+    """F.linear on (..., in) with the split-K weight gradient."""
+    return _Linear.apply(x, weight, bias)
+
+
+class _Conv1x1(Function):
+    """y[b] = W x[b] + bias for x (B,C,N) (a kernel-size-1 Conv1d)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        y = torch.matmul(weight, x)
+        if bias is not None:
+            y.add_(bias.view(1, -1, 1))
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        gy = gy.contiguous()
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.matmul(weight.t(), gy)
+        if ctx.needs_input_grad[1]:
+            B, O, N = gy.shape
+            C = x.shape[1]
+            # split the (B*N) reduction: B batches, each further split along N
+            c = max(1, min(_MAX_CHUNKS // max(B, 1), N // _MIN_ROWS_PER_CHUNK))
+            if c > 1 and N % c == 0:
+                gyc = gy.view(B, O, c, N // c).permute(0, 2, 1, 3).reshape(B * c, O, N // c)
+                xc = x.contiguous().view(B, C, c, N // c).permute(0, 2, 3, 1).reshape(B * c, N // c, C)
+                gw = torch.bmm(gyc, xc).sum(0)
+            else:
+                gw = torch.bmm(gy, x.transpose(1, 2)).sum(0)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = gy.sum((0, 2))
+        return gx, gw, gb
+
+
+def conv1x1(x, conv):
+    """Apply an nn.Conv1d (kernel 1) module to x (B,C,N)."""
+    w = conv.weight.view(conv.out_channels, conv.in_channels)
+    return _Conv1x1.apply(x, w, conv.bias)
+
+
+def linear_1x1(conv, x):
+    """Apply a kernel-1 nn.Conv1d/nn.Conv2d to a channel-last tensor (..., C_in)."""
+    return _Linear.apply(x, conv.weight.view(conv.out_channels, conv.in_channels), conv.bias)

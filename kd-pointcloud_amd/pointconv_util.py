@@ -21,6 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 import kdpc_native as _nat
+from dense import conv1x1, linear, linear_1x1
 from pointnet2 import pointnet2_utils
 
 LEAKY_RATE = 0.1
@@ -44,7 +45,10 @@ class Conv1d(nn.Module):
             act)
 
     def forward(self, x):
-        return self.composed_module(x)
+        conv, norm, act = self.composed_module
+        if conv.kernel_size != (1,) or conv.stride != (1,) or conv.padding != (0,):
+            return self.composed_module(x)
+        return act(norm(conv1x1(x, conv)))
 
 
 class Conv2d(nn.Module):
@@ -68,14 +72,10 @@ class Conv2d(nn.Module):
 
     def channel_last(self, x):
         """Same op on (..., C) tensors (1x1 kernel, no BN)."""
-        conv = self.composed_module[0]
-        y = F.linear(x, conv.weight.view(conv.out_channels, conv.in_channels), conv.bias)
-        return self.composed_module[2](y)
+        return self.composed_module[2](linear_1x1(self.composed_module[0], x))
 
 
-def _linear_1x1(conv, x):
-    """Apply a 1x1 nn.Conv1d/nn.Conv2d to a channel-last tensor (..., C_in)."""
-    return F.linear(x, conv.weight.view(conv.out_channels, conv.in_channels), conv.bias)
+_linear_1x1 = linear_1x1
 
 
 # ------------------------------------------------------------------------------ point ops
@@ -89,9 +89,23 @@ def square_distance(src, dst):
     return dist
 
 
+_knn_override = None
+
+
+def set_knn_override(fn):
+    """Test seam: route knn_point through `fn(nsample, xyz, new_xyz) -> int32 idx` (used by
+    the parity tests to replay the reference's own neighbour choices); None restores the
+    HIP kernel.  Returns the previous override."""
+    global _knn_override
+    prev, _knn_override = _knn_override, fn
+    return prev
+
+
 def knn_point(nsample, xyz, new_xyz):
     """Reference: pointconv_util.py:96-107.  xyz (B,N,C) refs, new_xyz (B,S,C) queries ->
     (B,S,nsample) int32, ascending by (distance, index)."""
+    if _knn_override is not None:
+        return _knn_override(nsample, xyz, new_xyz)
     return _nat.knn_point(nsample, xyz.contiguous(), new_xyz.contiguous())
 
 
@@ -197,7 +211,7 @@ def _pointconv_contract(new_points, weights):
 class _PointConvBase(nn.Module):
     def _finish(self, new_points):
         """Linear(16C->out) + optional BN1d + activation; (B,S,16C) -> (B,out,S)."""
-        new_points = self.linear(new_points)
+        new_points = linear(new_points, self.linear.weight, self.linear.bias)
         new_points = new_points.permute(0, 2, 1)
         if self.bn:
             new_points = self.bn_linear(new_points)
@@ -320,13 +334,13 @@ class CrossLayerLight(nn.Module):
         xb = torch.cat([pc2, pc1], 0)
         fa = torch.cat([feat1, feat2], 0)
         fb = torch.cat([feat2, feat1], 0)
-        both = self.cross(xa, xb, self.cross_t11(fa), self.cross_t22(fb), self.pos1, self.mlp1,
-                          self.bn1)
+        both = self.cross(xa, xb, conv1x1(fa, self.cross_t11), conv1x1(fb, self.cross_t22),
+                          self.pos1, self.mlp1, self.bn1)
         feat1_new, feat2_new = both[:B], both[B:]
         if self.mlp2 is False:
             return feat1_new, feat2_new
-        feat1_new = self.cross_t1(feat1_new)
-        feat2_new = self.cross_t2(feat2_new)
+        feat1_new = conv1x1(feat1_new, self.cross_t1)
+        feat2_new = conv1x1(feat2_new, self.cross_t2)
         feat1_final = self.cross(pc1, pc2, feat1_new, feat2_new, self.pos2, self.mlp2, self.bn2)
         return feat1_new, feat2_new, feat1_final
 
@@ -353,8 +367,8 @@ class FlowEmbeddingLayer(nn.Module):
             def act(x):
                 shp = x.shape
                 return self.relu(self.bn(x.reshape(-1, shp[-1], 1, 1)).view(shp))
-        return _cost_volume(self.nsample, xyz1, xyz2, self.t11(points1), self.t22(points2),
-                            self.pos, self.mlp, act)
+        return _cost_volume(self.nsample, xyz1, xyz2, conv1x1(points1, self.t11),
+                            conv1x1(points2, self.t22), self.pos, self.mlp, act)
 
 
 class PointConvFlow(nn.Module):
@@ -471,6 +485,6 @@ class SceneFlowEstimatorResidual(nn.Module):
             new_points = pointconv(xyz, new_points)
         for conv in self.mlp_convs:
             new_points = conv(new_points)
-        flow_local = self.fc(new_points).clamp(self.clamp[0], self.clamp[1])
+        flow_local = conv1x1(new_points, self.fc).clamp(self.clamp[0], self.clamp[1])
         flow = flow_local if flow is None else flow_local + flow
         return new_points, flow

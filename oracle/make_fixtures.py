@@ -223,6 +223,57 @@ def make_model(R, n=4096):
     np.savez_compressed(os.path.join(GOLDEN, f"model_ref_n{n}.npz"), **out)
 
 
+def make_model_knn_trace(R, n=2048):
+    """Teacher (eval) + student (train) forward at N=n with EVERY knn_point call recorded
+    (K, query/ref checksums, indices): lets the GPU model run with the reference's own
+    neighbour choices, isolating arithmetic parity from near-tie kNN flips."""
+    calls = []
+    orig = {m: m.knn_point for m in (R.pcu, sys.modules["pointconv_util2"])}
+
+    def make(fn):
+        def rec(nsample, xyz, new_xyz):
+            idx = fn(nsample, xyz, new_xyz)
+            calls.append((nsample, _np(xyz).astype(np.float64), _np(new_xyz).astype(np.float64),
+                          _np(idx)))
+            return idx
+        return rec
+    for m, fn in orig.items():
+        m.knn_point = make(fn)
+    try:
+        p1, p2, fl = synthetic.ft3d_pair(n, seed=8, pair=0)
+        pos1, pos2, flow = (torch.from_numpy(a[None]) for a in (p1, p2, fl))
+        teacher = _synth(R.teacher.PointConvBidirection(), seed=1).eval()
+        student = _synth(R.student.PointConvBidirection(), seed=2).train()
+        with torch.no_grad():
+            t_out = teacher(pos1, pos2, pos1, pos2)
+        s_out = student(pos1, pos2, pos1, pos2)
+        flows, f1i, f2i, _, _, feat1s, feat2s, _ = s_out
+        msl = R.loss.multiScaleLoss(flows, flow, f1i)
+        kd = R.loss.biDirection_loss_ht(flows, feat1s, feat2s, f1i, f2i, flow, t_out[0],
+                                        t_out[5], t_out[6], t_out[1], t_out[2], 0.3, 0.8, layer=3)
+        kd.backward()
+    finally:
+        for m, fn in orig.items():
+            m.knn_point = fn
+    out = dict(pos1=p1[None], pos2=p2[None], flow=fl[None], msl=_np(msl), kd=_np(kd),
+               n_calls=np.array(len(calls)))
+    for i, (k, xyz, q, idx) in enumerate(calls):
+        out[f"knn{i}_k"] = np.array(k)
+        out[f"knn{i}_rsum"] = np.concatenate([xyz[0].sum(0), (xyz[0] ** 2).sum(0)])
+        out[f"knn{i}_qsum"] = np.concatenate([q[0].sum(0), (q[0] ** 2).sum(0)])
+        out[f"knn{i}_idx"] = idx[0].astype(np.int16)
+    for tag, o in (("t", t_out), ("s", s_out)):
+        for i, f in enumerate(o[0]):
+            out[f"{tag}_flow{i}"] = _np(f)
+        out[f"{tag}_feat1_3"] = _np(o[5][3])
+    out["s_epe3d"] = _np(torch.norm(flows[0].permute(0, 2, 1) - flow, dim=2).mean())
+    out["grad_sum"] = np.array([float(p.grad.sum()) if p.grad is not None else 0.0
+                                for _, p in student.named_parameters()], dtype=np.float64)
+    out["grad_abs"] = np.array([float(p.grad.abs().sum()) if p.grad is not None else 0.0
+                                for _, p in student.named_parameters()], dtype=np.float64)
+    np.savez_compressed(os.path.join(GOLDEN, f"model_knntrace_n{n}.npz"), **out)
+
+
 def main():
     os.makedirs(GOLDEN, exist_ok=True)
     torch.set_num_threads(min(8, os.cpu_count() or 1))
@@ -231,6 +282,7 @@ def main():
     make_losses(R)
     make_layers(R)
     make_model(R)
+    make_model_knn_trace(R)
     print("fixtures written to", GOLDEN)
 
 

@@ -104,3 +104,75 @@ def test_model_backward_matches_reference(model_run):
         pre_bn = name.endswith("linear.bias") and "pointconv_list" in name
         tol = 1e-5 if pre_bn else 1e-4 * ga + 1e-6
         assert abs(got - gs) <= tol, (name, got, gs, ga)
+
+
+class _KnnReplay:
+    """Serve every knn_point call with the index the reference computed for the same
+    (K, reference cloud, query cloud), matched by coordinate checksums per batch element."""
+
+    def __init__(self, g):
+        self.recs = []
+        for i in range(int(g["n_calls"])):
+            self.recs.append((int(g[f"knn{i}_k"]), g[f"knn{i}_rsum"], g[f"knn{i}_qsum"],
+                              g[f"knn{i}_idx"].astype(np.int32)))
+        self.worst = 0.0
+
+    def __call__(self, nsample, xyz, new_xyz):
+        x = xyz.detach().double().cpu().numpy()
+        q = new_xyz.detach().double().cpu().numpy()
+        out = []
+        for b in range(x.shape[0]):
+            rs = np.concatenate([x[b].sum(0), (x[b] ** 2).sum(0)])
+            qs = np.concatenate([q[b].sum(0), (q[b] ** 2).sum(0)])
+            best, err = None, np.inf
+            for k, rr, qq, idx in self.recs:
+                if k != nsample or idx.shape != (q.shape[1], nsample):
+                    continue
+                e = np.abs(rr - rs).max() / (np.abs(rr).max() + 1) + \
+                    np.abs(qq - qs).max() / (np.abs(qq).max() + 1)
+                if e < err:
+                    best, err = idx, e
+            assert best is not None, (nsample, x.shape, q.shape)
+            self.worst = max(self.worst, err)
+            out.append(best)
+        return torch.from_numpy(np.stack(out)).to(xyz.device)
+
+
+def test_model_matches_reference_with_reference_neighbours(golden):
+    """Arithmetic parity of the whole teacher/student forward and the KD loss at 1e-5 when
+    both sides use the same neighbour indices (the reference's, replayed)."""
+    import loss_functions as L
+    import pointconv_util as P
+    from models_bid_pointconv import PointConvBidirection as Net
+    g = golden("model_knntrace_n2048.npz")
+    pos1, pos2, flow = _t(g["pos1"]), _t(g["pos2"]), _t(g["flow"])
+    replay = _KnnReplay(g)
+    prev = P.set_knn_override(replay)
+    try:
+        teacher = load_synthetic(Net(), seed=1).to(DEV).eval()
+        student = load_synthetic(Net(), seed=2).to(DEV).train()
+        with torch.no_grad():
+            t_out = teacher(pos1, pos2, pos1, pos2)
+        s_out = student(pos1, pos2, pos1, pos2)
+        flows, f1i, f2i, _, _, feat1s, feat2s, _ = s_out
+        msl = L.multiScaleLoss(flows, flow, f1i)
+        kd = L.biDirection_loss_ht(flows, feat1s, feat2s, f1i, f2i, flow, t_out[0], t_out[5],
+                                   t_out[6], t_out[1], t_out[2], 0.3, 0.8, layer=3)
+        kd.backward()
+    finally:
+        P.set_knn_override(prev)
+    assert replay.worst < 1e-5, replay.worst  # every call matched a recorded one
+    for tag, out in (("t", t_out), ("s", s_out)):
+        for i in range(4):
+            _close(out[0][i], g[f"{tag}_flow{i}"], name=f"{tag} flow{i}")
+        _close(out[5][3], g[f"{tag}_feat1_3"], name=f"{tag} feat1s[3]")
+    _close(msl, g["msl"], name="multiScaleLoss")
+    _close(kd, g["kd"], name="KD loss")
+    epe = torch.norm(flows[0].permute(0, 2, 1) - flow, dim=2).mean()
+    _close(epe, g["s_epe3d"], name="EPE3D")
+    for (name, p), gs, ga in zip(student.named_parameters(), g["grad_sum"], g["grad_abs"]):
+        if p.grad is None:
+            continue
+        pre_bn = name.endswith("linear.bias") and "pointconv_list" in name
+        tol = 1e-5 if pre_bn else 1e-4 * ga + 1e-6
+        assert abs(float(p.grad.double().sum()) - gs) <= tol, (name, float(p.grad.sum()), gs)
