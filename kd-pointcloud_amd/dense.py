@@ -42,23 +42,22 @@ def splitk_tn(a, b):
 
 
 class _Linear(Function):
+    """2-D only: callers reshape outside, so no view is created inside the Function (a view
+    returned from a custom Function may not be modified in place, e.g. by LeakyReLU)."""
+
     @staticmethod
-    def forward(ctx, x, weight, bias):
-        shape = x.shape
-        x2 = x.reshape(-1, shape[-1])
+    def forward(ctx, x2, weight, bias):
         y = torch.addmm(bias, x2, weight.t()) if bias is not None else x2.mm(weight.t())
         ctx.save_for_backward(x2, weight)
         ctx.has_bias = bias is not None
-        ctx.shape = shape
-        return y.view(*shape[:-1], weight.shape[0])
+        return y
 
     @staticmethod
-    def backward(ctx, gy):
+    def backward(ctx, g2):
         x2, weight = ctx.saved_tensors
-        g2 = gy.reshape(-1, weight.shape[0])
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
-            gx = g2.mm(weight).view(ctx.shape)
+            gx = g2.mm(weight)
         if ctx.needs_input_grad[1]:
             gw = splitk_tn(g2.contiguous(), x2)
         if ctx.has_bias and ctx.needs_input_grad[2]:
@@ -68,7 +67,8 @@ class _Linear(Function):
 
 def linear(x, weight, bias=None):
     """F.linear on (..., in) with the split-K weight gradient."""
-    return _Linear.apply(x, weight, bias)
+    y = _Linear.apply(x.reshape(-1, x.shape[-1]), weight, bias)
+    return y.view(*x.shape[:-1], weight.shape[0])
 
 
 class _Conv1x1(Function):
@@ -114,4 +114,4 @@ def conv1x1(x, conv):
 
 def linear_1x1(conv, x):
     """Apply a kernel-1 nn.Conv1d/nn.Conv2d to a channel-last tensor (..., C_in)."""
-    return _Linear.apply(x, conv.weight.view(conv.out_channels, conv.in_channels), conv.bias)
+    return linear(x, conv.weight.view(conv.out_channels, conv.in_channels), conv.bias)

@@ -114,11 +114,13 @@ class _GroupRows(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, points, idx):
+        """idx (B,...) -> flat (B,P,C); the caller views the result (no output view is made
+        in here).  The CSR built in backward is cached on this idx object, so every grouping
+        through the same kNN index (xyz and features) shares one inverse index."""
         B, N, C = points.shape
-        flat = _nat.group_rows(points, idx.reshape(B, -1))
         ctx.save_for_backward(idx)
         ctx.shape = (B, N, C)
-        return flat.view(*idx.shape, C)
+        return _nat.group_rows(points, idx.view(B, -1))
 
     @staticmethod
     def backward(ctx, grad_out):
@@ -132,14 +134,21 @@ def _as_idx32(idx):
     return idx if idx.dtype == torch.int32 else idx.int()
 
 
+def _group_rows(points, idx):
+    idx = _as_idx32(idx).contiguous()
+    B = idx.shape[0]
+    out = _GroupRows.apply(points.contiguous(), idx)
+    return out.view(*idx.shape, points.shape[-1])
+
+
 def index_points_gather(points, fps_idx):
     """Reference: pointconv_util.py:109-120.  points (B,N,C), fps_idx (B,S) -> (B,S,C)."""
-    return _GroupRows.apply(points.contiguous(), _as_idx32(fps_idx).contiguous())
+    return _group_rows(points, fps_idx)
 
 
 def index_points_group(points, knn_idx):
     """Reference: pointconv_util.py:122-133.  points (B,N,C), knn_idx (B,N,K) -> (B,N,K,C)."""
-    return _GroupRows.apply(points.contiguous(), _as_idx32(knn_idx).contiguous())
+    return _group_rows(points, knn_idx)
 
 
 def group(nsample, xyz, points):
