@@ -128,6 +128,30 @@ int kdpc_three_interpolate_grad_csr(int b, int c, int n, int m, const float *gra
                                     const float *weight, const int *offsets, const int *perm,
                                     float *grad_points, void *stream);
 
+/* ---- fused cost volume (CrossLayerLight.cross / FlowEmbeddingLayer,
+ *      pointconv_util.py:1826-1850 / :1497-1517) ----------------------------------------- */
+
+/* out[b,n,:] = max_k LeakyReLU(W1 LeakyReLU((P2[idx]+P1[n]) + Wpos(x2[idx]-x1[n]) + bpos) + b1)
+ * x1 (B,N1,3), x2 (B,N2,3), idx (B,N1,K) int32, p1 (B,N1,Din), p2 (B,N2,Din), wpos (Din,3),
+ * bpos (Din), w1 (Dout,Din), b1 (Dout) -> out (B,N1,Dout) channel-last, amax (B,N1,Dout) u8.
+ * Din, Dout in {32,64}; 1 <= K <= 32. */
+int kdpc_cost_volume_fwd(int b, int n1, int n2, int k, int din, int dout, const float *x1,
+                         const float *x2, const int *idx, const float *p1, const float *p2,
+                         const float *wpos, const float *bpos, const float *w1, const float *b1,
+                         float *out, unsigned char *amax, void *stream);
+
+/* Backward: dout_grad (B,N1,Dout) -> dp1 (B,N1,Din), dp2_rows (B,N1,K,Din), dx1 (B,N1,3),
+ * ddir_rows (B,N1,K,3), dparams = [dW1 (Dout*Din) | db1 (Dout) | dWpos^T (3*Din) | dbpos (Din)].
+ * dp2_rows/ddir_rows are per-neighbour rows: sum them per reference point with
+ * kdpc_group_rows_grad_csr over the CSR of idx.  workspace: see *_workspace_bytes. */
+size_t kdpc_cost_volume_bwd_workspace_bytes(int b, int n1, int din, int dout);
+int kdpc_cost_volume_bwd(int b, int n1, int n2, int k, int din, int dout, const float *x1,
+                         const float *x2, const int *idx, const float *p1, const float *p2,
+                         const float *wpos, const float *bpos, const float *w1, const float *out,
+                         const unsigned char *amax, const float *dout_grad, float *dp1,
+                         float *dp2_rows, float *dx1, float *ddir_rows, void *workspace,
+                         size_t workspace_bytes, float *dparams, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -62,6 +62,60 @@ __global__ __launch_bounds__(256) void group_points_kernel(int c, int n, int p_t
   }
 }
 
+// LDS-staged variant for N <= 16384: a workgroup owns CG whole channel rows of one cloud
+// (CG*N*4 <= 64 KiB, loaded once with coalesced float4 reads) and a slice of positions;
+// every output is then a random LDS read instead of a random 4-byte global gather, and
+// the only HBM streams are the coalesced float4 stores and the int4 index reads.
+constexpr int kRowLdsBytes = 64 * 1024;
+
+template <int CG>
+__global__ __launch_bounds__(256) void group_points_lds_kernel(int c, int n, int p_total,
+                                                               int p_slice,
+                                                               const float* __restrict__ points,
+                                                               const int* __restrict__ idx,
+                                                               float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float rows[];  // [CG][n]
+  const int nslice = gridDim.x;
+  const int slice = blockIdx.x;
+  const int c0 = blockIdx.y * CG;
+  const int bi = blockIdx.z;
+  const int cg = min(CG, c - c0);
+  const float* pb = points + ((long long)bi * c + c0) * n;
+  for (int cc = 0; cc < cg; ++cc) {
+    const float* src = pb + (long long)cc * n;
+    if ((n & 3) == 0) {
+      for (int e = threadIdx.x * 4; e < n; e += 256 * 4)
+        *reinterpret_cast<float4*>(rows + cc * n + e) = *reinterpret_cast<const float4*>(src + e);
+    } else {
+      for (int e = threadIdx.x; e < n; e += 256) rows[cc * n + e] = src[e];
+    }
+  }
+  __syncthreads();
+  const int pbeg = slice * p_slice;
+  const int pend = min(p_total, pbeg + p_slice);
+  const int* ib = idx + (long long)bi * p_total;
+  float* ob = out + ((long long)bi * c + c0) * p_total;
+  (void)nslice;
+  for (int p4 = pbeg + threadIdx.x * 4; p4 < pend; p4 += 256 * 4) {
+    if (p4 + 3 < pend) {
+      const int4 q = *reinterpret_cast<const int4*>(ib + p4);
+#pragma unroll
+      for (int cc = 0; cc < CG; ++cc) {
+        if (cc < cg) {
+          const float* r = rows + cc * n;
+          *reinterpret_cast<float4*>(ob + (long long)cc * p_total + p4) =
+              make_float4(r[q.x], r[q.y], r[q.z], r[q.w]);
+        }
+      }
+    } else {
+      for (int t = p4; t < pend; ++t) {
+        const int q = ib[t];
+        for (int cc = 0; cc < cg; ++cc) ob[(long long)cc * p_total + t] = rows[cc * n + q];
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // ball_query (reference ball_query_gpu.cu:9-45): the first nsample k (ascending) with
 // d2 < r^2; if any hit, the remaining slots repeat the first hit; no hit -> zeros.
@@ -204,10 +258,35 @@ KDPC_API int kdpc_group_points(int b, int c, int n, int npoints, int nsample, co
   if ((long long)b * c * p_total == 0) return (int)hipSuccess;
   KDPC_CHECK_ARG(points && idx && out && p_total < (1ll << 31));
   KDPC_CHECK_ARG(b <= 65535);
+  hipStream_t st = (hipStream_t)stream;
+  const int cg = kRowLdsBytes / (4 * n);
+  if (cg >= 1 && (p_total % 4) == 0) {
+    // channel groups of CG rows; slices so that the grid covers >= ~512 workgroups
+    const int CG = cg >= 4 ? 4 : (cg >= 2 ? 2 : 1);
+    const int groups = divup(c, CG);
+    int nslice = divup(512, b * groups);
+    const int min_slice = 4096;
+    nslice = max(1, min(nslice, (int)divupll(p_total, min_slice)));
+    int p_slice = (int)divupll(divupll(p_total, nslice), 4) * 4;
+    nslice = (int)divupll(p_total, p_slice);
+    KDPC_CHECK_ARG(groups <= 65535);
+    dim3 grid(nslice, groups, b);
+    const size_t lds = (size_t)CG * n * sizeof(float);
+    if (CG == 4)
+      hipLaunchKernelGGL(group_points_lds_kernel<4>, grid, dim3(256), lds, st, c, n, (int)p_total,
+                         p_slice, points, idx, out);
+    else if (CG == 2)
+      hipLaunchKernelGGL(group_points_lds_kernel<2>, grid, dim3(256), lds, st, c, n, (int)p_total,
+                         p_slice, points, idx, out);
+    else
+      hipLaunchKernelGGL(group_points_lds_kernel<1>, grid, dim3(256), lds, st, c, n, (int)p_total,
+                         p_slice, points, idx, out);
+    KDPC_RETURN_LAUNCH();
+  }
   dim3 grid(divup((int)divupll(p_total, 4), 256), divup(c, kGroupCG), b);
   KDPC_CHECK_ARG(grid.y <= 65535);
-  hipLaunchKernelGGL(group_points_kernel, grid, dim3(256), 0, (hipStream_t)stream, c, n,
-                     (int)p_total, points, idx, out);
+  hipLaunchKernelGGL(group_points_kernel, grid, dim3(256), 0, st, c, n, (int)p_total, points, idx,
+                     out);
   KDPC_RETURN_LAUNCH();
 }
 

@@ -121,6 +121,39 @@ __global__ __launch_bounds__(256) void csr_sum_cm_kernel(int b, int c, int n, in
   }
 }
 
+// LDS-staged channel-major gather-sum for P <= 40960: one workgroup per (b, c) stages the
+// whole gradient row src[b,c,:] (coalesced float4, read exactly once from HBM) and then
+// walks the CSR segments of every n reading LDS; the result row is written coalesced.
+// Same ascending-position summation order as csr_sum_cm_kernel (bit-identical results).
+constexpr int kSumRowLdsBytes = 160 * 1024;
+
+__global__ __launch_bounds__(256) void csr_sum_cm_lds_kernel(int c, int n, int p,
+                                                             const float* __restrict__ src,
+                                                             const int* __restrict__ offsets,
+                                                             const int* __restrict__ perm,
+                                                             float* __restrict__ dst) {
+  extern __shared__ __attribute__((aligned(16))) float row[];  // [p]
+  const int ci = blockIdx.x;
+  const int bi = blockIdx.y;
+  const float* s = src + ((long long)bi * c + ci) * p;
+  if ((p & 3) == 0) {
+    for (int e = threadIdx.x * 4; e < p; e += 256 * 4)
+      *reinterpret_cast<float4*>(row + e) = *reinterpret_cast<const float4*>(s + e);
+  } else {
+    for (int e = threadIdx.x; e < p; e += 256) row[e] = s[e];
+  }
+  __syncthreads();
+  const int* off = offsets + (long long)bi * n;
+  const int base = bi * p;
+  float* d = dst + ((long long)bi * c + ci) * n;
+  for (int ni = threadIdx.x; ni < n; ni += 256) {
+    const int j0 = off[ni], j1 = off[ni + 1];
+    float acc = 0.f;
+    for (int j = j0; j < j1; ++j) acc = __fadd_rn(acc, row[perm[j] - base]);
+    d[ni] = acc;
+  }
+}
+
 // three_interpolate_grad: positions are (n,t) of idx (B,N,3); contribution g[b,c,n]*w[b,n,t]
 __global__ __launch_bounds__(256) void csr_sum_interp_kernel(int b, int c, int n, int m,
                                                              const float* __restrict__ grad_out,
@@ -271,6 +304,17 @@ KDPC_API int kdpc_csr_sum_channels(int b, int c, int n, int p, const float* src,
   const long long total = (long long)b * c * n;
   if (total == 0) return (int)hipSuccess;
   KDPC_CHECK_ARG(dst && offsets && (p == 0 || (src && perm)));
+  if (p > 0 && (size_t)p * sizeof(float) <= kSumRowLdsBytes && c <= 65535 && b <= 65535) {
+    static bool attr = false;
+    if (!attr) {
+      hipFuncSetAttribute((const void*)csr_sum_cm_lds_kernel,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, kSumRowLdsBytes);
+      attr = true;
+    }
+    hipLaunchKernelGGL(csr_sum_cm_lds_kernel, dim3(c, b), dim3(256), (size_t)p * sizeof(float),
+                       (hipStream_t)stream, c, n, p, src, offsets, perm, dst);
+    KDPC_RETURN_LAUNCH();
+  }
   hipLaunchKernelGGL(csr_sum_cm_kernel, dim3(grid_for(total, 256)), dim3(256), 0,
                      (hipStream_t)stream, b, c, n, p, src, offsets, perm, dst);
   KDPC_RETURN_LAUNCH();

@@ -33,8 +33,11 @@ _SIGNATURES = {
     "kdpc_csr_sum_channels": [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
     "kdpc_three_interpolate_grad_csr": [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp,
                                         _vp, _vp],
+    "kdpc_cost_volume_fwd": [_c_int] * 6 + [_vp] * 12,
+    "kdpc_cost_volume_bwd_workspace_bytes": [_c_int] * 4,
+    "kdpc_cost_volume_bwd": [_c_int] * 6 + [_vp] * 15 + [_c_size, _vp, _vp],
 }
-_RESTYPES = {"kdpc_csr_workspace_bytes": _c_size}
+_RESTYPES = {"kdpc_csr_workspace_bytes": _c_size, "kdpc_cost_volume_bwd_workspace_bytes": _c_size}
 
 EXPORTED = tuple(_SIGNATURES)
 
@@ -288,3 +291,51 @@ def three_interpolate_grad(grad_out, idx, weight, m):
           _dev(weight, torch.float32, "weight"), csr.offsets.data_ptr(), csr.perm.data_ptr(),
           _dev(out, torch.float32, "grad_points"), _stream(grad_out))
     return out
+
+
+# ------------------------------------------------------------------ fused cost volume
+def cost_volume_supported(din, dout, k):
+    return din in (32, 64) and dout in (32, 64) and 1 <= k <= 32
+
+
+def cost_volume_fwd(x1, x2, idx, p1, p2, wpos, bpos, w1, b1):
+    """-> out (B,N1,Dout) f32, amax (B,N1,Dout) u8.  See include/kdpc.h."""
+    B, N1, _ = x1.shape
+    N2 = x2.shape[1]
+    K = idx.shape[2]
+    din, dout = p1.shape[2], w1.shape[0]
+    out = torch.empty((B, N1, dout), dtype=torch.float32, device=x1.device)
+    amax = torch.empty((B, N1, dout), dtype=torch.uint8, device=x1.device)
+    f = torch.float32
+    _call("kdpc_cost_volume_fwd", B, N1, N2, K, din, dout, _dev(x1, f, "x1"), _dev(x2, f, "x2"),
+          _dev(idx, torch.int32, "idx"), _dev(p1, f, "p1"), _dev(p2, f, "p2"),
+          _dev(wpos, f, "wpos"), _dev(bpos, f, "bpos"), _dev(w1, f, "w1"), _dev(b1, f, "b1"),
+          _dev(out, f, "out"), _dev(amax, torch.uint8, "amax"), _stream(x1),
+          work=(4 * B * N1 * (3 + K + din + K * din + 2 * dout) + B * N1 * dout,
+                2.0 * B * N1 * K * din * dout))
+    return out, amax
+
+
+def cost_volume_bwd(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout):
+    """-> dp1 (B,N1,Din), dp2_rows (B,N1,K,Din), dx1 (B,N1,3), ddir_rows (B,N1,K,3), dparams."""
+    B, N1, _ = x1.shape
+    N2 = x2.shape[1]
+    K = idx.shape[2]
+    din, dout = p1.shape[2], w1.shape[0]
+    dev = x1.device
+    f = torch.float32
+    dp1 = torch.empty((B, N1, din), dtype=f, device=dev)
+    dp2_rows = torch.empty((B, N1, K, din), dtype=f, device=dev)
+    dx1 = torch.empty((B, N1, 3), dtype=f, device=dev)
+    ddir_rows = torch.empty((B, N1, K, 3), dtype=f, device=dev)
+    dparams = torch.empty((dout * din + dout + 4 * din,), dtype=f, device=dev)
+    lib = load_library()
+    ws_bytes = lib.kdpc_cost_volume_bwd_workspace_bytes(B, N1, din, dout)
+    ws = torch.empty((max(ws_bytes, 4),), dtype=torch.uint8, device=dev)
+    _call("kdpc_cost_volume_bwd", B, N1, N2, K, din, dout, _dev(x1, f, "x1"), _dev(x2, f, "x2"),
+          _dev(idx, torch.int32, "idx"), _dev(p1, f, "p1"), _dev(p2, f, "p2"),
+          _dev(wpos, f, "wpos"), _dev(bpos, f, "bpos"), _dev(w1, f, "w1"), _dev(out, f, "out"),
+          _dev(amax, torch.uint8, "amax"), _dev(gout, f, "dout"), _dev(dp1, f, "dp1"),
+          _dev(dp2_rows, f, "dp2_rows"), _dev(dx1, f, "dx1"), _dev(ddir_rows, f, "ddir_rows"),
+          ws.data_ptr(), ws_bytes, _dev(dparams, f, "dparams"), _stream(x1))
+    return dp1, dp2_rows, dx1, ddir_rows, dparams

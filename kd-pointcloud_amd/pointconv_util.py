@@ -276,6 +276,50 @@ class PointConvD(_PointConvBase):
         return new_xyz.permute(0, 2, 1), new_points, fps_idx
 
 
+class _CostVolume(torch.autograd.Function):
+    """Fused cost volume (csrc/cost_volume.hip): x1 (B,N1,3), x2 (B,N2,3), idx (B,N1,K),
+    p1 (B,N1,D), p2 (B,N2,D) channel-last -> (B,N1,Dout) channel-last."""
+
+    @staticmethod
+    def forward(ctx, x1, x2, idx, p1, p2, wpos, bpos, w1, b1):
+        out, amax = _nat.cost_volume_fwd(x1, x2, idx, p1, p2, wpos, bpos, w1, b1)
+        ctx.save_for_backward(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax = ctx.saved_tensors
+        B, N1, K = idx.shape
+        N2 = x2.shape[1]
+        din, dout = p1.shape[2], w1.shape[0]
+        dp1, dp2_rows, dx1, ddir_rows, dpar = _nat.cost_volume_bwd(
+            x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout.contiguous())
+        csr = _nat.csr_of(idx, N2)
+        dp2 = _nat.group_rows_grad(dp2_rows.view(B, N1 * K, din), csr, B, N2, din)
+        dx2 = _nat.group_rows_grad(ddir_rows.view(B, N1 * K, 3), csr, B, N2, 3)
+        o = dout * din
+        dw1 = dpar[:o].view(dout, din)
+        db1 = dpar[o:o + dout]
+        dwpos = dpar[o + dout:o + dout + 3 * din].view(3, din).t()
+        dbpos = dpar[o + dout + 3 * din:]
+        return dx1, dx2, None, dp1, dp2, dwpos, dbpos, dw1, db1
+
+
+_FUSED_COST_VOLUME = True  # test seam: False forces the unfused torch formulation
+
+
+def _fusable(nsample, pos, mlp, act, din):
+    if not _FUSED_COST_VOLUME:
+        return False
+    if not isinstance(act, nn.LeakyReLU) or act.negative_slope != LEAKY_RATE or len(mlp) != 1:
+        return False
+    conv, norm, a2 = mlp[0].composed_module
+    if not isinstance(norm, nn.Identity) or not isinstance(a2, nn.LeakyReLU) \
+            or a2.negative_slope != LEAKY_RATE or conv.bias is None:
+        return False
+    return _nat.cost_volume_supported(din, conv.out_channels, nsample) and pos.bias is not None
+
+
 def _cost_volume(nsample, xyz1, xyz2, points1, points2, pos, mlp, act):
     """Shared math of CrossLayerLight.cross (pointconv_util.py:1826-1850) and
     FlowEmbeddingLayer.forward (:1497-1517) on the point-major layout:
@@ -287,6 +331,13 @@ def _cost_volume(nsample, xyz1, xyz2, points1, points2, pos, mlp, act):
     p1 = points1.permute(0, 2, 1)
     p2 = points2.permute(0, 2, 1)
     knn_idx = knn_point(nsample, x2, x1)
+    din = p1.shape[-1]
+    if _fusable(nsample, pos, mlp, act, din):
+        conv = mlp[0].composed_module[0]
+        out = _CostVolume.apply(x1, x2, knn_idx, p1.contiguous(), p2.contiguous(),
+                                pos.weight.view(din, 3), pos.bias,
+                                conv.weight.view(conv.out_channels, din), conv.bias)
+        return out.permute(0, 2, 1)
     direction = index_points_group(x2, knn_idx) - x1.view(B, N1, 1, C)
     grouped_points2 = index_points_group(p2, knn_idx)
     h = act((grouped_points2 + p1.unsqueeze(2)) + _linear_1x1(pos, direction))
@@ -325,7 +376,7 @@ class CrossLayerLight(nn.Module):
 
     def _act(self, bn):
         if isinstance(bn, nn.Identity):
-            return self.relu
+            return self.relu  # plain LeakyReLU: eligible for the fused kernel
 
         def f(x):  # BN2d over channels of a channel-last tensor
             shp = x.shape

@@ -1,0 +1,52 @@
+"""GPU: the fused kernels equal the unfused (reference-formulated) torch path on the same
+inputs — forward values and every gradient (rtol 1e-5 of the tensor scale)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _scale_close(a, b, rtol=1e-5, name=""):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    tol = rtol * max(float(b.abs().max()), 1e-6)
+    err = float((a - b).abs().max())
+    assert err <= tol, (name, err, tol)
+
+
+@pytest.mark.parametrize("din,dout,n1,n2,bsz", [(32, 32, 1000, 900, 2), (64, 64, 513, 700, 3),
+                                                (32, 64, 300, 300, 1), (64, 32, 257, 600, 2)])
+def test_cost_volume_fused_equals_unfused(din, dout, n1, n2, bsz):
+    import pointconv_util as P
+    import synthetic
+    torch.manual_seed(din + dout + n1)
+    layer = P.CrossLayerLight(32, din + 5, [din, dout], [dout, dout]).to(DEV)
+    x1 = torch.from_numpy(synthetic.ft3d_batch(bsz, n1, seed=1)[0]).to(DEV).permute(0, 2, 1)
+    x2 = torch.from_numpy(synthetic.ft3d_batch(bsz, n2, seed=2)[0]).to(DEV).permute(0, 2, 1)
+    f1 = torch.randn(bsz, din, n1, device=DEV)
+    f2 = torch.randn(bsz, din, n2, device=DEV)
+    outs, grads = [], []
+    for fused in (True, False):
+        P._FUSED_COST_VOLUME = fused
+        try:
+            a1 = x1.detach().clone().requires_grad_(True)
+            a2 = x2.detach().clone().requires_grad_(True)
+            g1 = f1.detach().clone().requires_grad_(True)
+            g2 = f2.detach().clone().requires_grad_(True)
+            layer.zero_grad()
+            # one cost volume with mlp1 (din -> dout) in both directions
+            o = layer.cross(a1, a2, g1, g2, layer.pos1, layer.mlp1, layer.bn1)
+            torch.manual_seed(7)
+            w = torch.randn_like(o)
+            (o * w).sum().backward()
+            outs.append(o.detach())
+            grads.append([a1.grad, a2.grad, g1.grad, g2.grad, layer.pos1.weight.grad,
+                          layer.pos1.bias.grad, layer.mlp1[0].composed_module[0].weight.grad,
+                          layer.mlp1[0].composed_module[0].bias.grad])
+        finally:
+            P._FUSED_COST_VOLUME = True
+    _scale_close(outs[0], outs[1], name="out")
+    names = ["dx1", "dx2", "dp1", "dp2", "dWpos", "dbpos", "dW1", "db1"]
+    for n, a, b in zip(names, grads[0], grads[1]):
+        _scale_close(a.reshape(b.shape), b, rtol=2e-5, name=n)
