@@ -152,6 +152,22 @@ int kdpc_cost_volume_bwd(int b, int n1, int n2, int k, int din, int dout, const 
                          float *dp2_rows, float *dx1, float *ddir_rows, void *workspace,
                          size_t workspace_bytes, float *dparams, void *stream);
 
+/* ---- fused PointConv neighbourhood contraction (pointconv_util.py:217-258, 401-446) ---- */
+
+/* out[b,s, c*16+w] = sum_k G[b,s,k,c] * wt[b,s,k,w],  G = cat(xyz[idx]-center, feats[idx]).
+ * xyz (B,N,3), center (B,S,3), feats (B,N,D), idx (B,S,K) int32, wt (B,S,K,16),
+ * out (B,S,16*(3+D)). */
+int kdpc_pointconv_contract_fwd(int b, int n, int s, int k, int d, const float *xyz,
+                                const float *center, const float *feats, const int *idx,
+                                const float *wt, float *out, void *stream);
+
+/* dout (B,S,16*(3+D)) -> dg_rows (B,S,K,3+D) per-neighbour rows of dG (sum per point with
+ * kdpc_group_rows_grad_csr), dwt (B,S,K,16), dcenter (B,S,3) = -sum_k dG[..., 0:3]. */
+int kdpc_pointconv_contract_bwd(int b, int n, int s, int k, int d, const float *xyz,
+                                const float *center, const float *feats, const int *idx,
+                                const float *wt, const float *dout, float *dg_rows, float *dwt,
+                                float *dcenter, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -34,8 +34,10 @@ _SIGNATURES = {
     "kdpc_three_interpolate_grad_csr": [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp,
                                         _vp, _vp],
     "kdpc_cost_volume_fwd": [_c_int] * 6 + [_vp] * 12,
+    "kdpc_pointconv_contract_fwd": [_c_int] * 5 + [_vp] * 7,
+    "kdpc_pointconv_contract_bwd": [_c_int] * 5 + [_vp] * 10,
     "kdpc_cost_volume_bwd_workspace_bytes": [_c_int] * 4,
-    "kdpc_cost_volume_bwd": [_c_int] * 6 + [_vp] * 15 + [_c_size, _vp, _vp],
+    "kdpc_cost_volume_bwd": [_c_int] * 6 + [_vp] * 16 + [_c_size, _vp, _vp],
 }
 _RESTYPES = {"kdpc_csr_workspace_bytes": _c_size, "kdpc_cost_volume_bwd_workspace_bytes": _c_size}
 
@@ -339,3 +341,37 @@ def cost_volume_bwd(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout):
           _dev(dp2_rows, f, "dp2_rows"), _dev(dx1, f, "dx1"), _dev(ddir_rows, f, "ddir_rows"),
           ws.data_ptr(), ws_bytes, _dev(dparams, f, "dparams"), _stream(x1))
     return dp1, dp2_rows, dx1, ddir_rows, dparams
+
+
+# ------------------------------------------------------------------ PointConv contraction
+def pointconv_contract_fwd(xyz, center, feats, idx, wt):
+    """-> A (B,S,16*(3+D)), c-major (the reference's .view(B,S,-1) of (B,S,C,16))."""
+    B, N, _ = xyz.shape
+    S, K = idx.shape[1], idx.shape[2]
+    D = feats.shape[2]
+    C = 3 + D
+    out = torch.empty((B, S, 16 * C), dtype=torch.float32, device=xyz.device)
+    f = torch.float32
+    _call("kdpc_pointconv_contract_fwd", B, N, S, K, D, _dev(xyz, f, "xyz"),
+          _dev(center, f, "center"), _dev(feats, f, "feats"), _dev(idx, torch.int32, "idx"),
+          _dev(wt, f, "wt"), _dev(out, f, "out"), _stream(xyz),
+          work=(4 * B * S * (K + K * C + 16 * K + 16 * C), 2.0 * B * S * K * C * 16))
+    return out
+
+
+def pointconv_contract_bwd(xyz, center, feats, idx, wt, dout):
+    """-> dg_rows (B,S,K,3+D), dwt (B,S,K,16), dcenter (B,S,3)."""
+    B, N, _ = xyz.shape
+    S, K = idx.shape[1], idx.shape[2]
+    D = feats.shape[2]
+    C = 3 + D
+    dev = xyz.device
+    f = torch.float32
+    dg_rows = torch.empty((B, S, K, C), dtype=f, device=dev)
+    dwt = torch.empty((B, S, K, 16), dtype=f, device=dev)
+    dcenter = torch.empty((B, S, 3), dtype=f, device=dev)
+    _call("kdpc_pointconv_contract_bwd", B, N, S, K, D, _dev(xyz, f, "xyz"),
+          _dev(center, f, "center"), _dev(feats, f, "feats"), _dev(idx, torch.int32, "idx"),
+          _dev(wt, f, "wt"), _dev(dout, f, "dout"), _dev(dg_rows, f, "dg_rows"),
+          _dev(dwt, f, "dwt"), _dev(dcenter, f, "dcenter"), _stream(xyz))
+    return dg_rows, dwt, dcenter

@@ -211,6 +211,42 @@ class WeightNet(nn.Module):
         return w
 
 
+class _PointConvContract(torch.autograd.Function):
+    """Fused gather + cat + per-point (C x K)(K x 16) contraction (csrc/pointconv.hip)."""
+
+    @staticmethod
+    def forward(ctx, xyz, center, feats, idx, wt):
+        ctx.save_for_backward(xyz, center, feats, idx, wt)
+        return _nat.pointconv_contract_fwd(xyz, center, feats, idx, wt)
+
+    @staticmethod
+    def backward(ctx, gout):
+        xyz, center, feats, idx, wt = ctx.saved_tensors
+        B, N, _ = xyz.shape
+        S, K = idx.shape[1], idx.shape[2]
+        C = 3 + feats.shape[2]
+        dg_rows, dwt, dcenter = _nat.pointconv_contract_bwd(xyz, center, feats, idx, wt,
+                                                             gout.contiguous())
+        dsum = _nat.group_rows_grad(dg_rows.view(B, S * K, C), _nat.csr_of(idx, N), B, N, C)
+        return dsum[..., :3], dcenter, dsum[..., 3:], None, dwt
+
+
+_FUSED_POINTCONV = True  # test seam: False forces the reference formulation
+
+
+def _pointconv_features(nsample, weightnet, xyz, center, points, idx):
+    """A (B,S,16C) for PointConv/PointConvD: xyz (B,N,3), center (B,S,3) point-major,
+    points (B,N,D) point-major, idx (B,S,K) int32."""
+    B, S, _ = center.shape
+    grouped_xyz_norm = index_points_group(xyz, idx) - center.view(B, S, 1, 3)
+    weights = weightnet.channel_last(grouped_xyz_norm)
+    if _FUSED_POINTCONV and weights.shape[-1] == 16:
+        return _PointConvContract.apply(xyz.contiguous(), center.contiguous(),
+                                        points.contiguous(), idx, weights.contiguous())
+    new_points = torch.cat([grouped_xyz_norm, index_points_group(points, idx)], dim=-1)
+    return _pointconv_contract(new_points, weights)
+
+
 def _pointconv_contract(new_points, weights):
     """(B,S,K,C) x (B,S,K,W) -> (B,S,C*W) with c-major flattening (reference :237,437)."""
     B, S = new_points.shape[:2]
@@ -242,11 +278,10 @@ class PointConv(_PointConvBase):
 
     def forward(self, xyz, points):
         """xyz (B,3,N), points (B,D,N) -> (B,out,N)."""
-        xyz = xyz.permute(0, 2, 1)
+        xyz = xyz.permute(0, 2, 1).contiguous()
         points = points.permute(0, 2, 1)
-        new_points, grouped_xyz_norm = group(self.nsample, xyz, points)
-        weights = self.weightnet.channel_last(grouped_xyz_norm)
-        return self._finish(_pointconv_contract(new_points, weights))
+        idx = knn_point(self.nsample, xyz, xyz)  # group(): self-kNN
+        return self._finish(_pointconv_features(self.nsample, self.weightnet, xyz, xyz, points, idx))
 
 
 class PointConvD(_PointConvBase):
@@ -270,9 +305,9 @@ class PointConvD(_PointConvBase):
         points = points.permute(0, 2, 1)
         fps_idx = pointnet2_utils.furthest_point_sample(xyz, self.npoint)
         new_xyz = index_points_gather(xyz, fps_idx)
-        new_points, grouped_xyz_norm = group_query(self.nsample, xyz, new_xyz, points)
-        weights = self.weightnet.channel_last(grouped_xyz_norm)
-        new_points = self._finish(_pointconv_contract(new_points, weights))
+        idx = knn_point(self.nsample, xyz, new_xyz)  # group_query()
+        new_points = self._finish(
+            _pointconv_features(self.nsample, self.weightnet, xyz, new_xyz, points, idx))
         return new_xyz.permute(0, 2, 1), new_points, fps_idx
 
 

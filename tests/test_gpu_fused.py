@@ -50,3 +50,34 @@ def test_cost_volume_fused_equals_unfused(din, dout, n1, n2, bsz):
     names = ["dx1", "dx2", "dp1", "dp2", "dWpos", "dbpos", "dW1", "db1"]
     for n, a, b in zip(names, grads[0], grads[1]):
         _scale_close(a.reshape(b.shape), b, rtol=2e-5, name=n)
+
+
+@pytest.mark.parametrize("down,d,n,bsz", [(True, 64, 2048, 2), (False, 128, 1024, 2),
+                                          (True, 512, 256, 1), (False, 5, 300, 3)])
+def test_pointconv_fused_equals_unfused(down, d, n, bsz):
+    import pointconv_util as P
+    import synthetic
+    torch.manual_seed(d + n)
+    layer = (P.PointConvD(n // 4, 16, d + 3, 64) if down else
+             P.PointConv(9, d + 3, 96, bn=True)).to(DEV).train()
+    xyz = torch.from_numpy(synthetic.ft3d_batch(bsz, n, seed=3)[0]).to(DEV).permute(0, 2, 1)
+    feats = torch.randn(bsz, d, n, device=DEV)
+    outs, grads = [], []
+    for fused in (True, False):
+        P._FUSED_POINTCONV = fused
+        try:
+            x = xyz.detach().clone().requires_grad_(True)
+            f = feats.detach().clone().requires_grad_(True)
+            layer.zero_grad()
+            o = layer(x, f)
+            o = o[1] if down else o
+            torch.manual_seed(9)
+            (o * torch.randn_like(o)).sum().backward()
+            outs.append(o.detach())
+            grads.append([x.grad, f.grad] + [p.grad for p in layer.parameters() if p.grad is not None])
+        finally:
+            P._FUSED_POINTCONV = True
+    _scale_close(outs[0], outs[1], name="out")
+    assert len(grads[0]) == len(grads[1])
+    for i, (a, b) in enumerate(zip(grads[0], grads[1])):
+        _scale_close(a, b, rtol=2e-5, name=f"grad{i}")

@@ -52,3 +52,32 @@ def test_opt_n_threads_matches_reference_rule():
     import pointnet2_oracle as O
     for n in (1, 2, 3, 63, 64, 100, 512, 1000, 1024, 4096, 8192, 100000):
         assert lib.kdpc_opt_n_threads(n) == O.opt_n_threads(n)
+
+
+def _declared_arity():
+    src = open(os.path.join(ROOT, "include", "kdpc.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b(kdpc_\w+)\s*\(([^;]*?)\)\s*;", src, flags=re.S):
+        params = [p for p in m.group(2).split(",") if p.strip() and p.strip() != "void"]
+        out[m.group(1)] = params
+    return out
+
+
+def test_ctypes_signatures_match_header():
+    """Every ctypes binding passes exactly the header's parameters, with matching kinds
+    (pointer / size_t / float / int)."""
+    decl = _declared_arity()
+    for name, argtypes in kdpc_native._SIGNATURES.items():
+        params = decl[name]
+        assert len(params) == len(argtypes), (name, len(params), len(argtypes))
+        for p, t in zip(params, argtypes):
+            p = p.strip()
+            if "*" in p:
+                assert t is ctypes.c_void_p, (name, p)
+            elif p.startswith("size_t"):
+                assert t is ctypes.c_size_t, (name, p)
+            elif p.startswith("float"):
+                assert t is ctypes.c_float, (name, p)
+            else:
+                assert t is ctypes.c_int, (name, p)
