@@ -104,16 +104,18 @@ class PointConvBidirection(nn.Module):
                     (1, self.cross1, self.flow1, self.deconv2_1),
                     (0, self.cross0, self.flow0, self.deconv1_0)]
         for lv, cross, flow_est, deconv in decoders:
-            # bidirectional features of the coarser level, upsampled for both clouds at once
-            f_up = deconv(self.upsample(pcs[lv], pcs[lv + 1], torch.cat([f1n, f2n], 0)))
+            # one 3-NN search per level pair serves all three upsamplings (both clouds'
+            # features, and pc1's flow and estimator features: its first B rows)
+            up_idx = self.upsample.neighbours(pcs[lv], pcs[lv + 1])
+            f_up = deconv(self.upsample(pcs[lv], pcs[lv + 1], torch.cat([f1n, f2n], 0), up_idx))
             up_feats.append(f_up)
             c_feat = torch.cat([feats[lv], f_up], dim=1)
             pc1_lv, pc2_lv = one(pcs[lv]), two(pcs[lv])
-            up_flow = self.upsample(pc1_lv, one(pcs[lv + 1]), self.scale * flow)
+            up_flow = self.upsample(pc1_lv, one(pcs[lv + 1]), self.scale * flow, up_idx[:B])
             pc2_warp = self.warping(pc1_lv, pc2_lv, up_flow)
             out = cross(pc1_lv, pc2_warp, one(c_feat), two(c_feat))
             f1n, f2n, cost = out
-            feat_up = self.upsample(pc1_lv, one(pcs[lv + 1]), feat_est)
+            feat_up = self.upsample(pc1_lv, one(pcs[lv + 1]), feat_est, up_idx[:B])
             new_feat1 = torch.cat([one(feats[lv]), feat_up], dim=1)
             feat_est, flow = flow_est(pc1_lv, new_feat1, cost, up_flow)
             flows.insert(0, flow)

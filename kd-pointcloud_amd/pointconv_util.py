@@ -276,11 +276,12 @@ class PointConv(_PointConvBase):
             self.bn_linear = nn.BatchNorm1d(out_channel)
         self.relu = nn.LeakyReLU(LEAKY_RATE, inplace=True) if use_leaky else nn.ReLU(inplace=True)
 
-    def forward(self, xyz, points):
-        """xyz (B,3,N), points (B,D,N) -> (B,out,N)."""
+    def forward(self, xyz, points, knn_idx=None):
+        """xyz (B,3,N), points (B,D,N) -> (B,out,N).  knn_idx: optional precomputed
+        self-kNN (B,N,nsample) of xyz (the estimator's two PointConvs share one)."""
         xyz = xyz.permute(0, 2, 1).contiguous()
         points = points.permute(0, 2, 1)
-        idx = knn_point(self.nsample, xyz, xyz)  # group(): self-kNN
+        idx = knn_point(self.nsample, xyz, xyz) if knn_idx is None else knn_idx
         return self._finish(_pointconv_features(self.nsample, self.weightnet, xyz, xyz, points, idx))
 
 
@@ -355,7 +356,7 @@ def _fusable(nsample, pos, mlp, act, din):
     return _nat.cost_volume_supported(din, conv.out_channels, nsample) and pos.bias is not None
 
 
-def _cost_volume(nsample, xyz1, xyz2, points1, points2, pos, mlp, act):
+def _cost_volume(nsample, xyz1, xyz2, points1, points2, pos, mlp, act, knn_idx=None):
     """Shared math of CrossLayerLight.cross (pointconv_util.py:1826-1850) and
     FlowEmbeddingLayer.forward (:1497-1517) on the point-major layout:
         h = act(P2[idx] + P1 + pos(x2[idx] - x1)); h = mlp(h); max over K.
@@ -365,7 +366,8 @@ def _cost_volume(nsample, xyz1, xyz2, points1, points2, pos, mlp, act):
     x2 = xyz2.permute(0, 2, 1).contiguous()
     p1 = points1.permute(0, 2, 1)
     p2 = points2.permute(0, 2, 1)
-    knn_idx = knn_point(nsample, x2, x1)
+    if knn_idx is None:
+        knn_idx = knn_point(nsample, x2, x1)
     din = p1.shape[-1]
     if _fusable(nsample, pos, mlp, act, din):
         conv = mlp[0].composed_module[0]
@@ -418,8 +420,9 @@ class CrossLayerLight(nn.Module):
             return self.relu(bn(x.reshape(-1, shp[-1], 1, 1)).view(shp))
         return f
 
-    def cross(self, xyz1, xyz2, points1, points2, pos, mlp, bn):
-        return _cost_volume(self.nsample, xyz1, xyz2, points1, points2, pos, mlp, self._act(bn))
+    def cross(self, xyz1, xyz2, points1, points2, pos, mlp, bn, knn_idx=None):
+        return _cost_volume(self.nsample, xyz1, xyz2, points1, points2, pos, mlp, self._act(bn),
+                            knn_idx)
 
     def forward(self, pc1, pc2, feat1, feat2):
         """Both directions of the first cost volume run as ONE batch of 2B (shared weights,
@@ -429,14 +432,19 @@ class CrossLayerLight(nn.Module):
         xb = torch.cat([pc2, pc1], 0)
         fa = torch.cat([feat1, feat2], 0)
         fb = torch.cat([feat2, feat1], 0)
+        # one kNN serves both directions, and its pc1 half is exactly the neighbour set of
+        # the refinement cross(pc1, pc2) below (the reference searches it twice)
+        idx = knn_point(self.nsample, xb.permute(0, 2, 1).contiguous(),
+                        xa.permute(0, 2, 1).contiguous())
         both = self.cross(xa, xb, conv1x1(fa, self.cross_t11), conv1x1(fb, self.cross_t22),
-                          self.pos1, self.mlp1, self.bn1)
+                          self.pos1, self.mlp1, self.bn1, idx)
         feat1_new, feat2_new = both[:B], both[B:]
         if self.mlp2 is False:
             return feat1_new, feat2_new
         feat1_new = conv1x1(feat1_new, self.cross_t1)
         feat2_new = conv1x1(feat2_new, self.cross_t2)
-        feat1_final = self.cross(pc1, pc2, feat1_new, feat2_new, self.pos2, self.mlp2, self.bn2)
+        feat1_final = self.cross(pc1, pc2, feat1_new, feat2_new, self.pos2, self.mlp2, self.bn2,
+                                 idx[:B])
         return feat1_new, feat2_new, feat1_final
 
 
@@ -543,12 +551,20 @@ class PointWarping(nn.Module):
 class UpsampleFlow(nn.Module):
     """Reference: pointconv_util.py:2153-2172 (3-NN inverse-distance interpolation)."""
 
-    def forward(self, xyz, sparse_xyz, sparse_flow):
+    @staticmethod
+    def neighbours(xyz, sparse_xyz):
+        """The 3-NN index this layer uses for (xyz, sparse_xyz); pass it back as knn_idx to
+        reuse it across upsamplings between the same two levels."""
+        return knn_point(3, sparse_xyz.permute(0, 2, 1).contiguous(),
+                         xyz.permute(0, 2, 1).contiguous())
+
+    def forward(self, xyz, sparse_xyz, sparse_flow, knn_idx=None):
         B, C, N = xyz.shape
         x = xyz.permute(0, 2, 1).contiguous()
         sx = sparse_xyz.permute(0, 2, 1).contiguous()
         sf = sparse_flow.permute(0, 2, 1)
-        knn_idx = knn_point(3, sx, x)
+        if knn_idx is None:
+            knn_idx = knn_point(3, sx, x)
         grouped_xyz_norm = index_points_group(sx, knn_idx) - x.view(B, N, 1, C)
         return _inverse_distance_blend(grouped_xyz_norm,
                                        index_points_group(sf, knn_idx)).permute(0, 2, 1)
@@ -576,8 +592,12 @@ class SceneFlowEstimatorResidual(nn.Module):
 
     def forward(self, xyz, feats, cost_volume, flow=None):
         new_points = torch.cat([feats, cost_volume], dim=1)
+        # every PointConv here groups the same cloud with the same K: one self-kNN
+        x = xyz.permute(0, 2, 1).contiguous()
+        knn_idx = knn_point(self.pointconv_list[0].nsample, x, x) if len(self.pointconv_list) else None
         for pointconv in self.pointconv_list:
-            new_points = pointconv(xyz, new_points)
+            same = pointconv.nsample == self.pointconv_list[0].nsample
+            new_points = pointconv(xyz, new_points, knn_idx if same else None)
         for conv in self.mlp_convs:
             new_points = conv(new_points)
         flow_local = conv1x1(new_points, self.fc).clamp(self.clamp[0], self.clamp[1])
