@@ -8,9 +8,9 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def _scale_close(a, b, rtol=1e-5, name=""):
+def _scale_close(a, b, rtol=1e-5, name="", floor=1e-6):
     a, b = a.detach().double().cpu(), b.detach().double().cpu()
-    tol = rtol * max(float(b.abs().max()), 1e-6)
+    tol = rtol * max(float(b.abs().max()), floor)
     err = float((a - b).abs().max())
     assert err <= tol, (name, err, tol)
 
@@ -79,5 +79,10 @@ def test_pointconv_fused_equals_unfused(down, d, n, bsz):
             P._FUSED_POINTCONV = True
     _scale_close(outs[0], outs[1], name="out")
     assert len(grads[0]) == len(grads[1])
+    # Gradients that cancel to ~0 (WeightNet BatchNorm biases in train mode: their upstream
+    # grads sum to nearly nothing over B*S*K terms) carry only summation-order noise, whose
+    # size follows the summands, not the result: floor their scale at 5% of the layer's
+    # largest gradient.
+    g_max = max(float(b.abs().max()) for b in grads[1])
     for i, (a, b) in enumerate(zip(grads[0], grads[1])):
-        _scale_close(a, b, rtol=2e-5, name=f"grad{i}")
+        _scale_close(a, b, rtol=2e-5, name=f"grad{i}", floor=0.05 * g_max)

@@ -118,7 +118,7 @@ def test_model_backward_matches_reference(model_run):
         if p.grad is None:
             continue
         got = float(p.grad.double().sum())
-        pre_bn = name.endswith("linear.bias") and "pointconv_list" in name
+        pre_bn = name.endswith(".linear.bias") and "pointconv_list" in name
         tol = 1e-5 if pre_bn else 1e-2 * ga + 1e-6
         assert abs(got - gs) <= tol, (name, got, gs, ga)
 
@@ -155,15 +155,18 @@ class _KnnReplay:
         return torch.from_numpy(np.stack(out)).to(xyz.device)
 
 
-def test_model_matches_reference_with_reference_neighbours(golden):
-    """Arithmetic parity of the whole teacher/student forward and the KD loss at 1e-5 when
-    both sides use the same neighbour indices (the reference's, replayed)."""
+class _KnnReplayReversed(_KnnReplay):
+    """The same replayed neighbours in reversed K-order: a pure summation-order change."""
+
+    def __call__(self, nsample, xyz, new_xyz):
+        return super().__call__(nsample, xyz, new_xyz).flip(-1).contiguous()
+
+
+def _replayed_run(g, replay):
     import loss_functions as L
     import pointconv_util as P
     from models_bid_pointconv import PointConvBidirection as Net
-    g = golden("model_knntrace_n2048.npz")
     pos1, pos2, flow = _t(g["pos1"]), _t(g["pos2"]), _t(g["flow"])
-    replay = _KnnReplay(g)
     prev = P.set_knn_override(replay)
     try:
         teacher = load_synthetic(Net(), seed=1).to(DEV).eval()
@@ -179,17 +182,38 @@ def test_model_matches_reference_with_reference_neighbours(golden):
     finally:
         P.set_knn_override(prev)
     assert replay.worst < 1e-5, replay.worst  # every call matched a recorded one
+    epe = torch.norm(flows[0].permute(0, 2, 1) - flow, dim=2).mean()
+    grads = {n: (None if p.grad is None else float(p.grad.double().sum()))
+             for n, p in student.named_parameters()}
+    return t_out, s_out, msl, kd, epe, grads
+
+
+def test_model_matches_reference_with_reference_neighbours(golden):
+    """Arithmetic parity of the whole teacher/student forward and the KD loss at 1e-5 when
+    both sides use the same neighbour indices (the reference's, replayed).
+
+    Gradients: per-parameter sums within 1e-4 of the parameter's |grad| sum, plus 3x the
+    summation-order noise measured on this GPU by re-running with every neighbour list in
+    reversed order (same neighbours, different fp32 summation order: it moves a few
+    WeightNet gradient sums by up to ~8e-4 of |grad|, round 1 profiles/round01_parity_report.txt);
+    that noise itself must stay below 2e-3 of |grad|."""
+    g = golden("model_knntrace_n2048.npz")
+    t_out, s_out, msl, kd, epe, grads = _replayed_run(g, _KnnReplay(g))
+    *_, grads_rev = _replayed_run(g, _KnnReplayReversed(g))
     for tag, out in (("t", t_out), ("s", s_out)):
         for i in range(4):
             _close(out[0][i], g[f"{tag}_flow{i}"], name=f"{tag} flow{i}")
         _close(out[5][3], g[f"{tag}_feat1_3"], name=f"{tag} feat1s[3]")
     _close(msl, g["msl"], name="multiScaleLoss")
     _close(kd, g["kd"], name="KD loss")
-    epe = torch.norm(flows[0].permute(0, 2, 1) - flow, dim=2).mean()
     _close(epe, g["s_epe3d"], name="EPE3D")
-    for (name, p), gs, ga in zip(student.named_parameters(), g["grad_sum"], g["grad_abs"]):
-        if p.grad is None:
+    for (name, got), gs, ga in zip(grads.items(), g["grad_sum"], g["grad_abs"]):
+        if got is None:
             continue
-        pre_bn = name.endswith("linear.bias") and "pointconv_list" in name
-        tol = 1e-5 if pre_bn else 1e-4 * ga + 1e-6
-        assert abs(float(p.grad.double().sum()) - gs) <= tol, (name, float(p.grad.sum()), gs)
+        pre_bn = name.endswith(".linear.bias") and "pointconv_list" in name
+        if pre_bn:  # zero up to rounding (train-mode BatchNorm follows)
+            assert abs(got - gs) <= 1e-5, (name, got, gs)
+            continue
+        noise = abs(got - grads_rev[name])
+        assert noise <= 2e-3 * ga + 1e-6, (name, "order noise", noise, ga)
+        assert abs(got - gs) <= 1e-4 * ga + 3 * noise + 1e-6, (name, got, gs, ga, noise)

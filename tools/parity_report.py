@@ -24,6 +24,31 @@ def rel(a, b):
     return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-12))
 
 
+class _Reversed(_KnnReplay):
+    """Same neighbours, K-order reversed: a pure summation-order perturbation."""
+
+    def __call__(self, nsample, xyz, new_xyz):
+        return super().__call__(nsample, xyz, new_xyz).flip(-1).contiguous()
+
+
+def grad_sums(g, knn):
+    t = lambda k: torch.from_numpy(np.ascontiguousarray(g[k])).to(DEV)  # noqa: E731
+    pos1, pos2, flow = t("pos1"), t("pos2"), t("flow")
+    prev = P.set_knn_override(knn)
+    try:
+        teacher = load_synthetic(Net(), seed=1).to(DEV).eval()
+        student = load_synthetic(Net(), seed=2).to(DEV).train()
+        with torch.no_grad():
+            to = teacher(pos1, pos2, pos1, pos2)
+        so = student(pos1, pos2, pos1, pos2)
+        kd = L.biDirection_loss_ht(so[0], so[5], so[6], so[1], so[2], flow, to[0], to[5], to[6],
+                                   to[1], to[2], 0.3, 0.8, layer=3)
+        kd.backward()
+    finally:
+        P.set_knn_override(prev)
+    return {n: float(p.grad.double().sum()) for n, p in student.named_parameters() if p.grad is not None}
+
+
 def run(g, replay):
     t = lambda k: torch.from_numpy(np.ascontiguousarray(g[k])).to(DEV)  # noqa: E731
     pos1, pos2, flow = t("pos1"), t("pos2"), t("flow")
@@ -37,6 +62,7 @@ def run(g, replay):
         msl = L.multiScaleLoss(so[0], flow, so[1])
         kd = L.biDirection_loss_ht(so[0], so[5], so[6], so[1], so[2], flow, to[0], to[5], to[6],
                                    to[1], to[2], 0.3, 0.8, layer=3)
+        kd.backward()
     finally:
         P.set_knn_override(prev)
     epe = torch.norm(so[0][0].permute(0, 2, 1) - flow, dim=2).mean()
@@ -45,6 +71,13 @@ def run(g, replay):
     out["kd"] = rel(kd, g["kd"])
     out["s_epe3d"] = rel(epe, g["s_epe3d"])
     out["s_epe3d_value"] = float(epe)
+    # gradient sums vs the reference's, relative to the parameter's |grad| sum; worst 4
+    worst = []
+    for (name, p), gs, ga in zip(student.named_parameters(), g["grad_sum"], g["grad_abs"]):
+        if p.grad is not None and not (name.endswith(".linear.bias") and "pointconv_list" in name):
+            worst.append((abs(float(p.grad.double().sum()) - gs) / max(ga, 1e-12), name))
+    worst.sort(reverse=True)
+    out["grad_worst"] = [f"{r:.1e} {n}" for r, n in worst[:4]]
     return out
 
 
@@ -54,4 +87,15 @@ if __name__ == "__main__":
     for name, g, rp in (("n4096 free kNN", g4, False), ("n2048 free kNN", g2, False),
                         ("n2048 replayed reference kNN", g2, True)):
         r = run(g, rp)
-        print(name, {k: (f"{v:.2e}" if "value" not in k else f"{v:.6f}") for k, v in r.items()})
+        print(name, {k: (v if k == "grad_worst" else f"{v:.2e}" if "value" not in k else f"{v:.6f}")
+                     for k, v in r.items()})
+    for fpc, fcv in ((False, True), (True, False), (False, False)):
+        P._FUSED_POINTCONV, P._FUSED_COST_VOLUME = fpc, fcv
+        r = run(g2, True)
+        print(f"n2048 replayed, fused pointconv={fpc} cost volume={fcv}", r["grad_worst"])
+    P._FUSED_POINTCONV = P._FUSED_COST_VOLUME = True
+    a, b = grad_sums(g2, _KnnReplay(g2)), grad_sums(g2, _Reversed(g2))
+    ga = dict(zip([n for n, _ in Net().named_parameters()], g2["grad_abs"]))
+    noise = sorted(((abs(a[n] - b[n]) / max(ga[n], 1e-12), n) for n in a
+                    if not (n.endswith(".linear.bias") and "pointconv_list" in n)), reverse=True)
+    print("GPU vs GPU, K-order reversed (summation-order noise):", [f"{r:.1e} {n}" for r, n in noise[:6]])
