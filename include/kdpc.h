@@ -168,6 +168,34 @@ int kdpc_pointconv_contract_bwd(int b, int n, int s, int k, int d, const float *
                                 const float *wt, const float *dout, float *dg_rows, float *dwt,
                                 float *dcenter, void *stream);
 
+/* ---- fused PointConv layer: gather + WeightNet contraction + Linear on the f32 matrix
+ *      cores (pointconv_util.py:217-258 PointConv, :401-446 PointConvD, both without the
+ *      BatchNorm/activation that follows the Linear) ------------------------------------ */
+
+/* 1 if (K, D, O) is handled: 1 <= K <= 16, O in {64, 128, 256}, WeightNet width 16. */
+int kdpc_pointconv_supported(int k, int d, int o);
+
+/* y (B,S,O) = A wl^T + bias,  A[b,s, c*16+w] = sum_k G[b,s,k,c] wt[b,s,k,w],
+ * G = cat(xyz[idx] - center, feats[idx]) (C = 3+D channels); A is never stored.
+ * xyz (B,N,3), center (B,S,3), feats (B,N,D), idx (B,S,K) int32, wt (B,S,K,16),
+ * wl (O, 16C) (nn.Linear weight), bias (O).  workspace: *_fwd_workspace_bytes (may be 0). */
+size_t kdpc_pointconv_fwd_workspace_bytes(int b, int s, int k, int d, int o);
+int kdpc_pointconv_fwd(int b, int n, int s, int k, int d, int o, const float *xyz,
+                       const float *center, const float *feats, const int *idx, const float *wt,
+                       const float *wl, const float *bias, float *y, void *workspace,
+                       size_t workspace_bytes, void *stream);
+
+/* Backward of kdpc_pointconv_fwd for dy (B,S,O): dxyz (B,N,3) (NULL to skip), dfeats (B,N,D),
+ * dcenter (B,S,3), dwt (B,S,K,16), dwl (O,16C), all overwritten (bias grad = column sums of
+ * dy, left to the caller).  offsets/perm: kdpc_csr_build of idx with key space N.
+ * Deterministic: every sum runs in a fixed order. */
+size_t kdpc_pointconv_bwd_workspace_bytes(int b, int s, int k, int d, int o);
+int kdpc_pointconv_bwd(int b, int n, int s, int k, int d, int o, const float *xyz,
+                       const float *center, const float *feats, const int *idx, const float *wt,
+                       const float *wl, const float *dy, const int *offsets, const int *perm,
+                       float *dxyz, float *dfeats, float *dcenter, float *dwt, float *dwl,
+                       void *workspace, size_t workspace_bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

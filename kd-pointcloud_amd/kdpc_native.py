@@ -38,8 +38,15 @@ _SIGNATURES = {
     "kdpc_pointconv_contract_bwd": [_c_int] * 5 + [_vp] * 10,
     "kdpc_cost_volume_bwd_workspace_bytes": [_c_int] * 4,
     "kdpc_cost_volume_bwd": [_c_int] * 6 + [_vp] * 16 + [_c_size, _vp, _vp],
+    "kdpc_pointconv_supported": [_c_int] * 3,
+    "kdpc_pointconv_fwd_workspace_bytes": [_c_int] * 5,
+    "kdpc_pointconv_fwd": [_c_int] * 6 + [_vp] * 9 + [_c_size, _vp],
+    "kdpc_pointconv_bwd_workspace_bytes": [_c_int] * 5,
+    "kdpc_pointconv_bwd": [_c_int] * 6 + [_vp] * 15 + [_c_size, _vp],
 }
-_RESTYPES = {"kdpc_csr_workspace_bytes": _c_size, "kdpc_cost_volume_bwd_workspace_bytes": _c_size}
+_RESTYPES = {"kdpc_csr_workspace_bytes": _c_size, "kdpc_cost_volume_bwd_workspace_bytes": _c_size,
+             "kdpc_pointconv_fwd_workspace_bytes": _c_size,
+             "kdpc_pointconv_bwd_workspace_bytes": _c_size}
 
 EXPORTED = tuple(_SIGNATURES)
 
@@ -375,3 +382,66 @@ def pointconv_contract_bwd(xyz, center, feats, idx, wt, dout):
           _dev(wt, f, "wt"), _dev(dout, f, "dout"), _dev(dg_rows, f, "dg_rows"),
           _dev(dwt, f, "dwt"), _dev(dcenter, f, "dcenter"), _stream(xyz))
     return dg_rows, dwt, dcenter
+
+
+# ------------------------------------------------------------------ fused PointConv layer
+def pointconv_supported(k, d, o):
+    return bool(load_library().kdpc_pointconv_supported(k, d, o))
+
+
+def _workspace(nbytes, device):
+    return torch.empty((max(int(nbytes), 1),), dtype=torch.uint8, device=device)
+
+
+def pointconv_fwd(xyz, center, feats, idx, wt, wl, bias):
+    """Fused gather + contraction + Linear: -> y (B,S,O) = A wl^T + bias, A never stored.
+    xyz (B,N,3), center (B,S,3), feats (B,N,D), idx (B,S,K) i32, wt (B,S,K,16), wl (O,16C)."""
+    B, N, _ = xyz.shape
+    S, K = idx.shape[1], idx.shape[2]
+    D = feats.shape[2]
+    O = wl.shape[0]
+    C = 3 + D
+    f = torch.float32
+    lib = load_library()
+    ws_bytes = lib.kdpc_pointconv_fwd_workspace_bytes(B, S, K, D, O)
+    ws = _workspace(ws_bytes, xyz.device)
+    y = torch.empty((B, S, O), dtype=f, device=xyz.device)
+    R = B * S
+    _call("kdpc_pointconv_fwd", B, N, S, K, D, O, _dev(xyz, f, "xyz"), _dev(center, f, "center"),
+          _dev(feats, f, "feats"), _dev(idx, torch.int32, "idx"), _dev(wt, f, "wt"),
+          _dev(wl, f, "wl"), _dev(bias, f, "bias"), _dev(y, f, "y"), ws.data_ptr(), ws_bytes,
+          _stream(xyz),
+          work=(4 * R * (K + K * C + 16 * K + O) + 4 * O * 16 * C,
+                2.0 * R * K * C * 16 + 2.0 * R * 16 * C * O))
+    return y
+
+
+def pointconv_bwd(xyz, center, feats, idx, wt, wl, dy, csr, need_xyz=True):
+    """Backward of pointconv_fwd for dy (B,S,O) -> (dxyz|None, dfeats, dcenter, dwt, dwl)."""
+    B, N, _ = xyz.shape
+    S, K = idx.shape[1], idx.shape[2]
+    D = feats.shape[2]
+    O = wl.shape[0]
+    C = 3 + D
+    f = torch.float32
+    dev = xyz.device
+    lib = load_library()
+    ws_bytes = lib.kdpc_pointconv_bwd_workspace_bytes(B, S, K, D, O)
+    if ws_bytes == 0:
+        raise KdpcError("kdpc_pointconv_bwd_workspace_bytes returned 0 (invalid sizes?)")
+    ws = _workspace(ws_bytes, dev)
+    dxyz = torch.empty((B, N, 3), dtype=f, device=dev) if need_xyz else None
+    dfeats = torch.empty((B, N, D), dtype=f, device=dev)
+    dcenter = torch.empty((B, S, 3), dtype=f, device=dev)
+    dwt = torch.empty((B, S, K, 16), dtype=f, device=dev)
+    dwl = torch.empty((O, 16 * C), dtype=f, device=dev)
+    R = B * S
+    _call("kdpc_pointconv_bwd", B, N, S, K, D, O, _dev(xyz, f, "xyz"), _dev(center, f, "center"),
+          _dev(feats, f, "feats"), _dev(idx, torch.int32, "idx"), _dev(wt, f, "wt"),
+          _dev(wl, f, "wl"), _dev(dy, f, "dy"), csr.offsets.data_ptr(), csr.perm.data_ptr(),
+          dxyz.data_ptr() if need_xyz else None, _dev(dfeats, f, "dfeats"),
+          _dev(dcenter, f, "dcenter"), _dev(dwt, f, "dwt"), _dev(dwl, f, "dwl"), ws.data_ptr(),
+          ws_bytes, _stream(xyz),
+          work=(4 * R * (2 * K * C + 32 * K + 2 * O) + 8 * O * 16 * C,
+                4.0 * R * K * C * 16 + 4.0 * R * 16 * C * O))
+    return dxyz, dfeats, dcenter, dwt, dwl

@@ -231,6 +231,26 @@ class _PointConvContract(torch.autograd.Function):
         return dsum[..., :3], dcenter, dsum[..., 3:], None, dwt
 
 
+class _PointConvLayer(torch.autograd.Function):
+    """Fused gather + contraction + Linear (csrc/pointconv_fused.hip): the (B,S,16C)
+    contraction A is never materialised."""
+
+    @staticmethod
+    def forward(ctx, xyz, center, feats, idx, wt, wl, bias):
+        ctx.save_for_backward(xyz, center, feats, idx, wt, wl)
+        return _nat.pointconv_fwd(xyz, center, feats, idx, wt, wl, bias)
+
+    @staticmethod
+    def backward(ctx, gy):
+        xyz, center, feats, idx, wt, wl = ctx.saved_tensors
+        gy = gy.contiguous()
+        dxyz, dfeats, dcenter, dwt, dwl = _nat.pointconv_bwd(
+            xyz, center, feats, idx, wt, wl, gy, _nat.csr_of(idx, xyz.shape[1]),
+            need_xyz=ctx.needs_input_grad[0])
+        dbias = gy.view(-1, gy.shape[-1]).sum(0) if ctx.needs_input_grad[6] else None
+        return (dxyz, dcenter if ctx.needs_input_grad[1] else None, dfeats, None, dwt, dwl, dbias)
+
+
 _FUSED_POINTCONV = True  # test seam: False forces the reference formulation
 
 
@@ -254,9 +274,24 @@ def _pointconv_contract(new_points, weights):
 
 
 class _PointConvBase(nn.Module):
+    def _linear_features(self, xyz, center, points, idx):
+        """Linear(16C->out)(A) as (B,S,out): the fused MFMA layer where the shape is
+        supported (K <= 16, out in {64,128,256}, WeightNet width 16), else the contraction
+        followed by the Linear GEMM."""
+        B, S, _ = center.shape
+        K, D = idx.shape[-1], points.shape[-1]
+        if _FUSED_POINTCONV and self.weightnet.mlp_convs[-1].out_channels == 16 \
+                and _nat.pointconv_supported(K, D, self.linear.out_features):
+            grouped_xyz_norm = index_points_group(xyz, idx) - center.view(B, S, 1, 3)
+            weights = self.weightnet.channel_last(grouped_xyz_norm)
+            return _PointConvLayer.apply(xyz.contiguous(), center.contiguous(),
+                                         points.contiguous(), idx, weights.contiguous(),
+                                         self.linear.weight, self.linear.bias)
+        a = _pointconv_features(self.nsample, self.weightnet, xyz, center, points, idx)
+        return linear(a, self.linear.weight, self.linear.bias)
+
     def _finish(self, new_points):
-        """Linear(16C->out) + optional BN1d + activation; (B,S,16C) -> (B,out,S)."""
-        new_points = linear(new_points, self.linear.weight, self.linear.bias)
+        """(B,S,out) -> optional BN1d + activation -> (B,out,S)."""
         new_points = new_points.permute(0, 2, 1)
         if self.bn:
             new_points = self.bn_linear(new_points)
@@ -282,7 +317,7 @@ class PointConv(_PointConvBase):
         xyz = xyz.permute(0, 2, 1).contiguous()
         points = points.permute(0, 2, 1)
         idx = knn_point(self.nsample, xyz, xyz) if knn_idx is None else knn_idx
-        return self._finish(_pointconv_features(self.nsample, self.weightnet, xyz, xyz, points, idx))
+        return self._finish(self._linear_features(xyz, xyz, points, idx))
 
 
 class PointConvD(_PointConvBase):
@@ -307,8 +342,7 @@ class PointConvD(_PointConvBase):
         fps_idx = pointnet2_utils.furthest_point_sample(xyz, self.npoint)
         new_xyz = index_points_gather(xyz, fps_idx)
         idx = knn_point(self.nsample, xyz, new_xyz)  # group_query()
-        new_points = self._finish(
-            _pointconv_features(self.nsample, self.weightnet, xyz, new_xyz, points, idx))
+        new_points = self._finish(self._linear_features(xyz, new_xyz, points, idx))
         return new_xyz.permute(0, 2, 1), new_points, fps_idx
 
 

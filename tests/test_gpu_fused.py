@@ -52,14 +52,19 @@ def test_cost_volume_fused_equals_unfused(din, dout, n1, n2, bsz):
         _scale_close(a.reshape(b.shape), b, rtol=2e-5, name=n)
 
 
-@pytest.mark.parametrize("down,d,n,bsz", [(True, 64, 2048, 2), (False, 128, 1024, 2),
-                                          (True, 512, 256, 1), (False, 5, 300, 3)])
-def test_pointconv_fused_equals_unfused(down, d, n, bsz):
+# (PointConvD?, D, N, B, out, bn): the model's level-1/2/4 and estimator shapes, odd sizes
+# (rows not a multiple of 32, channels not a multiple of 8), and an out width the fused
+# layer does not take (96: contraction kernel + Linear GEMM).
+@pytest.mark.parametrize("down,d,n,bsz,out,bn", [
+    (True, 64, 2048, 2, 64, False), (False, 128, 1024, 2, 128, True),
+    (True, 512, 256, 1, 256, False), (False, 61, 700, 2, 256, False),
+    (False, 125, 4096, 2, 128, True), (False, 5, 300, 3, 96, True)])
+def test_pointconv_fused_equals_unfused(down, d, n, bsz, out, bn):
     import pointconv_util as P
     import synthetic
     torch.manual_seed(d + n)
-    layer = (P.PointConvD(n // 4, 16, d + 3, 64) if down else
-             P.PointConv(9, d + 3, 96, bn=True)).to(DEV).train()
+    layer = (P.PointConvD(n // 4, 16, d + 3, out, bn=bn) if down else
+             P.PointConv(9, d + 3, out, bn=bn)).to(DEV).train()
     xyz = torch.from_numpy(synthetic.ft3d_batch(bsz, n, seed=3)[0]).to(DEV).permute(0, 2, 1)
     feats = torch.randn(bsz, d, n, device=DEV)
     outs, grads = [], []
@@ -79,10 +84,49 @@ def test_pointconv_fused_equals_unfused(down, d, n, bsz):
             P._FUSED_POINTCONV = True
     _scale_close(outs[0], outs[1], name="out")
     assert len(grads[0]) == len(grads[1])
-    # Gradients that cancel to ~0 (WeightNet BatchNorm biases in train mode: their upstream
-    # grads sum to nearly nothing over B*S*K terms) carry only summation-order noise, whose
-    # size follows the summands, not the result: floor their scale at 5% of the layer's
-    # largest gradient.
+    # Gradients that cancel to ~0 (the Linear bias feeding a train-mode BatchNorm: its
+    # upstream grads sum to nearly nothing over the B*S rows) carry only summation-order
+    # noise, whose size follows the summands, not the result: floor their scale at 5% of the
+    # layer's largest gradient.
     g_max = max(float(b.abs().max()) for b in grads[1])
     for i, (a, b) in enumerate(zip(grads[0], grads[1])):
         _scale_close(a, b, rtol=2e-5, name=f"grad{i}", floor=0.05 * g_max)
+
+
+@pytest.mark.parametrize("b,n,s,k,d,o", [(2, 700, 700, 9, 61, 256), (1, 256, 64, 16, 512, 256),
+                                         (3, 300, 300, 9, 5, 64), (2, 2048, 512, 16, 128, 128),
+                                         (1, 100, 37, 1, 0, 64)])
+def test_pointconv_layer_vs_fp64(b, n, s, k, d, o):
+    """The fused layer's C entry points against an fp64 torch evaluation of the reference
+    formulation (group -> cat -> matmul -> Linear) on the same inputs: forward and every
+    gradient within 1e-5 of the tensor scale."""
+    import kdpc_native as nat
+    g = torch.Generator(device="cpu").manual_seed(b * 1000 + n + k + d + o)
+    r = lambda *sh: torch.randn(*sh, generator=g).to(DEV)  # noqa: E731
+    xyz = r(b, n, 3)
+    center = xyz[:, :s].contiguous()
+    feats = r(b, n, d)
+    idx = torch.randint(0, n, (b, s, k), generator=g, dtype=torch.int32).to(DEV)
+    wt = r(b, s, k, 16)
+    c = 3 + d
+    wl = r(o, 16 * c) / (16 * c) ** 0.5
+    bias = r(o)
+    dy = r(b, s, o)
+    y = nat.pointconv_fwd(xyz, center, feats, idx, wt, wl, bias)
+    dxyz, dfeats, dcenter, dwt, dwl = nat.pointconv_bwd(xyz, center, feats, idx, wt, wl, dy,
+                                                        nat.csr_of(idx, n))
+    # fp64 reference with autograd
+    X, Cn, F, Wt, Wl, Bb = (t.double().requires_grad_(True) for t in (xyz, center, feats, wt, wl, bias))
+    il = idx.long()
+    bi = torch.arange(b, device=DEV).view(b, 1, 1)
+    G = torch.cat([X[bi, il] - Cn.unsqueeze(2), F[bi, il]], dim=-1)       # (B,S,K,C)
+    A = torch.matmul(G.transpose(2, 3), Wt).reshape(b, s, -1)              # (B,S,16C)
+    Y = A @ Wl.t() + Bb
+    Y.backward(dy.double())
+    _scale_close(y, Y, name="y")
+    _scale_close(dxyz, X.grad, name="dxyz")
+    if d:
+        _scale_close(dfeats, F.grad, name="dfeats")
+    _scale_close(dcenter, Cn.grad, name="dcenter")
+    _scale_close(dwt, Wt.grad, name="dwt")
+    _scale_close(dwl, Wl.grad, name="dwl")
