@@ -6,21 +6,23 @@
 //   y[r, o]  = sum_j A[r,j] * wl[o,j] + bias[o]
 //
 // The reference materialises A (R x 16C: 549 MB for the level-0 scene-flow estimator at
-// batch 8) and runs the Linear as a separate GEMM.  Here a workgroup owns 32 rows and walks
-// the channels in chunks of 8 (128 columns of A): it gathers the chunk's neighbour
-// channels into LDS, forms the 32 x 128 block of A on the VALU (K fmas per element, the
-// WeightNet weights held in registers), and multiplies it into the 32 x O output tile with
-// v_mfma_f32_32x32x2_f32 (exact f32 products, f32 accumulation; the Linear weight streams
-// from L2).  A never touches HBM.
+// batch 8) and runs the Linear as a separate GEMM.  Here a workgroup owns a tile of 32 or
+// 64 rows and walks the channels in chunks of 8 (128 columns of A): the chunk's neighbour
+// channels are gathered into LDS (software-pipelined: the next chunk's gather is in flight
+// in registers while this chunk computes), the tile's block of A is formed on the VALU (K
+// fmas per element, WeightNet weights held in registers), and multiplied into the output
+// tile with v_mfma_f32_32x32x2_f32 (exact f32 products, f32 accumulation; the Linear
+// weight streams from L2, one block ahead).  A never touches HBM.
 //
-// Backward (two kernels + deterministic reductions, no float atomics):
+// Backward (no float atomics; every sum in a fixed order):
 //   data:   dA = dy wl per chunk (MFMA), then per (row, neighbour) on the VALU
-//             dG[r,k,c]  = sum_w dA[r,c*16+w] wt[r,k,w]   -> chunk-major rows, summed per
-//                                                          point through the kNN CSR
+//             dG[r,k,c]  = sum_w dA[r,c*16+w] wt[r,k,w]   -> rows [R*K][C8], summed per point
+//                                                          through the kNN CSR
 //             dwt[r,k,w] = sum_c dA[r,c*16+w] G[r,k,c]
 //             dcenter[r] = -sum_k dG[r,k,0:3]
-//   weight: dwl[o, j] = sum_r dy[r,o] A[r,j]  with A recomputed per (chunk, row split),
-//           per-split partial tiles summed in split order.
+//   weight: dwl[o, j] = sum_r dy[r,o] A[r,j] with A recomputed per (chunk, row split) and
+//           the splits' partial tiles summed in split order.  Splits are placed so that
+//           every chunk of one split runs on the same XCD (they share its dy / wt rows in L2).
 //
 // MFMA operand mapping (v_mfma_f32_32x32x2_f32, wave64): lane l supplies A[l&31][l>>5] and
 // B[l>>5][l&31]; the result register i of lane l is D[(i&3) + 8*(i>>2) + 4*(l>>5)][l&31].
@@ -38,33 +40,28 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kW = 16;              // WeightNet width (weightnet=16 in every model layer)
-constexpr int kTM = 32;             // rows per tile (one MFMA M tile)
 constexpr int kCC = 8;              // channels per chunk
 constexpr int kNC = kCC * kW;       // A columns per chunk (128)
 constexpr int kKMax = 16;           // neighbours per row supported
-constexpr int kThreads = 256;
-constexpr int kBlk = kTM * 4 + 16;  // floats per 4-column block of an MFMA-A-layout tile
-constexpr int kTS = kTM + 4;        // row stride of transposed (inner = row) tiles
+constexpr int kBlk = 32 * 4 + 16;   // floats per 4-column block of a 32-row MFMA-A tile
+constexpr int kTS = 32 + 4;         // row stride of transposed (inner = row) 32-row tiles
 constexpr int kDaS = kNC + 4;       // row stride of the dA chunk
 constexpr int kTargetWG = 512;      // grid size the split heuristics aim for
 
 struct Geo {
-  int n, s, k, d, c, r, nch;  // c = 3 + d, r = B*S rows, nch = ceil(c / kCC)
-  const float* xyz;           // (B,N,3)
-  const float* center;        // (B,S,3)
-  const float* feats;         // (B,N,D)
-  const int* idx;             // (B,S,K)
+  int n, s, k, d, c, r, nch, c8;  // c = 3 + d, r = B*S rows, nch = ceil(c/8), c8 = 8*nch
+  int bn;                         // B*N points
+  const float* xyz;               // (B,N,3)
+  const float* center;            // (B,S,3)
+  const float* feats;             // (B,N,D)
+  const int* idx;                 // (B,S,K)
 };
 
-__device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
-}
-
 __device__ __forceinline__ f32x16 mfma4(float4 a, float4 b, f32x16 c) {
-  c = mfma(a.x, b.x, c);
-  c = mfma(a.y, b.y, c);
-  c = mfma(a.z, b.z, c);
-  return mfma(a.w, b.w, c);
+  c = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, c, 0, 0, 0);
 }
 
 __device__ __forceinline__ f32x16 zero16() {
@@ -74,178 +71,233 @@ __device__ __forceinline__ f32x16 zero16() {
   return z;
 }
 
-// per-tile row metadata: batch offset (b*N, -1 for rows past the end) and center
-__device__ __forceinline__ void load_rows(const Geo& g, int row0, int* rbase, float* rctr) {
-  const int t = threadIdx.x;
-  if (t < kTM) {
-    const int row = row0 + t;
-    const bool ok = row < g.r;
-    rbase[t] = ok ? (row / g.s) * g.n : -1;
-    rctr[t * 3 + 0] = ok ? g.center[(long long)row * 3 + 0] : 0.f;
-    rctr[t * 3 + 1] = ok ? g.center[(long long)row * 3 + 1] : 0.f;
-    rctr[t * 3 + 2] = ok ? g.center[(long long)row * 3 + 2] : 0.f;
-  }
+// global row of neighbour kk of row `row` (b*N + idx), -1 past the last row
+__device__ __forceinline__ int nbr_of(const Geo& g, int row, int kk) {
+  if (row >= g.r) return -1;
+  return (row / g.s) * g.n + g.idx[(long long)row * g.k + kk];
 }
 
-// G[row, k, cg] for neighbour point j of a batch whose first point is `base`
-__device__ __forceinline__ float g_value(const Geo& g, int base, const float* ctr, int j, int cg) {
-  if (cg < 3) return g.xyz[(long long)(base + j) * 3 + cg] - ctr[cg];
-  if (cg < g.c) return g.feats[(long long)(base + j) * g.d + (cg - 3)];
+// Gathers go through buffer loads: 32-bit byte offsets (one VGPR per in-flight slot instead
+// of a 64-bit address) and hardware bounds checks (an offset past the buffer reads 0).
+constexpr unsigned kOOB = 0x80000000u;  // byte offset that is always out of range
+
+struct Srcs {
+  __amdgpu_buffer_rsrc_t xyz, center, feats;
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, long long nfloats) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, (int)(nfloats * 4),
+                                           0x00020000);
+}
+
+__device__ __forceinline__ Srcs srcs_of(const Geo& g) {
+  Srcs s;
+  s.xyz = rsrc(g.xyz, (long long)g.bn * 3);
+  s.center = rsrc(g.center, (long long)g.r * 3);
+  s.feats = rsrc(g.feats, (long long)g.bn * g.d);
+  return s;
+}
+
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, unsigned byte_off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)byte_off, 0, 0));
+}
+
+// byte offset of neighbour nb's feature row (kOOB for none)
+__device__ __forceinline__ unsigned feat_off(const Geo& g, int nb) {
+  return nb < 0 ? kOOB : (unsigned)nb * (unsigned)g.d * 4u;
+}
+
+// G value of channel cg for neighbour row nb of row `row`
+__device__ __forceinline__ float g_fetch(const Geo& g, const Srcs& s, int nb, int row, int cg) {
+  if (nb < 0) return 0.f;
+  if (cg < 3)
+    return bload(s.xyz, ((unsigned)nb * 3u + cg) * 4u) - bload(s.center, ((unsigned)row * 3u + cg) * 4u);
+  if (cg < g.c) return bload(s.feats, (unsigned)nb * (unsigned)g.d * 4u + (unsigned)(cg - 3) * 4u);
   return 0.f;
 }
 
-// gl[(r*K + k)*kCC + c] = G[row0+r, k, c0+c]  (0 past the last row / channel)
-__device__ __forceinline__ void stage_g(const Geo& g, int row0, int c0, const int* rbase,
-                                        const float* rctr, float* gl) {
-  const int c = threadIdx.x & (kCC - 1);
-  const int total = kTM * g.k;
-  for (int rk = threadIdx.x / kCC; rk < total; rk += kThreads / kCC) {
-    const int r = rk / g.k;
-    const int kk = rk - r * g.k;
-    const int base = rbase[r];
-    float v = 0.f;
-    if (base >= 0) {
-      const int j = g.idx[(long long)(row0 + r) * g.k + kk];
-      v = g_value(g, base, rctr + r * 3, j, c0 + c);
-    }
-    gl[rk * kCC + c] = v;
-  }
-}
-
-// builder thread (w = t & 15, rows rr = t >> 4 and rr + 16): its WeightNet weights
-__device__ __forceinline__ void load_wt(const Geo& g, const float* __restrict__ wt, int row0,
-                                        float (&wr)[2][kKMax]) {
-  const int w = threadIdx.x & (kW - 1), rr = threadIdx.x >> 4;
+// acc[c] = sum_k G[r,k,c] wk[k] over the tile's LDS gather (ascending k, one fma each)
+template <int KM>
+__device__ __forceinline__ void build_row(const float* gl, int r, int k_n, const float* wk,
+                                          float (&a)[kCC]) {
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int row = row0 + rr + 16 * q;
+  for (int c = 0; c < kCC; ++c) a[c] = 0.f;
 #pragma unroll
-    for (int k = 0; k < kKMax; ++k)
-      wr[q][k] = (row < g.r && k < g.k) ? wt[((long long)row * g.k + k) * kW + w] : 0.f;
-  }
-}
-
-// a[q][cl] = A[row0 + rr + 16q, (c0 + cl)*16 + w] = sum_k G * wt  (ascending k, one fma each)
-__device__ __forceinline__ void build_a(const Geo& g, const float* gl, const float (&wr)[2][kKMax],
-                                        float (&a)[2][kCC]) {
-  const int rr = threadIdx.x >> 4;
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int r = rr + 16 * q;
-#pragma unroll
-    for (int c = 0; c < kCC; ++c) a[q][c] = 0.f;
-#pragma unroll
-    for (int k = 0; k < kKMax; ++k) {
-      if (k < g.k) {
-        const float4 lo = *reinterpret_cast<const float4*>(gl + (r * g.k + k) * kCC);
-        const float4 hi = *reinterpret_cast<const float4*>(gl + (r * g.k + k) * kCC + 4);
-        const float wk = wr[q][k];
-        a[q][0] = __builtin_fmaf(lo.x, wk, a[q][0]);
-        a[q][1] = __builtin_fmaf(lo.y, wk, a[q][1]);
-        a[q][2] = __builtin_fmaf(lo.z, wk, a[q][2]);
-        a[q][3] = __builtin_fmaf(lo.w, wk, a[q][3]);
-        a[q][4] = __builtin_fmaf(hi.x, wk, a[q][4]);
-        a[q][5] = __builtin_fmaf(hi.y, wk, a[q][5]);
-        a[q][6] = __builtin_fmaf(hi.z, wk, a[q][6]);
-        a[q][7] = __builtin_fmaf(hi.w, wk, a[q][7]);
-      }
+  for (int k = 0; k < KM; ++k) {
+    if (k < k_n) {
+      const float4 lo = *reinterpret_cast<const float4*>(gl + (r * k_n + k) * kCC);
+      const float4 hi = *reinterpret_cast<const float4*>(gl + (r * k_n + k) * kCC + 4);
+      const float w = wk[k];
+      a[0] = __builtin_fmaf(lo.x, w, a[0]);
+      a[1] = __builtin_fmaf(lo.y, w, a[1]);
+      a[2] = __builtin_fmaf(lo.z, w, a[2]);
+      a[3] = __builtin_fmaf(lo.w, w, a[3]);
+      a[4] = __builtin_fmaf(hi.x, w, a[4]);
+      a[5] = __builtin_fmaf(hi.y, w, a[5]);
+      a[6] = __builtin_fmaf(hi.z, w, a[6]);
+      a[7] = __builtin_fmaf(hi.w, w, a[7]);
     }
   }
 }
 
 // ------------------------------------------------------------------------------ forward
-// grid (row tiles, channel splits).  A split > 1 writes a partial tile to slab[split].
-template <int O>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2)))
+// grid (row tiles, channel splits); a split > 1 writes a partial tile to slab[split].
+// 256 threads.  Tile = 32*MT rows; output tiles 32x32 spread over the 4 waves.
+template <int O, int KM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 void pc_fwd_kernel(Geo g, const float* __restrict__ wt, const float* __restrict__ wl,
                    const float* __restrict__ bias, float* __restrict__ y,
                    float* __restrict__ slab, int chunks_per_split) {
-  __shared__ int rbase[kTM];
-  __shared__ float rctr[kTM * 3];
-  __shared__ __attribute__((aligned(16))) float gl[kTM * kKMax * kCC];
-  __shared__ __attribute__((aligned(16))) float al[(kNC / 4) * kBlk];
-  constexpr int NT = O / 32;                  // output column tiles
-  constexpr int TPW = NT >= 4 ? NT / 4 : 1;   // tiles per wave
-  constexpr int KG = NT >= 4 ? 1 : 4 / NT;    // waves splitting a chunk's inner index
-  constexpr int GB = 16 / KG;                 // 8-column blocks per wave and chunk
-  const int row0 = blockIdx.x * kTM;
+  constexpr int MT = KM <= 9 ? 2 : 1;
+  constexpr int TM = 32 * MT;
+  constexpr int NT = O / 32;
+  constexpr bool SPLIT_M = (MT == 2 && NT < 4);   // O = 64: waves split the two row tiles
+  constexpr int KG = (MT * NT < 4) ? 4 / (MT * NT) : 1;  // O = 64, 32 rows: waves split the
+                                                           // chunk's inner index in KG groups
+  constexpr int MPW = (MT == 2 && !SPLIT_M) ? 2 : 1;
+  constexpr int NPW = KG > 1 ? 1 : (MT * NT / 4) / MPW;
+  constexpr int RPT = TM / 16;                    // builder rows per thread
+  constexpr int GS = TM * KM / 32;                // gather slots per thread
+  __shared__ __attribute__((aligned(16))) float gl[TM * KM * kCC];
+  __shared__ __attribute__((aligned(16))) float al[MT][(kNC / 4) * kBlk];
+
+  const int row0 = blockIdx.x * TM;
   const int split = blockIdx.y;
   const int ch0 = split * chunks_per_split;
   const int ch1 = min(g.nch, ch0 + chunks_per_split);
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, half = lane >> 5, l32 = lane & 31;
-  const int w = t & (kW - 1), rr = t >> 4;
-  const int tile0 = (wv % (4 / KG)) * TPW;
-  const int kgrp = wv / (4 / KG);
+  const int w = t & (kW - 1), rr = t >> 4, cs = t & (kCC - 1);
+  const int m0 = SPLIT_M ? (wv >> 1) : 0;
+  const int n0 = SPLIT_M ? (wv & 1) : (KG > 1 ? wv % (4 / KG) : wv * NPW);
+  const int kgrp = KG > 1 ? wv / (4 / KG) : 0;
+  constexpr int GB = 16 / KG;  // 8-column blocks per wave and chunk
   const long long c16 = (long long)g.c * kW;
+  const int tk = TM * g.k;
 
-  load_rows(g, row0, rbase, rctr);
-  float wr[2][kKMax];
-  load_wt(g, wt, row0, wr);
-  f32x16 acc[TPW];
+  float wr[RPT][KM];
 #pragma unroll
-  for (int i = 0; i < TPW; ++i) acc[i] = zero16();
+  for (int q = 0; q < RPT; ++q) {
+    const int row = row0 + rr + 16 * q;
+#pragma unroll
+    for (int k = 0; k < KM; ++k)
+      wr[q][k] = (row < g.r && k < g.k) ? wt[((long long)row * g.k + k) * kW + w] : 0.f;
+  }
+  const Srcs src = srcs_of(g);
+  unsigned nbf[GS];  // byte offsets of the slots' neighbour feature rows
+  float gr[GS];
+#pragma unroll
+  for (int i = 0; i < GS; ++i) {
+    const int rk = (t >> 3) + 32 * i;
+    const int r = rk / g.k;
+    const int nb = rk < tk ? nbr_of(g, row0 + r, rk - r * g.k) : -1;
+    nbf[i] = feat_off(g, nb);
+    gr[i] = g_fetch(g, src, nb, row0 + r, ch0 * kCC + cs);
+  }
+  f32x16 acc[MPW][NPW];
+#pragma unroll
+  for (int i = 0; i < MPW; ++i)
+#pragma unroll
+    for (int j = 0; j < NPW; ++j) acc[i][j] = zero16();
 
   for (int ch = ch0; ch < ch1; ++ch) {
     const int c0 = ch * kCC;
-    __syncthreads();  // row metadata ready / previous chunk's MFMAs done with `al`
-    stage_g(g, row0, c0, rbase, rctr, gl);
+    __syncthreads();  // previous chunk's MFMAs are done with al; gl is free
+#pragma unroll
+    for (int i = 0; i < GS; ++i) {
+      const int rk = (t >> 3) + 32 * i;
+      if (rk < tk) gl[rk * kCC + cs] = gr[i];
+    }
     __syncthreads();
-    float a[2][kCC];
-    build_a(g, gl, wr, a);
+    if (ch + 1 < ch1) {  // next chunk's gather (feature channels only), in flight during
+                         // build + MFMA
+      const int cg = c0 + kCC + cs;
+      const unsigned co = (unsigned)(cg - 3) * 4u;
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
+      for (int i = 0; i < GS; ++i) gr[i] = cg < g.c ? bload(src.feats, nbf[i] + co) : 0.f;
+    }
 #pragma unroll
-      for (int cl = 0; cl < kCC; ++cl) {
-        const int col = cl * kW + w;
-        al[(col >> 2) * kBlk + (rr + 16 * q) * 4 + (col & 3)] = a[q][cl];
+    for (int q = 0; q < RPT; ++q) {
+      const int r = rr + 16 * q;
+      float a[kCC];
+      build_row<KM>(gl, r, g.k, wr[q], a);
+      float* at = al[r >> 5] + (r & 31) * 4;
+#pragma unroll
+      for (int c = 0; c < kCC; ++c) {
+        const int col = c * kW + w;
+        at[(col >> 2) * kBlk + (col & 3)] = a[c];
       }
+      __builtin_amdgcn_sched_barrier(0);  // keep the rows' LDS reads from piling up
+    }
     __syncthreads();
-#pragma unroll 4
-    for (int gb = kgrp * GB; gb < (kgrp + 1) * GB; ++gb) {
-      const float4 av = *reinterpret_cast<const float4*>(al + (2 * gb + half) * kBlk + l32 * 4);
-      const int col = c0 * kW + 8 * gb + 4 * half;  // this lane's 4 inner indices
-      const bool ok = (col >> 4) < g.c;
+    // 16 blocks of 8 inner indices; the Linear weight is loaded one block ahead
+    const float* wrow[NPW];
 #pragma unroll
-      for (int i = 0; i < TPW; ++i) {
-        const int n = (tile0 + i) * 32 + l32;
-        const float4 bv = ok ? *reinterpret_cast<const float4*>(wl + n * c16 + col)
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
-        acc[i] = mfma4(av, bv, acc[i]);
+    for (int j = 0; j < NPW; ++j) wrow[j] = wl + ((long long)((n0 + j) * 32 + l32)) * c16;
+    float4 bcur[NPW], bnxt[NPW];
+    const int gbeg = kgrp * GB;
+#pragma unroll
+    for (int j = 0; j < NPW; ++j) {
+      const bool ok0 = c0 + (gbeg >> 1) < g.c;
+      bcur[j] = ok0 ? *reinterpret_cast<const float4*>(wrow[j] + c0 * kW + 8 * gbeg + 4 * half)
+                    : make_float4(0.f, 0.f, 0.f, 0.f);
+      bnxt[j] = bcur[j];
+    }
+#pragma unroll 2
+    for (int gi = 0; gi < GB; ++gi) {
+      const int gb = gbeg + gi;
+      if (gi + 1 < GB) {
+        const int col = c0 * kW + 8 * (gb + 1) + 4 * half;
+        const bool ok = c0 + ((gb + 1) >> 1) < g.c;
+#pragma unroll
+        for (int j = 0; j < NPW; ++j)
+          bnxt[j] = ok ? *reinterpret_cast<const float4*>(wrow[j] + col)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
       }
+      float4 av[MPW];
+#pragma unroll
+      for (int i = 0; i < MPW; ++i)
+        av[i] = *reinterpret_cast<const float4*>(al[m0 + i] + (2 * gb + half) * kBlk + l32 * 4);
+#pragma unroll
+      for (int i = 0; i < MPW; ++i)
+#pragma unroll
+        for (int j = 0; j < NPW; ++j) acc[i][j] = mfma4(av[i], bcur[j], acc[i][j]);
+#pragma unroll
+      for (int j = 0; j < NPW; ++j) bcur[j] = bnxt[j];
     }
   }
 
-  if (KG > 1) {  // fold the inner-index groups (fixed order: group 0 + group 1 + ...)
+  if (KG > 1) {  // fold the inner-index groups in group order
     __syncthreads();
-    float* red = gl;  // 16 KB: (KG-1) * (4/KG) waves * 16 regs * 64 lanes floats
+    float* red = gl;  // (KG-1) * (4/KG) waves x 16 registers x 64 lanes
     if (kgrp > 0) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i)
-        red[(((kgrp - 1) * (4 / KG) + (wv % (4 / KG))) * 16 + i) * 64 + lane] = acc[0][i];
+      for (int e = 0; e < 16; ++e)
+        red[(((kgrp - 1) * (4 / KG) + n0) * 16 + e) * 64 + lane] = acc[0][0][e];
     }
     __syncthreads();
-    if (kgrp == 0) {
-      for (int k2 = 1; k2 < KG; ++k2)
+    if (kgrp > 0) return;
+    for (int k2 = 1; k2 < KG; ++k2)
 #pragma unroll
-        for (int i = 0; i < 16; ++i)
-          acc[0][i] = __fadd_rn(acc[0][i], red[(((k2 - 1) * (4 / KG) + wv) * 16 + i) * 64 + lane]);
-    }
+      for (int e = 0; e < 16; ++e)
+        acc[0][0][e] = __fadd_rn(acc[0][0][e], red[(((k2 - 1) * (4 / KG) + n0) * 16 + e) * 64 + lane]);
   }
-  if (kgrp != 0) return;
+
 #pragma unroll
-  for (int i = 0; i < TPW; ++i) {
-    const int n = (tile0 + i) * 32 + l32;
+  for (int j = 0; j < NPW; ++j) {
+    const int n = (n0 + j) * 32 + l32;
     const float bn = slab ? 0.f : bias[n];
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int row = row0 + (e & 3) + 8 * (e >> 2) + 4 * half;
-      if (row < g.r) {
-        if (slab)
-          slab[((long long)split * g.r + row) * O + n] = acc[i][e];
-        else
-          y[(long long)row * O + n] = __fadd_rn(acc[i][e], bn);
+    for (int i = 0; i < MPW; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = row0 + (m0 + i) * 32 + (e & 3) + 8 * (e >> 2) + 4 * half;
+        if (row < g.r) {
+          if (slab)
+            slab[((long long)split * g.r + row) * O + n] = acc[i][j][e];
+          else
+            y[(long long)row * O + n] = __fadd_rn(acc[i][j][e], bn);
+        }
       }
-    }
   }
 }
 
@@ -264,48 +316,46 @@ __global__ __launch_bounds__(256) void pc_slab_sum_kernel(int nslabs, long long 
 }
 
 // -------------------------------------------------------------------- backward: data
-// grid (row tiles, channel splits).  dgc: chunk-major dG rows [nch][R*K][kCC].
-template <int O>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2)))
+// grid (32-row tiles, channel splits), 256 threads; each thread owns (row, neighbour)
+// pairs t and t+256.  dgr: dG rows [R*K][C8].
+template <int O, int KM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float* __restrict__ wl,
-                        const float* __restrict__ dy, float* __restrict__ dgc,
+                        const float* __restrict__ dy, float* __restrict__ dgr,
                         float* __restrict__ dwt, float* __restrict__ dcenter,
                         int chunks_per_split) {
-  __shared__ int rbase[kTM];
-  __shared__ float rctr[kTM * 3];
+  constexpr int PP = (32 * KM + 255) / 256;  // pairs per thread
   __shared__ __attribute__((aligned(16))) float dyl[(O / 4) * kBlk];
-  __shared__ __attribute__((aligned(16))) float dal[kTM * kDaS];
-  __shared__ float dcl[kTM * kKMax * 3];
-  const int row0 = blockIdx.x * kTM;
+  __shared__ __attribute__((aligned(16))) float dal[32 * kDaS];
+  __shared__ float dcl[32 * KM * 3];
+  const int row0 = blockIdx.x * 32;
   const int split = blockIdx.y;
   const int ch0 = split * chunks_per_split;
   const int ch1 = min(g.nch, ch0 + chunks_per_split);
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, half = lane >> 5, l32 = lane & 31;
   const long long c16 = (long long)g.c * kW;
   const long long rk_total = (long long)g.r * g.k;
+  const Srcs src = srcs_of(g);
 
-  load_rows(g, row0, rbase, rctr);
-  for (int e = t; e < kTM * O; e += kThreads) {
+  for (int e = t; e < 32 * O; e += 256) {
     const int r = e / O, o = e % O;
     const int row = row0 + r;
     dyl[(o >> 2) * kBlk + r * 4 + (o & 3)] = row < g.r ? dy[(long long)row * O + o] : 0.f;
   }
-  // (row, neighbour) pairs owned by this thread: p = t and t + 256
-  const int P = kTM * g.k;
-  float wp[2][kW], dw[2][kW];
-  int pr[2], pk[2];
-  bool pv[2];
+  float wp[PP][kW], dw[PP][kW];
+  int pr[PP], pk[PP], pn[PP];
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int p = t + kThreads * q;
+  for (int q = 0; q < PP; ++q) {
+    const int p = t + 256 * q;
     pr[q] = p / g.k;
     pk[q] = p - pr[q] * g.k;
-    pv[q] = p < P && row0 + pr[q] < g.r;
+    const bool ok = p < 32 * g.k && row0 + pr[q] < g.r;
+    pn[q] = ok ? nbr_of(g, row0 + pr[q], pk[q]) : -1;
     const long long pos = (long long)(row0 + pr[q]) * g.k + pk[q];
 #pragma unroll
     for (int v = 0; v < kW / 4; ++v) {
-      const float4 x = pv[q] ? reinterpret_cast<const float4*>(wt + pos * kW)[v]
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 x = ok ? reinterpret_cast<const float4*>(wt + pos * kW)[v]
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
       wp[q][4 * v + 0] = x.x;
       wp[q][4 * v + 1] = x.y;
       wp[q][4 * v + 2] = x.z;
@@ -319,37 +369,44 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float* __rest
   const int n0 = wv * 32;  // this wave's 32 dA columns of the chunk
   for (int ch = ch0; ch < ch1; ++ch) {
     const int c0 = ch * kCC;
+    // this chunk's neighbour channels, in flight during the MFMAs
+    float gv[PP][kCC];
+#pragma unroll
+    for (int q = 0; q < PP; ++q)
+#pragma unroll
+      for (int c = 0; c < kCC; ++c) gv[q][c] = g_fetch(g, src, pn[q], row0 + pr[q], c0 + c);
     const int colg = c0 * kW + n0 + l32;
     const bool ok = (colg >> 4) < g.c;
+    const float* wcol = wl + colg;
     f32x16 acc = zero16();
+    float4 bcur, bnxt = make_float4(0.f, 0.f, 0.f, 0.f);
+    bcur.x = ok ? wcol[(4 * half + 0) * c16] : 0.f;
+    bcur.y = ok ? wcol[(4 * half + 1) * c16] : 0.f;
+    bcur.z = ok ? wcol[(4 * half + 2) * c16] : 0.f;
+    bcur.w = ok ? wcol[(4 * half + 3) * c16] : 0.f;
 #pragma unroll 4
     for (int og = 0; og < O / 8; ++og) {
-      const float4 av = *reinterpret_cast<const float4*>(dyl + (2 * og + half) * kBlk + l32 * 4);
-      const int ob = 8 * og + 4 * half;
-      float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ok) {
-        bv.x = wl[(ob + 0) * c16 + colg];
-        bv.y = wl[(ob + 1) * c16 + colg];
-        bv.z = wl[(ob + 2) * c16 + colg];
-        bv.w = wl[(ob + 3) * c16 + colg];
+      if (og + 1 < O / 8) {
+        const int ob = 8 * (og + 1) + 4 * half;
+        bnxt.x = ok ? wcol[(ob + 0) * c16] : 0.f;
+        bnxt.y = ok ? wcol[(ob + 1) * c16] : 0.f;
+        bnxt.z = ok ? wcol[(ob + 2) * c16] : 0.f;
+        bnxt.w = ok ? wcol[(ob + 3) * c16] : 0.f;
       }
-      acc = mfma4(av, bv, acc);
+      const float4 av = *reinterpret_cast<const float4*>(dyl + (2 * og + half) * kBlk + l32 * 4);
+      acc = mfma4(av, bcur, acc);
+      bcur = bnxt;
     }
 #pragma unroll
     for (int e = 0; e < 16; ++e)
       dal[((e & 3) + 8 * (e >> 2) + 4 * half) * kDaS + n0 + l32] = acc[e];
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      if (!pv[q]) continue;
+    for (int q = 0; q < PP; ++q) {
+      if (pn[q] < 0) continue;
       const int r = pr[q];
-      const int base = rbase[r];
-      const int j = g.idx[(long long)(row0 + r) * g.k + pk[q]];
-      float gv[kCC];
-#pragma unroll
-      for (int c = 0; c < kCC; ++c) gv[c] = g_value(g, base, rctr + r * 3, j, c0 + c);
       const long long pos = (long long)(row0 + r) * g.k + pk[q];
-      float* dgo = dgc + ((long long)ch * rk_total + pos) * kCC;
+      float* dgo = dgr + pos * g.c8 + c0;
 #pragma unroll 2
       for (int cl = 0; cl < kCC; ++cl) {
         float da[kW];
@@ -366,14 +423,14 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float* __rest
         for (int w = 0; w < kW; ++w) s = __builtin_fmaf(da[w], wp[q][w], s);
         dgo[cl] = s;
         if (c0 == 0 && cl < 3) dcl[(r * g.k + pk[q]) * 3 + cl] = s;
-        const float gc = gv[cl];
+        const float gc = gv[q][cl];
 #pragma unroll
         for (int w = 0; w < kW; ++w) dw[q][w] = __builtin_fmaf(da[w], gc, dw[q][w]);
       }
     }
     __syncthreads();
   }
-  if (ch0 == 0 && t < kTM * 3) {
+  if (ch0 == 0 && t < 32 * 3) {
     const int r = t / 3, i = t - (t / 3) * 3;
     const int row = row0 + r;
     if (row < g.r) {
@@ -382,10 +439,10 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float* __rest
       dcenter[(long long)row * 3 + i] = -s;
     }
   }
-  float* dwt_dst = dwt + (long long)split * rk_total * kW;  // slab when split > 0 exists
+  float* dwt_dst = dwt + (long long)split * rk_total * kW;  // slab index when split
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    if (!pv[q]) continue;
+  for (int q = 0; q < PP; ++q) {
+    if (pn[q] < 0) continue;
     const long long pos = (long long)(row0 + pr[q]) * g.k + pk[q];
     float4* dst = reinterpret_cast<float4*>(dwt_dst + pos * kW);
 #pragma unroll
@@ -394,120 +451,178 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float* __rest
   }
 }
 
-// per point (one wave each): d_xyz / d_feats = sum of its dG rows in CSR (ascending position)
-__global__ __launch_bounds__(256) void pc_csr_sum_kernel(long long npts, int c, int d,
-                                                         long long rk_total,
-                                                         const float* __restrict__ dgc,
+// d_xyz / d_feats of every point = sum of its dG rows through the CSR (ascending
+// position); one thread per (point, 4 channels)
+__global__ __launch_bounds__(256) void pc_csr_sum_kernel(long long npts, int c, int c8, int d,
+                                                         const float* __restrict__ dgr,
                                                          const int* __restrict__ offsets,
                                                          const int* __restrict__ perm,
                                                          float* __restrict__ dxyz,
                                                          float* __restrict__ dfeats) {
-  const long long key = (long long)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
-  if (key >= npts) return;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int j0 = offsets[key], j1 = offsets[key + 1];
-  for (int ch = dxyz ? lane : 3 + lane; ch < c; ch += kWave) {
-    const float* src = dgc + (long long)(ch / kCC) * rk_total * kCC + (ch % kCC);
-    float s = 0.f;
-    for (int j = j0; j < j1; ++j) s = __fadd_rn(s, src[(long long)perm[j] * kCC]);
-    if (ch < 3)
-      dxyz[key * 3 + ch] = s;
-    else
-      dfeats[key * d + (ch - 3)] = s;
+  const int nv = c8 / 4;
+  const long long total = npts * nv;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const long long key = e / nv;
+    const int v = (int)(e - key * nv);
+    const int j0 = offsets[key], j1 = offsets[key + 1];
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int j = j0; j < j1; ++j) {
+      const float4 x = *reinterpret_cast<const float4*>(dgr + (long long)perm[j] * c8 + 4 * v);
+      s.x = __fadd_rn(s.x, x.x);
+      s.y = __fadd_rn(s.y, x.y);
+      s.z = __fadd_rn(s.z, x.z);
+      s.w = __fadd_rn(s.w, x.w);
+    }
+    const float sv[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ch = 4 * v + i;
+      if (ch < 3) {
+        if (dxyz) dxyz[key * 3 + ch] = sv[i];
+      } else if (ch < c) {
+        dfeats[key * d + (ch - 3)] = sv[i];
+      }
+    }
   }
 }
 
 // ------------------------------------------------------------------ backward: weight
-// grid (channel chunks, row splits); dwl tile (O x 128) of this chunk over the split's rows
-template <int O>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2)))
+// 1-D grid of nch x splits workgroups (512 threads); each owns the O x 128 tile of dwl for
+// one chunk over one split's rows.  With >= 8 splits, the chunks of split s all run on XCD
+// s % 8 (workgroups are dealt to the XCDs round-robin by linear id).
+template <int O, int KM>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
 void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __restrict__ dy,
-                          float* __restrict__ dwl, int rows_per_split) {
-  __shared__ int rbase[kTM];
-  __shared__ float rctr[kTM * 3];
-  __shared__ __attribute__((aligned(16))) float gl[kTM * kKMax * kCC];
+                          float* __restrict__ dwl, int rows_per_split, int nsplit, int xcd_map) {
+  constexpr int MT = O / 32;
+  constexpr int MPW = MT / 2;              // 8 waves: 4 column tiles x 2 row-tile groups
+  constexpr int GS = (32 * KM + 63) / 64;  // gather slots per thread
+  constexpr int DS = O / 16;               // dy slots per thread
+  __shared__ __attribute__((aligned(16))) float gl[32 * KM * kCC];
   __shared__ __attribute__((aligned(16))) float dyt[O * kTS];
   __shared__ __attribute__((aligned(16))) float at[kNC * kTS];
-  constexpr int MT = O / 32;
-  constexpr int MPW = MT >= 4 ? MT / 4 : 1;
-  constexpr int NPW = MT >= 4 ? 4 : 2;
-  const int ch = blockIdx.x, split = blockIdx.y;
+
+  const int L = blockIdx.x;
+  int ch, split;
+  if (xcd_map) {
+    const int q = L >> 3;
+    split = (L & 7) + 8 * (q / g.nch);
+    ch = q % g.nch;
+  } else {
+    ch = L % g.nch;
+    split = L / g.nch;
+  }
+  if (split >= nsplit) return;
   const int c0 = ch * kCC;
   const int rbeg = split * rows_per_split;
   const int rend = min(g.r, rbeg + rows_per_split);
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, half = lane >> 5, l32 = lane & 31;
-  const int w = t & (kW - 1), rr = t >> 4;
-  const int m0 = MT >= 4 ? wv * MPW : (wv & 1);
-  const int nb0 = MT >= 4 ? 0 : (wv >> 1) * 2;
+  const int w = t & (kW - 1), rb = t >> 4, cs = t & (kCC - 1);
+  const int nt = wv & 3;
+  const int m0 = (wv >> 2) * MPW;
   const long long c16 = (long long)g.c * kW;
+  const int tk = 32 * g.k;
+  const Srcs src = srcs_of(g);
 
-  f32x16 acc[MPW][NPW];
+  // registers prefetched one tile ahead
+  float wr[KM], gr[GS], dr[DS];
+  auto fetch = [&](int row0) {
+    const int row = row0 + rb;
 #pragma unroll
-  for (int i = 0; i < MPW; ++i)
+    for (int k = 0; k < KM; ++k)
+      wr[k] = (row < rend && k < g.k) ? wt[((long long)row * g.k + k) * kW + w] : 0.f;
 #pragma unroll
-    for (int j = 0; j < NPW; ++j) acc[i][j] = zero16();
+    for (int i = 0; i < GS; ++i) {
+      const int rk = (t >> 3) + 64 * i;
+      const int r = rk / g.k;
+      const int rw = row0 + r;
+      const int nb = (rk < tk && rw < rend) ? nbr_of(g, rw, rk - r * g.k) : -1;
+      gr[i] = g_fetch(g, src, nb, rw, c0 + cs);
+    }
+#pragma unroll
+    for (int i = 0; i < DS; ++i) {
+      const int e = t + 512 * i;
+      const int rw = row0 + e / O;
+      dr[i] = rw < rend ? dy[(long long)rw * O + (e % O)] : 0.f;
+    }
+  };
 
-  for (int row0 = rbeg; row0 < rend; row0 += kTM) {
-    __syncthreads();  // previous tile's MFMAs done with dyt / at
-    load_rows(g, row0, rbase, rctr);
-    float wr[2][kKMax];
-    load_wt(g, wt, row0, wr);
-    for (int e = t; e < kTM * O; e += kThreads) {
-      const int r = e / O, o = e % O;
-      const int row = row0 + r;
-      dyt[o * kTS + r] = row < rend ? dy[(long long)row * O + o] : 0.f;
+  f32x16 acc[MPW];
+#pragma unroll
+  for (int i = 0; i < MPW; ++i) acc[i] = zero16();
+  fetch(rbeg);
+  for (int row0 = rbeg; row0 < rend; row0 += 32) {
+    __syncthreads();  // previous tile's MFMAs are done with dyt / at
+#pragma unroll
+    for (int i = 0; i < GS; ++i) {
+      const int rk = (t >> 3) + 64 * i;
+      if (rk < tk) gl[rk * kCC + cs] = gr[i];
+    }
+#pragma unroll
+    for (int i = 0; i < DS; ++i) {
+      const int e = t + 512 * i;
+      dyt[(e % O) * kTS + e / O] = dr[i];
+    }
+    float wc[KM];
+#pragma unroll
+    for (int k = 0; k < KM; ++k) wc[k] = wr[k];
+    __syncthreads();
+    if (row0 + 32 < rend) fetch(row0 + 32);
+    {
+      float a[kCC];
+      build_row<KM>(gl, rb, g.k, wc, a);
+#pragma unroll
+      for (int c = 0; c < kCC; ++c) at[(c * kW + w) * kTS + rb] = a[c];
     }
     __syncthreads();
-    stage_g(g, row0, c0, rbase, rctr, gl);
-    __syncthreads();
-    float a[2][kCC];
-    build_a(g, gl, wr, a);
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const bool live = row0 + rr + 16 * q < rend;
+    for (int gb = 0; gb < 4; ++gb) {
+      const float4 bv = *reinterpret_cast<const float4*>(at + (nt * 32 + l32) * kTS + 8 * gb + 4 * half);
 #pragma unroll
-      for (int cl = 0; cl < kCC; ++cl) at[(cl * kW + w) * kTS + rr + 16 * q] = live ? a[q][cl] : 0.f;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int gb = 0; gb < kTM / 8; ++gb) {
-      float4 av[MPW], bv[NPW];
-#pragma unroll
-      for (int i = 0; i < MPW; ++i)
-        av[i] = *reinterpret_cast<const float4*>(dyt + ((m0 + i) * 32 + l32) * kTS + 8 * gb + 4 * half);
-#pragma unroll
-      for (int j = 0; j < NPW; ++j)
-        bv[j] = *reinterpret_cast<const float4*>(at + ((nb0 + j) * 32 + l32) * kTS + 8 * gb + 4 * half);
-#pragma unroll
-      for (int i = 0; i < MPW; ++i)
-#pragma unroll
-        for (int j = 0; j < NPW; ++j) acc[i][j] = mfma4(av[i], bv[j], acc[i][j]);
+      for (int i = 0; i < MPW; ++i) {
+        const float4 av =
+            *reinterpret_cast<const float4*>(dyt + ((m0 + i) * 32 + l32) * kTS + 8 * gb + 4 * half);
+        acc[i] = mfma4(av, bv, acc[i]);
+      }
     }
   }
-  float* dst = dwl + (long long)split * O * c16;  // slab when the rows are split
+  const long long col = (long long)c0 * kW + nt * 32 + l32;
+  if (col >= c16) return;
+  float* dst = dwl + (long long)split * O * c16;  // slab index when the rows are split
 #pragma unroll
   for (int i = 0; i < MPW; ++i)
 #pragma unroll
-    for (int j = 0; j < NPW; ++j) {
-      const long long col = (long long)c0 * kW + (nb0 + j) * 32 + l32;
-      if (col >= c16) continue;
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int o = (m0 + i) * 32 + (e & 3) + 8 * (e >> 2) + 4 * half;
-        dst[o * c16 + col] = acc[i][j][e];
-      }
+    for (int e = 0; e < 16; ++e) {
+      const int o = (m0 + i) * 32 + (e & 3) + 8 * (e >> 2) + 4 * half;
+      dst[o * c16 + col] = acc[i][e];
     }
 }
 
 // ------------------------------------------------------------------------------- host
 struct Plan {
-  int r, c, nch, rt;
-  int ks, cps;   // channel splits (fwd and bwd-data) and chunks per split
-  int rs, rps;   // row splits (bwd-weight) and rows per split
-  size_t fwd_slab, dgc, dwt_slab, dwl_slab;  // bytes
+  int r, c, nch, c8, tm, rt;  // tm: forward tile rows
+  int ks, cps;                 // fwd channel splits / chunks per split
+  int bks, bcps;               // bwd-data channel splits (32-row tiles)
+  int rs, rps, xcd, wgs;       // bwd-weight row splits, rows per split, XCD map, grid
+  size_t fwd_slab, dgr, dwt_slab, dwl_slab;  // bytes
 };
 
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+inline int km_of(int k) { return k <= 9 ? 9 : 16; }
+
+// every gathered table must be addressable by a 31-bit byte offset (buffer loads)
+inline bool fits_buffers(long long b, long long n, long long s, int d) {
+  const long long lim = 1ll << 31;
+  return b * n * 4 * std::max(d, 3) < lim && b * s * 12 < lim;
+}
+
+void channel_split(int nch, int tiles, int* ks, int* cps) {
+  int s = tiles > 0 ? std::min(nch, std::max(1, divup(kTargetWG, tiles))) : 1;
+  *cps = divup(nch, s);
+  *ks = divup(nch, *cps);
+}
 
 bool plan_of(int b, int s, int k, int d, int o, Plan* p) {
   if (b < 0 || s < 0 || k < 1 || k > kKMax || d < 0 || !(o == 64 || o == 128 || o == 256))
@@ -517,17 +632,22 @@ bool plan_of(int b, int s, int k, int d, int o, Plan* p) {
   p->r = (int)r;
   p->c = 3 + d;
   p->nch = divup(p->c, kCC);
-  p->rt = divup(p->r, kTM);
-  int ks = p->rt > 0 ? std::min(p->nch, std::max(1, divup(kTargetWG, p->rt))) : 1;
-  p->cps = divup(p->nch, ks);
-  p->ks = divup(p->nch, p->cps);
-  int rs = std::max(1, std::min(std::max(p->rt, 1), divup(kTargetWG, p->nch)));
-  p->rps = divup(std::max(p->rt, 1), rs) * kTM;
+  p->c8 = p->nch * kCC;
+  p->tm = km_of(k) <= 9 ? 64 : 32;
+  p->rt = divup(p->r, p->tm);
+  channel_split(p->nch, p->rt, &p->ks, &p->cps);
+  channel_split(p->nch, divup(p->r, 32), &p->bks, &p->bcps);
+  const int t32 = std::max(1, divup(p->r, 32));
+  int rs = std::max(1, std::min(t32, divup(kTargetWG, p->nch)));
+  p->rps = divup(t32, rs) * 32;
   p->rs = std::max(1, divup(p->r, p->rps));
+  p->xcd = p->rs >= 8 ? 1 : 0;
+  const int rs_pad = p->xcd ? divup(p->rs, 8) * 8 : p->rs;
+  p->wgs = p->nch * rs_pad;
   const size_t c16 = (size_t)p->c * kW;
   p->fwd_slab = p->ks > 1 ? align256((size_t)p->ks * p->r * o * 4) : 0;
-  p->dgc = align256((size_t)p->nch * p->r * k * kCC * 4);
-  p->dwt_slab = p->ks > 1 ? align256((size_t)p->ks * p->r * k * kW * 4) : 0;
+  p->dgr = align256((size_t)p->r * k * p->c8 * 4);
+  p->dwt_slab = p->bks > 1 ? align256((size_t)p->bks * p->r * k * kW * 4) : 0;
   p->dwl_slab = p->rs > 1 ? align256((size_t)p->rs * o * c16 * 4) : 0;
   return true;
 }
@@ -540,42 +660,44 @@ hipError_t slab_sum(int nslabs, long long len, const float* slab, const float* b
   return hipGetLastError();
 }
 
-template <int O>
+template <int O, int KM>
 hipError_t fwd_launch(const Geo& g, const Plan& p, const float* wt, const float* wl,
                       const float* bias, float* y, float* slab, hipStream_t st) {
-  hipLaunchKernelGGL((pc_fwd_kernel<O>), dim3(p.rt, p.ks), dim3(kThreads), 0, st, g, wt, wl, bias,
+  hipLaunchKernelGGL((pc_fwd_kernel<O, KM>), dim3(p.rt, p.ks), dim3(256), 0, st, g, wt, wl, bias,
                      y, p.ks > 1 ? slab : nullptr, p.cps);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || p.ks == 1) return e;
   return slab_sum(p.ks, (long long)p.r * O, slab, bias, O, y, st);
 }
 
-template <int O>
+template <int O, int KM>
 hipError_t bwd_launch(const Geo& g, const Plan& p, int b, const float* wt, const float* wl,
                       const float* dy, const int* offsets, const int* perm, float* dxyz,
                       float* dfeats, float* dcenter, float* dwt, float* dwl, char* ws,
                       hipStream_t st) {
-  float* dgc = reinterpret_cast<float*>(ws);
-  float* dwt_slab = reinterpret_cast<float*>(ws + p.dgc);
-  float* dwl_slab = reinterpret_cast<float*>(ws + p.dgc + p.dwt_slab);
+  float* dgr = reinterpret_cast<float*>(ws);
+  float* dwt_slab = reinterpret_cast<float*>(ws + p.dgr);
+  float* dwl_slab = reinterpret_cast<float*>(ws + p.dgr + p.dwt_slab);
   const long long rk = (long long)p.r * g.k;
-  hipLaunchKernelGGL((pc_bwd_data_kernel<O>), dim3(p.rt, p.ks), dim3(kThreads), 0, st, g, wt, wl,
-                     dy, dgc, p.ks > 1 ? dwt_slab : dwt, dcenter, p.cps);
+  hipLaunchKernelGGL((pc_bwd_data_kernel<O, KM>), dim3(divup(p.r, 32), p.bks), dim3(256), 0, st,
+                     g, wt, wl, dy, dgr, p.bks > 1 ? dwt_slab : dwt, dcenter, p.bcps);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  if (p.ks > 1 && (e = slab_sum(p.ks, rk * kW, dwt_slab, nullptr, 1, dwt, st)) != hipSuccess)
+  if (p.bks > 1 && (e = slab_sum(p.bks, rk * kW, dwt_slab, nullptr, 1, dwt, st)) != hipSuccess)
     return e;
   const long long npts = (long long)b * g.n;
-  hipLaunchKernelGGL(pc_csr_sum_kernel, dim3((unsigned)divupll(npts, 4)), dim3(256), 0, st, npts,
-                     g.c, g.d, rk, dgc, offsets, perm, dxyz, dfeats);
+  const long long work = npts * (p.c8 / 4);
+  hipLaunchKernelGGL(pc_csr_sum_kernel,
+                     dim3((unsigned)std::min<long long>(divupll(work, 256), 1 << 20)), dim3(256),
+                     0, st, npts, g.c, p.c8, g.d, dgr, offsets, perm, dxyz, dfeats);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL((pc_bwd_weight_kernel<O>), dim3(p.nch, p.rs), dim3(kThreads), 0, st, g, wt,
-                     dy, p.rs > 1 ? dwl_slab : dwl, p.rps);
+  hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM>), dim3(p.wgs), dim3(512), 0, st, g, wt, dy,
+                     p.rs > 1 ? dwl_slab : dwl, p.rps, p.rs, p.xcd);
   if ((e = hipGetLastError()) != hipSuccess || p.rs == 1) return e;
   return slab_sum(p.rs, (long long)O * g.c * kW, dwl_slab, nullptr, 1, dwl, st);
 }
 
-Geo geo_of(int n, int s, int k, int d, const Plan& p, const float* xyz, const float* center,
+Geo geo_of(int b, int n, int s, int k, int d, const Plan& p, const float* xyz, const float* center,
            const float* feats, const int* idx) {
   Geo g;
   g.n = n;
@@ -585,12 +707,22 @@ Geo geo_of(int n, int s, int k, int d, const Plan& p, const float* xyz, const fl
   g.c = p.c;
   g.r = p.r;
   g.nch = p.nch;
+  g.c8 = p.c8;
+  g.bn = b * n;
   g.xyz = xyz;
   g.center = center;
   g.feats = feats;
   g.idx = idx;
   return g;
 }
+
+// instantiate FN<O, KM> for the runtime (o, k)
+#define KDPC_PC_DISPATCH(FN, ...)                                                         \
+  (km_of(k) == 9                                                                          \
+       ? (o == 64 ? FN<64, 9>(__VA_ARGS__)                                                \
+                  : (o == 128 ? FN<128, 9>(__VA_ARGS__) : FN<256, 9>(__VA_ARGS__)))       \
+       : (o == 64 ? FN<64, 16>(__VA_ARGS__)                                               \
+                  : (o == 128 ? FN<128, 16>(__VA_ARGS__) : FN<256, 16>(__VA_ARGS__))))
 
 }  // namespace
 
@@ -609,22 +741,19 @@ KDPC_API int kdpc_pointconv_fwd(int b, int n, int s, int k, int d, int o, const 
                                 const float* wt, const float* wl, const float* bias, float* y,
                                 void* workspace, size_t workspace_bytes, void* stream) {
   Plan p;
-  KDPC_CHECK_ARG(n > 0 && b <= 65535 && plan_of(b, s, k, d, o, &p));
+  KDPC_CHECK_ARG(n > 0 && b <= 65535 && plan_of(b, s, k, d, o, &p) && fits_buffers(b, n, s, d));
   if (p.r == 0) return (int)hipSuccess;
   KDPC_CHECK_ARG(xyz && center && idx && wt && wl && bias && y && (d == 0 || feats));
   KDPC_CHECK_ARG(workspace_bytes >= p.fwd_slab && (p.fwd_slab == 0 || workspace));
-  const Geo g = geo_of(n, s, k, d, p, xyz, center, feats, idx);
+  const Geo g = geo_of(b, n, s, k, d, p, xyz, center, feats, idx);
   float* slab = reinterpret_cast<float*>(workspace);
   hipStream_t st = (hipStream_t)stream;
-  hipError_t e = o == 64    ? fwd_launch<64>(g, p, wt, wl, bias, y, slab, st)
-                 : o == 128 ? fwd_launch<128>(g, p, wt, wl, bias, y, slab, st)
-                            : fwd_launch<256>(g, p, wt, wl, bias, y, slab, st);
-  return (int)e;
+  return (int)KDPC_PC_DISPATCH(fwd_launch, g, p, wt, wl, bias, y, slab, st);
 }
 
 KDPC_API size_t kdpc_pointconv_bwd_workspace_bytes(int b, int s, int k, int d, int o) {
   Plan p;
-  return plan_of(b, s, k, d, o, &p) ? p.dgc + p.dwt_slab + p.dwl_slab : 0;
+  return plan_of(b, s, k, d, o, &p) ? p.dgr + p.dwt_slab + p.dwl_slab : 0;
 }
 
 KDPC_API int kdpc_pointconv_bwd(int b, int n, int s, int k, int d, int o, const float* xyz,
@@ -634,7 +763,7 @@ KDPC_API int kdpc_pointconv_bwd(int b, int n, int s, int k, int d, int o, const 
                                 float* dcenter, float* dwt, float* dwl, void* workspace,
                                 size_t workspace_bytes, void* stream) {
   Plan p;
-  KDPC_CHECK_ARG(n > 0 && b <= 65535 && plan_of(b, s, k, d, o, &p));
+  KDPC_CHECK_ARG(n > 0 && b <= 65535 && plan_of(b, s, k, d, o, &p) && fits_buffers(b, n, s, d));
   hipStream_t st = (hipStream_t)stream;
   if (p.r == 0) {
     hipError_t e = hipSuccess;
@@ -645,12 +774,9 @@ KDPC_API int kdpc_pointconv_bwd(int b, int n, int s, int k, int d, int o, const 
   }
   KDPC_CHECK_ARG(xyz && center && idx && wt && wl && dy && offsets && perm && dcenter && dwt &&
                  dwl && (d == 0 || (feats && dfeats)));
-  KDPC_CHECK_ARG(workspace && workspace_bytes >= p.dgc + p.dwt_slab + p.dwl_slab);
-  const Geo g = geo_of(n, s, k, d, p, xyz, center, feats, idx);
+  KDPC_CHECK_ARG(workspace && workspace_bytes >= p.dgr + p.dwt_slab + p.dwl_slab);
+  const Geo g = geo_of(b, n, s, k, d, p, xyz, center, feats, idx);
   char* ws = reinterpret_cast<char*>(workspace);
-  hipError_t e =
-      o == 64    ? bwd_launch<64>(g, p, b, wt, wl, dy, offsets, perm, dxyz, dfeats, dcenter, dwt, dwl, ws, st)
-      : o == 128 ? bwd_launch<128>(g, p, b, wt, wl, dy, offsets, perm, dxyz, dfeats, dcenter, dwt, dwl, ws, st)
-                 : bwd_launch<256>(g, p, b, wt, wl, dy, offsets, perm, dxyz, dfeats, dcenter, dwt, dwl, ws, st);
-  return (int)e;
+  return (int)KDPC_PC_DISPATCH(bwd_launch, g, p, b, wt, wl, dy, offsets, perm, dxyz, dfeats,
+                               dcenter, dwt, dwl, ws, st);
 }
