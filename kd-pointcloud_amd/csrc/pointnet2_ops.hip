@@ -62,56 +62,89 @@ __global__ __launch_bounds__(256) void group_points_kernel(int c, int n, int p_t
   }
 }
 
-// LDS-staged variant for N <= 16384: a workgroup owns CG whole channel rows of one cloud
-// (CG*N*4 <= 64 KiB, loaded once with coalesced float4 reads) and a slice of positions;
-// every output is then a random LDS read instead of a random 4-byte global gather, and
-// the only HBM streams are the coalesced float4 stores and the int4 index reads.
-constexpr int kRowLdsBytes = 64 * 1024;
+// LDS-staged variant: a workgroup owns CG whole channel rows of one cloud (CG*N*4 <= 80 KiB,
+// so two workgroups share a CU; loaded once with coalesced float4 reads) and a slice of the
+// S*K positions.  Every output is a random LDS read instead of a random 4-byte global
+// gather; the HBM streams are the coalesced float4 stores and the int4 index reads.  A
+// thread keeps kGU int4 index loads in flight (the loop would otherwise wait one L2/MALL
+// round trip per 1024 positions), and the first batch is issued before the row staging so
+// the two overlap.  Work units (cloud, slice) are spread so that the C/CG channel groups
+// reading the same index slice run on one XCD (`xcd_units`), keeping those re-reads in its L2.
+constexpr int kRowLdsBytes = 80 * 1024;
+constexpr int kGU = 4;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <int CG>
 __global__ __launch_bounds__(256) void group_points_lds_kernel(int c, int n, int p_total,
-                                                               int p_slice,
+                                                               int p_slice, int nslice,
+                                                               int groups, int xcd_units,
                                                                const float* __restrict__ points,
                                                                const int* __restrict__ idx,
                                                                float* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) float rows[];  // [CG][n]
-  const int nslice = gridDim.x;
-  const int slice = blockIdx.x;
-  const int c0 = blockIdx.y * CG;
-  const int bi = blockIdx.z;
-  const int cg = min(CG, c - c0);
-  const float* pb = points + ((long long)bi * c + c0) * n;
-  for (int cc = 0; cc < cg; ++cc) {
-    const float* src = pb + (long long)cc * n;
-    if ((n & 3) == 0) {
-      for (int e = threadIdx.x * 4; e < n; e += 256 * 4)
-        *reinterpret_cast<float4*>(rows + cc * n + e) = *reinterpret_cast<const float4*>(src + e);
-    } else {
-      for (int e = threadIdx.x; e < n; e += 256) rows[cc * n + e] = src[e];
-    }
+  int unit, grp;
+  const int id = blockIdx.x;
+  if (xcd_units > 0) {  // units % 8 == 0: XCD x (= id % 8) owns units [x*xcd_units, ...)
+    const int j = id >> 3;
+    unit = (id & 7) * xcd_units + j / groups;
+    grp = j % groups;
+  } else {
+    unit = id / groups;
+    grp = id % groups;
   }
-  __syncthreads();
+  const int bi = unit / nslice;
+  const int slice = unit % nslice;
+  const int c0 = grp * CG;
+  const int cg = min(CG, c - c0);
   const int pbeg = slice * p_slice;
   const int pend = min(p_total, pbeg + p_slice);
   const int* ib = idx + (long long)bi * p_total;
   float* ob = out + ((long long)bi * c + c0) * p_total;
-  (void)nslice;
-  for (int p4 = pbeg + threadIdx.x * 4; p4 < pend; p4 += 256 * 4) {
-    if (p4 + 3 < pend) {
-      const int4 q = *reinterpret_cast<const int4*>(ib + p4);
+
+  // first index batch in flight while the rows are staged
+  int4 q[kGU];
+  int p4 = pbeg + threadIdx.x * 4;
 #pragma unroll
-      for (int cc = 0; cc < CG; ++cc) {
-        if (cc < cg) {
-          const float* r = rows + cc * n;
-          *reinterpret_cast<float4*>(ob + (long long)cc * p_total + p4) =
-              make_float4(r[q.x], r[q.y], r[q.z], r[q.w]);
+  for (int u = 0; u < kGU; ++u) {
+    const int pu = p4 + u * 1024;
+    q[u] = pu + 3 < pend ? *reinterpret_cast<const int4*>(ib + pu) : make_int4(0, 0, 0, 0);
+  }
+  const float* pb = points + ((long long)bi * c + c0) * n;
+  if ((n & 3) == 0) {
+    const int n4 = n >> 2;
+    for (int e = threadIdx.x; e < cg * n4; e += 256)
+      reinterpret_cast<float4*>(rows)[e] = reinterpret_cast<const float4*>(pb)[e];
+  } else {
+    for (int e = threadIdx.x; e < cg * n; e += 256) rows[e] = pb[e];
+  }
+  __syncthreads();
+
+  for (; p4 < pend; p4 += kGU * 1024) {
+#pragma unroll
+    for (int u = 0; u < kGU; ++u) {
+      const int pu = p4 + u * 1024;
+      if (pu + 3 < pend) {
+#pragma unroll
+        for (int cc = 0; cc < CG; ++cc) {
+          if (cc < cg) {
+            const float* r = rows + cc * n;
+            const f32x4 v = {r[q[u].x], r[q[u].y], r[q[u].z], r[q[u].w]};
+            __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(ob + (long long)cc * p_total + pu));
+          }
+        }
+      } else {
+        for (int t = pu; t < pend; ++t) {
+          const int qq = ib[t];
+          for (int cc = 0; cc < cg; ++cc) ob[(long long)cc * p_total + t] = rows[cc * n + qq];
         }
       }
-    } else {
-      for (int t = p4; t < pend; ++t) {
-        const int q = ib[t];
-        for (int cc = 0; cc < cg; ++cc) ob[(long long)cc * p_total + t] = rows[cc * n + q];
-      }
+    }
+    // next batch
+    const int pn = p4 + kGU * 1024;
+#pragma unroll
+    for (int u = 0; u < kGU; ++u) {
+      const int pu = pn + u * 1024;
+      if (pu + 3 < pend) q[u] = *reinterpret_cast<const int4*>(ib + pu);
     }
   }
 }
@@ -228,6 +261,22 @@ __global__ __launch_bounds__(256) void three_interpolate_kernel(int b, int c, in
   }
 }
 
+template <int CG>
+hipError_t launch_group_lds(dim3 grid, size_t lds, hipStream_t st, int c, int n, int p_total,
+                            int p_slice, int nslice, int groups, int xcd_units,
+                            const float* points, const int* idx, float* out) {
+  auto k = group_points_lds_kernel<CG>;
+  static bool attr_set = false;  // one process per GPU: set once
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              kRowLdsBytes);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(k, grid, dim3(256), lds, st, c, n, p_total, p_slice, nslice, groups,
+                     xcd_units, points, idx, out);
+  return hipGetLastError();
+}
+
 inline int grid_for(long long total, int block) {
   long long g = divupll(total, block);
   if (g > 65536) g = 65536;
@@ -262,26 +311,28 @@ KDPC_API int kdpc_group_points(int b, int c, int n, int npoints, int nsample, co
   const int cg = kRowLdsBytes / (4 * n);
   if (cg >= 1 && (p_total % 4) == 0) {
     // channel groups of CG rows; slices so that the grid covers >= ~512 workgroups
-    const int CG = cg >= 4 ? 4 : (cg >= 2 ? 2 : 1);
+    const int CG = cg >= 8 ? 8 : (cg >= 4 ? 4 : (cg >= 2 ? 2 : 1));
     const int groups = divup(c, CG);
     int nslice = divup(512, b * groups);
     const int min_slice = 4096;
     nslice = max(1, min(nslice, (int)divupll(p_total, min_slice)));
     int p_slice = (int)divupll(divupll(p_total, nslice), 4) * 4;
     nslice = (int)divupll(p_total, p_slice);
-    KDPC_CHECK_ARG(groups <= 65535);
-    dim3 grid(nslice, groups, b);
+    const long long units = (long long)b * nslice;
+    const long long wgs = units * groups;
+    KDPC_CHECK_ARG(wgs < (1ll << 31));
+    const int xcd_units = (units % 8 == 0) ? (int)(units / 8) : 0;
     const size_t lds = (size_t)CG * n * sizeof(float);
-    if (CG == 4)
-      hipLaunchKernelGGL(group_points_lds_kernel<4>, grid, dim3(256), lds, st, c, n, (int)p_total,
-                         p_slice, points, idx, out);
-    else if (CG == 2)
-      hipLaunchKernelGGL(group_points_lds_kernel<2>, grid, dim3(256), lds, st, c, n, (int)p_total,
-                         p_slice, points, idx, out);
-    else
-      hipLaunchKernelGGL(group_points_lds_kernel<1>, grid, dim3(256), lds, st, c, n, (int)p_total,
-                         p_slice, points, idx, out);
-    KDPC_RETURN_LAUNCH();
+    const dim3 grid((unsigned)wgs);
+    const int pt = (int)p_total;
+    hipError_t e;
+    switch (CG) {
+      case 8: e = launch_group_lds<8>(grid, lds, st, c, n, pt, p_slice, nslice, groups, xcd_units, points, idx, out); break;
+      case 4: e = launch_group_lds<4>(grid, lds, st, c, n, pt, p_slice, nslice, groups, xcd_units, points, idx, out); break;
+      case 2: e = launch_group_lds<2>(grid, lds, st, c, n, pt, p_slice, nslice, groups, xcd_units, points, idx, out); break;
+      default: e = launch_group_lds<1>(grid, lds, st, c, n, pt, p_slice, nslice, groups, xcd_units, points, idx, out);
+    }
+    return (int)e;
   }
   dim3 grid(divup((int)divupll(p_total, 4), 256), divup(c, kGroupCG), b);
   KDPC_CHECK_ARG(grid.y <= 65535);

@@ -13,7 +13,7 @@ ok_or_stop() {  # $1 = exit code; 0/1 (pytest pass/fail) continue, anything else
 }
 
 echo "== pytest -m gpu"
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu_$TAG.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1
 rc=$?; tail -5 gpurun_out/pytest_gpu_$TAG.log; ok_or_stop $rc
 
 echo "== bench"
