@@ -32,16 +32,28 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
-FP32_MFMA_PEAK_TF = 157.3  # dense f32 MFMA / vector peak
+FP32_MFMA_PEAK_TF = 157.3  # dense f32 MFMA peak (MI355X_MICROARCH.md, F32 row)
 FP32_VALU_PEAK_TF = 157.3
 
-# kernel -> (bound, unit, peak)
+# C entry point -> (bound, unit, peak, HIP kernels it launches).  An entry point is the unit
+# the live timer brackets; tools/roofline_check.py sums the listed kernels' rocprofv3
+# durations per entry launch to cross-check the live average.
 ROOFLINE = {
-    "kdpc_group_rows": ("hbm", "GB/s", HBM_PEAK_GBS),
-    "kdpc_group_rows_grad_csr": ("hbm", "GB/s", HBM_PEAK_GBS),
-    "kdpc_group_points": ("hbm", "GB/s", HBM_PEAK_GBS),
-    "kdpc_knn_point": ("valu", "TFLOP/s", FP32_VALU_PEAK_TF),
+    "kdpc_pointconv_bwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF,
+                           ["pc_bwd_data_kernel", "pc_csr_sum_kernel", "pc_bwd_weight_kernel",
+                            "pc_slab_sum_kernel"]),
+    "kdpc_pointconv_fwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF,
+                           ["pc_fwd_kernel", "pc_slab_sum_kernel"]),
+    "kdpc_group_rows": ("hbm", "GB/s", HBM_PEAK_GBS, ["group_rows_kernel"]),
+    "kdpc_group_points": ("hbm", "GB/s", HBM_PEAK_GBS, ["group_points_lds_kernel",
+                                                         "group_points_kernel"]),
+    "kdpc_knn_point": ("valu", "TFLOP/s", FP32_VALU_PEAK_TF, ["knn_kernel"]),
 }
+# the step's dominant entry point (rocprofv3 step profile, profiles/) and the gather-bound
+# one the north star names
+PRIMARY_KERNEL = "kdpc_pointconv_bwd"
+GATHER_KERNEL = "kdpc_group_rows"
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
 def parse():
@@ -52,7 +64,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=8, help="pairs per GPU")
     ap.add_argument("--npoints", type=int, default=8192)
     ap.add_argument("--mode", choices=["train", "kd"], default="train")
-    ap.add_argument("--roofline-kernel", default="kdpc_group_rows")
+    ap.add_argument("--roofline-kernel", default=PRIMARY_KERNEL)
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -90,6 +102,38 @@ def cpu_baseline(args):
                       f"steps after 1 warm-up ({med:.2f} s/step); oracle/torch_model.py "
                       f"(square_distance+topk kNN, torch.gather, FPS->randperm); "
                       f"host os.cpu_count()={os.cpu_count()}"}
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc passes
+    (tools/pmc_traffic.py; FETCH_SIZE and WRITE_SIZE in separate passes, FETCH_SIZE doubled
+    per MI355X_MICROARCH.md §HBM), or None when that kernel was not measured."""
+    try:
+        with open(PMC_FILE) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    e = d.get("entries", {}).get(kernel)
+    return None if e is None else e.get("hbm_bytes_per_launch")
+
+
+def roofline(kernel, summ):
+    """Live roofline of one C entry point from the HIP-event launch timer."""
+    if not summ or summ["ms"] <= 0:
+        return None
+    bound, unit, peak, kernels = ROOFLINE.get(kernel, ("hbm", "GB/s", HBM_PEAK_GBS, []))
+    per_launch_ms = summ["ms"] / summ["launches"]
+    if unit == "GB/s":
+        achieved = summ["bytes"] / (summ["ms"] * 1e-3) / 1e9
+    else:
+        achieved = summ["flops"] / (summ["ms"] * 1e-3) / 1e12
+    return {"bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
+            "frac": round(achieved / peak, 4), "traffic": pmc_traffic(kernel),
+            "kernel": kernel, "hip_kernels": kernels, "launches": summ["launches"],
+            "avg_launch_us": round(per_launch_ms * 1e3, 2),
+            "algorithmic_bytes_per_launch": round(summ["bytes"] / summ["launches"]),
+            "algorithmic_flops_per_launch": round(summ["flops"] / summ["launches"]),
+            "traffic_source": os.path.relpath(PMC_FILE, ROOT) if os.path.exists(PMC_FILE) else None}
 
 
 def main():
@@ -130,7 +174,7 @@ def main():
 
     for i in range(args.warmup):
         step(*batches[i % nb])
-    timer = kdpc_native.LaunchTimer([args.roofline_kernel])
+    timer = kdpc_native.LaunchTimer([args.roofline_kernel, GATHER_KERNEL])
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -148,19 +192,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
-    summ = timer.summary().get(args.roofline_kernel)
-    roof = None
-    if summ and summ["ms"] > 0:
-        bound, unit, peak = ROOFLINE.get(args.roofline_kernel, ("hbm", "GB/s", HBM_PEAK_GBS))
-        per_launch_ms = summ["ms"] / summ["launches"]
-        if unit == "GB/s":
-            achieved = summ["bytes"] / (summ["ms"] * 1e-3) / 1e9
-        else:
-            achieved = summ["flops"] / (summ["ms"] * 1e-3) / 1e12
-        roof = {"bound": bound, "kernel": args.roofline_kernel, "achieved": round(achieved, 2),
-                "peak": peak, "unit": unit, "frac": round(achieved / peak, 4), "traffic": None,
-                "launches": summ["launches"], "avg_launch_us": round(per_launch_ms * 1e3, 2),
-                "algorithmic_bytes_per_launch": round(summ["bytes"] / summ["launches"])}
+    summary = timer.summary()
+    roof = roofline(args.roofline_kernel, summary.get(args.roofline_kernel))
+    roof_gather = roofline(GATHER_KERNEL, summary.get(GATHER_KERNEL))
 
     pairs = world * args.batch * args.steps
     line = {
@@ -178,6 +212,7 @@ def main():
                    "batch_per_gpu": args.batch, "global_batch": world * args.batch,
                    "npoints": args.npoints, "parallelism": f"ddp{world}"},
         "roofline": roof,
+        "roofline_gather": roof_gather,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args)

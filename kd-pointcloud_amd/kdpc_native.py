@@ -229,10 +229,10 @@ def group_rows(points, idx):
     B, N, C = points.shape
     P = idx.shape[1]
     out = torch.empty((B, P, C), dtype=torch.float32, device=points.device)
-    # algorithmic bytes: idx read + gathered rows read + rows written (B*(4P + 8PC))
+    # algorithmic bytes: table read once + idx read + rows written
     _call("kdpc_group_rows", B, N, C, P, _dev(points, torch.float32, "points"),
           _dev(idx, torch.int32, "idx"), _dev(out, torch.float32, "out"), _stream(points),
-          work=(B * (4 * P + 8 * P * C), 0))
+          work=(B * (4 * N * C + 4 * P + 4 * P * C), 0))
     return out
 
 

@@ -63,41 +63,45 @@ class PointConvBidirection(nn.Module):
         self.upsample = UpsampleFlow()
 
     # ---------------------------------------------------------------------------------
+    # Every tensor below is point-major, (batch, points, channels), contiguous: a 1x1 conv is
+    # one GEMM over the points, a concatenation is along the last dim, and the HIP gathers
+    # read whole rows.  Only the returned views are permuted to the reference's (B,C,N).
     def _encode(self, pc, color):
         """Shared encoder on the pair batch (2B).  Returns per-level xyz, features, fps idx."""
-        feat_l0 = self.level0_1(self.level0(color))
-        feat_l0_1 = self.level0_2(feat_l0)
+        feat_l0 = self.level0_1.cl(self.level0.cl(color))
+        feat_l0_1 = self.level0_2.cl(feat_l0)
         levels = [(self.level1, self.level1_0, self.level1_1),
                   (self.level2, self.level2_0, self.level2_1),
                   (self.level3, self.level3_0, self.level3_1)]
         pcs, feats, feats_out, fps = [pc], [feat_l0], [feat_l0_1], []
         x, f = pc, feat_l0_1
         for down, mix, widen in levels:
-            x, f, idx = down(x, f)
-            f = mix(f)
+            x, f, idx = down.forward_cl(x, f)
+            f = mix.cl(f)
             pcs.append(x)
             feats.append(f)
             fps.append(idx)
-            f = widen(f)
+            f = widen.cl(f)
             feats_out.append(f)
-        pc_l4, feat_l4, _ = self.level4(x, f)
-        feat_l4_3 = self.deconv4_3(self.upsample(x, pc_l4, feat_l4))
+        pc_l4, feat_l4, _ = self.level4.forward_cl(x, f)
+        feat_l4_3 = self.deconv4_3.cl(self.upsample.forward_cl(x, pc_l4, feat_l4))
         return pcs, feats, feats_out, fps, feat_l4_3
 
     def forward(self, xyz1, xyz2, color1, color2):
         """xyz*, color*: (B,N,3).  Returns (flows, fps_pc1_idxs, fps_pc2_idxs, pc1, pc2,
-        feat1s, feat2s, crosses) exactly as the reference (models_bid_pointconv.py:198-207)."""
+        feat1s, feat2s, crosses) exactly as the reference (models_bid_pointconv.py:198-207):
+        flows/pcs/features as (B,C,N) (views of the point-major tensors)."""
         B = xyz1.shape[0]
-        pc = torch.cat([xyz1, xyz2], 0).permute(0, 2, 1)
-        color = torch.cat([color1, color2], 0).permute(0, 2, 1)
+        pc = torch.cat([xyz1, xyz2], 0)
+        color = torch.cat([color1, color2], 0)
         pcs, feats, feats_out, fps, feat_l4_3 = self._encode(pc, color)
         one = lambda t: t[:B]  # noqa: E731
         two = lambda t: t[B:]  # noqa: E731
 
         # ---- level 3 (coarsest): no prior flow
-        c_feat_l3 = torch.cat([feats[3], feat_l4_3], dim=1)
-        f1n, f2n, cross3 = self.cross3(one(pcs[3]), two(pcs[3]), one(c_feat_l3), two(c_feat_l3))
-        feat_est, flow = self.flow3(one(pcs[3]), one(feats[3]), cross3)
+        c_feat_l3 = torch.cat([feats[3], feat_l4_3], dim=-1)
+        f1n, f2n, cross3 = self.cross3.forward_pair(pcs[3], c_feat_l3)
+        feat_est, flow = self.flow3.forward_cl(one(pcs[3]), one(feats[3]), cross3)
         flows, crosses, up_feats = [flow], [cross3], []
 
         decoders = [(2, self.cross2, self.flow2, self.deconv3_2),
@@ -107,26 +111,30 @@ class PointConvBidirection(nn.Module):
             # one 3-NN search per level pair serves all three upsamplings (both clouds'
             # features, and pc1's flow and estimator features: its first B rows)
             up_idx = self.upsample.neighbours(pcs[lv], pcs[lv + 1])
-            f_up = deconv(self.upsample(pcs[lv], pcs[lv + 1], torch.cat([f1n, f2n], 0), up_idx))
+            f_up = deconv.cl(self.upsample.forward_cl(pcs[lv], pcs[lv + 1],
+                                                      torch.cat([f1n, f2n], 0), up_idx))
             up_feats.append(f_up)
-            c_feat = torch.cat([feats[lv], f_up], dim=1)
+            c_feat = torch.cat([feats[lv], f_up], dim=-1)
             pc1_lv, pc2_lv = one(pcs[lv]), two(pcs[lv])
-            up_flow = self.upsample(pc1_lv, one(pcs[lv + 1]), self.scale * flow, up_idx[:B])
-            pc2_warp = self.warping(pc1_lv, pc2_lv, up_flow)
-            out = cross(pc1_lv, pc2_warp, one(c_feat), two(c_feat))
-            f1n, f2n, cost = out
-            feat_up = self.upsample(pc1_lv, one(pcs[lv + 1]), feat_est, up_idx[:B])
-            new_feat1 = torch.cat([one(feats[lv]), feat_up], dim=1)
-            feat_est, flow = flow_est(pc1_lv, new_feat1, cost, up_flow)
+            sflow = flow if self.scale == 1.0 else self.scale * flow  # x1.0 is exact
+            up_flow = self.upsample.forward_cl(pc1_lv, one(pcs[lv + 1]), sflow,
+                                               up_idx[:B])
+            pc2_warp = self.warping.forward_cl(pc1_lv, pc2_lv, up_flow)
+            f1n, f2n, cost = cross.forward_pair(torch.cat([pc1_lv, pc2_warp], 0), c_feat)
+            feat_up = self.upsample.forward_cl(pc1_lv, one(pcs[lv + 1]), feat_est, up_idx[:B])
+            new_feat1 = torch.cat([one(feats[lv]), feat_up], dim=-1)
+            feat_est, flow = flow_est.forward_cl(pc1_lv, new_feat1, cost, up_flow)
             flows.insert(0, flow)
             crosses.insert(0, cost)
 
-        pc1 = [one(p) for p in pcs]
-        pc2 = [two(p) for p in pcs]
+        cn = lambda t: t.permute(0, 2, 1)  # noqa: E731  point-major -> reference (B,C,N) view
+        pc1 = [cn(one(p)) for p in pcs]
+        pc2 = [cn(two(p)) for p in pcs]
         fps_pc1_idxs = [one(i) for i in fps]
         fps_pc2_idxs = [two(i) for i in fps]
         # feat{1,2}s = [l0_1, l1_2, l2_3, l3_4, l3_2, l2_1, l1_0] (reference :203-204)
         enc = feats_out[:4]
-        feat1s = [one(t) for t in enc] + [one(t) for t in up_feats]
-        feat2s = [two(t) for t in enc] + [two(t) for t in up_feats]
-        return flows, fps_pc1_idxs, fps_pc2_idxs, pc1, pc2, feat1s, feat2s, crosses
+        feat1s = [cn(one(t)) for t in enc] + [cn(one(t)) for t in up_feats]
+        feat2s = [cn(two(t)) for t in enc] + [cn(two(t)) for t in up_feats]
+        return ([cn(f) for f in flows], fps_pc1_idxs, fps_pc2_idxs, pc1, pc2, feat1s, feat2s,
+                [cn(c) for c in crosses])

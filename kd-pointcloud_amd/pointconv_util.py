@@ -50,6 +50,14 @@ class Conv1d(nn.Module):
             return self.composed_module(x)
         return act(norm(conv1x1(x, conv)))
 
+    def cl(self, x):
+        """The same layer on a point-major tensor (..., C_in) -> (..., C_out): one GEMM over
+        the points, no layout change."""
+        conv, norm, act = self.composed_module
+        if conv.kernel_size != (1,) or conv.stride != (1,) or conv.padding != (0,):
+            return self(x.transpose(-1, -2)).transpose(-1, -2)
+        return act(_bn_last(norm, linear_1x1(conv, x)))
+
 
 class Conv2d(nn.Module):
     """1x1 Conv2d + (BN | Identity) + activation.  Reference: pointconv_util.py:37-54."""
@@ -78,6 +86,20 @@ class Conv2d(nn.Module):
 _linear_1x1 = linear_1x1
 
 
+_BN_CHANNEL_MAJOR = False  # test seam: True runs BN on the (B,C,N) view (rounding probe)
+
+
+def _bn_last(norm, y):
+    """BatchNorm over the last (channel) dim of a point-major tensor: the same per-channel
+    statistics as the reference's BN on (B,C,N), computed over all other dims."""
+    if isinstance(norm, nn.Identity):
+        return y
+    shp = y.shape
+    if _BN_CHANNEL_MAJOR and y.dim() == 3:
+        return norm(y.permute(0, 2, 1).contiguous()).permute(0, 2, 1)
+    return norm(y.reshape(-1, shp[-1])).view(shp)
+
+
 # ------------------------------------------------------------------------------ point ops
 def square_distance(src, dst):
     """Reference: pointconv_util.py:73-94 (expanded form, materialised (B,N,M))."""
@@ -87,6 +109,11 @@ def square_distance(src, dst):
     dist += torch.sum(src ** 2, -1).view(B, N, 1)
     dist += torch.sum(dst ** 2, -1).view(B, 1, M)
     return dist
+
+
+def _cl(t):
+    """(B,C,N) reference layout -> contiguous point-major (B,N,C)."""
+    return t.permute(0, 2, 1).contiguous()
 
 
 _knn_override = None
@@ -291,10 +318,9 @@ class _PointConvBase(nn.Module):
         return linear(a, self.linear.weight, self.linear.bias)
 
     def _finish(self, new_points):
-        """(B,S,out) -> optional BN1d + activation -> (B,out,S)."""
-        new_points = new_points.permute(0, 2, 1)
+        """(B,S,out) -> optional BN1d (per channel, over B and S) + activation, point-major."""
         if self.bn:
-            new_points = self.bn_linear(new_points)
+            new_points = _bn_last(self.bn_linear, new_points)
         return self.relu(new_points)
 
 
@@ -314,10 +340,13 @@ class PointConv(_PointConvBase):
     def forward(self, xyz, points, knn_idx=None):
         """xyz (B,3,N), points (B,D,N) -> (B,out,N).  knn_idx: optional precomputed
         self-kNN (B,N,nsample) of xyz (the estimator's two PointConvs share one)."""
-        xyz = xyz.permute(0, 2, 1).contiguous()
-        points = points.permute(0, 2, 1)
+        return self.forward_cl(_cl(xyz), _cl(points), knn_idx).permute(0, 2, 1)
+
+    def forward_cl(self, xyz, points, knn_idx=None):
+        """Point-major: xyz (B,N,3), points (B,N,D) -> (B,N,out)."""
+        xyz = xyz.contiguous()
         idx = knn_point(self.nsample, xyz, xyz) if knn_idx is None else knn_idx
-        return self._finish(self._linear_features(xyz, xyz, points, idx))
+        return self._finish(self._linear_features(xyz, xyz, points.contiguous(), idx))
 
 
 class PointConvD(_PointConvBase):
@@ -337,13 +366,20 @@ class PointConvD(_PointConvBase):
 
     def forward(self, xyz, points):
         """xyz (B,3,N), points (B,D,N) -> (new_xyz (B,3,S), feats (B,out,S), fps_idx (B,S))."""
-        xyz = xyz.permute(0, 2, 1).contiguous()
-        points = points.permute(0, 2, 1)
-        fps_idx = pointnet2_utils.furthest_point_sample(xyz, self.npoint)
+        new_xyz, new_points, fps_idx = self.forward_cl(_cl(xyz), _cl(points))
+        return new_xyz.permute(0, 2, 1), new_points.permute(0, 2, 1), fps_idx
+
+    def forward_cl(self, xyz, points, fps_idx=None):
+        """Point-major: xyz (B,N,3), points (B,N,D) -> (new_xyz (B,S,3), feats (B,S,out),
+        fps_idx (B,S)).  fps_idx: optional precomputed FPS of xyz (the model runs the whole
+        FPS chain ahead, on a side stream)."""
+        xyz = xyz.contiguous()
+        if fps_idx is None:
+            fps_idx = pointnet2_utils.furthest_point_sample(xyz, self.npoint)
         new_xyz = index_points_gather(xyz, fps_idx)
         idx = knn_point(self.nsample, xyz, new_xyz)  # group_query()
-        new_points = self._finish(self._linear_features(xyz, new_xyz, points, idx))
-        return new_xyz.permute(0, 2, 1), new_points, fps_idx
+        new_points = self._finish(self._linear_features(xyz, new_xyz, points.contiguous(), idx))
+        return new_xyz, new_points, fps_idx
 
 
 class _CostVolume(torch.autograd.Function):
@@ -391,30 +427,63 @@ def _fusable(nsample, pos, mlp, act, din):
 
 
 def _cost_volume(nsample, xyz1, xyz2, points1, points2, pos, mlp, act, knn_idx=None):
+    """Reference layout wrapper: xyz (B,3,N*), points (B,D,N*) -> (B,D_out,N1)."""
+    return _cost_volume_cl(nsample, _cl(xyz1), _cl(xyz2), _cl(points1), _cl(points2), pos, mlp,
+                           act, knn_idx).permute(0, 2, 1)
+
+
+def _cost_volume_cl(nsample, x1, x2, p1, p2, pos, mlp, act, knn_idx=None):
     """Shared math of CrossLayerLight.cross (pointconv_util.py:1826-1850) and
     FlowEmbeddingLayer.forward (:1497-1517) on the point-major layout:
         h = act(P2[idx] + P1 + pos(x2[idx] - x1)); h = mlp(h); max over K.
-    xyz (B,3,N*), points (B,D,N*) -> (B,D_out,N1)."""
-    B, C, N1 = xyz1.shape
-    x1 = xyz1.permute(0, 2, 1).contiguous()
-    x2 = xyz2.permute(0, 2, 1).contiguous()
-    p1 = points1.permute(0, 2, 1)
-    p2 = points2.permute(0, 2, 1)
+    x* (B,N*,3), p* (B,N*,D) -> (B,N1,D_out)."""
+    B, N1, C = x1.shape
+    x1 = x1.contiguous()
+    x2 = x2.contiguous()
     if knn_idx is None:
         knn_idx = knn_point(nsample, x2, x1)
     din = p1.shape[-1]
     if _fusable(nsample, pos, mlp, act, din):
         conv = mlp[0].composed_module[0]
-        out = _CostVolume.apply(x1, x2, knn_idx, p1.contiguous(), p2.contiguous(),
-                                pos.weight.view(din, 3), pos.bias,
-                                conv.weight.view(conv.out_channels, din), conv.bias)
-        return out.permute(0, 2, 1)
+        return _CostVolume.apply(x1, x2, knn_idx, p1.contiguous(), p2.contiguous(),
+                                 pos.weight.view(din, 3), pos.bias,
+                                 conv.weight.view(conv.out_channels, din), conv.bias)
     direction = index_points_group(x2, knn_idx) - x1.view(B, N1, 1, C)
     grouped_points2 = index_points_group(p2, knn_idx)
     h = act((grouped_points2 + p1.unsqueeze(2)) + _linear_1x1(pos, direction))
     for conv in mlp:
         h = conv.channel_last(h)
-    return h.max(dim=2)[0].permute(0, 2, 1)
+    return _max_over_neighbours(h)
+
+
+class _MaxFirst(torch.autograd.Function):
+    """max over dim 2 of (B,N,K,C) with the reference's tie rule: F.max_pool2d over the K
+    window (pointconv_util.py:1848) keeps the FIRST maximal neighbour in K order, and its
+    backward routes the gradient there.  (torch.max(dim) does not promise an order for
+    ties on the GPU; exact ties do occur, e.g. between neighbours whose post-LReLU rows
+    coincide.)"""
+
+    @staticmethod
+    def forward(ctx, h):
+        B, N, K, C = h.shape
+        m = h.amax(dim=2, keepdim=True)
+        ks = torch.arange(K, device=h.device, dtype=torch.int32).view(1, 1, K, 1)
+        first = torch.where(h == m, ks, K).amin(dim=2, keepdim=True)
+        ctx.save_for_backward(first)
+        ctx.k = K
+        return m.squeeze(2)
+
+    @staticmethod
+    def backward(ctx, g):
+        (first,) = ctx.saved_tensors
+        B, N, _, C = first.shape
+        out = g.new_zeros((B, N, ctx.k, C))
+        out.scatter_(2, first.long(), g.unsqueeze(2))
+        return out
+
+
+def _max_over_neighbours(h):
+    return _MaxFirst.apply(h)
 
 
 class CrossLayerLight(nn.Module):
@@ -459,26 +528,35 @@ class CrossLayerLight(nn.Module):
                             knn_idx)
 
     def forward(self, pc1, pc2, feat1, feat2):
-        """Both directions of the first cost volume run as ONE batch of 2B (shared weights,
-        no BN between them), then the pc1-side refinement with pos2/mlp2."""
-        B = pc1.shape[0]
-        xa = torch.cat([pc1, pc2], 0)
-        xb = torch.cat([pc2, pc1], 0)
-        fa = torch.cat([feat1, feat2], 0)
-        fb = torch.cat([feat2, feat1], 0)
+        """Reference layout: pc* (B,3,N), feat* (B,C,N) -> (B,D,N) tensors."""
+        out = self.forward_cl(_cl(pc1), _cl(pc2), _cl(feat1), _cl(feat2))
+        return tuple(t.permute(0, 2, 1) for t in out)
+
+    def forward_cl(self, pc1, pc2, feat1, feat2):
+        """Point-major: pc* (B,N,3), feat* (B,N,C)."""
+        return self.forward_pair(torch.cat([pc1, pc2], 0), torch.cat([feat1, feat2], 0))
+
+    def forward_pair(self, xa, fa):
+        """Point-major pair batch: xa = cat(pc1, pc2) (2B,N,3), fa = cat(feat1, feat2).
+        Both directions of the first cost volume run as ONE batch of 2B (shared weights, no
+        BN between them), then the pc1-side refinement with pos2/mlp2."""
+        B = xa.shape[0] // 2
+        xb = torch.cat([xa[B:], xa[:B]], 0)
         # one kNN serves both directions, and its pc1 half is exactly the neighbour set of
         # the refinement cross(pc1, pc2) below (the reference searches it twice)
-        idx = knn_point(self.nsample, xb.permute(0, 2, 1).contiguous(),
-                        xa.permute(0, 2, 1).contiguous())
-        both = self.cross(xa, xb, conv1x1(fa, self.cross_t11), conv1x1(fb, self.cross_t22),
-                          self.pos1, self.mlp1, self.bn1, idx)
+        idx = knn_point(self.nsample, xb, xa)
+        ta = _linear_1x1(self.cross_t11, fa)
+        tb = _linear_1x1(self.cross_t22, fa)  # t22 of cat(feat2, feat1) = halves swapped
+        tb = torch.cat([tb[B:], tb[:B]], 0)
+        both = _cost_volume_cl(self.nsample, xa, xb, ta, tb, self.pos1, self.mlp1,
+                               self._act(self.bn1), idx)
         feat1_new, feat2_new = both[:B], both[B:]
         if self.mlp2 is False:
             return feat1_new, feat2_new
-        feat1_new = conv1x1(feat1_new, self.cross_t1)
-        feat2_new = conv1x1(feat2_new, self.cross_t2)
-        feat1_final = self.cross(pc1, pc2, feat1_new, feat2_new, self.pos2, self.mlp2, self.bn2,
-                                 idx[:B])
+        feat1_new = _linear_1x1(self.cross_t1, feat1_new)
+        feat2_new = _linear_1x1(self.cross_t2, feat2_new)
+        feat1_final = _cost_volume_cl(self.nsample, xa[:B], xa[B:], feat1_new, feat2_new,
+                                      self.pos2, self.mlp2, self._act(self.bn2), idx[:B])
         return feat1_new, feat2_new, feat1_final
 
 
@@ -504,8 +582,10 @@ class FlowEmbeddingLayer(nn.Module):
             def act(x):
                 shp = x.shape
                 return self.relu(self.bn(x.reshape(-1, shp[-1], 1, 1)).view(shp))
-        return _cost_volume(self.nsample, xyz1, xyz2, conv1x1(points1, self.t11),
-                            conv1x1(points2, self.t22), self.pos, self.mlp, act)
+        return _cost_volume_cl(self.nsample, _cl(xyz1), _cl(xyz2),
+                               _linear_1x1(self.t11, _cl(points1)),
+                               _linear_1x1(self.t22, _cl(points2)), self.pos, self.mlp,
+                               act).permute(0, 2, 1)
 
 
 class PointConvFlow(nn.Module):
@@ -571,15 +651,19 @@ class PointWarping(nn.Module):
     def forward(self, xyz1, xyz2, flow1=None):
         if flow1 is None:
             return xyz2
-        B, C, N1 = xyz1.shape
-        N2 = xyz2.shape[2]
-        xyz1_to_2 = (xyz1 + flow1).permute(0, 2, 1).contiguous()
-        x2 = xyz2.permute(0, 2, 1).contiguous()
-        f1 = flow1.permute(0, 2, 1)
+        return self.forward_cl(_cl(xyz1), _cl(xyz2), _cl(flow1)).permute(0, 2, 1)
+
+    def forward_cl(self, x1, x2, flow1=None):
+        """Point-major: x1 (B,N1,3), x2 (B,N2,3), flow1 (B,N1,3) -> warped x2 (B,N2,3)."""
+        if flow1 is None:
+            return x2
+        B, N2, C = x2.shape
+        xyz1_to_2 = (x1 + flow1).contiguous()
+        x2 = x2.contiguous()
         knn_idx = knn_point(3, xyz1_to_2, x2)
         grouped_xyz_norm = index_points_group(xyz1_to_2, knn_idx) - x2.view(B, N2, 1, C)
-        flow2 = _inverse_distance_blend(grouped_xyz_norm, index_points_group(f1, knn_idx))
-        return (x2 - flow2).permute(0, 2, 1)
+        flow2 = _inverse_distance_blend(grouped_xyz_norm, index_points_group(flow1, knn_idx))
+        return x2 - flow2
 
 
 class UpsampleFlow(nn.Module):
@@ -587,21 +671,21 @@ class UpsampleFlow(nn.Module):
 
     @staticmethod
     def neighbours(xyz, sparse_xyz):
-        """The 3-NN index this layer uses for (xyz, sparse_xyz); pass it back as knn_idx to
-        reuse it across upsamplings between the same two levels."""
-        return knn_point(3, sparse_xyz.permute(0, 2, 1).contiguous(),
-                         xyz.permute(0, 2, 1).contiguous())
+        """The 3-NN index this layer uses for point-major (xyz, sparse_xyz); pass it back as
+        knn_idx to reuse it across upsamplings between the same two levels."""
+        return knn_point(3, sparse_xyz.contiguous(), xyz.contiguous())
 
     def forward(self, xyz, sparse_xyz, sparse_flow, knn_idx=None):
-        B, C, N = xyz.shape
-        x = xyz.permute(0, 2, 1).contiguous()
-        sx = sparse_xyz.permute(0, 2, 1).contiguous()
-        sf = sparse_flow.permute(0, 2, 1)
+        return self.forward_cl(_cl(xyz), _cl(sparse_xyz), _cl(sparse_flow),
+                               knn_idx).permute(0, 2, 1)
+
+    def forward_cl(self, x, sx, sf, knn_idx=None):
+        """Point-major: x (B,N,3), sx (B,S,3), sf (B,S,C) -> (B,N,C)."""
+        B, N, C = x.shape
         if knn_idx is None:
-            knn_idx = knn_point(3, sx, x)
+            knn_idx = knn_point(3, sx.contiguous(), x.contiguous())
         grouped_xyz_norm = index_points_group(sx, knn_idx) - x.view(B, N, 1, C)
-        return _inverse_distance_blend(grouped_xyz_norm,
-                                       index_points_group(sf, knn_idx)).permute(0, 2, 1)
+        return _inverse_distance_blend(grouped_xyz_norm, index_points_group(sf, knn_idx))
 
 
 class SceneFlowEstimatorResidual(nn.Module):
@@ -625,15 +709,22 @@ class SceneFlowEstimatorResidual(nn.Module):
         self.fc = nn.Conv1d(last_channel, 3, 1)
 
     def forward(self, xyz, feats, cost_volume, flow=None):
-        new_points = torch.cat([feats, cost_volume], dim=1)
+        new_points, flow = self.forward_cl(_cl(xyz), _cl(feats), _cl(cost_volume),
+                                           None if flow is None else _cl(flow))
+        return new_points.permute(0, 2, 1), flow.permute(0, 2, 1)
+
+    def forward_cl(self, xyz, feats, cost_volume, flow=None):
+        """Point-major: xyz (B,N,3), feats (B,N,F), cost (B,N,C), flow (B,N,3)."""
+        new_points = torch.cat([feats, cost_volume], dim=-1)
         # every PointConv here groups the same cloud with the same K: one self-kNN
-        x = xyz.permute(0, 2, 1).contiguous()
-        knn_idx = knn_point(self.pointconv_list[0].nsample, x, x) if len(self.pointconv_list) else None
+        xyz = xyz.contiguous()
+        knn_idx = knn_point(self.pointconv_list[0].nsample, xyz, xyz) \
+            if len(self.pointconv_list) else None
         for pointconv in self.pointconv_list:
             same = pointconv.nsample == self.pointconv_list[0].nsample
-            new_points = pointconv(xyz, new_points, knn_idx if same else None)
+            new_points = pointconv.forward_cl(xyz, new_points, knn_idx if same else None)
         for conv in self.mlp_convs:
-            new_points = conv(new_points)
-        flow_local = conv1x1(new_points, self.fc).clamp(self.clamp[0], self.clamp[1])
+            new_points = conv.cl(new_points)
+        flow_local = _linear_1x1(self.fc, new_points).clamp(self.clamp[0], self.clamp[1])
         flow = flow_local if flow is None else flow_local + flow
         return new_points, flow

@@ -1,0 +1,92 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.  Float64 run of the REFERENCE model on the kNN-trace
+fixture (tests/golden/model_knntrace_n2048.npz), for the gradient parity tolerance.
+
+The fixture's fp32 reference gradients carry the reference's own fp32 rounding error.  Some
+per-parameter gradient sums are near-cancelling (layers just upstream of train-mode
+BatchNorm, LeakyReLU pre-activations within rounding of 0), so two correct fp32
+implementations can differ there by more than a fixed 1e-4 of |grad|.  This script runs the
+same reference code (imported as in make_fixtures.py) in float64, with every knn_point call
+replaying the recorded fp32 reference indices in call order and FPS computed by the C
+restatement on the (exactly gathered) fp32 coordinates, and stores the float64 gradient
+sums: the test then allows the GPU build the reference's own fp32 error |g32 - g64| per
+parameter.
+
+    python oracle/make_f64_fixture.py    -> tests/golden/model_knntrace_n2048_f64.npz
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import make_fixtures as MF  # noqa: E402
+
+
+def main(n=2048):
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    R = MF.setup_reference()
+    g = np.load(os.path.join(MF.GOLDEN, f"model_knntrace_n{n}.npz"))
+    calls = [(int(g[f"knn{i}_k"]), g[f"knn{i}_rsum"], g[f"knn{i}_qsum"],
+              g[f"knn{i}_idx"].astype(np.int64)) for i in range(int(g["n_calls"]))]
+    pos = {"i": 0, "worst": 0.0}
+
+    def replay(nsample, xyz, new_xyz):
+        k, rs, qs, idx = calls[pos["i"]]
+        pos["i"] += 1
+        x = xyz.detach().double().numpy()[0]
+        q = new_xyz.detach().double().numpy()[0]
+        e = max(np.abs(np.concatenate([x.sum(0), (x ** 2).sum(0)]) - rs).max() / (np.abs(rs).max() + 1),
+                np.abs(np.concatenate([q.sum(0), (q ** 2).sum(0)]) - qs).max() / (np.abs(qs).max() + 1))
+        assert k == nsample and idx.shape == (q.shape[0], nsample), (pos["i"], k, nsample)
+        pos["worst"] = max(pos["worst"], e)
+        return torch.from_numpy(idx[None])
+
+    stub = sys.modules["pointnet2_cuda"]
+    fps32 = stub.furthest_point_sampling_wrapper
+
+    def fps(b, n_, npoint, points, temp, idx):
+        return fps32(b, n_, npoint, points.float(), temp, idx)
+    stub.furthest_point_sampling_wrapper = fps
+    mods = (R.pcu, sys.modules["pointconv_util2"])
+    orig = {m: m.knn_point for m in mods}
+    f32 = torch.cuda.FloatTensor
+    torch.cuda.FloatTensor = lambda *s: torch.empty(*s, dtype=torch.float64)
+    for m in mods:
+        m.knn_point = replay
+    try:
+        pos1, pos2, flow = (torch.from_numpy(g[k]).double() for k in ("pos1", "pos2", "flow"))
+        teacher = MF._synth(R.teacher.PointConvBidirection(), seed=1).double().eval()
+        student = MF._synth(R.student.PointConvBidirection(), seed=2).double().train()
+        with torch.no_grad():
+            t_out = teacher(pos1, pos2, pos1, pos2)
+        s_out = student(pos1, pos2, pos1, pos2)
+        flows, f1i, f2i, _, _, feat1s, feat2s, _ = s_out
+        kd = R.loss.biDirection_loss_ht(flows, feat1s, feat2s, f1i, f2i, flow, t_out[0],
+                                        t_out[5], t_out[6], t_out[1], t_out[2], 0.3, 0.8, layer=3)
+        kd.backward()
+    finally:
+        for m, fn in orig.items():
+            m.knn_point = fn
+        torch.cuda.FloatTensor = f32
+        stub.furthest_point_sampling_wrapper = fps32
+    assert pos["i"] == len(calls), (pos["i"], len(calls))
+    out = {
+        "grad_sum_f64": np.array([float(p.grad.sum()) if p.grad is not None else 0.0
+                                  for _, p in student.named_parameters()]),
+        "kd_f64": kd.detach().numpy(),
+        "replay_worst": np.array(pos["worst"]),
+    }
+    for i in range(4):
+        out[f"s_flow{i}_f64"] = flows[i].detach().numpy()
+    path = os.path.join(MF.GOLDEN, f"model_knntrace_n{n}_f64.npz")
+    np.savez_compressed(path, **out)
+    d = np.abs(out["grad_sum_f64"] - g["grad_sum"]) / (g["grad_abs"] + 1e-12)
+    print("replay worst", pos["worst"], "kd32", float(g["kd"]), "kd64", float(out["kd_f64"]))
+    print("reference fp32 vs fp64 grad-sum error / |grad|: max", d.max(), "median", np.median(d))
+    print("wrote", path)
+
+
+if __name__ == "__main__":
+    main()

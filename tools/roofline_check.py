@@ -1,0 +1,48 @@
+"""Cross-check bench.py's live roofline against a rocprofv3 --kernel-trace of the same command.
+
+    python tools/roofline_check.py <rocprof dir with *kernel_trace.csv> <bench json line file>
+
+For each roofline entry point in the bench line: rocprof per-launch duration = the summed
+durations of its HIP kernels / launches of its first kernel, next to the live HIP-event
+average (avg_launch_us).
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import bench
+    d, bench_file = sys.argv[1], sys.argv[2]
+    line = None
+    for ln in open(bench_file):
+        ln = ln.strip()
+        if ln.startswith("{") and '"metric"' in ln:
+            line = json.loads(ln)
+    trace = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)[0]
+    rows = list(csv.DictReader(open(trace)))
+    out = {}
+    for key in ("roofline", "roofline_gather"):
+        r = line.get(key) if line else None
+        if not r:
+            continue
+        kernels = bench.ROOFLINE[r["kernel"]][3]
+        head = kernels[0]
+        n = sum(1 for x in rows if head in x["Kernel_Name"])
+        tot = sum(int(x["End_Timestamp"]) - int(x["Start_Timestamp"]) for x in rows
+                  if any(k in x["Kernel_Name"] for k in kernels))
+        rp = tot / max(n, 1) / 1e3
+        out[key] = {"entry": r["kernel"], "hip_kernels": kernels, "rocprof_launches": n,
+                    "rocprof_avg_us_per_launch": round(rp, 2),
+                    "live_hip_event_avg_us": r["avg_launch_us"],
+                    "ratio_live_over_rocprof": round(r["avg_launch_us"] / rp, 3) if rp else None}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
