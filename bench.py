@@ -67,6 +67,12 @@ def parse():
     ap.add_argument("--roofline-kernel", default=PRIMARY_KERNEL)
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the step from HIP graphs (distill.GraphedStep) instead of the "
+                         "eager step (DDP for N>1); round 1: the eager step is GPU-bound and "
+                         "the graph replay was ~10 %% slower, so eager is the default")
+    ap.add_argument("--measure-steps", type=int, default=2,
+                    help="eager steps after the timed region for the per-kernel roofline")
     return ap.parse_args()
 
 
@@ -150,19 +156,9 @@ def main():
 
     import kdpc_native
     import synthetic
-    from distill import FlowTrainStep, KDTrainStep, make_optimizer, wrap_ddp
+    from distill import (FlowTrainStep, KDTrainStep, graphed_flow_step, graphed_kd_step,
+                         make_optimizer, wrap_ddp)
     from models_bid_pointconv import PointConvBidirection
-
-    torch.manual_seed(0)
-    student = PointConvBidirection().to(dev)
-    model = wrap_ddp(student, dev)
-    opt = make_optimizer(model)
-    if args.mode == "kd":
-        torch.manual_seed(1)
-        teacher = PointConvBidirection().to(dev)
-        step = KDTrainStep(teacher, model, opt)
-    else:
-        step = FlowTrainStep(model, opt)
 
     # inputs resident in HBM before timing; a few distinct batches per rank, cycled
     nb = 4
@@ -172,13 +168,34 @@ def main():
                                           first_pair=i * args.batch)
         batches.append(tuple(torch.from_numpy(a).to(dev) for a in (p1, p2, fl)))
 
+    torch.manual_seed(0)
+    student = PointConvBidirection().to(dev)
+    teacher = None
+    if args.mode == "kd":
+        torch.manual_seed(1)
+        teacher = PointConvBidirection().to(dev)
+    if args.graph:
+        if world > 1:  # replicas start identical (DDP does this broadcast at construction)
+            for t in list(student.parameters()) + list(student.buffers()):
+                dist.broadcast(t.data, 0)
+        opt = make_optimizer(student, capturable=True)
+        if args.mode == "kd":
+            step = graphed_kd_step(teacher, student, opt, batches[0])
+        else:
+            step = graphed_flow_step(student, opt, batches[0])
+        eager = (KDTrainStep(teacher, student, opt) if args.mode == "kd"
+                 else FlowTrainStep(student, opt))
+    else:
+        model = wrap_ddp(student, dev)
+        opt = make_optimizer(model)
+        step = KDTrainStep(teacher, model, opt) if args.mode == "kd" else FlowTrainStep(model, opt)
+        eager = step
+
     for i in range(args.warmup):
         step(*batches[i % nb])
-    timer = kdpc_native.LaunchTimer([args.roofline_kernel, GATHER_KERNEL])
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    kdpc_native.set_launch_timer(timer)
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(*batches[i % nb])
@@ -186,12 +203,20 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    kdpc_native.set_launch_timer(None)
     if world > 1:
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
+    # per-kernel roofline: HIP events around every launch of the named C entry points, over
+    # eager replays of the same step after the timed region (a graph replay has no
+    # per-launch host hook); kernel durations do not depend on how the launch was issued
+    timer = kdpc_native.LaunchTimer([args.roofline_kernel, GATHER_KERNEL])
+    kdpc_native.set_launch_timer(timer)
+    for i in range(args.measure_steps):
+        eager(*batches[i % nb])
+    torch.cuda.synchronize()
+    kdpc_native.set_launch_timer(None)
     summary = timer.summary()
     roof = roofline(args.roofline_kernel, summary.get(args.roofline_kernel))
     roof_gather = roofline(GATHER_KERNEL, summary.get(GATHER_KERNEL))
@@ -210,7 +235,8 @@ def main():
                    "KD step: teacher fwd + student fwd+bwd + biDirection_loss_ht (configs[3])",
                    "model": "models_bid_pointconv.PointConvBidirection",
                    "batch_per_gpu": args.batch, "global_batch": world * args.batch,
-                   "npoints": args.npoints, "parallelism": f"ddp{world}"},
+                   "npoints": args.npoints, "parallelism": f"dp{world}",
+                   "step": "hip-graph" if args.graph else "eager"},
         "roofline": roof,
         "roofline_gather": roof_gather,
     }

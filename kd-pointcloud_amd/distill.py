@@ -36,10 +36,11 @@ def wrap_ddp(model, device=None):
     return torch.nn.parallel.DistributedDataParallel(model, **kw)
 
 
-def make_optimizer(model, lr=1e-3, weight_decay=1e-4):
-    """Adam as configured by config_train_kd_pointconv.yaml:15-24 / distilTrain.py:134-135."""
+def make_optimizer(model, lr=1e-3, weight_decay=1e-4, capturable=False):
+    """Adam as configured by config_train_kd_pointconv.yaml:15-24 / distilTrain.py:134-135.
+    capturable=True keeps the step counters on the device (required by GraphedStep)."""
     return torch.optim.Adam(model.parameters(), lr=lr, betas=(0.9, 0.999), eps=1e-08,
-                            weight_decay=weight_decay)
+                            weight_decay=weight_decay, capturable=capturable)
 
 
 class FlowTrainStep:
@@ -99,3 +100,110 @@ def epe3d(model, pos1, pos2, flow):
     model.eval()
     flows = model(pos1, pos2, pos1, pos2)[0]
     return torch.norm(flows[0].permute(0, 2, 1) - flow, dim=2).mean()
+
+
+class GraphedStep:
+    """One training step replayed from HIP graphs (MI355X: the eager step issues ~2000
+    launches per iteration from Python, ~27 ms of host time, more than the GPU needs).
+
+        graph A: forward + loss + backward (+ packing the gradients into one flat buffer)
+        eager:   one all_reduce of the flat gradient buffer (world > 1; RCCL over xGMI)
+        graph B: unpack the averaged gradients + optimizer step (Adam, capturable=True)
+
+    The collective stays outside the graphs on purpose: it is one 31.8 MB all-reduce per
+    step, and keeping it eager avoids depending on collective capture.  `loss_fn(*inputs)`
+    must run the whole forward (model call(s) and loss) and return the loss; the inputs are
+    copied into static buffers before each replay.  Warm-up iterations run eagerly on a side
+    stream (they allocate lazily-initialised state: optimizer moments, cached attributes)."""
+
+    def __init__(self, loss_fn, params, optimizer, example_inputs, warmup=3):
+        self.loss_fn = loss_fn
+        self.opt = optimizer
+        self.params = [p for p in params if p.requires_grad]
+        self.static = [t.detach().clone() for t in example_inputs]
+        self.world = dist.get_world_size() if is_dist() else 1
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self.opt.zero_grad(set_to_none=True)
+                loss = self.loss_fn(*self.static)
+                loss.backward()
+                self._allreduce_eager()
+                self.opt.step()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        # graph A: forward + backward; .grad tensors are allocated inside (static addresses)
+        self.opt.zero_grad(set_to_none=True)
+        self.graph_a = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph_a):
+            self.loss = self.loss_fn(*self.static)
+            self.loss.backward()
+            self.grads = [p.grad for p in self.params if p.grad is not None]
+            self.flat = torch.cat([g.reshape(-1) for g in self.grads]) if self.world > 1 else None
+        # graph B: unpack + optimizer step
+        self.graph_b = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph_b, pool=self.graph_a.pool()):
+            if self.world > 1:
+                self._unpack()
+            self.opt.step()
+        torch.cuda.synchronize()
+
+    def _unpack(self):
+        off = 0
+        for g in self.grads:
+            n = g.numel()
+            g.copy_(self.flat[off:off + n].view_as(g))
+            off += n
+        torch._foreach_div_(self.grads, float(self.world))
+
+    def _allreduce_eager(self):
+        """Warm-up path: the same averaging as the graphed step, eagerly."""
+        if self.world == 1:
+            return
+        grads = [p.grad for p in self.params if p.grad is not None]
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        dist.all_reduce(flat)
+        off = 0
+        for g in grads:
+            g.copy_(flat[off:off + g.numel()].view_as(g))
+            off += g.numel()
+        torch._foreach_div_(grads, float(self.world))
+
+    def __call__(self, *inputs):
+        for s, t in zip(self.static, inputs):
+            s.copy_(t, non_blocking=True)
+        self.graph_a.replay()
+        if self.world > 1:
+            dist.all_reduce(self.flat)
+        self.graph_b.replay()
+        return self.loss.detach()
+
+
+def graphed_flow_step(model, optimizer, example_inputs, loss_fn=None, warmup=3):
+    """FlowTrainStep as a GraphedStep (model: the bare module, not DDP-wrapped)."""
+    loss_fn = loss_fn or loss_functions.multiScaleLoss
+    model.train()
+
+    def run(pos1, pos2, flow):
+        flows, fps1, _, _, _, _, _, _ = model(pos1, pos2, pos1, pos2)
+        return loss_fn(flows, flow, fps1)
+    return GraphedStep(run, model.parameters(), optimizer, example_inputs, warmup)
+
+
+def graphed_kd_step(teacher, student, optimizer, example_inputs, gamma=0.3, beta=0.8, layer=3,
+                    warmup=3):
+    """KDTrainStep (distilTrain.py:164-182) as a GraphedStep."""
+    for p in teacher.parameters():
+        p.requires_grad_(False)
+    teacher.eval()
+    student.train()
+
+    def run(pos1, pos2, flow):
+        with torch.no_grad():
+            t_flows, t_fps1, t_fps2, _, _, t_feat1s, t_feat2s, _ = teacher(pos1, pos2, pos1, pos2)
+        flows, fps1, fps2, _, _, feat1s, feat2s, _ = student(pos1, pos2, pos1, pos2)
+        return loss_functions.biDirection_loss_ht(
+            flows, feat1s, feat2s, fps1, fps2, flow, t_flows, t_feat1s, t_feat2s, t_fps1, t_fps2,
+            gamma, beta, layer=layer)
+    return GraphedStep(run, student.parameters(), optimizer, example_inputs, warmup)
