@@ -196,6 +196,27 @@ int kdpc_pointconv_bwd(int b, int n, int s, int k, int d, int o, const float *xy
                        float *dxyz, float *dfeats, float *dcenter, float *dwt, float *dwl,
                        void *workspace, size_t workspace_bytes, void *stream);
 
+/* ---- fused WeightNet over grouped offsets (pointconv_util.py:184-215 as used by
+ *      PointConv/PointConvD :217-258, :401-446: weightnet=16, hidden [8, 8], no BN) ------ */
+
+/* Packed parameter layout (floats): W0 (8,3) | b0 (8) | W1 (8,8) | b1 (8) | W2 (16,8) |
+ * b2 (16), row-major nn.Conv2d weights; kdpc_weightnet_param_count() = 248. */
+int kdpc_weightnet_param_count(void);
+
+/* wt (B,S,K,16) = ReLU(W2 ReLU(W1 ReLU(W0 rel + b0) + b1) + b2) with
+ * rel = xyz[b, idx[b,s,k]] - center[b,s].  xyz (B,N,3), center (B,S,3), idx (B,S,K). */
+int kdpc_weightnet_fwd(int b, int n, int s, int k, const float *xyz, const float *center,
+                       const int *idx, const float *params, float *wt, void *stream);
+
+/* Scratch bytes kdpc_weightnet_bwd needs (independent of the problem size). */
+size_t kdpc_weightnet_bwd_workspace_bytes(void);
+
+/* Backward of kdpc_weightnet_fwd for dwt (B,S,K,16): overwrites dparams (packed, 248) with
+ * deterministic fixed-order sums (no atomics) and, if drel != NULL, writes drel (B,S,K,3). */
+int kdpc_weightnet_bwd(int b, int n, int s, int k, const float *xyz, const float *center,
+                       const int *idx, const float *params, const float *dwt, float *drel,
+                       float *dparams, void *workspace, size_t workspace_bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -43,10 +43,15 @@ _SIGNATURES = {
     "kdpc_pointconv_fwd": [_c_int] * 6 + [_vp] * 9 + [_c_size, _vp],
     "kdpc_pointconv_bwd_workspace_bytes": [_c_int] * 5,
     "kdpc_pointconv_bwd": [_c_int] * 6 + [_vp] * 15 + [_c_size, _vp],
+    "kdpc_weightnet_param_count": [],
+    "kdpc_weightnet_fwd": [_c_int] * 4 + [_vp] * 6,
+    "kdpc_weightnet_bwd_workspace_bytes": [],
+    "kdpc_weightnet_bwd": [_c_int] * 4 + [_vp] * 8 + [_c_size, _vp],
 }
 _RESTYPES = {"kdpc_csr_workspace_bytes": _c_size, "kdpc_cost_volume_bwd_workspace_bytes": _c_size,
              "kdpc_pointconv_fwd_workspace_bytes": _c_size,
-             "kdpc_pointconv_bwd_workspace_bytes": _c_size}
+             "kdpc_pointconv_bwd_workspace_bytes": _c_size,
+             "kdpc_weightnet_bwd_workspace_bytes": _c_size}
 
 EXPORTED = tuple(_SIGNATURES)
 
@@ -445,3 +450,36 @@ def pointconv_bwd(xyz, center, feats, idx, wt, wl, dy, csr, need_xyz=True):
           work=(4 * R * (2 * K * C + 32 * K + 2 * O) + 8 * O * 16 * C,
                 4.0 * R * K * C * 16 + 4.0 * R * 16 * C * O))
     return dxyz, dfeats, dcenter, dwt, dwl
+
+
+# ------------------------------------------------------------------- fused WeightNet
+def weightnet_fwd(xyz, center, idx, params):
+    """wt (B,S,K,16) from xyz (B,N,3), center (B,S,3), idx (B,S,K) i32 and the packed
+    WeightNet parameters (248 floats: W0 (8,3) b0 W1 (8,8) b1 W2 (16,8) b2)."""
+    B, N, _ = xyz.shape
+    S, K = idx.shape[1], idx.shape[2]
+    f = torch.float32
+    wt = torch.empty((B, S, K, 16), dtype=f, device=xyz.device)
+    _call("kdpc_weightnet_fwd", B, N, S, K, _dev(xyz, f, "xyz"), _dev(center, f, "center"),
+          _dev(idx, torch.int32, "idx"), _dev(params, f, "params"), _dev(wt, f, "wt"),
+          _stream(xyz),
+          work=(B * (12 * N + 12 * S + S * K * (4 + 64)), 2.0 * B * S * K * (24 + 64 + 128)))
+    return wt
+
+
+def weightnet_bwd(xyz, center, idx, params, dwt, need_rel=False):
+    """-> (drel (B,S,K,3) | None, dparams (248,) packed like params)."""
+    B, N, _ = xyz.shape
+    S, K = idx.shape[1], idx.shape[2]
+    f = torch.float32
+    dev = xyz.device
+    lib = load_library()
+    ws_bytes = lib.kdpc_weightnet_bwd_workspace_bytes()
+    ws = torch.empty((ws_bytes,), dtype=torch.uint8, device=dev)
+    dparams = torch.empty_like(params)
+    drel = torch.empty((B, S, K, 3), dtype=f, device=dev) if need_rel else None
+    _call("kdpc_weightnet_bwd", B, N, S, K, _dev(xyz, f, "xyz"), _dev(center, f, "center"),
+          _dev(idx, torch.int32, "idx"), _dev(params, f, "params"), _dev(dwt, f, "dwt"),
+          drel.data_ptr() if need_rel else None, _dev(dparams, f, "dparams"), ws.data_ptr(),
+          ws_bytes, _stream(xyz))
+    return drel, dparams

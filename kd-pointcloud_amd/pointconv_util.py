@@ -226,6 +226,23 @@ class WeightNet(nn.Module):
             w = F.relu(w)
         return w
 
+    def fusable(self):
+        """The shape the HIP kernel implements: 3 -> 8 -> 8 -> 16, ReLU, no BN (every
+        WeightNet of the KD models)."""
+        widths = [c.in_channels for c in self.mlp_convs] + [self.mlp_convs[-1].out_channels]
+        return _FUSED_WEIGHTNET and not self.bn and widths == [3, 8, 8, 16]
+
+    def grouped(self, xyz, center, idx):
+        """WeightNet of the grouped offsets xyz[idx] - center: xyz (B,N,3), center (B,S,3),
+        idx (B,S,K) int32 -> (B,S,K,out).  One fused HIP kernel each way where supported
+        (csrc/weightnet.hip); otherwise group + channel_last."""
+        if self.fusable():
+            params = torch.cat([t.reshape(-1) for c in self.mlp_convs for t in (c.weight, c.bias)])
+            return _WeightNetFn.apply(xyz.contiguous(), center.contiguous(),
+                                      _as_idx32(idx).contiguous(), params)
+        B, S, _ = center.shape
+        return self.channel_last(index_points_group(xyz, idx) - center.view(B, S, 1, 3))
+
     def channel_last(self, localized_xyz):
         """(..., 3) -> (..., out): the same MLP on the point-major layout."""
         w = localized_xyz
@@ -236,6 +253,33 @@ class WeightNet(nn.Module):
                 w = self.mlp_bns[i](w.reshape(-1, shp[-1])).view(shp)
             w = F.relu(w)
         return w
+
+
+_FUSED_WEIGHTNET = True  # test seam: False forces group + channel_last
+
+
+class _WeightNetFn(torch.autograd.Function):
+    """Fused grouped-offset WeightNet (csrc/weightnet.hip), packed parameters."""
+
+    @staticmethod
+    def forward(ctx, xyz, center, idx, params):
+        ctx.save_for_backward(xyz, center, idx, params)
+        return _nat.weightnet_fwd(xyz, center, idx, params)
+
+    @staticmethod
+    def backward(ctx, dwt):
+        xyz, center, idx, params = ctx.saved_tensors
+        need_rel = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
+        drel, dparams = _nat.weightnet_bwd(xyz, center, idx, params, dwt.contiguous(), need_rel)
+        dxyz = dcenter = None
+        if need_rel:
+            B, S, K, _ = drel.shape
+            N = xyz.shape[1]
+            if ctx.needs_input_grad[0]:
+                dxyz = _nat.group_rows_grad(drel.view(B, S * K, 3), _nat.csr_of(idx, N), B, N, 3)
+            if ctx.needs_input_grad[1]:
+                dcenter = -drel.sum(2)
+        return dxyz, dcenter, None, dparams
 
 
 class _PointConvContract(torch.autograd.Function):
@@ -309,8 +353,7 @@ class _PointConvBase(nn.Module):
         K, D = idx.shape[-1], points.shape[-1]
         if _FUSED_POINTCONV and self.weightnet.mlp_convs[-1].out_channels == 16 \
                 and _nat.pointconv_supported(K, D, self.linear.out_features):
-            grouped_xyz_norm = index_points_group(xyz, idx) - center.view(B, S, 1, 3)
-            weights = self.weightnet.channel_last(grouped_xyz_norm)
+            weights = self.weightnet.grouped(xyz, center, idx)
             return _PointConvLayer.apply(xyz.contiguous(), center.contiguous(),
                                          points.contiguous(), idx, weights.contiguous(),
                                          self.linear.weight, self.linear.bias)

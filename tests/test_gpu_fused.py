@@ -131,3 +131,37 @@ def test_pointconv_layer_vs_fp64(b, n, s, k, d, o):
     _scale_close(dcenter, Cn.grad, name="dcenter")
     _scale_close(dwt, Wt.grad, name="dwt")
     _scale_close(dwl, Wl.grad, name="dwl")
+
+
+@pytest.mark.parametrize("b,n,s,k", [(2, 700, 300, 9), (1, 100, 64, 16), (3, 50, 50, 1)])
+def test_weightnet_fused_vs_fp64(b, n, s, k):
+    """csrc/weightnet.hip (fwd, parameter grads, input grads) against an fp64 torch
+    evaluation of the reference WeightNet on the grouped offsets."""
+    import pointconv_util as P
+    g = torch.Generator(device="cpu").manual_seed(b * 100 + n + k)
+    wn = P.WeightNet(3, 16).to(DEV)
+    with torch.no_grad():
+        for c in wn.mlp_convs:  # some negative pre-activations at every layer
+            c.bias.copy_(torch.randn(c.bias.shape, generator=g) * 0.3)
+    xyz = torch.randn(b, n, 3, generator=g).to(DEV).requires_grad_(True)
+    center = torch.randn(b, s, 3, generator=g).to(DEV).requires_grad_(True)
+    idx = torch.randint(0, n, (b, s, k), generator=g, dtype=torch.int32).to(DEV)
+    dwt = torch.randn(b, s, k, 16, generator=g).to(DEV)
+    wt = wn.grouped(xyz, center, idx)
+    wt.backward(dwt)
+    got = [wt, xyz.grad, center.grad] + [t.grad for c in wn.mlp_convs for t in (c.weight, c.bias)]
+    # fp64 reference formulation
+    wn64 = P.WeightNet(3, 16).to(DEV).double()
+    wn64.load_state_dict({k2: v.double() for k2, v in wn.state_dict().items()})
+    X = xyz.detach().double().requires_grad_(True)
+    C = center.detach().double().requires_grad_(True)
+    bi = torch.arange(b, device=DEV).view(b, 1, 1)
+    rel = X[bi, idx.long()] - C.unsqueeze(2)
+    W = rel
+    for conv in wn64.mlp_convs:
+        W = torch.relu(W @ conv.weight.view(conv.out_channels, -1).t() + conv.bias)
+    W.backward(dwt.double())
+    want = [W, X.grad, C.grad] + [t.grad for c in wn64.mlp_convs for t in (c.weight, c.bias)]
+    names = ["wt", "dxyz", "dcenter", "dW0", "db0", "dW1", "db1", "dW2", "db2"]
+    for a, w, nm in zip(got, want, names):
+        _scale_close(a, w, rtol=2e-5, name=nm)

@@ -47,6 +47,15 @@ def main():
         f.write(prof.key_averages(group_by_input_shape=True).table(
             sort_by="self_device_time_total", row_limit=60, max_name_column_width=40,
             max_shapes_column_width=80))
+        f.write("\n\n==== ops by input shape (self device us per step, calls per step)\n")
+        shp = []
+        for e in prof.key_averages(group_by_input_shape=True):
+            t = getattr(e, "self_device_time_total", 0.0)
+            if t > 0 and e.key.startswith("aten::"):
+                shp.append((t / 2, e.count / 2, e.key, str(e.input_shapes)[:150]))
+        shp.sort(reverse=True)
+        for t, c, k, sh in shp[:150]:
+            f.write(f"{t:9.1f} {c:6.1f} {k:28s} {sh}\n")
         f.write("\n\n==== by call site (self device us per step, calls per step, op, stack)\n")
         rows = []
         for e in prof.key_averages(group_by_stack_n=8):
