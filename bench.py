@@ -191,14 +191,16 @@ def main():
         step = KDTrainStep(teacher, model, opt) if args.mode == "kd" else FlowTrainStep(model, opt)
         eager = step
 
+    # the eager steps issue the next batch's FPS chain on a side stream (distill.FpsPrefetch)
+    nxt = (lambda i: {"next_batch": batches[(i + 1) % nb]}) if not args.graph else (lambda i: {})
     for i in range(args.warmup):
-        step(*batches[i % nb])
+        step(*batches[i % nb], **nxt(i))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(*batches[i % nb])
+    for i in range(args.warmup, args.warmup + args.steps):
+        step(*batches[i % nb], **nxt(i))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -18,6 +18,7 @@ from pointconv_util import (PointConvD, PointWarping, UpsampleFlow, CrossLayerLi
                             SceneFlowEstimatorResidual, Conv1d)
 from pointconv_util import index_points_gather as index_points, index_points_group, square_distance  # noqa: F401
 from loss_functions import multiScaleLoss  # noqa: F401  (the reference defines it here too)
+from pointnet2 import pointnet2_utils
 
 scale = 1.0
 
@@ -66,8 +67,24 @@ class PointConvBidirection(nn.Module):
     # Every tensor below is point-major, (batch, points, channels), contiguous: a 1x1 conv is
     # one GEMM over the points, a concatenation is along the last dim, and the HIP gathers
     # read whole rows.  Only the returned views are permuted to the reference's (B,C,N).
-    def _encode(self, pc, color):
-        """Shared encoder on the pair batch (2B).  Returns per-level xyz, features, fps idx."""
+    def precompute_fps(self, xyz1, xyz2):
+        """The encoder's whole FPS chain for a pair batch, (2B, S_l) int32 per level
+        (levels 1-4).  It depends on the coordinates only, so a training loop can run it for
+        the NEXT batch on a side stream while this batch's forward/backward runs
+        (distill.FpsPrefetch), and a KD step can share it between teacher and student (same
+        clouds, same deterministic FPS)."""
+        x = torch.cat([xyz1, xyz2], 0)
+        out = []
+        for down in (self.level1, self.level2, self.level3, self.level4):
+            idx = pointnet2_utils.furthest_point_sample(x, down.npoint)
+            out.append(idx)
+            x = index_points(x, idx)
+        return out
+
+    def _encode(self, pc, color, fps_idx=None):
+        """Shared encoder on the pair batch (2B).  Returns per-level xyz, features, fps idx.
+        fps_idx: optional precompute_fps() result for this batch."""
+        pre = fps_idx if fps_idx is not None else [None] * 4
         feat_l0 = self.level0_1.cl(self.level0.cl(color))
         feat_l0_1 = self.level0_2.cl(feat_l0)
         levels = [(self.level1, self.level1_0, self.level1_1),
@@ -75,26 +92,26 @@ class PointConvBidirection(nn.Module):
                   (self.level3, self.level3_0, self.level3_1)]
         pcs, feats, feats_out, fps = [pc], [feat_l0], [feat_l0_1], []
         x, f = pc, feat_l0_1
-        for down, mix, widen in levels:
-            x, f, idx = down.forward_cl(x, f)
+        for lv, (down, mix, widen) in enumerate(levels):
+            x, f, idx = down.forward_cl(x, f, pre[lv])
             f = mix.cl(f)
             pcs.append(x)
             feats.append(f)
             fps.append(idx)
             f = widen.cl(f)
             feats_out.append(f)
-        pc_l4, feat_l4, _ = self.level4.forward_cl(x, f)
+        pc_l4, feat_l4, _ = self.level4.forward_cl(x, f, pre[3])
         feat_l4_3 = self.deconv4_3.cl(self.upsample.forward_cl(x, pc_l4, feat_l4))
         return pcs, feats, feats_out, fps, feat_l4_3
 
-    def forward(self, xyz1, xyz2, color1, color2):
+    def forward(self, xyz1, xyz2, color1, color2, fps_idx=None):
         """xyz*, color*: (B,N,3).  Returns (flows, fps_pc1_idxs, fps_pc2_idxs, pc1, pc2,
         feat1s, feat2s, crosses) exactly as the reference (models_bid_pointconv.py:198-207):
         flows/pcs/features as (B,C,N) (views of the point-major tensors)."""
         B = xyz1.shape[0]
         pc = torch.cat([xyz1, xyz2], 0)
         color = torch.cat([color1, color2], 0)
-        pcs, feats, feats_out, fps, feat_l4_3 = self._encode(pc, color)
+        pcs, feats, feats_out, fps, feat_l4_3 = self._encode(pc, color, fps_idx)
         one = lambda t: t[:B]  # noqa: E731
         two = lambda t: t[B:]  # noqa: E731
 

@@ -45,3 +45,21 @@ def test_graphed_step_equals_eager(mode):
         assert le == lg, losses
     for (n, pe), pg in zip(eager_model.named_parameters(), graph_model.parameters()):
         assert torch.equal(pe, pg), n
+
+
+def test_fps_prefetch_equals_inline():
+    """FlowTrainStep with the next batch's FPS issued on a side stream gives the same losses
+    and parameters as computing FPS inside the forward."""
+    from distill import FlowTrainStep, make_optimizer
+    from models_bid_pointconv import PointConvBidirection
+    torch.manual_seed(0)
+    base = PointConvBidirection().to(DEV)
+    batches = [_batch(2, 2048, s) for s in (4, 5, 6)]
+    m1, m2 = copy.deepcopy(base), copy.deepcopy(base)
+    s1, s2 = FlowTrainStep(m1, make_optimizer(m1)), FlowTrainStep(m2, make_optimizer(m2))
+    l1 = [float(s1(*b)) for b in batches]
+    l2 = [float(s2(*b, next_batch=batches[i + 1] if i + 1 < len(batches) else None))
+          for i, b in enumerate(batches)]
+    assert l1 == l2, (l1, l2)
+    for (n, a), b in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.equal(a, b), n
