@@ -175,14 +175,26 @@ __global__ __launch_bounds__(256) void cost_volume_bwd_kernel(
     float* __restrict__ ddir_rows, float* __restrict__ slab) {
   constexpr int LD = D_IN + 1;
   constexpr int RPP = 64 / D_IN;
-  __shared__ float lds_h_all[kWaves][kRows * LD];
-  __shared__ float lds_d_all[kWaves][kRows * LD];
-  __shared__ float red[kWaves][D_OUT * D_IN + D_OUT + 4 * D_IN];
+  constexpr int TI = D_IN / 32;  // 32-column tiles of dh0
+  constexpr int SLAB = D_OUT * D_IN + D_OUT + 4 * D_IN;
+  constexpr int PER_WAVE = 2 * kRows * LD;
+  // the per-wave h0 / dh0 tiles and, after the query loop, the workgroup's partial-sum
+  // buffer share one LDS block (2 workgroups per CU instead of 1)
+  constexpr int LDS_FLOATS = kWaves * (PER_WAVE > SLAB ? PER_WAVE : SLAB);
+  __shared__ float lds_all[LDS_FLOATS];
   const int b = blockIdx.y;
   const int wave = threadIdx.x >> 6;
   const int lane = lane_id();
-  float* lds_h = lds_h_all[wave];
-  float* lds_d = lds_d_all[wave];
+  const int half = lane >> 5, l32 = lane & 31;
+  float* lds_h = lds_all + wave * PER_WAVE;
+  float* lds_d = lds_h + kRows * LD;
+  // B fragments of W1 for dh0 = M W1 (inner index d = output channel): lane l supplies
+  // W1[2s + half][32t + l32]
+  float bwt[TI][D_OUT / 2];
+#pragma unroll
+  for (int t = 0; t < TI; ++t)
+#pragma unroll
+    for (int s2 = 0; s2 < D_OUT / 2; ++s2) bwt[t][s2] = w1[(2 * s2 + half) * D_IN + 32 * t + l32];
   const float* x1b = x1 + (long long)b * n1 * 3;
   const float* x2b = x2 + (long long)b * n2 * 3;
   const int* idxb = idx + (long long)b * n1 * k;
@@ -204,23 +216,42 @@ __global__ __launch_bounds__(256) void cost_volume_bwd_kernel(
     int j;
     float dx, dy, dz;
     build_h0<D_IN>(n, k, x1b, x2b, idxb, p1b, p2b, wpos, bpos, lds_h, j, dx, dy, dz);
-    // zero dh0
-    for (int e = lane; e < kRows * LD; e += kWave) lds_d[e] = 0.f;
-    __builtin_amdgcn_wave_barrier();
     // g'[d] = dout[d] * LeakyReLU'(z1[am[d], d]); sign(z1) at the argmax == sign(out[d])
     const long long ob = ((long long)b * n1 + n) * D_OUT;
     const int dl = lane % D_OUT;
     const float od = out[ob + dl];
     const float gd_l = dout[ob + dl] * (od > 0.f ? 1.f : kSlope);
     const int am_l = amax[ob + dl];
-    // dh0[am[d], :] += g'[d] * W1[d, :]   (ascending d; lanes over channels)
+    // dh0 = M W1 on the matrix cores, M[r][d] = g'[d] [am[d] == r] (one nonzero per column):
+    // the MFMA's f32 accumulation is the fma chain over ascending d, i.e. the same sums as
+    // scattering g'[d] W1[d, :] into row am[d] in ascending d
+    f32x16 dacc[TI];
+#pragma unroll
+    for (int t = 0; t < TI; ++t) dacc[t] = f32x16{0};
+#pragma unroll
+    for (int s2 = 0; s2 < D_OUT / 2; ++s2) {
+      const float g_lo = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gd_l), 2 * s2));
+      const float g_hi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gd_l), 2 * s2 + 1));
+      const int r_lo = __builtin_amdgcn_readlane(am_l, 2 * s2);
+      const int r_hi = __builtin_amdgcn_readlane(am_l, 2 * s2 + 1);
+      const float a = half ? (r_hi == l32 ? g_hi : 0.f) : (r_lo == l32 ? g_lo : 0.f);
+#pragma unroll
+      for (int t = 0; t < TI; ++t)
+        dacc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bwt[t][s2], dacc[t], 0, 0, 0);
+    }
+#pragma unroll
+    for (int t = 0; t < TI; ++t)
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        lds_d[((e & 3) + 8 * (e >> 2) + 4 * half) * LD + 32 * t + l32] = dacc[t][e];
+    // dW1[d, :] += g'[d] * h0[am[d], :]
+#pragma unroll
     for (int d = 0; d < D_OUT; ++d) {
-      const float gd = __shfl(gd_l, d, kWave);
-      const int r = __shfl(am_l, d, kWave);
-      if (sub == 0) lds_d[r * LD + c] = __builtin_fmaf(gd, w1[d * D_IN + c], lds_d[r * LD + c]);
-      // dW1[d, :] += g'[d] * h0[am[d], :]
+      const float gd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gd_l), d));
+      const int r = __builtin_amdgcn_readlane(am_l, d);
       gw1[d] = __builtin_fmaf(gd, lds_h[r * LD + c], gw1[d]);
     }
+    __builtin_amdgcn_wave_barrier();
     if (lane < D_OUT) gb1 += gd_l;
     __builtin_amdgcn_wave_barrier();
     // dz0 = dh0 * LeakyReLU'(h0) in place; rows written out; per-lane channel sums
@@ -279,7 +310,8 @@ __global__ __launch_bounds__(256) void cost_volume_bwd_kernel(
     __builtin_amdgcn_wave_barrier();
   }
   // workgroup partials: waves write their accumulators, wave 0 sums them in wave order
-  float* rw = red[wave];
+  __syncthreads();  // every wave is done with its h0/dh0 tiles (the buffer is reused)
+  float* rw = lds_all + wave * SLAB;
   if (sub == 0) {
 #pragma unroll
     for (int d = 0; d < D_OUT; ++d) rw[d * D_IN + c] = gw1[d];
@@ -290,11 +322,10 @@ __global__ __launch_bounds__(256) void cost_volume_bwd_kernel(
   }
   if (lane < D_OUT) rw[D_OUT * D_IN + lane] = gb1;
   __syncthreads();
-  constexpr int SLAB = D_OUT * D_IN + D_OUT + 4 * D_IN;
   float* sb = slab + ((long long)blockIdx.y * gridDim.x + blockIdx.x) * SLAB;
   for (int e = threadIdx.x; e < SLAB; e += blockDim.x) {
-    float v = red[0][e];
-    for (int w = 1; w < kWaves; ++w) v = __fadd_rn(v, red[w][e]);
+    float v = lds_all[e];
+    for (int w = 1; w < kWaves; ++w) v = __fadd_rn(v, lds_all[w * SLAB + e]);
     sb[e] = v;
   }
 }

@@ -38,9 +38,14 @@ def wrap_ddp(model, device=None):
 
 def make_optimizer(model, lr=1e-3, weight_decay=1e-4, capturable=False):
     """Adam as configured by config_train_kd_pointconv.yaml:15-24 / distilTrain.py:134-135.
-    capturable=True keeps the step counters on the device (required by GraphedStep)."""
-    return torch.optim.Adam(model.parameters(), lr=lr, betas=(0.9, 0.999), eps=1e-08,
-                            weight_decay=weight_decay, capturable=capturable)
+    capturable=True keeps the step counters on the device (required by GraphedStep).  On
+    the GPU the fused (single multi-tensor kernel) implementation is used: the same Adam
+    update (L2 weight decay, not AdamW) in one launch instead of ~10 foreach passes."""
+    params = list(model.parameters())
+    fused = len(params) > 0 and all(p.is_cuda for p in params)
+    return torch.optim.Adam(params, lr=lr, betas=(0.9, 0.999), eps=1e-08,
+                            weight_decay=weight_decay, capturable=capturable,
+                            fused=True if fused else None)
 
 
 def _core(model):

@@ -499,34 +499,11 @@ def _cost_volume_cl(nsample, x1, x2, p1, p2, pos, mlp, act, knn_idx=None):
     return _max_over_neighbours(h)
 
 
-class _MaxFirst(torch.autograd.Function):
-    """max over dim 2 of (B,N,K,C) with the reference's tie rule: F.max_pool2d over the K
-    window (pointconv_util.py:1848) keeps the FIRST maximal neighbour in K order, and its
-    backward routes the gradient there.  (torch.max(dim) does not promise an order for
-    ties on the GPU; exact ties do occur, e.g. between neighbours whose post-LReLU rows
-    coincide.)"""
-
-    @staticmethod
-    def forward(ctx, h):
-        B, N, K, C = h.shape
-        m = h.amax(dim=2, keepdim=True)
-        ks = torch.arange(K, device=h.device, dtype=torch.int32).view(1, 1, K, 1)
-        first = torch.where(h == m, ks, K).amin(dim=2, keepdim=True)
-        ctx.save_for_backward(first)
-        ctx.k = K
-        return m.squeeze(2)
-
-    @staticmethod
-    def backward(ctx, g):
-        (first,) = ctx.saved_tensors
-        B, N, _, C = first.shape
-        out = g.new_zeros((B, N, ctx.k, C))
-        out.scatter_(2, first.long(), g.unsqueeze(2))
-        return out
-
-
 def _max_over_neighbours(h):
-    return _MaxFirst.apply(h)
+    """max over the K neighbours (dim 2) of (B,N,K,C).  The reference's F.max_pool2d
+    (pointconv_util.py:1848) keeps the first maximal neighbour; torch.max(dim) returns the
+    first maximal index as well, so the backward routes to the same row."""
+    return h.max(dim=2)[0]
 
 
 class CrossLayerLight(nn.Module):
