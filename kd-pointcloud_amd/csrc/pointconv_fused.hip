@@ -143,7 +143,7 @@ __device__ __forceinline__ void build_row(const float* gl, int r, int k_n, const
 // ------------------------------------------------------------------------------ forward
 // grid (row tiles, channel splits); a split > 1 writes a partial tile to slab[split].
 // 256 threads.  Tile = 32*MT rows; output tiles 32x32 spread over the 4 waves.
-template <int O, int KM>
+template <int O, int KM, bool EX>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 void pc_fwd_kernel(Geo g, const float* __restrict__ wt, const float* __restrict__ wl,
                    const float* __restrict__ bias, float* __restrict__ y,
@@ -162,6 +162,7 @@ void pc_fwd_kernel(Geo g, const float* __restrict__ wt, const float* __restrict_
   __shared__ __attribute__((aligned(16))) float al[MT][(kNC / 4) * kBlk];
 
   const int row0 = blockIdx.x * TM;
+  const int kk = EX ? KM : g.k;  // exact-K instantiation: constant trip counts
   const int split = blockIdx.y;
   const int ch0 = split * chunks_per_split;
   const int ch1 = min(g.nch, ch0 + chunks_per_split);
@@ -171,8 +172,9 @@ void pc_fwd_kernel(Geo g, const float* __restrict__ wt, const float* __restrict_
   const int n0 = SPLIT_M ? (wv & 1) : (KG > 1 ? wv % (4 / KG) : wv * NPW);
   const int kgrp = KG > 1 ? wv / (4 / KG) : 0;
   constexpr int GB = 16 / KG;  // 8-column blocks per wave and chunk
+  constexpr int PF = NPW > 1 ? 4 : (KM <= 9 ? (GB < 6 ? GB : 6) : GB);  // B blocks issued ahead of the gathers
   const long long c16 = (long long)g.c * kW;
-  const int tk = TM * g.k;
+  const int tk = TM * kk;
 
   float wr[RPT][KM];
 #pragma unroll
@@ -180,7 +182,7 @@ void pc_fwd_kernel(Geo g, const float* __restrict__ wt, const float* __restrict_
     const int row = row0 + rr + 16 * q;
 #pragma unroll
     for (int k = 0; k < KM; ++k)
-      wr[q][k] = (row < g.r && k < g.k) ? wt[((long long)row * g.k + k) * kW + w] : 0.f;
+      wr[q][k] = (row < g.r && k < kk) ? wt[((long long)row * kk + k) * kW + w] : 0.f;
   }
   const Srcs src = srcs_of(g);
   unsigned nbf[GS];  // byte offsets of the slots' neighbour feature rows
@@ -188,8 +190,8 @@ void pc_fwd_kernel(Geo g, const float* __restrict__ wt, const float* __restrict_
 #pragma unroll
   for (int i = 0; i < GS; ++i) {
     const int rk = (t >> 3) + 32 * i;
-    const int r = rk / g.k;
-    const int nb = rk < tk ? nbr_of(g, row0 + r, rk - r * g.k) : -1;
+    const int r = rk / kk;
+    const int nb = rk < tk ? nbr_of(g, row0 + r, rk - r * kk) : -1;
     nbf[i] = feat_off(g, nb);
     gr[i] = g_fetch(g, src, nb, row0 + r, ch0 * kCC + cs);
   }
@@ -208,18 +210,45 @@ void pc_fwd_kernel(Geo g, const float* __restrict__ wt, const float* __restrict_
       if (rk < tk) gl[rk * kCC + cs] = gr[i];
     }
     __syncthreads();
-    if (ch + 1 < ch1) {  // next chunk's gather (feature channels only), in flight during
-                         // build + MFMA
+    // The chunk's Linear-weight fragments (MFMA B operand, served from L2): the first PF
+    // of its GB blocks are issued now and land while the A block is built; each later
+    // one is issued PF blocks ahead of its MFMAs.
+    const float* wrow[NPW];
+#pragma unroll
+    for (int j = 0; j < NPW; ++j) wrow[j] = wl + ((long long)((n0 + j) * 32 + l32)) * c16;
+    const int gbeg = kgrp * GB;
+    // unconditional load (a clamped address) + select: no branch around the load, so the
+    // compiler can count outstanding loads exactly (a branchy load forces vmcnt(0))
+    auto bfrag = [&](int gb, int j) -> float4 {
+      const bool ok = c0 + (gb >> 1) < g.c;
+      const float4 v =
+          *reinterpret_cast<const float4*>(wrow[j] + (ok ? c0 * kW + 8 * gb + 4 * half : 0));
+      return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    float4 bq[PF][NPW];
+#pragma unroll
+    for (int p2 = 0; p2 < PF; ++p2)
+#pragma unroll
+      for (int j = 0; j < NPW; ++j) bq[p2][j] = bfrag(gbeg + p2, j);
+    // next chunk's gather (feature channels only), in flight during build + MFMA.  Issued
+    // AFTER the B fragments: vmcnt retires loads in issue order, so an MFMA waiting on a
+    // B fragment issued after the gathers would wait for the gathers too.
+    // (issued on the last chunk too -- the values are unused there -- so the loop body is
+    // straight-line code and the compiler's load counting stays exact)
+    {
       const int cg = c0 + kCC + cs;
       const unsigned co = (unsigned)(cg - 3) * 4u;
 #pragma unroll
-      for (int i = 0; i < GS; ++i) gr[i] = cg < g.c ? bload(src.feats, nbf[i] + co) : 0.f;
+      for (int i = 0; i < GS; ++i) {
+        const float v = bload(src.feats, nbf[i] + co);  // out-of-range offsets read 0
+        gr[i] = cg < g.c ? v : 0.f;
+      }
     }
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
       const int r = rr + 16 * q;
       float a[kCC];
-      build_row<KM>(gl, r, g.k, wr[q], a);
+      build_row<KM>(gl, r, kk, wr[q], a);
       float* at = al[r >> 5] + (r & 31) * 4;
 #pragma unroll
       for (int c = 0; c < kCC; ++c) {
@@ -229,40 +258,30 @@ void pc_fwd_kernel(Geo g, const float* __restrict__ wt, const float* __restrict_
       __builtin_amdgcn_sched_barrier(0);  // keep the rows' LDS reads from piling up
     }
     __syncthreads();
-    // 16 blocks of 8 inner indices; the Linear weight is loaded one block ahead
-    const float* wrow[NPW];
+    // GB blocks of 8 inner indices; the A fragments are read from LDS one block ahead
+    float4 avc[MPW], avn[MPW];
 #pragma unroll
-    for (int j = 0; j < NPW; ++j) wrow[j] = wl + ((long long)((n0 + j) * 32 + l32)) * c16;
-    float4 bcur[NPW], bnxt[NPW];
-    const int gbeg = kgrp * GB;
+    for (int i = 0; i < MPW; ++i)
+      avc[i] = *reinterpret_cast<const float4*>(al[m0 + i] + (2 * gbeg + half) * kBlk + l32 * 4);
 #pragma unroll
-    for (int j = 0; j < NPW; ++j) {
-      const bool ok0 = c0 + (gbeg >> 1) < g.c;
-      bcur[j] = ok0 ? *reinterpret_cast<const float4*>(wrow[j] + c0 * kW + 8 * gbeg + 4 * half)
-                    : make_float4(0.f, 0.f, 0.f, 0.f);
-      bnxt[j] = bcur[j];
-    }
-#pragma unroll 2
     for (int gi = 0; gi < GB; ++gi) {
       const int gb = gbeg + gi;
       if (gi + 1 < GB) {
-        const int col = c0 * kW + 8 * (gb + 1) + 4 * half;
-        const bool ok = c0 + ((gb + 1) >> 1) < g.c;
 #pragma unroll
-        for (int j = 0; j < NPW; ++j)
-          bnxt[j] = ok ? *reinterpret_cast<const float4*>(wrow[j] + col)
-                       : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int i = 0; i < MPW; ++i)
+          avn[i] = *reinterpret_cast<const float4*>(al[m0 + i] + (2 * gb + 2 + half) * kBlk +
+                                                    l32 * 4);
       }
-      float4 av[MPW];
-#pragma unroll
-      for (int i = 0; i < MPW; ++i)
-        av[i] = *reinterpret_cast<const float4*>(al[m0 + i] + (2 * gb + half) * kBlk + l32 * 4);
 #pragma unroll
       for (int i = 0; i < MPW; ++i)
 #pragma unroll
-        for (int j = 0; j < NPW; ++j) acc[i][j] = mfma4(av[i], bcur[j], acc[i][j]);
+        for (int j = 0; j < NPW; ++j) acc[i][j] = mfma4(avc[i], bq[gi % PF][j], acc[i][j]);
+      if (gi + PF < GB) {
 #pragma unroll
-      for (int j = 0; j < NPW; ++j) bcur[j] = bnxt[j];
+        for (int j = 0; j < NPW; ++j) bq[gi % PF][j] = bfrag(gb + PF, j);
+      }
+#pragma unroll
+      for (int i = 0; i < MPW; ++i) avc[i] = avn[i];
     }
   }
 
@@ -491,7 +510,7 @@ __global__ __launch_bounds__(256) void pc_csr_sum_kernel(long long npts, int c, 
 // 1-D grid of nch x splits workgroups (512 threads); each owns the O x 128 tile of dwl for
 // one chunk over one split's rows.  With >= 8 splits, the chunks of split s all run on XCD
 // s % 8 (workgroups are dealt to the XCDs round-robin by linear id).
-template <int O, int KM>
+template <int O, int KM, bool EX>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
 void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __restrict__ dy,
                           float* __restrict__ dwl, int rows_per_split, int nsplit, int xcd_map) {
@@ -515,6 +534,7 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
   }
   if (split >= nsplit) return;
   const int c0 = ch * kCC;
+  const int kk = EX ? KM : g.k;  // exact-K instantiation: constant trip counts
   const int rbeg = split * rows_per_split;
   const int rend = min(g.r, rbeg + rows_per_split);
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, half = lane >> 5, l32 = lane & 31;
@@ -522,7 +542,7 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
   const int nt = wv & 3;
   const int m0 = (wv >> 2) * MPW;
   const long long c16 = (long long)g.c * kW;
-  const int tk = 32 * g.k;
+  const int tk = 32 * kk;
   const Srcs src = srcs_of(g);
 
   // registers prefetched one tile ahead
@@ -531,13 +551,13 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
     const int row = row0 + rb;
 #pragma unroll
     for (int k = 0; k < KM; ++k)
-      wr[k] = (row < rend && k < g.k) ? wt[((long long)row * g.k + k) * kW + w] : 0.f;
+      wr[k] = (row < rend && k < kk) ? wt[((long long)row * kk + k) * kW + w] : 0.f;
 #pragma unroll
     for (int i = 0; i < GS; ++i) {
       const int rk = (t >> 3) + 64 * i;
-      const int r = rk / g.k;
+      const int r = rk / kk;
       const int rw = row0 + r;
-      const int nb = (rk < tk && rw < rend) ? nbr_of(g, rw, rk - r * g.k) : -1;
+      const int nb = (rk < tk && rw < rend) ? nbr_of(g, rw, rk - r * kk) : -1;
       gr[i] = g_fetch(g, src, nb, rw, c0 + cs);
     }
 #pragma unroll
@@ -571,7 +591,7 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
     if (row0 + 32 < rend) fetch(row0 + 32);
     {
       float a[kCC];
-      build_row<KM>(gl, rb, g.k, wc, a);
+      build_row<KM>(gl, rb, kk, wc, a);
 #pragma unroll
       for (int c = 0; c < kCC; ++c) at[(c * kW + w) * kTS + rb] = a[c];
     }
@@ -663,8 +683,12 @@ hipError_t slab_sum(int nslabs, long long len, const float* slab, const float* b
 template <int O, int KM>
 hipError_t fwd_launch(const Geo& g, const Plan& p, const float* wt, const float* wl,
                       const float* bias, float* y, float* slab, hipStream_t st) {
-  hipLaunchKernelGGL((pc_fwd_kernel<O, KM>), dim3(p.rt, p.ks), dim3(256), 0, st, g, wt, wl, bias,
-                     y, p.ks > 1 ? slab : nullptr, p.cps);
+  if (g.k == KM)
+    hipLaunchKernelGGL((pc_fwd_kernel<O, KM, true>), dim3(p.rt, p.ks), dim3(256), 0, st, g, wt, wl,
+                       bias, y, p.ks > 1 ? slab : nullptr, p.cps);
+  else
+    hipLaunchKernelGGL((pc_fwd_kernel<O, KM, false>), dim3(p.rt, p.ks), dim3(256), 0, st, g, wt, wl,
+                       bias, y, p.ks > 1 ? slab : nullptr, p.cps);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || p.ks == 1) return e;
   return slab_sum(p.ks, (long long)p.r * O, slab, bias, O, y, st);
@@ -691,8 +715,12 @@ hipError_t bwd_launch(const Geo& g, const Plan& p, int b, const float* wt, const
                      dim3((unsigned)std::min<long long>(divupll(work, 256), 1 << 20)), dim3(256),
                      0, st, npts, g.c, p.c8, g.d, dgr, offsets, perm, dxyz, dfeats);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM>), dim3(p.wgs), dim3(512), 0, st, g, wt, dy,
-                     p.rs > 1 ? dwl_slab : dwl, p.rps, p.rs, p.xcd);
+  if (g.k == KM)
+    hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM, true>), dim3(p.wgs), dim3(512), 0, st, g, wt,
+                       dy, p.rs > 1 ? dwl_slab : dwl, p.rps, p.rs, p.xcd);
+  else
+    hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM, false>), dim3(p.wgs), dim3(512), 0, st, g, wt,
+                       dy, p.rs > 1 ? dwl_slab : dwl, p.rps, p.rs, p.xcd);
   if ((e = hipGetLastError()) != hipSuccess || p.rs == 1) return e;
   return slab_sum(p.rs, (long long)O * g.c * kW, dwl_slab, nullptr, 1, dwl, st);
 }

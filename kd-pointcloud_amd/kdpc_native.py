@@ -9,7 +9,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libkdpc_hip.so")
+LIB_PATH = os.environ.get("KDPC_LIB", os.path.join(_HERE, "lib", "libkdpc_hip.so"))
 
 _c_int, _c_float, _c_size, _vp = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 
