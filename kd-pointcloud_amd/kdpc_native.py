@@ -260,12 +260,32 @@ class Csr:
               self.offsets.data_ptr(), self.perm.data_ptr(), _stream(idx2d))
 
 
+def batch_prefix(idx, b):
+    """idx[:b] (the first b batch entries) whose CSR is derived from idx's own: keys are
+    batch-major (b*N + idx), so the inverted index of the first b batches is exactly the
+    prefix offsets[:b*N+1], perm[:b*P] of the parent's -- no second sort."""
+    child = idx[:b]
+    try:
+        child._kdpc_parent = (idx, b)
+    except AttributeError:
+        pass
+    return child
+
+
 def csr_of(idx, n):
     """CSR for idx (B,...) flattened to (B,P), cached on the index tensor object."""
     cache = getattr(idx, "_kdpc_csr", None)
     if cache is not None and cache.n == n:
         return cache
-    csr = Csr(idx.reshape(idx.shape[0], -1), n)
+    parent = getattr(idx, "_kdpc_parent", None)
+    if parent is not None:
+        pidx, b = parent
+        pc = csr_of(pidx, n)
+        csr = Csr.__new__(Csr)
+        csr.offsets, csr.perm = pc.offsets[:b * n + 1], pc.perm[:b * pc.p]
+        csr.n, csr.p = n, pc.p
+    else:
+        csr = Csr(idx.reshape(idx.shape[0], -1), n)
     try:
         idx._kdpc_csr = csr
     except AttributeError:

@@ -18,6 +18,7 @@ from pointconv_util import (PointConvD, PointWarping, UpsampleFlow, CrossLayerLi
                             SceneFlowEstimatorResidual, Conv1d)
 from pointconv_util import index_points_gather as index_points, index_points_group, square_distance  # noqa: F401
 from loss_functions import multiScaleLoss  # noqa: F401  (the reference defines it here too)
+import kdpc_native
 from pointnet2 import pointnet2_utils
 
 scale = 1.0
@@ -132,13 +133,13 @@ class PointConvBidirection(nn.Module):
                                                       torch.cat([f1n, f2n], 0), up_idx))
             up_feats.append(f_up)
             c_feat = torch.cat([feats[lv], f_up], dim=-1)
+            up_idx1 = kdpc_native.batch_prefix(up_idx, B)  # pc1 half, CSR shared with up_idx
             pc1_lv, pc2_lv = one(pcs[lv]), two(pcs[lv])
             sflow = flow if self.scale == 1.0 else self.scale * flow  # x1.0 is exact
-            up_flow = self.upsample.forward_cl(pc1_lv, one(pcs[lv + 1]), sflow,
-                                               up_idx[:B])
+            up_flow = self.upsample.forward_cl(pc1_lv, one(pcs[lv + 1]), sflow, up_idx1)
             pc2_warp = self.warping.forward_cl(pc1_lv, pc2_lv, up_flow)
             f1n, f2n, cost = cross.forward_pair(torch.cat([pc1_lv, pc2_warp], 0), c_feat)
-            feat_up = self.upsample.forward_cl(pc1_lv, one(pcs[lv + 1]), feat_est, up_idx[:B])
+            feat_up = self.upsample.forward_cl(pc1_lv, one(pcs[lv + 1]), feat_est, up_idx1)
             new_feat1 = torch.cat([one(feats[lv]), feat_up], dim=-1)
             feat_est, flow = flow_est.forward_cl(pc1_lv, new_feat1, cost, up_flow)
             flows.insert(0, flow)

@@ -576,7 +576,8 @@ class CrossLayerLight(nn.Module):
         feat1_new = _linear_1x1(self.cross_t1, feat1_new)
         feat2_new = _linear_1x1(self.cross_t2, feat2_new)
         feat1_final = _cost_volume_cl(self.nsample, xa[:B], xa[B:], feat1_new, feat2_new,
-                                      self.pos2, self.mlp2, self._act(self.bn2), idx[:B])
+                                      self.pos2, self.mlp2, self._act(self.bn2),
+                                      _nat.batch_prefix(idx, B))
         return feat1_new, feat2_new, feat1_final
 
 
