@@ -217,6 +217,35 @@ int kdpc_weightnet_bwd(int b, int n, int s, int k, const float *xyz, const float
                        const int *idx, const float *params, const float *dwt, float *drel,
                        float *dparams, void *workspace, size_t workspace_bytes, void *stream);
 
+/* ---- BatchNorm1d + LeakyReLU over point-major rows (pointconv_util.py:217-258, bn=True
+ *      estimator PointConvs: Linear -> BatchNorm1d -> LeakyReLU(0.1)) ------------------- */
+
+/* Scratch bytes for kdpc_batchnorm_lrelu_fwd / _bwd on an (R, C) tensor. */
+size_t kdpc_batchnorm_workspace_bytes(int r, int c);
+
+/* Train mode: per-column statistics of x (R, C) (biased variance for the normalisation,
+ * unbiased for the running update, as torch.nn.BatchNorm1d), y = LeakyReLU_slope(
+ * (x - mean) * invstd * weight + bias).  mean/invstd (C) are written for the backward;
+ * run_mean/run_var updated with `momentum` (both NULL: not tracked).  C % 4 == 0,
+ * C <= 1024.  Fixed-order reductions (deterministic). */
+int kdpc_batchnorm_lrelu_fwd(int r, int c, const float *x, const float *weight, const float *bias,
+                             float eps, float momentum, float slope, float *run_mean,
+                             float *run_var, float *mean, float *invstd, float *y,
+                             void *workspace, size_t workspace_bytes, void *stream);
+
+/* y = LeakyReLU_slope((x - mean) * invstd * weight + bias) with given statistics (eval). */
+int kdpc_batchnorm_lrelu_apply(int r, int c, const float *x, const float *mean,
+                               const float *invstd, const float *weight, const float *bias,
+                               float slope, float *y, void *stream);
+
+/* Backward of kdpc_batchnorm_lrelu_fwd: dy_act and y_act (the forward output), x (its
+ * input) -> dx (R, C), dweight, dbias (C). */
+int kdpc_batchnorm_lrelu_bwd(int r, int c, const float *dy_act, const float *y_act,
+                             const float *x, const float *weight, const float *mean,
+                             const float *invstd, float slope, float *dx, float *dweight,
+                             float *dbias, void *workspace, size_t workspace_bytes,
+                             void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -43,6 +43,12 @@ _SIGNATURES = {
     "kdpc_pointconv_fwd": [_c_int] * 6 + [_vp] * 9 + [_c_size, _vp],
     "kdpc_pointconv_bwd_workspace_bytes": [_c_int] * 5,
     "kdpc_pointconv_bwd": [_c_int] * 6 + [_vp] * 15 + [_c_size, _vp],
+    "kdpc_batchnorm_workspace_bytes": [_c_int, _c_int],
+    "kdpc_batchnorm_lrelu_fwd": [_c_int, _c_int] + [_vp] * 3 + [_c_float] * 3 + [_vp] * 6
+                                + [_c_size, _vp],
+    "kdpc_batchnorm_lrelu_apply": [_c_int, _c_int] + [_vp] * 5 + [_c_float, _vp, _vp],
+    "kdpc_batchnorm_lrelu_bwd": [_c_int, _c_int] + [_vp] * 6 + [_c_float] + [_vp] * 4
+                                + [_c_size, _vp],
     "kdpc_weightnet_param_count": [],
     "kdpc_weightnet_fwd": [_c_int] * 4 + [_vp] * 6,
     "kdpc_weightnet_bwd_workspace_bytes": [],
@@ -51,7 +57,8 @@ _SIGNATURES = {
 _RESTYPES = {"kdpc_csr_workspace_bytes": _c_size, "kdpc_cost_volume_bwd_workspace_bytes": _c_size,
              "kdpc_pointconv_fwd_workspace_bytes": _c_size,
              "kdpc_pointconv_bwd_workspace_bytes": _c_size,
-             "kdpc_weightnet_bwd_workspace_bytes": _c_size}
+             "kdpc_weightnet_bwd_workspace_bytes": _c_size,
+             "kdpc_batchnorm_workspace_bytes": _c_size}
 
 EXPORTED = tuple(_SIGNATURES)
 
@@ -503,3 +510,50 @@ def weightnet_bwd(xyz, center, idx, params, dwt, need_rel=False):
           drel.data_ptr() if need_rel else None, _dev(dparams, f, "dparams"), ws.data_ptr(),
           ws_bytes, _stream(xyz))
     return drel, dparams
+
+
+# ------------------------------------------------------- BatchNorm1d + LeakyReLU (rows)
+def batchnorm_lrelu_fwd(x2, weight, bias, eps, momentum, slope, run_mean, run_var):
+    """Train mode over x2 (R, C): -> (y, mean, invstd); running stats updated in place."""
+    R, C = x2.shape
+    f = torch.float32
+    dev = x2.device
+    lib = load_library()
+    ws = _workspace(lib.kdpc_batchnorm_workspace_bytes(R, C), dev)
+    y = torch.empty_like(x2)
+    mean = torch.empty((C,), dtype=f, device=dev)
+    invstd = torch.empty((C,), dtype=f, device=dev)
+    _call("kdpc_batchnorm_lrelu_fwd", R, C, _dev(x2, f, "x"), _dev(weight, f, "weight"),
+          _dev(bias, f, "bias"), float(eps), float(momentum), float(slope),
+          None if run_mean is None else _dev(run_mean, f, "running_mean"),
+          None if run_var is None else _dev(run_var, f, "running_var"),
+          mean.data_ptr(), invstd.data_ptr(), y.data_ptr(), ws.data_ptr(), ws.numel(),
+          _stream(x2), work=(12 * R * C, 0))
+    return y, mean, invstd
+
+
+def batchnorm_lrelu_apply(x2, mean, invstd, weight, bias, slope):
+    R, C = x2.shape
+    f = torch.float32
+    y = torch.empty_like(x2)
+    _call("kdpc_batchnorm_lrelu_apply", R, C, _dev(x2, f, "x"), _dev(mean, f, "mean"),
+          _dev(invstd, f, "invstd"), _dev(weight, f, "weight"), _dev(bias, f, "bias"),
+          float(slope), y.data_ptr(), _stream(x2))
+    return y
+
+
+def batchnorm_lrelu_bwd(dy, y, x2, weight, mean, invstd, slope):
+    """-> (dx, dweight, dbias)."""
+    R, C = x2.shape
+    f = torch.float32
+    dev = x2.device
+    lib = load_library()
+    ws = _workspace(lib.kdpc_batchnorm_workspace_bytes(R, C), dev)
+    dx = torch.empty_like(x2)
+    dw = torch.empty((C,), dtype=f, device=dev)
+    db = torch.empty((C,), dtype=f, device=dev)
+    _call("kdpc_batchnorm_lrelu_bwd", R, C, _dev(dy, f, "dy"), _dev(y, f, "y"), _dev(x2, f, "x"),
+          _dev(weight, f, "weight"), _dev(mean, f, "mean"), _dev(invstd, f, "invstd"),
+          float(slope), dx.data_ptr(), dw.data_ptr(), db.data_ptr(), ws.data_ptr(), ws.numel(),
+          _stream(x2), work=(20 * R * C, 0))
+    return dx, dw, db

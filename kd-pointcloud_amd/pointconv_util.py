@@ -87,6 +87,56 @@ _linear_1x1 = linear_1x1
 
 
 _BN_CHANNEL_MAJOR = False  # test seam: True runs BN on the (B,C,N) view (rounding probe)
+_FUSED_BN = True  # test seam: False uses torch's BatchNorm1d + LeakyReLU
+
+
+class _BnLReLU(torch.autograd.Function):
+    """Train-mode BatchNorm1d over the rows of (R, C) + LeakyReLU (csrc/batchnorm.hip)."""
+
+    @staticmethod
+    def forward(ctx, x2, weight, bias, eps, momentum, slope, run_mean, run_var):
+        y, mean, invstd = _nat.batchnorm_lrelu_fwd(x2, weight, bias, eps, momentum, slope,
+                                                   run_mean, run_var)
+        ctx.save_for_backward(x2, weight, mean, invstd, y)
+        ctx.slope = slope
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight, mean, invstd, y = ctx.saved_tensors
+        dx, dw, db = _nat.batchnorm_lrelu_bwd(dy.contiguous(), y, x2, weight, mean, invstd,
+                                              ctx.slope)
+        return dx, dw, db, None, None, None, None, None
+
+
+def _bn_lrelu_fusable(bn, act, x):
+    return (_FUSED_BN and not _BN_CHANNEL_MAJOR and isinstance(bn, nn.BatchNorm1d)
+            and isinstance(act, nn.LeakyReLU) and bn.affine and x.is_cuda
+            and x.shape[-1] % 4 == 0 and x.shape[-1] <= 1024
+            and (bn.training or bn.track_running_stats) and bn.momentum is not None)
+
+
+def _bn_lrelu(bn, slope, y):
+    """LeakyReLU(BatchNorm1d(y)) over the last dim of a point-major tensor."""
+    shp = y.shape
+    x2 = y.reshape(-1, shp[-1]).contiguous()
+    if bn.training:
+        if bn.track_running_stats:
+            bn.num_batches_tracked.add_(1)
+        out = _BnLReLU.apply(x2, bn.weight, bn.bias, bn.eps, bn.momentum, slope,
+                             bn.running_mean if bn.track_running_stats else None,
+                             bn.running_var if bn.track_running_stats else None)
+    elif torch.is_grad_enabled() and (y.requires_grad or bn.weight.requires_grad):
+        return bn_act_ref(bn, slope, y)
+    else:
+        invstd = (bn.running_var + bn.eps).rsqrt()
+        out = _nat.batchnorm_lrelu_apply(x2, bn.running_mean, invstd, bn.weight, bn.bias, slope)
+    return out.view(shp)
+
+
+def bn_act_ref(bn, slope, y):
+    """torch formulation of _bn_lrelu (eval with gradients, and the tests' reference)."""
+    return F.leaky_relu(_bn_last(bn, y), slope)
 
 
 def _bn_last(norm, y):
@@ -363,6 +413,8 @@ class _PointConvBase(nn.Module):
     def _finish(self, new_points):
         """(B,S,out) -> optional BN1d (per channel, over B and S) + activation, point-major."""
         if self.bn:
+            if _bn_lrelu_fusable(self.bn_linear, self.relu, new_points):
+                return _bn_lrelu(self.bn_linear, self.relu.negative_slope, new_points)
             new_points = _bn_last(self.bn_linear, new_points)
         return self.relu(new_points)
 

@@ -165,3 +165,41 @@ def test_weightnet_fused_vs_fp64(b, n, s, k):
     names = ["wt", "dxyz", "dcenter", "dW0", "db0", "dW1", "db1", "dW2", "db2"]
     for a, w, nm in zip(got, want, names):
         _scale_close(a, w, rtol=2e-5, name=nm)
+
+
+@pytest.mark.parametrize("r,c", [(65536, 128), (1000, 128), (37, 8)])
+def test_batchnorm_lrelu_vs_torch(r, c):
+    """csrc/batchnorm.hip (train-mode BatchNorm1d + LeakyReLU over point-major rows): output,
+    running statistics and gradients against torch's BatchNorm1d + LeakyReLU in fp64; the
+    eval-mode apply against the running-statistics formula."""
+    import pointconv_util as P
+    g = torch.Generator(device="cpu").manual_seed(r + c)
+    x = (torch.randn(r, c, generator=g) * 3 + 1).to(DEV)
+    dy = torch.randn(r, c, generator=g).to(DEV)
+    bn = torch.nn.BatchNorm1d(c).to(DEV).train()
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(c, generator=g) + 0.5)
+        bn.bias.copy_(torch.randn(c, generator=g) * 0.1)
+    bn64 = torch.nn.BatchNorm1d(c).to(DEV).double().train()
+    bn64.load_state_dict({k: v.double() if v.is_floating_point() else v
+                          for k, v in bn.state_dict().items()})
+    xa = x.clone().requires_grad_(True)
+    y = P._bn_lrelu(bn, 0.1, xa.view(1, r, c))
+    y.backward(dy.view(1, r, c))
+    xb = x.double().requires_grad_(True)
+    y64 = torch.nn.functional.leaky_relu(bn64(xb), 0.1)
+    y64.backward(dy.double())
+    _scale_close(y.view(r, c), y64, rtol=1e-5, name="y")
+    _scale_close(xa.grad, xb.grad, rtol=1e-5, name="dx")
+    _scale_close(bn.weight.grad, bn64.weight.grad, rtol=1e-5, name="dweight")
+    _scale_close(bn.bias.grad, bn64.bias.grad, rtol=1e-5, name="dbias")
+    _scale_close(bn.running_mean, bn64.running_mean, rtol=1e-5, name="running_mean")
+    _scale_close(bn.running_var, bn64.running_var, rtol=1e-5, name="running_var")
+    assert int(bn.num_batches_tracked) == 1
+    bn.eval()
+    with torch.no_grad():
+        ye = P._bn_lrelu(bn, 0.1, x.view(1, r, c)).view(r, c)
+        ref = torch.nn.functional.leaky_relu(
+            (x.double() - bn.running_mean.double()) / torch.sqrt(bn.running_var.double() + bn.eps)
+            * bn.weight.double() + bn.bias.double(), 0.1)
+    _scale_close(ye, ref, rtol=1e-5, name="eval")
