@@ -49,10 +49,9 @@ ROOFLINE = {
                                                          "group_points_kernel"]),
     "kdpc_knn_point": ("valu", "TFLOP/s", FP32_VALU_PEAK_TF, ["knn_kernel"]),
 }
-# the step's dominant entry point (rocprofv3 step profile, profiles/) and the gather-bound
-# one the north star names
+# the step's dominant entry point (rocprofv3 step profile, profiles/); the gather-bound
+# grouping_operation the north star names is measured by gather_roofline()
 PRIMARY_KERNEL = "kdpc_pointconv_bwd"
-GATHER_KERNEL = "kdpc_group_rows"
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
@@ -121,6 +120,39 @@ def pmc_traffic(kernel):
         return None
     e = d.get("entries", {}).get(kernel)
     return None if e is None else e.get("hbm_bytes_per_launch")
+
+
+def gather_roofline(dev, iters=20):
+    """The north star's gather target at BASELINE configs[1]: grouping_operation (reference
+    (B,C,N) layout) at B=8, C=64, N=8192, S=2048, K=16 on FPS centres + ball_query(r=0.5)
+    indices, timed with HIP events over `iters` back-to-back launches on the launch stream
+    (single ~15 us launches cannot be bracketed individually: the event packets cost as
+    much as the kernel).  Algorithmic bytes B*(4CN + 4SK + 4CSK)."""
+    import kdpc_native as K
+    import synthetic
+    B, C, N, S, Kn = 8, 64, 8192, 2048, 16
+    xyz = torch.from_numpy(synthetic.ft3d_batch(B, N, seed=7)[0]).to(dev)
+    centres = K.group_rows(xyz, K.furthest_point_sampling(xyz, S))
+    idx = K.ball_query(0.5, Kn, xyz, centres)
+    feats = torch.randn(B, C, N, device=dev)
+    for _ in range(3):
+        K.group_points(feats, idx)
+    stream = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(iters):
+        K.group_points(feats, idx)
+    e1.record(stream)
+    e1.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / iters
+    nbytes = B * (4 * C * N + 4 * S * Kn + 4 * C * S * Kn)
+    achieved = nbytes / (us * 1e-6) / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("kdpc_group_points"),
+            "kernel": "kdpc_group_points", "hip_kernels": ROOFLINE["kdpc_group_points"][3],
+            "workload": "grouping_operation B=8 C=64 N=8192 S=2048 K=16 (configs[1]), "
+                        f"{iters} back-to-back launches",
+            "avg_launch_us": round(us, 2), "algorithmic_bytes_per_launch": nbytes}
 
 
 def roofline(kernel, summ):
@@ -213,7 +245,7 @@ def main():
     # per-kernel roofline: HIP events around every launch of the named C entry points, over
     # eager replays of the same step after the timed region (a graph replay has no
     # per-launch host hook); kernel durations do not depend on how the launch was issued
-    timer = kdpc_native.LaunchTimer([args.roofline_kernel, GATHER_KERNEL])
+    timer = kdpc_native.LaunchTimer([args.roofline_kernel])
     kdpc_native.set_launch_timer(timer)
     for i in range(args.measure_steps):
         eager(*batches[i % nb])
@@ -221,7 +253,7 @@ def main():
     kdpc_native.set_launch_timer(None)
     summary = timer.summary()
     roof = roofline(args.roofline_kernel, summary.get(args.roofline_kernel))
-    roof_gather = roofline(GATHER_KERNEL, summary.get(GATHER_KERNEL))
+    roof_gather = gather_roofline(dev)
 
     pairs = world * args.batch * args.steps
     line = {
