@@ -7,10 +7,11 @@
 // channels-last BatchNorm kernels took ~150 us per (65536, 128) pass on MI355X, ~10x the
 // bytes-moved bound.  Here:
 //   forward : bn_stats (per-block Welford partials, fixed block -> slab order)
-//             bn_finalize (Chan merge of the slabs in slab order; mean, invstd, running stats)
+//             bn_finalize (Chan merges of the slabs in a fixed order: one wave per channel;
+//                          mean, invstd, running stats)
 //             bn_apply  (y = act((x - mean) * invstd * w + b), float4 rows)
 //   backward: bn_bwd_reduce (per-block sums of dy and dy*xhat, dy = dy_act * slope(y))
-//             bn_bwd_finalize (slab sums in order -> dweight, dbias)
+//             colsum (slab column sums, fixed order -> dbias, dweight)
 //             bn_bwd_apply (dx = w * invstd * (dy - sum(dy)/R - xhat * sum(dy*xhat)/R))
 // Every reduction has a fixed order (no atomics): results depend only on the shape.
 #include <algorithm>
@@ -101,17 +102,39 @@ __global__ __launch_bounds__(kBlock) void bn_stats_kernel(int r, int c, int rpb,
   }
 }
 
-__global__ void bn_finalize_kernel(int r, int c, int nslab, const float* __restrict__ slab,
-                                   float eps, float momentum, float* __restrict__ mean,
-                                   float* __restrict__ invstd, float* __restrict__ run_mean,
-                                   float* __restrict__ run_var) {
-  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch >= c) return;
+// one wave per channel: lane l merges slabs l, l+64, ... in order, then a fixed xor
+// butterfly merges the lanes (deterministic)
+__global__ __launch_bounds__(kBlock) void bn_finalize_kernel(int r, int c, int nslab,
+                                                             const float* __restrict__ slab,
+                                                             float eps, float momentum,
+                                                             float* __restrict__ mean,
+                                                             float* __restrict__ invstd,
+                                                             float* __restrict__ run_mean,
+                                                             float* __restrict__ run_var) {
+  const int ch = (blockIdx.x * kBlock + threadIdx.x) / kWave;
+  const int lane = lane_id();
+  if (ch >= c) return;  // wave-uniform
   float N = 0.f, M = 0.f, M2 = 0.f;
-  for (int s = 0; s < nslab; ++s) {
+  for (int s = lane; s < nslab; s += kWave) {
     const float* p = slab + (long long)s * 3 * c + ch;
     welford_merge(N, M, M2, p[0], p[c], p[2 * c]);
   }
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const float nb = __shfl_xor(N, o, kWave), mb = __shfl_xor(M, o, kWave);
+    const float m2b = __shfl_xor(M2, o, kWave);
+    // merge in lane order so both partners compute the identical result
+    if (lane & o) {
+      float n2 = nb, mm = mb, mq = m2b;
+      welford_merge(n2, mm, mq, N, M, M2);
+      N = n2;
+      M = mm;
+      M2 = mq;
+    } else {
+      welford_merge(N, M, M2, nb, mb, m2b);
+    }
+  }
+  if (lane != 0) return;
   const float var = M2 / N;  // biased (normalisation)
   mean[ch] = M;
   invstd[ch] = 1.f / sqrtf(var + eps);
@@ -197,17 +220,12 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(int r, int c, int
   }
 }
 
-__global__ void bn_bwd_finalize_kernel(int c, int nslab, const float* __restrict__ slab,
-                                       float* __restrict__ dbias, float* __restrict__ dweight) {
+__global__ void bn_bwd_copy_kernel(int c, const float* __restrict__ sums,
+                                   float* __restrict__ dbias, float* __restrict__ dweight) {
   const int ch = blockIdx.x * blockDim.x + threadIdx.x;
   if (ch >= c) return;
-  float a = 0.f, b2 = 0.f;
-  for (int s = 0; s < nslab; ++s) {
-    a += slab[(long long)s * 2 * c + ch];
-    b2 += slab[(long long)s * 2 * c + c + ch];
-  }
-  dbias[ch] = a;
-  dweight[ch] = b2;
+  dbias[ch] = sums[ch];
+  dweight[ch] = sums[c + ch];
 }
 
 __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(long long n4, int cv, float rinv,
@@ -250,7 +268,8 @@ inline int ew_grid(long long n4) {
 KDPC_API size_t kdpc_batchnorm_workspace_bytes(int r, int c) {
   if (r <= 0 || c <= 0) return 0;
   const long long nblk = divupll(r, rows_per_block(r));
-  return (size_t)(nblk * 3 * c) * sizeof(float);
+  // slab (nblk, 3, C) | column sums (2C) | colsum scratch
+  return (size_t)(nblk * 3 * c + 2 * c + colsum_scratch_floats((int)nblk, 2 * c)) * sizeof(float);
 }
 
 // Train-mode forward.  x, y (R, C) row-major; C % 4 == 0 and C <= 1024; mean/invstd (C)
@@ -273,8 +292,8 @@ KDPC_API int kdpc_batchnorm_lrelu_fwd(int r, int c, const float* x, const float*
                      c, rpb, x, slab);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(divup(c, 256)), dim3(256), 0, st, r, c, nblk, slab,
-                     eps, momentum, mean, invstd, run_mean, run_var);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(divup(c * kWave, kBlock)), dim3(kBlock), 0, st, r,
+                     c, nblk, slab, eps, momentum, mean, invstd, run_mean, run_var);
   if ((e = hipGetLastError()) != hipSuccess) return (int)e;
   const long long n4 = (long long)r * c / 4;
   hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(n4)), dim3(kBlock), 0, st, n4, c / 4, slope, x,
@@ -315,12 +334,14 @@ KDPC_API int kdpc_batchnorm_lrelu_bwd(int r, int c, const float* dy_act, const f
                      r, c, rpb, slope, dy_act, y_act, x, mean, invstd, slab);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(divup(c, 256)), dim3(256), 0, st, c, nblk, slab,
-                     dbias, dweight);
-  if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+  float* sums = slab + (size_t)nblk * 3 * c;  // [sum dy (C) | sum dy*xhat (C)]
+  if ((e = colsum(nblk, 2 * c, slab, sums, sums + 2 * c, st)) != hipSuccess) return (int)e;
   const long long n4 = (long long)r * c / 4;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(n4)), dim3(kBlock), 0, st, n4, c / 4,
-                     1.f / (float)r, slope, dy_act, y_act, x, mean, invstd, weight, dbias,
-                     dweight, dx);
+                     1.f / (float)r, slope, dy_act, y_act, x, mean, invstd, weight, sums,
+                     sums + c, dx);
+  if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(bn_bwd_copy_kernel, dim3(divup(c, 256)), dim3(256), 0, st, c, sums, dbias,
+                     dweight);
   KDPC_RETURN_LAUNCH();
 }

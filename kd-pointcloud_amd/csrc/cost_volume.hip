@@ -330,17 +330,6 @@ __global__ __launch_bounds__(256) void cost_volume_bwd_kernel(
   }
 }
 
-// sum the per-workgroup slabs in ascending workgroup order (deterministic)
-__global__ __launch_bounds__(256) void slab_sum_kernel(int nslabs, int slab_len,
-                                                       const float* __restrict__ slab,
-                                                       float* __restrict__ dst) {
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < slab_len; e += gridDim.x * blockDim.x) {
-    float v = 0.f;
-    for (int s = 0; s < nslabs; ++s) v = __fadd_rn(v, slab[(long long)s * slab_len + e]);
-    dst[e] = v;
-  }
-}
-
 constexpr int kFwdQPW = 8;
 constexpr int kBwdQPW = 32;
 
@@ -371,9 +360,8 @@ hipError_t bwd_launch(int b, int n1, int n2, int k, const float* x1, const float
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int len = slab_len(DI, DO);
-  hipLaunchKernelGGL(slab_sum_kernel, dim3(divup(len, 256)), dim3(256), 0, st,
-                     (int)(grid.x * grid.y), len, slab, dparams);
-  return hipGetLastError();
+  const int nslab = (int)(grid.x * grid.y);
+  return colsum(nslab, len, slab, dparams, slab + (size_t)nslab * len, st);
 }
 
 bool supported(int din, int dout, int k) {
@@ -410,7 +398,8 @@ KDPC_API int kdpc_cost_volume_fwd(int b, int n1, int n2, int k, int din, int dou
 KDPC_API size_t kdpc_cost_volume_bwd_workspace_bytes(int b, int n1, int din, int dout) {
   if (b <= 0 || n1 <= 0 || !supported(din, dout, 1)) return 0;
   const long long nslabs = (long long)divup(n1, kWaves * kBwdQPW) * b;
-  return (size_t)(nslabs * slab_len(din, dout)) * sizeof(float);
+  const int len = slab_len(din, dout);
+  return (size_t)(nslabs * len + colsum_scratch_floats((int)nslabs, len)) * sizeof(float);
 }
 
 // Backward.  dout (B,N1,Dout) channel-last gradient of out.  Writes

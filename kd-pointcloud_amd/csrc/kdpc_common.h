@@ -70,6 +70,13 @@ __device__ __forceinline__ unsigned long long lanemask_lt() {
   return l == 0 ? 0ull : (~0ull >> (64 - l));
 }
 
+// Deterministic column sums of partial slabs (csrc/colsum.hip): dst[i] = sum_s slab[s][i]
+// for s < nrows, i < len, summed in fixed-size chunks (fixed order); scratch holds
+// colsum_scratch_floats(nrows, len) floats.
+size_t colsum_scratch_floats(int nrows, long long len);
+hipError_t colsum(int nrows, long long len, const float* slab, float* dst, float* scratch,
+                  hipStream_t st);
+
 }  // namespace kdpc
 
 // Argument validation shared by every C entry point: a bad size is an error code,

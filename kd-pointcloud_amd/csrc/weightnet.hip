@@ -194,22 +194,12 @@ __global__ __launch_bounds__(kBlock) void wn_bwd_kernel(int rows, int s, int k, 
   if (pi < kNP) slab[(long long)blockIdx.x * kNP + pi] = acc;
 }
 
-// dparams[i] = sum over slabs (ascending) of slab[s][i]
-__global__ void wn_slab_sum_kernel(int nslab, const float* __restrict__ slab,
-                                   float* __restrict__ dparams) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= kNP) return;
-  float a = 0.f;
-  for (int q = 0; q < nslab; ++q) a = __fadd_rn(a, slab[(long long)q * kNP + i]);
-  dparams[i] = a;
-}
-
 }  // namespace
 
 KDPC_API int kdpc_weightnet_param_count(void) { return kNP; }
 
 KDPC_API size_t kdpc_weightnet_bwd_workspace_bytes(void) {
-  return (size_t)kBwdGrid * kNP * sizeof(float);
+  return ((size_t)kBwdGrid * kNP + colsum_scratch_floats(kBwdGrid, kNP)) * sizeof(float);
 }
 
 KDPC_API int kdpc_weightnet_fwd(int b, int n, int s, int k, const float* xyz, const float* center,
@@ -239,6 +229,5 @@ KDPC_API int kdpc_weightnet_bwd(int b, int n, int s, int k, const float* xyz,
                      center, idx, params, dwt, drel, slab);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(wn_slab_sum_kernel, dim3(1), dim3(kNP), 0, st, kBwdGrid, slab, dparams);
-  KDPC_RETURN_LAUNCH();
+  return (int)colsum(kBwdGrid, kNP, slab, dparams, slab + (size_t)kBwdGrid * kNP, st);
 }
