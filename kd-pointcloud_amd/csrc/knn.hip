@@ -26,6 +26,14 @@ using namespace kdpc;
 
 namespace {
 
+// torch's expanded form ((-2*dot + |q|^2) + |r|^2), one rounding fewer to issue: -2*dot is
+// exact, so fma(-2, dot, |q|^2) == round(round(-2*dot) + |q|^2) bit for bit.
+__device__ __forceinline__ float sqdist_fast(float qx, float qy, float qz, float sq, float rx,
+                                             float ry, float rz, float sr) {
+  const float dot = __builtin_fmaf(qz, rz, __builtin_fmaf(qy, ry, __fmul_rn(qx, rx)));
+  return __fadd_rn(__builtin_fmaf(-2.0f, dot, sq), sr);
+}
+
 constexpr int kTile = 2048;      // refs per LDS tile (32 KiB of float4)
 constexpr int kSerialMax = 8;    // candidates per chunk inserted one by one
 
@@ -115,7 +123,7 @@ __global__ __launch_bounds__(256) void knn_kernel(int n, int s, int k,
     qy[q] = qp[1];
     qz[q] = qp[2];
     qs[q] = sqnorm3(qx[q], qy[q], qz[q]);
-    thr[q] = INFINITY;
+    thr[q] = qbase + q < s ? INFINITY : -INFINITY;  // padding queries never take candidates
     ld[q] = INFINITY;
     li[q] = 0x7fffffff;
   }
@@ -134,14 +142,22 @@ __global__ __launch_bounds__(256) void knn_kernel(int n, int s, int k,
       const bool valid = j < tn;
       const float4 r = tile[valid ? j : 0];
       const int gi = t0 + j;
+      // every query's candidate mask first, then ONE scalar branch for the common case of
+      // no candidate in the chunk for any of the wave's queries
+      float d[QW];
+      unsigned long long m[QW];
+      unsigned long long any = 0ull;
 #pragma unroll
       for (int q = 0; q < QW; ++q) {
-        if (qbase + q >= s) continue;  // wave-uniform
-        const float d = sqdist_expanded(qx[q], qy[q], qz[q], qs[q], r.x, r.y, r.z, r.w);
-        const bool cand = valid && d < thr[q];
-        const unsigned long long mask = __ballot(cand);
-        if (mask == 0ull) continue;
-        insert_candidates(mask, cand, d, gi, ld[q], li[q]);
+        d[q] = sqdist_fast(qx[q], qy[q], qz[q], qs[q], r.x, r.y, r.z, r.w);
+        m[q] = __ballot(valid && d[q] < thr[q]);
+        any |= m[q];
+      }
+      if (any == 0ull) continue;
+#pragma unroll
+      for (int q = 0; q < QW; ++q) {
+        if (m[q] == 0ull) continue;  // wave-uniform
+        insert_candidates(m[q], valid && d[q] < thr[q], d[q], gi, ld[q], li[q]);
         thr[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ld[q]), k - 1));
       }
     }
@@ -168,7 +184,7 @@ KDPC_API int kdpc_knn_point(int b, int n, int s, int k, const float* xyz, const 
   KDPC_CHECK_ARG(b >= 0 && n > 0 && s >= 0 && k >= 1 && k <= 64 && k <= n && b <= 65535);
   if ((long long)b * s == 0) return (int)hipSuccess;
   KDPC_CHECK_ARG(xyz && new_xyz && idx);
-  constexpr int QW = 4;
+  constexpr int QW = 8;
   const int per_block = 4 * QW;
   hipLaunchKernelGGL(knn_kernel<QW>, dim3(divup(s, per_block), b), dim3(256), 0,
                      (hipStream_t)stream, n, s, k, xyz, new_xyz, idx, dist);
