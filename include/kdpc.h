@@ -199,23 +199,29 @@ int kdpc_pointconv_bwd(int b, int n, int s, int k, int d, int o, const float *xy
 /* ---- fused WeightNet over grouped offsets (pointconv_util.py:184-215 as used by
  *      PointConv/PointConvD :217-258, :401-446: weightnet=16, hidden [8, 8], no BN) ------ */
 
-/* Packed parameter layout (floats): W0 (8,3) | b0 (8) | W1 (8,8) | b1 (8) | W2 (16,8) |
- * b2 (16), row-major nn.Conv2d weights; kdpc_weightnet_param_count() = 248. */
+/* Parameter-gradient layout of kdpc_weightnet_bwd (floats): dW0 (8,3) | db0 (8) | dW1 (8,8) |
+ * db1 (8) | dW2 (16,8) | db2 (16); kdpc_weightnet_param_count() = 248. */
 int kdpc_weightnet_param_count(void);
 
 /* wt (B,S,K,16) = ReLU(W2 ReLU(W1 ReLU(W0 rel + b0) + b1) + b2) with
- * rel = xyz[b, idx[b,s,k]] - center[b,s].  xyz (B,N,3), center (B,S,3), idx (B,S,K). */
+ * rel = xyz[b, idx[b,s,k]] - center[b,s].  xyz (B,N,3), center (B,S,3), idx (B,S,K);
+ * W0 (8,3) b0 (8) W1 (8,8) b1 (8) W2 (16,8) b2 (16) (nn.Conv2d weights, row-major). */
 int kdpc_weightnet_fwd(int b, int n, int s, int k, const float *xyz, const float *center,
-                       const int *idx, const float *params, float *wt, void *stream);
+                       const int *idx, const float *w0, const float *b0, const float *w1,
+                       const float *b1, const float *w2, const float *b2, float *wt,
+                       void *stream);
 
 /* Scratch bytes kdpc_weightnet_bwd needs (independent of the problem size). */
 size_t kdpc_weightnet_bwd_workspace_bytes(void);
 
-/* Backward of kdpc_weightnet_fwd for dwt (B,S,K,16): overwrites dparams (packed, 248) with
- * deterministic fixed-order sums (no atomics) and, if drel != NULL, writes drel (B,S,K,3). */
+/* Backward of kdpc_weightnet_fwd for dwt (B,S,K,16): overwrites dparams (248, layout above)
+ * with deterministic fixed-order sums (no atomics) and, if drel != NULL, writes
+ * drel (B,S,K,3). */
 int kdpc_weightnet_bwd(int b, int n, int s, int k, const float *xyz, const float *center,
-                       const int *idx, const float *params, const float *dwt, float *drel,
-                       float *dparams, void *workspace, size_t workspace_bytes, void *stream);
+                       const int *idx, const float *w0, const float *b0, const float *w1,
+                       const float *b1, const float *w2, const float *b2, const float *dwt,
+                       float *drel, float *dparams, void *workspace, size_t workspace_bytes,
+                       void *stream);
 
 /* ---- BatchNorm1d + LeakyReLU over point-major rows (pointconv_util.py:217-258, bn=True
  *      estimator PointConvs: Linear -> BatchNorm1d -> LeakyReLU(0.1)) ------------------- */
@@ -245,6 +251,16 @@ int kdpc_batchnorm_lrelu_bwd(int r, int c, const float *dy_act, const float *y_a
                              const float *invstd, float slope, float *dx, float *dweight,
                              float *dbias, void *workspace, size_t workspace_bytes,
                              void *stream);
+
+/* ---- deterministic column sums (bias gradients, partial-slab reductions) -------------- */
+
+/* Scratch bytes for kdpc_colsum over an (nrows, len) matrix (0 for nrows <= 64). */
+size_t kdpc_colsum_workspace_bytes(int nrows, int len);
+
+/* dst[i] = sum_r src[r][i] for a row-major (nrows, len) src, summed in fixed chunks (the
+ * result depends only on the shape). */
+int kdpc_colsum(int nrows, int len, const float *src, float *dst, void *workspace,
+                size_t workspace_bytes, void *stream);
 
 #ifdef __cplusplus
 }

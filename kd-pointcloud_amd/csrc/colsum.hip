@@ -72,3 +72,22 @@ hipError_t colsum(int nrows, long long len, const float* slab, float* dst, float
 }
 
 }  // namespace kdpc
+
+// ------------------------------------------------------------------------------ C ABI
+KDPC_API size_t kdpc_colsum_workspace_bytes(int nrows, int len) {
+  if (nrows <= 0 || len <= 0) return 0;
+  return kdpc::colsum_scratch_floats(nrows, len) * sizeof(float);
+}
+
+// dst[i] = sum over rows r of src[r][i] (row-major (nrows, len)), fixed summation order.
+KDPC_API int kdpc_colsum(int nrows, int len, const float* src, float* dst, void* workspace,
+                         size_t workspace_bytes, void* stream) {
+  KDPC_CHECK_ARG(nrows >= 0 && len >= 0);
+  if (len == 0) return (int)hipSuccess;
+  KDPC_CHECK_ARG(dst);
+  if (nrows == 0) return (int)hipMemsetAsync(dst, 0, sizeof(float) * len, (hipStream_t)stream);
+  KDPC_CHECK_ARG(src && workspace_bytes >= kdpc_colsum_workspace_bytes(nrows, len));
+  KDPC_CHECK_ARG(workspace_bytes == 0 || workspace);
+  return (int)kdpc::colsum(nrows, len, src, dst, reinterpret_cast<float*>(workspace),
+                           (hipStream_t)stream);
+}

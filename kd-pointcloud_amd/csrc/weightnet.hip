@@ -65,24 +65,26 @@ __device__ __forceinline__ void relu(float (&y)[O]) {
   for (int o = 0; o < O; ++o) y[o] = y[o] > 0.f ? y[o] : 0.f;
 }
 
-// The parameters arrive packed in one device buffer (layout above).  Their addresses are
+// The six parameter tensors (nn.Conv2d weights/biases, row-major).  Their addresses are
 // uniform, so the compiler reads them with scalar loads into SGPRs: no VGPRs are held for
-// the 248 weights.
+// the 248 weights, and no packing copy is needed on the host side.
+struct Params {
+  const float *w0, *b0, *w1, *b1, *w2, *b2;
+};
 __global__ __launch_bounds__(kBlock) void wn_fwd_kernel(int rows, int s, int k, int n,
                                                         const float* __restrict__ xyz,
                                                         const float* __restrict__ center,
                                                         const int* __restrict__ idx,
-                                                        const float* __restrict__ sp,
-                                                        float* __restrict__ wt) {
+                                                        Params sp, float* __restrict__ wt) {
   const int r = blockIdx.x * kBlock + threadIdx.x;
   if (r >= rows) return;
   float rel[3], h0[kH0], h1[kH1], o[kOut];
   rel_of(r, s, k, n, xyz, center, idx, rel);
-  dense<kH0, kIn>(sp + oW0, sp + oB0, rel, h0);
+  dense<kH0, kIn>(sp.w0, sp.b0, rel, h0);
   relu(h0);
-  dense<kH1, kH0>(sp + oW1, sp + oB1, h0, h1);
+  dense<kH1, kH0>(sp.w1, sp.b1, h0, h1);
   relu(h1);
-  dense<kOut, kH1>(sp + oW2, sp + oB2, h1, o);
+  dense<kOut, kH1>(sp.w2, sp.b2, h1, o);
   relu(o);
   float4* dst = reinterpret_cast<float4*>(wt + (long long)r * kOut);
 #pragma unroll
@@ -104,7 +106,7 @@ __global__ __launch_bounds__(kBlock) void wn_bwd_kernel(int rows, int s, int k, 
                                                         const float* __restrict__ xyz,
                                                         const float* __restrict__ center,
                                                         const int* __restrict__ idx,
-                                                        const float* __restrict__ sp,
+                                                        Params sp,
                                                         const float* __restrict__ dwt,
                                                         float* __restrict__ drel,
                                                         float* __restrict__ slab) {
@@ -126,11 +128,11 @@ __global__ __launch_bounds__(kBlock) void wn_bwd_kernel(int rows, int s, int k, 
     if (r < rows) {
       float rel[3], h0[kH0], h1[kH1], o[kOut];
       rel_of(r, s, k, n, xyz, center, idx, rel);
-      dense<kH0, kIn>(sp + oW0, sp + oB0, rel, h0);
+      dense<kH0, kIn>(sp.w0, sp.b0, rel, h0);
       relu(h0);
-      dense<kH1, kH0>(sp + oW1, sp + oB1, h0, h1);
+      dense<kH1, kH0>(sp.w1, sp.b1, h0, h1);
       relu(h1);
-      dense<kOut, kH1>(sp + oW2, sp + oB2, h1, o);
+      dense<kOut, kH1>(sp.w2, sp.b2, h1, o);
       float d2[kOut];
       const float4* src = reinterpret_cast<const float4*>(dwt + (long long)r * kOut);
 #pragma unroll
@@ -148,7 +150,7 @@ __global__ __launch_bounds__(kBlock) void wn_bwd_kernel(int rows, int s, int k, 
       for (int i = 0; i < kH1; ++i) {
         float a = 0.f;
 #pragma unroll
-        for (int q = 0; q < kOut; ++q) a = __builtin_fmaf(sp[oW2 + q * kH1 + i], d2[q], a);
+        for (int q = 0; q < kOut; ++q) a = __builtin_fmaf(sp.w2[q * kH1 + i], d2[q], a);
         d1[i] = h1[i] > 0.f ? a : 0.f;
       }
       float d0[kH0];
@@ -156,7 +158,7 @@ __global__ __launch_bounds__(kBlock) void wn_bwd_kernel(int rows, int s, int k, 
       for (int i = 0; i < kH0; ++i) {
         float a = 0.f;
 #pragma unroll
-        for (int q = 0; q < kH1; ++q) a = __builtin_fmaf(sp[oW1 + q * kH0 + i], d1[q], a);
+        for (int q = 0; q < kH1; ++q) a = __builtin_fmaf(sp.w1[q * kH0 + i], d1[q], a);
         d0[i] = h0[i] > 0.f ? a : 0.f;
       }
       if (drel) {
@@ -164,7 +166,7 @@ __global__ __launch_bounds__(kBlock) void wn_bwd_kernel(int rows, int s, int k, 
         for (int i = 0; i < kIn; ++i) {
           float a = 0.f;
 #pragma unroll
-          for (int q = 0; q < kH0; ++q) a = __builtin_fmaf(sp[oW0 + q * kIn + i], d0[q], a);
+          for (int q = 0; q < kH0; ++q) a = __builtin_fmaf(sp.w0[q * kIn + i], d0[q], a);
           drel[(long long)r * 3 + i] = a;
         }
       }
@@ -203,30 +205,38 @@ KDPC_API size_t kdpc_weightnet_bwd_workspace_bytes(void) {
 }
 
 KDPC_API int kdpc_weightnet_fwd(int b, int n, int s, int k, const float* xyz, const float* center,
-                                const int* idx, const float* params, float* wt, void* stream) {
+                                const int* idx, const float* w0, const float* b0, const float* w1,
+                                const float* b1, const float* w2, const float* b2, float* wt,
+                                void* stream) {
   KDPC_CHECK_ARG(b >= 0 && n > 0 && s >= 0 && k >= 1);
   const long long rows = (long long)b * s * k;
   if (rows == 0) return (int)hipSuccess;
-  KDPC_CHECK_ARG(xyz && center && idx && params && wt && rows < (1ll << 31) - kBlock);
+  KDPC_CHECK_ARG(xyz && center && idx && w0 && b0 && w1 && b1 && w2 && b2 && wt &&
+                 rows < (1ll << 31) - kBlock);
+  const Params p{w0, b0, w1, b1, w2, b2};
   hipLaunchKernelGGL(wn_fwd_kernel, dim3((unsigned)divupll(rows, kBlock)), dim3(kBlock), 0,
-                     (hipStream_t)stream, (int)rows, s, k, n, xyz, center, idx, params, wt);
+                     (hipStream_t)stream, (int)rows, s, k, n, xyz, center, idx, p, wt);
   KDPC_RETURN_LAUNCH();
 }
 
 KDPC_API int kdpc_weightnet_bwd(int b, int n, int s, int k, const float* xyz,
-                                const float* center, const int* idx, const float* params,
-                                const float* dwt, float* drel, float* dparams, void* workspace,
-                                size_t workspace_bytes, void* stream) {
+                                const float* center, const int* idx, const float* w0,
+                                const float* b0, const float* w1, const float* b1,
+                                const float* w2, const float* b2, const float* dwt, float* drel,
+                                float* dparams, void* workspace, size_t workspace_bytes,
+                                void* stream) {
   KDPC_CHECK_ARG(b >= 0 && n > 0 && s >= 0 && k >= 1);
   const long long rows = (long long)b * s * k;
   KDPC_CHECK_ARG(dparams && workspace && workspace_bytes >= kdpc_weightnet_bwd_workspace_bytes());
-  KDPC_CHECK_ARG(rows == 0 || (xyz && center && idx && params && dwt));
+  KDPC_CHECK_ARG(rows == 0 ||
+                 (xyz && center && idx && w0 && b0 && w1 && b1 && w2 && b2 && dwt));
   KDPC_CHECK_ARG(rows < (1ll << 31) - (long long)kBwdGrid * kBlock);
   hipStream_t st = (hipStream_t)stream;
+  const Params p{w0, b0, w1, b1, w2, b2};
   float* slab = reinterpret_cast<float*>(workspace);
   // every slab row is written (rows == 0 -> all-zero partials)
   hipLaunchKernelGGL(wn_bwd_kernel, dim3(kBwdGrid), dim3(kBlock), 0, st, (int)rows, s, k, n, xyz,
-                     center, idx, params, dwt, drel, slab);
+                     center, idx, p, dwt, drel, slab);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   return (int)colsum(kBwdGrid, kNP, slab, dparams, slab + (size_t)kBwdGrid * kNP, st);

@@ -49,16 +49,19 @@ _SIGNATURES = {
     "kdpc_batchnorm_lrelu_apply": [_c_int, _c_int] + [_vp] * 5 + [_c_float, _vp, _vp],
     "kdpc_batchnorm_lrelu_bwd": [_c_int, _c_int] + [_vp] * 6 + [_c_float] + [_vp] * 4
                                 + [_c_size, _vp],
+    "kdpc_colsum_workspace_bytes": [_c_int, _c_int],
+    "kdpc_colsum": [_c_int, _c_int, _vp, _vp, _vp, _c_size, _vp],
     "kdpc_weightnet_param_count": [],
-    "kdpc_weightnet_fwd": [_c_int] * 4 + [_vp] * 6,
+    "kdpc_weightnet_fwd": [_c_int] * 4 + [_vp] * 11,
     "kdpc_weightnet_bwd_workspace_bytes": [],
-    "kdpc_weightnet_bwd": [_c_int] * 4 + [_vp] * 8 + [_c_size, _vp],
+    "kdpc_weightnet_bwd": [_c_int] * 4 + [_vp] * 13 + [_c_size, _vp],
 }
 _RESTYPES = {"kdpc_csr_workspace_bytes": _c_size, "kdpc_cost_volume_bwd_workspace_bytes": _c_size,
              "kdpc_pointconv_fwd_workspace_bytes": _c_size,
              "kdpc_pointconv_bwd_workspace_bytes": _c_size,
              "kdpc_weightnet_bwd_workspace_bytes": _c_size,
-             "kdpc_batchnorm_workspace_bytes": _c_size}
+             "kdpc_batchnorm_workspace_bytes": _c_size,
+             "kdpc_colsum_workspace_bytes": _c_size}
 
 EXPORTED = tuple(_SIGNATURES)
 
@@ -481,21 +484,21 @@ def pointconv_bwd(xyz, center, feats, idx, wt, wl, dy, csr, need_xyz=True):
 
 # ------------------------------------------------------------------- fused WeightNet
 def weightnet_fwd(xyz, center, idx, params):
-    """wt (B,S,K,16) from xyz (B,N,3), center (B,S,3), idx (B,S,K) i32 and the packed
-    WeightNet parameters (248 floats: W0 (8,3) b0 W1 (8,8) b1 W2 (16,8) b2)."""
+    """wt (B,S,K,16) from xyz (B,N,3), center (B,S,3), idx (B,S,K) i32 and the six WeightNet
+    tensors params = (W0 (8,3[,1,1]), b0, W1 (8,8), b1, W2 (16,8), b2)."""
     B, N, _ = xyz.shape
     S, K = idx.shape[1], idx.shape[2]
     f = torch.float32
     wt = torch.empty((B, S, K, 16), dtype=f, device=xyz.device)
+    ptrs = [_dev(p, f, f"weightnet param {i}") for i, p in enumerate(params)]
     _call("kdpc_weightnet_fwd", B, N, S, K, _dev(xyz, f, "xyz"), _dev(center, f, "center"),
-          _dev(idx, torch.int32, "idx"), _dev(params, f, "params"), _dev(wt, f, "wt"),
-          _stream(xyz),
+          _dev(idx, torch.int32, "idx"), *ptrs, _dev(wt, f, "wt"), _stream(xyz),
           work=(B * (12 * N + 12 * S + S * K * (4 + 64)), 2.0 * B * S * K * (24 + 64 + 128)))
     return wt
 
 
 def weightnet_bwd(xyz, center, idx, params, dwt, need_rel=False):
-    """-> (drel (B,S,K,3) | None, dparams (248,) packed like params)."""
+    """-> (drel (B,S,K,3) | None, dparams (248,): dW0 | db0 | dW1 | db1 | dW2 | db2)."""
     B, N, _ = xyz.shape
     S, K = idx.shape[1], idx.shape[2]
     f = torch.float32
@@ -503,12 +506,13 @@ def weightnet_bwd(xyz, center, idx, params, dwt, need_rel=False):
     lib = load_library()
     ws_bytes = lib.kdpc_weightnet_bwd_workspace_bytes()
     ws = torch.empty((ws_bytes,), dtype=torch.uint8, device=dev)
-    dparams = torch.empty_like(params)
+    dparams = torch.empty((lib.kdpc_weightnet_param_count(),), dtype=f, device=dev)
     drel = torch.empty((B, S, K, 3), dtype=f, device=dev) if need_rel else None
+    ptrs = [_dev(p, f, f"weightnet param {i}") for i, p in enumerate(params)]
     _call("kdpc_weightnet_bwd", B, N, S, K, _dev(xyz, f, "xyz"), _dev(center, f, "center"),
-          _dev(idx, torch.int32, "idx"), _dev(params, f, "params"), _dev(dwt, f, "dwt"),
-          drel.data_ptr() if need_rel else None, _dev(dparams, f, "dparams"), ws.data_ptr(),
-          ws_bytes, _stream(xyz))
+          _dev(idx, torch.int32, "idx"), *ptrs, _dev(dwt, f, "dwt"),
+          drel.data_ptr() if need_rel else None, dparams.data_ptr(), ws.data_ptr(), ws_bytes,
+          _stream(xyz))
     return drel, dparams
 
 
@@ -557,3 +561,16 @@ def batchnorm_lrelu_bwd(dy, y, x2, weight, mean, invstd, slope):
           float(slope), dx.data_ptr(), dw.data_ptr(), db.data_ptr(), ws.data_ptr(), ws.numel(),
           _stream(x2), work=(20 * R * C, 0))
     return dx, dw, db
+
+
+def colsum(x2):
+    """Column sums of a row-major (R, L) tensor, deterministic fixed-order: -> (L,)."""
+    R, L = x2.shape
+    f = torch.float32
+    lib = load_library()
+    nb = lib.kdpc_colsum_workspace_bytes(R, L)
+    ws = _workspace(nb, x2.device)
+    out = torch.empty((L,), dtype=f, device=x2.device)
+    _call("kdpc_colsum", R, L, _dev(x2, f, "src"), out.data_ptr(), ws.data_ptr(), nb,
+          _stream(x2))
+    return out

@@ -113,8 +113,18 @@ class PointConvBidirection(nn.Module):
         pc = torch.cat([xyz1, xyz2], 0)
         color = torch.cat([color1, color2], 0)
         pcs, feats, feats_out, fps, feat_l4_3 = self._encode(pc, color, fps_idx)
-        one = lambda t: t[:B]  # noqa: E731
-        two = lambda t: t[B:]  # noqa: E731
+        # pc1 / pc2 halves of a pair-batch tensor through ONE split per tensor: the backward
+        # of a split is one concatenation, where two separate slices would each allocate and
+        # zero a full-size gradient and copy into it, and then add the two
+        halves = {}
+
+        def _half(t, i):
+            h = halves.get(id(t))
+            if h is None:
+                h = halves[id(t)] = (t, t.split(B))
+            return h[1][i]
+        one = lambda t: _half(t, 0)  # noqa: E731
+        two = lambda t: _half(t, 1)  # noqa: E731
 
         # ---- level 3 (coarsest): no prior flow
         c_feat_l3 = torch.cat([feats[3], feat_l4_3], dim=-1)

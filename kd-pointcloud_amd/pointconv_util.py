@@ -287,9 +287,9 @@ class WeightNet(nn.Module):
         idx (B,S,K) int32 -> (B,S,K,out).  One fused HIP kernel each way where supported
         (csrc/weightnet.hip); otherwise group + channel_last."""
         if self.fusable():
-            params = torch.cat([t.reshape(-1) for c in self.mlp_convs for t in (c.weight, c.bias)])
+            params = [t for c in self.mlp_convs for t in (c.weight, c.bias)]
             return _WeightNetFn.apply(xyz.contiguous(), center.contiguous(),
-                                      _as_idx32(idx).contiguous(), params)
+                                      _as_idx32(idx).contiguous(), *params)
         B, S, _ = center.shape
         return self.channel_last(index_points_group(xyz, idx) - center.view(B, S, 1, 3))
 
@@ -312,15 +312,17 @@ class _WeightNetFn(torch.autograd.Function):
     """Fused grouped-offset WeightNet (csrc/weightnet.hip), packed parameters."""
 
     @staticmethod
-    def forward(ctx, xyz, center, idx, params):
-        ctx.save_for_backward(xyz, center, idx, params)
+    def forward(ctx, xyz, center, idx, *params):
+        ctx.save_for_backward(xyz, center, idx, *params)
         return _nat.weightnet_fwd(xyz, center, idx, params)
 
     @staticmethod
     def backward(ctx, dwt):
-        xyz, center, idx, params = ctx.saved_tensors
+        xyz, center, idx, *params = ctx.saved_tensors
         need_rel = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
-        drel, dparams = _nat.weightnet_bwd(xyz, center, idx, params, dwt.contiguous(), need_rel)
+        drel, dflat = _nat.weightnet_bwd(xyz, center, idx, params, dwt.contiguous(), need_rel)
+        dparams = [g.view_as(p) for g, p in
+                   zip(dflat.split([p.numel() for p in params]), params)]
         dxyz = dcenter = None
         if need_rel:
             B, S, K, _ = drel.shape
@@ -329,7 +331,7 @@ class _WeightNetFn(torch.autograd.Function):
                 dxyz = _nat.group_rows_grad(drel.view(B, S * K, 3), _nat.csr_of(idx, N), B, N, 3)
             if ctx.needs_input_grad[1]:
                 dcenter = -drel.sum(2)
-        return dxyz, dcenter, None, dparams
+        return (dxyz, dcenter, None, *dparams)
 
 
 class _PointConvContract(torch.autograd.Function):
@@ -613,21 +615,23 @@ class CrossLayerLight(nn.Module):
         Both directions of the first cost volume run as ONE batch of 2B (shared weights, no
         BN between them), then the pc1-side refinement with pos2/mlp2."""
         B = xa.shape[0] // 2
-        xb = torch.cat([xa[B:], xa[:B]], 0)
+        xa1, xa2 = xa.split(B)
+        xb = torch.cat([xa2, xa1], 0)
         # one kNN serves both directions, and its pc1 half is exactly the neighbour set of
         # the refinement cross(pc1, pc2) below (the reference searches it twice)
         idx = knn_point(self.nsample, xb, xa)
         ta = _linear_1x1(self.cross_t11, fa)
         tb = _linear_1x1(self.cross_t22, fa)  # t22 of cat(feat2, feat1) = halves swapped
-        tb = torch.cat([tb[B:], tb[:B]], 0)
+        tb1, tb2 = tb.split(B)
+        tb = torch.cat([tb2, tb1], 0)
         both = _cost_volume_cl(self.nsample, xa, xb, ta, tb, self.pos1, self.mlp1,
                                self._act(self.bn1), idx)
-        feat1_new, feat2_new = both[:B], both[B:]
+        feat1_new, feat2_new = both.split(B)
         if self.mlp2 is False:
             return feat1_new, feat2_new
         feat1_new = _linear_1x1(self.cross_t1, feat1_new)
         feat2_new = _linear_1x1(self.cross_t2, feat2_new)
-        feat1_final = _cost_volume_cl(self.nsample, xa[:B], xa[B:], feat1_new, feat2_new,
+        feat1_final = _cost_volume_cl(self.nsample, xa1, xa2, feat1_new, feat2_new,
                                       self.pos2, self.mlp2, self._act(self.bn2),
                                       _nat.batch_prefix(idx, B))
         return feat1_new, feat2_new, feat1_final
