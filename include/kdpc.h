@@ -99,6 +99,16 @@ int kdpc_three_interpolate_grad(int b, int c, int n, int m, const float *grad_ou
 int kdpc_knn_point(int b, int n, int s, int k, const float *xyz, const float *new_xyz, int *idx,
                    float *dist, void *stream);
 
+/* Scratch bytes for kdpc_knn_point_ws (0: the plain scan is used, pass workspace = NULL). */
+size_t kdpc_knn_workspace_bytes(int b, int n, int s);
+
+/* kdpc_knn_point with scratch: the refs are first counting-sorted into a Morton cell grid
+ * and each query's threshold is seeded with the exact K-th distance to the 256 sorted refs
+ * around its cell, so the scan inserts ~K candidates; results identical to kdpc_knn_point. */
+int kdpc_knn_point_ws(int b, int n, int s, int k, const float *xyz, const float *new_xyz,
+                      int *idx, float *dist, void *workspace, size_t workspace_bytes,
+                      void *stream);
+
 /* ---- point-major grouping + deterministic scatter (no reference counterpart: these
  *      replace index_points_group's permute/grouping_operation/permute chain,
  *      pointconv_util.py:122-133, and its atomicAdd backward) ------------------------- */

@@ -88,9 +88,9 @@ __device__ __forceinline__ void insert_candidates(unsigned long long mask, bool 
       mask &= mask - 1;
       const float cd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), j));
       const int ci = __builtin_amdgcn_readlane(gi, j);
-      const bool gt = ld > cd;
       const float pd = wave_shr1(ld, -INFINITY);
       const int pi = wave_shr1(li, 0);
+      const bool gt = ld > cd;
       const bool pgt = pd > cd;
       const float nd = gt ? (pgt ? pd : cd) : ld;
       const int ni = gt ? (pgt ? pi : ci) : li;
@@ -100,12 +100,194 @@ __device__ __forceinline__ void insert_candidates(unsigned long long mask, bool 
   }
 }
 
+// ------------------------------------------------------------ seeded threshold
+// The plain scan starts every query with an empty list, so the threshold only tightens as
+// the list fills: about K ln(N/K) insertions per query (~110 serial + several bitonic
+// merges for K=32, N=8192, random point order), several times the cost of the distances.
+// Visiting nearby refs first does not fix that (a near-first order inserts MORE: every
+// closer ref improves the list); a tight threshold from the start does:
+//   1. the refs are counting-sorted into a 16^3 Morton-ordered cell grid over their
+//      bounding box (one workgroup per cloud: LDS histogram, scan, scatter);
+//   2. each query takes the kWin sorted refs around its own cell and selects the K-th
+//      smallest of their distances exactly (32-step radix select on the order-preserving
+//      key, one ballot popcount per step, no LDS): T >= its true K-th distance, and tight
+//      because those refs are its spatial neighbours;
+//   3. the unchanged index-order scan then starts with threshold "d <= T" (strict
+//      d < nextafter(T)) instead of +inf: ~K candidates per query, spread over the chunks
+//      so they go in one by one, and nearly every chunk is skipped by the scalar branch.
+// Every ref is still scanned in index order and at least K refs satisfy d <= T, so the
+// result is identical to the unseeded scan.
+constexpr int kG = 16;                   // cells per axis
+constexpr int kCells = kG * kG * kG;     // 4096
+constexpr int kSortThreads = 1024;
+
+__device__ __forceinline__ int spread4(int v) {  // bits b3..b0 -> b9,b6,b3,b0
+  return (v & 1) | ((v & 2) << 2) | ((v & 4) << 4) | ((v & 8) << 6);
+}
+
+// bb = {min x, min y, min z, scale x, scale y, scale z}
+__device__ __forceinline__ int cell_of(float x, float y, float z, const float* bb) {
+  const float fx = fminf(fmaxf((x - bb[0]) * bb[3], 0.f), (float)(kG - 1));
+  const float fy = fminf(fmaxf((y - bb[1]) * bb[4], 0.f), (float)(kG - 1));
+  const float fz = fminf(fmaxf((z - bb[2]) * bb[5], 0.f), (float)(kG - 1));
+  return spread4((int)fx) | (spread4((int)fy) << 1) | (spread4((int)fz) << 2);
+}
+
+// in-place exclusive scan of cnt[kCells] by kSortThreads threads (4 cells each)
+__device__ void block_exclusive_scan(int* cnt, int* wsum) {
+  const int t = threadIdx.x, lane = lane_id(), wv = t >> 6;
+  int v[4], tot = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[i] = cnt[4 * t + i];
+    tot += v[i];
+  }
+  int inc = tot;  // inclusive wave scan
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int u = __shfl_up(inc, o, kWave);
+    if (lane >= o) inc += u;
+  }
+  if (lane == kWave - 1) wsum[wv] = inc;
+  __syncthreads();
+  int base = 0;
+  for (int w = 0; w < wv; ++w) base += wsum[w];
+  int run = base + inc - tot;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    cnt[4 * t + i] = run;
+    run += v[i];
+  }
+  __syncthreads();
+}
+
+// One workgroup per cloud: bounding box, cell histogram, offsets, scatter.
+// rs (B,N) float4 {x, y, z, |r|^2} in cell order, roff (B, kCells+1) first sorted position of
+// each cell, bbox (B,8) = {min xyz, scale xyz}.
+__global__ __launch_bounds__(kSortThreads) void ref_sort_kernel(int n,
+                                                                const float* __restrict__ xyz,
+                                                                float* __restrict__ bbox,
+                                                                int* __restrict__ roff,
+                                                                float4* __restrict__ rs) {
+  __shared__ int cnt[kCells];
+  __shared__ int wsum[kSortThreads / kWave];
+  __shared__ float red[6][kSortThreads / kWave];
+  __shared__ float bb[6];
+  const int b = blockIdx.x, t = threadIdx.x, lane = lane_id(), wv = t >> 6;
+  const float* p = xyz + (long long)b * n * 3;
+  float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int i = t; i < n; i += kSortThreads) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float v = p[i * 3 + c];
+      mn[c] = fminf(mn[c], v);
+      mx[c] = fmaxf(mx[c], v);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      mn[c] = fminf(mn[c], __shfl_xor(mn[c], o, kWave));
+      mx[c] = fmaxf(mx[c], __shfl_xor(mx[c], o, kWave));
+    }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      red[c][wv] = mn[c];
+      red[3 + c][wv] = mx[c];
+    }
+  }
+  for (int c = t; c < kCells; c += kSortThreads) cnt[c] = 0;
+  __syncthreads();
+  if (t < 3) {
+    float a = INFINITY, z = -INFINITY;
+    for (int w = 0; w < kSortThreads / kWave; ++w) {
+      a = fminf(a, red[t][w]);
+      z = fmaxf(z, red[3 + t][w]);
+    }
+    const float ext = z - a;
+    bb[t] = a;
+    bb[3 + t] = ext > 0.f ? (float)kG / ext : 0.f;
+    bbox[b * 8 + t] = bb[t];
+    bbox[b * 8 + 3 + t] = bb[3 + t];
+  }
+  __syncthreads();
+  for (int i = t; i < n; i += kSortThreads)
+    atomicAdd(&cnt[cell_of(p[i * 3], p[i * 3 + 1], p[i * 3 + 2], bb)], 1);
+  __syncthreads();
+  block_exclusive_scan(cnt, wsum);
+  int* ro = roff + (long long)b * (kCells + 1);
+  for (int c = t; c < kCells; c += kSortThreads) ro[c] = cnt[c];
+  if (t == 0) ro[kCells] = n;
+  __syncthreads();
+  float4* rso = rs + (long long)b * n;
+  for (int i = t; i < n; i += kSortThreads) {
+    const float x = p[i * 3], y = p[i * 3 + 1], z = p[i * 3 + 2];
+    const int pos = atomicAdd(&cnt[cell_of(x, y, z, bb)], 1);  // order within a cell: any
+    rso[pos] = make_float4(x, y, z, sqnorm3(x, y, z));
+  }
+}
+
+constexpr int kWin = 256;  // refs around a query's cell that seed its threshold
+
+// order-preserving float -> unsigned key (total order of non-NaN floats)
+__device__ __forceinline__ unsigned ord_key(float f) {
+  const unsigned u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float from_ord_key(unsigned k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+// Seed thr[q] (valid queries) with nextafter(T), T = the K-th smallest distance from the
+// query to the kWin sorted refs around its cell.
 template <int QW>
+__device__ __forceinline__ void seed_thresholds(int n, int k, int b, int qbase, int s,
+                                                const float* qx, const float* qy,
+                                                const float* qz, const float* qs,
+                                                const float4* __restrict__ rs,
+                                                const float* __restrict__ bbox,
+                                                const int* __restrict__ roff, float* thr) {
+  const float4* rb = rs + (long long)b * n;
+  float bb[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) bb[i] = bbox[b * 8 + i];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) {  // one query at a time: 4 key VGPRs live, not 4 * QW
+    unsigned key[kWin / kWave];
+    int w0 = roff[(long long)b * (kCells + 1) + cell_of(qx[q], qy[q], qz[q], bb)] - kWin / 2;
+    w0 = w0 < 0 ? w0 + n : w0;  // n >= kWin: one wrap at most
+#pragma unroll
+    for (int i = 0; i < kWin / kWave; ++i) {
+      int pz = w0 + lane_id() + kWave * i;
+      pz = pz >= n ? pz - n : pz;
+      const float4 r = rb[pz];
+      key[i] = ord_key(sqdist_fast(qx[q], qy[q], qz[q], qs[q], r.x, r.y, r.z, r.w));
+    }
+    unsigned ans = 0u;  // largest key with fewer than k window keys below it = k-th smallest
+    for (int bit = 31; bit >= 0; --bit) {
+      const unsigned t = ans | (1u << bit);
+      int cnt = 0;
+#pragma unroll
+      for (int i = 0; i < kWin / kWave; ++i) cnt += __popcll(__ballot(key[i] < t));
+      ans = cnt < k ? t : ans;
+    }
+    // d < nextafter(T) <=> d <= T; a K-th at +inf or NaN (NaN coordinates) leaves no bound
+    if (qbase + q < s && ans < ord_key(INFINITY)) thr[q] = from_ord_key(ans + 1u);
+  }
+}
+
+template <int QW, bool SEED>
 __global__ __launch_bounds__(256) void knn_kernel(int n, int s, int k,
                                                   const float* __restrict__ xyz,
                                                   const float* __restrict__ new_xyz,
                                                   int* __restrict__ idx,
-                                                  float* __restrict__ dist) {
+                                                  float* __restrict__ dist,
+                                                  const float4* __restrict__ rs,
+                                                  const float* __restrict__ bbox,
+                                                  const int* __restrict__ roff) {
   __shared__ float4 tile[kTile];
   const int b = blockIdx.y;
   const int wave = threadIdx.x >> 6;
@@ -127,6 +309,7 @@ __global__ __launch_bounds__(256) void knn_kernel(int n, int s, int k,
     ld[q] = INFINITY;
     li[q] = 0x7fffffff;
   }
+  if constexpr (SEED) seed_thresholds<QW>(n, k, b, qbase, s, qx, qy, qz, qs, rs, bbox, roff, thr);
 
   for (int t0 = 0; t0 < n; t0 += kTile) {
     const int tn = min(kTile, n - t0);
@@ -158,7 +341,9 @@ __global__ __launch_bounds__(256) void knn_kernel(int n, int s, int k,
       for (int q = 0; q < QW; ++q) {
         if (m[q] == 0ull) continue;  // wave-uniform
         insert_candidates(m[q], valid && d[q] < thr[q], d[q], gi, ld[q], li[q]);
-        thr[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ld[q]), k - 1));
+        // seeded: the list's K-th is <= T once K entries are in, +inf before
+        thr[q] = fminf(thr[q],
+                       __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ld[q]), k - 1)));
       }
     }
   }
@@ -174,6 +359,48 @@ __global__ __launch_bounds__(256) void knn_kernel(int n, int s, int k,
   }
 }
 
+struct SeedWs {
+  float* bbox;
+  int* roff;
+  float4* rs;
+  size_t bytes;
+};
+
+inline size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+SeedWs seed_ws(int b, int n, void* base) {
+  SeedWs w{};
+  char* p = reinterpret_cast<char*>(base);
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    char* q = p ? p + o : nullptr;
+    o += align256(bytes);
+    return q;
+  };
+  w.bbox = reinterpret_cast<float*>(take(sizeof(float) * 8 * b));
+  w.roff = reinterpret_cast<int*>(take(sizeof(int) * (size_t)b * (kCells + 1)));
+  w.rs = reinterpret_cast<float4*>(take(sizeof(float4) * (size_t)b * n));
+  w.bytes = o;
+  return w;
+}
+
+// The seed costs one sort launch (~10-20 us) and a 256-ref window per query; it pays once
+// the plain scan's insertion work dominates, i.e. thousands of refs.
+inline bool use_seed(int b, int n, int s) { return n >= 2048 && (long long)b * s >= 8192; }
+
+template <bool SEED>
+void launch_knn(int b, int n, int s, int k, const float* xyz, const float* new_xyz, int* idx,
+                float* dist, const SeedWs& w, hipStream_t st) {
+  // Large reference sets amortise the per-chunk scalar branch over 8 queries per wave; at
+  // the model's sizes (N <= 8192) 4 per wave measured faster.
+  if (n >= 32768)
+    hipLaunchKernelGGL((knn_kernel<8, SEED>), dim3(divup(s, 32), b), dim3(256), 0, st, n, s, k,
+                       xyz, new_xyz, idx, dist, w.rs, w.bbox, w.roff);
+  else
+    hipLaunchKernelGGL((knn_kernel<4, SEED>), dim3(divup(s, 16), b), dim3(256), 0, st, n, s, k,
+                       xyz, new_xyz, idx, dist, w.rs, w.bbox, w.roff);
+}
+
 }  // namespace
 
 // knn_point(nsample=k, xyz (B,N,3) refs, new_xyz (B,S,3) queries) -> idx (B,S,K) int32,
@@ -184,14 +411,31 @@ KDPC_API int kdpc_knn_point(int b, int n, int s, int k, const float* xyz, const 
   KDPC_CHECK_ARG(b >= 0 && n > 0 && s >= 0 && k >= 1 && k <= 64 && k <= n && b <= 65535);
   if ((long long)b * s == 0) return (int)hipSuccess;
   KDPC_CHECK_ARG(xyz && new_xyz && idx);
-  // Large reference sets amortise the per-chunk scalar branch over 8 queries per wave; at
-  // the model's sizes (N <= 8192) a wave's 8 queries disagree on insertions more often and 4
-  // per wave measured faster (177 vs 195 us at B=16, N=S=8192, K=32).
-  if (n >= 32768)
-    hipLaunchKernelGGL(knn_kernel<8>, dim3(divup(s, 32), b), dim3(256), 0, (hipStream_t)stream,
-                       n, s, k, xyz, new_xyz, idx, dist);
-  else
-    hipLaunchKernelGGL(knn_kernel<4>, dim3(divup(s, 16), b), dim3(256), 0, (hipStream_t)stream,
-                       n, s, k, xyz, new_xyz, idx, dist);
+  launch_knn<false>(b, n, s, k, xyz, new_xyz, idx, dist, SeedWs{}, (hipStream_t)stream);
+  KDPC_RETURN_LAUNCH();
+}
+
+// Scratch bytes for kdpc_knn_point_ws; 0 when the problem is small enough that the plain
+// scan is used (then pass workspace = NULL).
+KDPC_API size_t kdpc_knn_workspace_bytes(int b, int n, int s) {
+  if (b <= 0 || n <= 0 || s <= 0 || !use_seed(b, n, s)) return 0;
+  return seed_ws(b, n, nullptr).bytes;
+}
+
+// kdpc_knn_point with scratch for the seeded threshold (identical results).
+KDPC_API int kdpc_knn_point_ws(int b, int n, int s, int k, const float* xyz,
+                               const float* new_xyz, int* idx, float* dist, void* workspace,
+                               size_t workspace_bytes, void* stream) {
+  KDPC_CHECK_ARG(b >= 0 && n > 0 && s >= 0 && k >= 1 && k <= 64 && k <= n && b <= 65535);
+  if ((long long)b * s == 0) return (int)hipSuccess;
+  const size_t need = kdpc_knn_workspace_bytes(b, n, s);
+  if (need == 0 || workspace == nullptr)
+    return kdpc_knn_point(b, n, s, k, xyz, new_xyz, idx, dist, stream);
+  KDPC_CHECK_ARG(xyz && new_xyz && idx && workspace_bytes >= need);
+  hipStream_t st = (hipStream_t)stream;
+  const SeedWs w = seed_ws(b, n, workspace);
+  hipLaunchKernelGGL(ref_sort_kernel, dim3(b), dim3(kSortThreads), 0, st, n, xyz, w.bbox, w.roff,
+                     w.rs);
+  launch_knn<true>(b, n, s, k, xyz, new_xyz, idx, dist, w, st);
   KDPC_RETURN_LAUNCH();
 }

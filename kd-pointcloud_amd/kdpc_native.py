@@ -26,6 +26,8 @@ _SIGNATURES = {
     "kdpc_three_interpolate": [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
     "kdpc_three_interpolate_grad": [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
     "kdpc_knn_point": [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
+    "kdpc_knn_workspace_bytes": [_c_int] * 3,
+    "kdpc_knn_point_ws": [_c_int] * 4 + [_vp] * 5 + [_c_size, _vp],
     "kdpc_group_rows": [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp],
     "kdpc_csr_workspace_bytes": [_c_int, _c_int, _c_int],
     "kdpc_csr_build": [_c_int, _c_int, _c_int, _vp, _vp, _c_size, _vp, _vp, _vp],
@@ -61,7 +63,7 @@ _RESTYPES = {"kdpc_csr_workspace_bytes": _c_size, "kdpc_cost_volume_bwd_workspac
              "kdpc_pointconv_bwd_workspace_bytes": _c_size,
              "kdpc_weightnet_bwd_workspace_bytes": _c_size,
              "kdpc_batchnorm_workspace_bytes": _c_size,
-             "kdpc_colsum_workspace_bytes": _c_size}
+             "kdpc_colsum_workspace_bytes": _c_size, "kdpc_knn_workspace_bytes": _c_size}
 
 EXPORTED = tuple(_SIGNATURES)
 
@@ -223,17 +225,22 @@ def three_interpolate(points, idx, weight):
     return out
 
 
-def knn_point(nsample, xyz, new_xyz, return_dist=False):
-    """xyz (B,N,3) refs, new_xyz (B,S,3) queries -> idx (B,S,K) i32 ascending (dist, idx)."""
+def knn_point(nsample, xyz, new_xyz, return_dist=False, seeded=True):
+    """xyz (B,N,3) refs, new_xyz (B,S,3) queries -> idx (B,S,K) i32 ascending (dist, idx).
+    seeded: allow the seeded-threshold scan where it pays (identical results; False forces
+    the unseeded scan, for tests)."""
     B, N, _ = xyz.shape
     S = new_xyz.shape[1]
     if nsample > N:
         raise ValueError(f"knn_point: nsample={nsample} > number of points {N}")
     idx = torch.empty((B, S, nsample), dtype=torch.int32, device=xyz.device)
     dist = torch.empty((B, S, nsample), dtype=torch.float32, device=xyz.device) if return_dist else None
-    _call("kdpc_knn_point", B, N, S, int(nsample), _dev(xyz, torch.float32, "xyz"),
+    ws_bytes = load_library().kdpc_knn_workspace_bytes(B, N, S) if seeded else 0
+    ws = torch.empty((ws_bytes,), dtype=torch.uint8, device=xyz.device) if ws_bytes else None
+    _call("kdpc_knn_point_ws", B, N, S, int(nsample), _dev(xyz, torch.float32, "xyz"),
           _dev(new_xyz, torch.float32, "new_xyz"), _dev(idx, torch.int32, "idx"),
-          _dev(dist, torch.float32, "dist") if dist is not None else None, _stream(xyz),
+          _dev(dist, torch.float32, "dist") if dist is not None else None,
+          ws.data_ptr() if ws is not None else None, ws_bytes, _stream(xyz),
           work=(B * (12 * N + 12 * S + 4 * S * nsample * (2 if return_dist else 1)),
                 B * S * N * 8))
     return (idx, dist) if return_dist else idx

@@ -118,6 +118,57 @@ def test_knn_matches_oracle(nat, n, s, k):
     np.testing.assert_array_equal(dist.cpu().numpy().view(np.int32), dist_ref.view(np.int32))
 
 
+def _knn_both(nat, k, ref, qry):
+    r, q = _t(ref), _t(qry)
+    a = nat.knn_point(k, r, q, return_dist=True)
+    b = nat.knn_point(k, r, q, return_dist=True, seeded=False)
+    return [t.cpu().numpy() for t in a + b]
+
+
+@pytest.mark.parametrize("b,n,s,k", [(2, 4096, 4100, 32), (3, 2048, 3000, 9)])
+def test_knn_seeded_scan_matches_oracle(nat, b, n, s, k):
+    """The seeded-threshold scan (cell-sorted refs, per-query window radix select) against
+    the oracle, at sizes that select it (kdpc_knn_workspace_bytes > 0), padded tails."""
+    assert nat.load_library().kdpc_knn_workspace_bytes(b, n, s) > 0
+    ref = _cloud(b, n, seed=n + k + 1)
+    qry = _cloud(b, s, seed=s + 7)
+    idx, dist, idx_p, dist_p = _knn_both(nat, k, ref, qry)
+    idx_ref, dist_ref = O.knn(k, ref, qry)
+    np.testing.assert_array_equal(idx, idx_ref)
+    np.testing.assert_array_equal(dist.view(np.int32), dist_ref.view(np.int32))
+    np.testing.assert_array_equal(idx_p, idx_ref)
+
+
+@pytest.mark.parametrize("case", ["flyingthings", "ties", "same_point", "outlier", "large"])
+def test_knn_seeded_scan_equals_unseeded_scan(nat, case):
+    """Seeded and unseeded scans return identical idx/dist bits at the model's sizes and on
+    degenerate clouds (exact distance ties broken by index, zero extent, one far outlier)."""
+    rng = np.random.default_rng(11)
+    k = 32
+    if case == "flyingthings":
+        ref = _cloud(4, 8192, seed=3)
+        qry = _cloud(4, 8192, seed=4)
+    elif case == "ties":  # integer lattice: many equal distances
+        ref = rng.integers(-6, 7, (2, 8192, 3)).astype(np.float32)
+        qry = rng.integers(-6, 7, (2, 4096, 3)).astype(np.float32)
+    elif case == "same_point":
+        ref = np.full((2, 4096, 3), 1.5, np.float32)
+        qry = np.full((2, 4096, 3), 1.5, np.float32)
+    elif case == "outlier":
+        ref = _cloud(2, 4096, seed=5)
+        ref[:, 17] = 1e4
+        qry = _cloud(2, 4096, seed=6)
+    else:  # config-5-like: large reference set, K = 64
+        k = 64
+        ref = _cloud(1, 65536, seed=8)
+        qry = _cloud(1, 8192, seed=9)
+    idx, dist, idx_p, dist_p = _knn_both(nat, k, ref, qry)
+    np.testing.assert_array_equal(idx, idx_p)
+    np.testing.assert_array_equal(dist.view(np.int32), dist_p.view(np.int32))
+    if case == "same_point":  # all distances equal -> the K lowest indices
+        np.testing.assert_array_equal(idx, np.broadcast_to(np.arange(k), idx.shape))
+
+
 def test_knn_matches_reference_topk_sets(nat, golden):
     g = golden("knn_ref.npz")
     names = sorted({k.rsplit("_", 2)[0] for k in g.files if k.endswith("_idx_sorted")})

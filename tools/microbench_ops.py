@@ -94,8 +94,18 @@ def main():
     us = timeit(lambda: K.knn_point(32, x5, q5), iters=2, warmup=1)
     res["knn_K32_N65536_B4"] = {"us": us, "Gdist_per_s": 4 * 65536 * 65536 / (us * 1e-6) / 1e9,
                                 "algorithmic_bytes": 4 * (12 * 65536 * 2 + 4 * 65536 * 32)}
+    us = timeit(lambda: K.knn_point(32, x5, q5, seeded=False), iters=2, warmup=1)
+    res["knn_K32_N65536_B4_plain"] = {"us": us}
     us = timeit(lambda: K.knn_point(32, xyz, xyz), iters=5)
     res["knn_K32_self_N8192_B8"] = {"us": us, "Gdist_per_s": B * N * N / (us * 1e-6) / 1e9}
+    # the model's kNN shapes, seeded vs unseeded scan
+    x16 = cloud(16, N, 5)
+    for (b, n, s, k) in [(16, 8192, 8192, 32), (8, 8192, 8192, 9), (16, 2048, 2048, 32),
+                         (8, 2048, 2048, 9), (16, 512, 512, 32), (8, 8192, 2048, 3)]:
+        xr, xq = x16[:b, :n].contiguous(), x16[:b, :s].flip(1).contiguous()
+        for seeded in (True, False):
+            us = timeit(lambda: K.knn_point(k, xr, xq, seeded=seeded), iters=10)
+            res[f"knn_B{b}_N{n}_S{s}_K{k}_{'seeded' if seeded else 'plain'}"] = {"us": us}
     print(json.dumps(res, indent=1))
     if args.json:
         with open(args.json, "w") as f:
