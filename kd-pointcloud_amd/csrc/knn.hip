@@ -38,7 +38,8 @@ constexpr int kTile = 2048;      // refs per LDS tile (32 KiB of float4)
 constexpr int kSerialMax = 8;    // candidates per chunk inserted one by one
 
 __device__ __forceinline__ bool kv_less(float ad, int ai, float bd, int bi) {
-  return ad < bd || (ad == bd && ai < bi);
+  // non-short-circuit: lane masks combined with s_and / s_or, no exec-mask branches
+  return (ad < bd) | ((ad == bd) & (ai < bi));
 }
 
 // bitonic compare-exchange step across lanes l and l^jj
@@ -47,7 +48,8 @@ __device__ __forceinline__ void bitonic_step(float& d, int& i, int jj, bool up) 
   const int oi = __shfl_xor(i, jj, kWave);
   const bool lower = (lane_id() & jj) == 0;
   const bool o_less = kv_less(od, oi, d, i);
-  const bool take = (lower == up) ? o_less : !o_less && !(od == d && oi == i);
+  const bool same = (od == d) & (oi == i);
+  const bool take = (lower == up) ? o_less : (!o_less & !same);
   d = take ? od : d;
   i = take ? oi : i;
 }
@@ -67,9 +69,14 @@ __device__ __forceinline__ void bitonic_merge64(float& d, int& i) {
 }
 
 // Merge the chunk's candidates (cand lanes carry {d, gi}) into the sorted list {ld, li}.
+// ASC: candidates arrive in ascending index order, after every list entry (index-order
+// scan); otherwise any order, compared by (d, index).  SERIAL: most candidates inserted
+// one by one (each ~a dozen instructions; a bitonic merge is a chain of 27 cross-lane
+// steps).
+template <bool ASC = true, int SERIAL = kSerialMax>
 __device__ __forceinline__ void insert_candidates(unsigned long long mask, bool cand, float d,
                                                   int gi, float& ld, int& li) {
-  if (__popcll(mask) > kSerialMax) {
+  if (__popcll(mask) > SERIAL) {
     float cd = cand ? d : INFINITY;
     int ci = cand ? gi : 0x7fffffff;
     bitonic_sort64(cd, ci);
@@ -90,8 +97,8 @@ __device__ __forceinline__ void insert_candidates(unsigned long long mask, bool 
       const int ci = __builtin_amdgcn_readlane(gi, j);
       const float pd = wave_shr1(ld, -INFINITY);
       const int pi = wave_shr1(li, 0);
-      const bool gt = ld > cd;
-      const bool pgt = pd > cd;
+      const bool gt = ASC ? ld > cd : kv_less(cd, ci, ld, li);
+      const bool pgt = ASC ? pd > cd : kv_less(cd, ci, pd, pi);
       const float nd = gt ? (pgt ? pd : cd) : ld;
       const int ni = gt ? (pgt ? pi : ci) : li;
       ld = nd;
@@ -168,7 +175,8 @@ __global__ __launch_bounds__(kSortThreads) void ref_sort_kernel(int n,
                                                                 const float* __restrict__ xyz,
                                                                 float* __restrict__ bbox,
                                                                 int* __restrict__ roff,
-                                                                float4* __restrict__ rs) {
+                                                                float4* __restrict__ rs,
+                                                                int* __restrict__ ri) {
   __shared__ int cnt[kCells];
   __shared__ int wsum[kSortThreads / kWave];
   __shared__ float red[6][kSortThreads / kWave];
@@ -227,10 +235,71 @@ __global__ __launch_bounds__(kSortThreads) void ref_sort_kernel(int n,
     const float x = p[i * 3], y = p[i * 3 + 1], z = p[i * 3 + 2];
     const int pos = atomicAdd(&cnt[cell_of(x, y, z, bb)], 1);  // order within a cell: any
     rso[pos] = make_float4(x, y, z, sqnorm3(x, y, z));
+    if (ri) ri[(long long)b * n + pos] = i;
+  }
+}
+
+// Boxes of the sorted 64-ref chunks, one wave per chunk: cbox (B, nch, 2) =
+// {lo xyz, max |r|^2}, {hi xyz, 0}.
+__global__ __launch_bounds__(256) void chunk_box_kernel(int n, const float4* __restrict__ rs,
+                                                        float4* __restrict__ cbox) {
+  const int b = blockIdx.y, lane = lane_id();
+  const int nch = divup(n, kWave);
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= nch) return;
+  const int j = c * kWave + lane;
+  const float4 r = rs[(long long)b * n + (j < n ? j : c * kWave)];
+  float lo[4] = {r.x, r.y, r.z, -r.w}, hi[3] = {r.x, r.y, r.z};
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a) lo[a] = fminf(lo[a], __shfl_xor(lo[a], o, kWave));
+#pragma unroll
+    for (int a = 0; a < 3; ++a) hi[a] = fmaxf(hi[a], __shfl_xor(hi[a], o, kWave));
+  }
+  if (lane == 0) {
+    float4* cb = cbox + ((long long)b * nch + c) * 2;
+    cb[0] = make_float4(lo[0], lo[1], lo[2], -lo[3]);
+    cb[1] = make_float4(hi[0], hi[1], hi[2], 0.f);
   }
 }
 
 constexpr int kWin = 256;  // refs around a query's cell that seed its threshold
+
+// Queries of each cloud in the refs' cell order (so a wave's queries are spatial
+// neighbours): qrec (B,S) = {x, y, z, original index} and qwin (B,S) = first of the kWin
+// sorted refs around the query's cell, at each sorted position.  One dependent load per
+// query in the kNN kernel instead of index -> coordinates -> cell offset.
+__global__ __launch_bounds__(kSortThreads) void query_sort_kernel(int s, int n,
+                                                                  const float* __restrict__ new_xyz,
+                                                                  const float* __restrict__ bbox,
+                                                                  const int* __restrict__ roff,
+                                                                  float4* __restrict__ qrec,
+                                                                  int* __restrict__ qwin) {
+  __shared__ int cnt[kCells];
+  __shared__ int wsum[kSortThreads / kWave];
+  __shared__ float bb[6];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const float* p = new_xyz + (long long)b * s * 3;
+  if (t < 6) bb[t] = bbox[b * 8 + t];
+  for (int c = t; c < kCells; c += kSortThreads) cnt[c] = 0;
+  __syncthreads();
+  for (int i = t; i < s; i += kSortThreads)
+    atomicAdd(&cnt[cell_of(p[i * 3], p[i * 3 + 1], p[i * 3 + 2], bb)], 1);
+  __syncthreads();
+  block_exclusive_scan(cnt, wsum);
+  const int* ro = roff + (long long)b * (kCells + 1);
+  for (int i = t; i < s; i += kSortThreads) {
+    const float x = p[i * 3], y = p[i * 3 + 1], z = p[i * 3 + 2];
+    const int cell = cell_of(x, y, z, bb);
+    const int pos = atomicAdd(&cnt[cell], 1);
+    int w0 = ro[cell] - kWin / 2;
+    w0 = w0 < 0 ? w0 + n : w0;  // n >= kWin: one wrap at most
+    qrec[(long long)b * s + pos] = make_float4(x, y, z, __int_as_float(i));
+    qwin[(long long)b * s + pos] = w0;
+  }
+}
+
 
 // order-preserving float -> unsigned key (total order of non-NaN floats)
 __device__ __forceinline__ unsigned ord_key(float f) {
@@ -241,53 +310,56 @@ __device__ __forceinline__ float from_ord_key(unsigned k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
 }
 
-// Seed thr[q] (valid queries) with nextafter(T), T = the K-th smallest distance from the
-// query to the kWin sorted refs around its cell.
+// Seed thr[q] (valid queries) with nextafter(T): T >= the K-th smallest distance from the
+// query to the kWin sorted refs around its cell.  The radix select fixes the top 16 bits of
+// that K-th key (sign, exponent, 7 mantissa bits) and T sets the 16 low bits, so T is within
+// 2^-7 of the K-th, an upper bound of it and of the query's true K-th distance.  The QW
+// selects run interleaved (independent chains of ballot / popcount / select).
 template <int QW>
 __device__ __forceinline__ void seed_thresholds(int n, int k, int b, int qbase, int s,
                                                 const float* qx, const float* qy,
                                                 const float* qz, const float* qs,
-                                                const float4* __restrict__ rs,
-                                                const float* __restrict__ bbox,
-                                                const int* __restrict__ roff, float* thr) {
+                                                const int* w0, const float4* __restrict__ rs,
+                                                float* thr) {
   const float4* rb = rs + (long long)b * n;
-  float bb[6];
+  unsigned key[QW][kWin / kWave];
 #pragma unroll
-  for (int i = 0; i < 6; ++i) bb[i] = bbox[b * 8 + i];
-#pragma unroll
-  for (int q = 0; q < QW; ++q) {  // one query at a time: 4 key VGPRs live, not 4 * QW
-    unsigned key[kWin / kWave];
-    int w0 = roff[(long long)b * (kCells + 1) + cell_of(qx[q], qy[q], qz[q], bb)] - kWin / 2;
-    w0 = w0 < 0 ? w0 + n : w0;  // n >= kWin: one wrap at most
+  for (int q = 0; q < QW; ++q) {
 #pragma unroll
     for (int i = 0; i < kWin / kWave; ++i) {
-      int pz = w0 + lane_id() + kWave * i;
+      int pz = w0[q] + lane_id() + kWave * i;
       pz = pz >= n ? pz - n : pz;
       const float4 r = rb[pz];
-      key[i] = ord_key(sqdist_fast(qx[q], qy[q], qz[q], qs[q], r.x, r.y, r.z, r.w));
+      key[q][i] = ord_key(sqdist_fast(qx[q], qy[q], qz[q], qs[q], r.x, r.y, r.z, r.w));
     }
-    unsigned ans = 0u;  // largest key with fewer than k window keys below it = k-th smallest
-    for (int bit = 31; bit >= 0; --bit) {
-      const unsigned t = ans | (1u << bit);
+  }
+  unsigned ans[QW];  // largest prefix with fewer than k window keys below it
+#pragma unroll
+  for (int q = 0; q < QW; ++q) ans[q] = 0u;
+  for (int bit = 31; bit >= 16; --bit) {
+#pragma unroll
+    for (int q = 0; q < QW; ++q) {
+      const unsigned t = ans[q] | (1u << bit);
       int cnt = 0;
 #pragma unroll
-      for (int i = 0; i < kWin / kWave; ++i) cnt += __popcll(__ballot(key[i] < t));
-      ans = cnt < k ? t : ans;
+      for (int i = 0; i < kWin / kWave; ++i) cnt += __popcll(__ballot(key[q][i] < t));
+      ans[q] = cnt < k ? t : ans[q];
     }
-    // d < nextafter(T) <=> d <= T; a K-th at +inf or NaN (NaN coordinates) leaves no bound
-    if (qbase + q < s && ans < ord_key(INFINITY)) thr[q] = from_ord_key(ans + 1u);
+  }
+#pragma unroll
+  for (int q = 0; q < QW; ++q) {
+    const unsigned tk = ans[q] | 0xffffu;  // >= the window's K-th key
+    // d < nextafter(T) <=> d <= T; a bound at +inf or NaN (NaN coordinates) is no bound
+    if (qbase + q < s && tk < ord_key(INFINITY)) thr[q] = from_ord_key(tk + 1u);
   }
 }
 
-template <int QW, bool SEED>
+template <int QW>
 __global__ __launch_bounds__(256) void knn_kernel(int n, int s, int k,
                                                   const float* __restrict__ xyz,
                                                   const float* __restrict__ new_xyz,
                                                   int* __restrict__ idx,
-                                                  float* __restrict__ dist,
-                                                  const float4* __restrict__ rs,
-                                                  const float* __restrict__ bbox,
-                                                  const int* __restrict__ roff) {
+                                                  float* __restrict__ dist) {
   __shared__ float4 tile[kTile];
   const int b = blockIdx.y;
   const int wave = threadIdx.x >> 6;
@@ -309,7 +381,6 @@ __global__ __launch_bounds__(256) void knn_kernel(int n, int s, int k,
     ld[q] = INFINITY;
     li[q] = 0x7fffffff;
   }
-  if constexpr (SEED) seed_thresholds<QW>(n, k, b, qbase, s, qx, qy, qz, qs, rs, bbox, roff, thr);
 
   for (int t0 = 0; t0 < n; t0 += kTile) {
     const int tn = min(kTile, n - t0);
@@ -341,9 +412,7 @@ __global__ __launch_bounds__(256) void knn_kernel(int n, int s, int k,
       for (int q = 0; q < QW; ++q) {
         if (m[q] == 0ull) continue;  // wave-uniform
         insert_candidates(m[q], valid && d[q] < thr[q], d[q], gi, ld[q], li[q]);
-        // seeded: the list's K-th is <= T once K entries are in, +inf before
-        thr[q] = fminf(thr[q],
-                       __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ld[q]), k - 1)));
+        thr[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ld[q]), k - 1));
       }
     }
   }
@@ -359,16 +428,247 @@ __global__ __launch_bounds__(256) void knn_kernel(int n, int s, int k,
   }
 }
 
+constexpr int kBuf = 128;  // candidate slots per query (LDS)
+
+// Sort QW wave-wide lists (lane l holds entry l of each) ascending by (d, index); the QW
+// bitonic networks run interleaved.
+template <int QW>
+__device__ __forceinline__ void sort64_multi(float (&d)[QW], int (&i)[QW]) {
+#pragma unroll
+  for (int kk = 2; kk <= 64; kk <<= 1) {
+    const bool up = (lane_id() & kk) == 0 || kk == 64;
+#pragma unroll
+    for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+#pragma unroll
+      for (int q = 0; q < QW; ++q) bitonic_step(d[q], i[q], jj, up);
+    }
+  }
+}
+
+// Reduce a query's candidate buffer (cnt > 64 entries) to its 64 smallest, sorted, in
+// slots 0..63; tighten thr to the K-th of them.
+__device__ __noinline__ void compact_buffer(float2* buf, int& cnt, float& thr, int k) {
+  const int lane = lane_id();
+  const float2 a = lane < cnt ? buf[lane] : make_float2(INFINITY, __int_as_float(0x7fffffff));
+  const float2 c = lane + kWave < cnt ? buf[kWave + lane]
+                                      : make_float2(INFINITY, __int_as_float(0x7fffffff));
+  float ad = a.x, cd = c.x;
+  int ai = __float_as_int(a.y), ci = __float_as_int(c.y);
+  bitonic_sort64(ad, ai);
+  bitonic_sort64(cd, ci);
+  const float rd = __shfl(cd, 63 - lane, kWave);
+  const int ri = __shfl(ci, 63 - lane, kWave);
+  if (kv_less(rd, ri, ad, ai)) {
+    ad = rd;
+    ai = ri;
+  }
+  bitonic_merge64(ad, ai);
+  __builtin_amdgcn_wave_barrier();
+  buf[lane] = make_float2(ad, __int_as_float(ai));
+  __builtin_amdgcn_wave_barrier();
+  cnt = kWave;
+  const float kth = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ad), k - 1));
+  if (kth < INFINITY) thr = fminf(thr, from_ord_key(ord_key(kth) + 1u));
+}
+
+// Box-culled scan over the cell-sorted refs.  With the seeded threshold (d <= T, T an upper
+// bound of the query's true K-th distance, tight), a 64-ref chunk whose bounding box lies
+// farther than T from every query of the wave cannot hold a candidate and is skipped
+// without computing its distances.  A wave's queries are spatial neighbours (queries in
+// cell order), so a wave visits the few chunks around them: the scan is sub-linear in N.
+// Culling is exact: a chunk is skipped only if its box bound exceeds the threshold by more
+// than the rounding error of the expanded-form distance (|d - D| <= 12 eps (|q|^2+|r|^2)
+// for the fma chain; the margin allows 32 eps plus 16 eps |thr| for the bound's own
+// rounding).  Because T is tight, a query collects only ~K..1.5K candidates: they are
+// appended to an LDS buffer (no list maintenance during the scan) and sorted once by
+// (d, index) at the end; a buffer that would overflow is first compacted to its 64
+// smallest (K <= 64), which also tightens the threshold.
+// Keep only the buffer entries whose key is <= T, an upper bound of the K-th smallest
+// among them (16-bit radix select over the <= 128 entries, two per lane: ballot popcounts,
+// no cross-lane data movement), compacted in place; tighten thr to d <= T.  Everything
+// dropped is farther than K buffered candidates, so it is not among the K nearest.
+__device__ __noinline__ void shrink_buffer(float2* buf, int& cnt, float& thr, int k) {
+  const int lane = lane_id();
+  const bool v0 = lane < cnt, v1 = lane + kWave < cnt;
+  const float2 e0 = v0 ? buf[lane] : make_float2(INFINITY, 0.f);
+  const float2 e1 = v1 ? buf[kWave + lane] : make_float2(INFINITY, 0.f);
+  const unsigned k0 = v0 ? ord_key(e0.x) : 0xffffffffu;
+  const unsigned k1 = v1 ? ord_key(e1.x) : 0xffffffffu;
+  unsigned ans = 0u;
+  for (int bit = 31; bit >= 16; --bit) {
+    const unsigned t = ans | (1u << bit);
+    const int c = __popcll(__ballot(k0 < t)) + __popcll(__ballot(k1 < t));
+    ans = c < k ? t : ans;
+  }
+  const unsigned tk = ans | 0xffffu;
+  const unsigned long long m0 = __ballot(v0 && k0 <= tk), m1 = __ballot(v1 && k1 <= tk);
+  const int p0 = __builtin_amdgcn_mbcnt_hi((unsigned)(m0 >> 32),
+                                           __builtin_amdgcn_mbcnt_lo((unsigned)m0, 0u));
+  const int p1 = __popcll(m0) + __builtin_amdgcn_mbcnt_hi((unsigned)(m1 >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((unsigned)m1, 0u));
+  __builtin_amdgcn_wave_barrier();
+  if (v0 && k0 <= tk) buf[p0] = e0;
+  if (v1 && k1 <= tk) buf[p1] = e1;
+  __builtin_amdgcn_wave_barrier();
+  cnt = __popcll(m0) + __popcll(m1);
+  if (tk < ord_key(INFINITY)) thr = fminf(thr, from_ord_key(tk + 1u));
+}
+
+template <int QW>
+__global__ __launch_bounds__(256) void knn_cull_kernel(
+    int n, int s, int k, int* __restrict__ idx, float* __restrict__ dist,
+    const float4* __restrict__ rs, const int* __restrict__ ri, const float4* __restrict__ cbox,
+    const float4* __restrict__ qrec, const int* __restrict__ qwin) {
+  __shared__ float2 cand_buf[4][QW][kBuf];
+  const int b = blockIdx.y;
+  const int wave = threadIdx.x >> 6;
+  const int lane = lane_id();
+  const int qbase = (blockIdx.x * 4 + wave) * QW;  // sorted query positions
+  const int nch = divup(n, kWave);
+  const float4* rb = rs + (long long)b * n;
+  const int* ib = ri + (long long)b * n;
+  const float4* cb = cbox + (long long)b * nch * 2;
+
+  float qx[QW], qy[QW], qz[QW], qs[QW], thr[QW];
+  int qid[QW], cnt[QW], w0[QW];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) {
+    const long long pos = (long long)b * s + min(qbase + q, s - 1);
+    const float4 r = qrec[pos];
+    w0[q] = qwin[pos];
+    qx[q] = r.x;
+    qy[q] = r.y;
+    qz[q] = r.z;
+    qid[q] = __float_as_int(r.w);
+    qs[q] = sqnorm3(qx[q], qy[q], qz[q]);
+    thr[q] = qbase + q < s ? INFINITY : -INFINITY;  // padding queries never take candidates
+    cnt[q] = 0;
+  }
+  // the first block of chunk boxes is independent of the seed: in flight during it
+  float4 lo = lane < nch ? cb[2 * lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 hi = lane < nch ? cb[2 * lane + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+  seed_thresholds<QW>(n, k, b, qbase, s, qx, qy, qz, qs, w0, rs, thr);
+
+  // visit every chunk of `todo` (chunk cbase + bit), the next chunk's refs loaded while
+  // this one is used; candidates (d < thr) are appended to the query's buffer
+  auto run = [&](unsigned long long todo, int cbase) {
+    if (todo == 0ull) return;
+    int cc = cbase + __ffsll((long long)todo) - 1;
+    todo &= todo - 1;
+    int j = cc * kWave + lane;
+    float4 r = rb[j < n ? j : cc * kWave];
+    int gi = ib[j < n ? j : cc * kWave];
+    while (true) {
+      const bool valid = j < n;
+      const bool more = todo != 0ull;
+      const int cn = more ? cbase + __ffsll((long long)todo) - 1 : cc;
+      todo &= todo - 1;
+      const int jn = cn * kWave + lane;
+      const float4 rn = rb[jn < n ? jn : cn * kWave];
+      const int gn = ib[jn < n ? jn : cn * kWave];
+#pragma unroll
+      for (int q = 0; q < QW; ++q) {
+        const float d = sqdist_fast(qx[q], qy[q], qz[q], qs[q], r.x, r.y, r.z, r.w);
+        bool cand = valid && d < thr[q];
+        unsigned long long m = __ballot(cand);
+        if (m == 0ull) continue;  // wave-uniform
+        if (cnt[q] + __popcll(m) > kBuf) {
+          shrink_buffer(cand_buf[wave][q], cnt[q], thr[q], k);
+          if (cnt[q] + __popcll(m) > kBuf)  // exact ties keep > 64: sort-based fallback
+            compact_buffer(cand_buf[wave][q], cnt[q], thr[q], k);
+          cand = cand && d < thr[q];
+          m = __ballot(cand);
+        }
+        const int pos = cnt[q] + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+        if (cand) cand_buf[wave][q][pos] = make_float2(d, __int_as_float(gi));
+        cnt[q] += __popcll(m);
+      }
+      if (!more) break;
+      cc = cn;
+      j = jn;
+      r = rn;
+      gi = gn;
+    }
+  };
+  // per 64-chunk block: the chunks whose box contains a query first, then a tightened
+  // threshold from what they gave, then the remaining chunks re-tested against it
+  for (int cbase = 0; cbase < nch; cbase += kWave) {
+    const int c = cbase + lane;
+    if (cbase > 0 && c < nch) {
+      lo = cb[2 * c];
+      hi = cb[2 * c + 1];
+    }
+    float lbq[QW];
+    bool need = false, inside = false;
+#pragma unroll
+    for (int q = 0; q < QW; ++q) {
+      const float dx = fmaxf(fmaxf(lo.x - qx[q], qx[q] - hi.x), 0.f);
+      const float dy = fmaxf(fmaxf(lo.y - qy[q], qy[q] - hi.y), 0.f);
+      const float dz = fmaxf(fmaxf(lo.z - qz[q], qz[q] - hi.z), 0.f);
+      lbq[q] = dx * dx + dy * dy + dz * dz;
+      const float marg = (qs[q] + lo.w) * 0x1p-19f + fabsf(thr[q]) * 0x1p-20f;
+      const bool ok = c < nch && qbase + q < s;
+      need |= ok && !(lbq[q] > thr[q] + marg);
+      inside |= ok && lbq[q] == 0.f;
+    }
+    const unsigned long long near_m = __ballot(inside && need);
+    const unsigned long long need_m = __ballot(need);
+    if (need_m == 0ull) continue;
+    run(near_m, cbase);
+    if (need_m == near_m) continue;
+#pragma unroll
+    for (int q = 0; q < QW; ++q)
+      if (near_m != 0ull && cnt[q] >= k) shrink_buffer(cand_buf[wave][q], cnt[q], thr[q], k);
+    bool need2 = false;
+#pragma unroll
+    for (int q = 0; q < QW; ++q) {
+      const float marg = (qs[q] + lo.w) * 0x1p-19f + fabsf(thr[q]) * 0x1p-20f;
+      need2 |= c < nch && qbase + q < s && !(lbq[q] > thr[q] + marg);
+    }
+    run(__ballot(need2) & need_m & ~near_m, cbase);
+  }
+
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int q = 0; q < QW; ++q) {
+    if (cnt[q] > kWave) shrink_buffer(cand_buf[wave][q], cnt[q], thr[q], k);
+    if (cnt[q] > kWave) compact_buffer(cand_buf[wave][q], cnt[q], thr[q], k);
+  }
+  float ld[QW];
+  int li[QW];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) {
+    const float2 v = lane < cnt[q] ? cand_buf[wave][q][lane]
+                                   : make_float2(INFINITY, __int_as_float(0x7fffffff));
+    ld[q] = v.x;
+    li[q] = __float_as_int(v.y);
+  }
+  sort64_multi<QW>(ld, li);
+#pragma unroll
+  for (int q = 0; q < QW; ++q) {
+    if (qbase + q < s && lane < k) {
+      const long long o = ((long long)b * s + qid[q]) * k + lane;
+      idx[o] = li[q];
+      if (dist) dist[o] = ld[q];
+    }
+  }
+}
+
 struct SeedWs {
   float* bbox;
   int* roff;
   float4* rs;
+  int* ri;
+  float4* cbox;
+  float4* qrec;
+  int* qwin;
   size_t bytes;
 };
 
 inline size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
-SeedWs seed_ws(int b, int n, void* base) {
+SeedWs seed_ws(int b, int n, int s, void* base) {
   SeedWs w{};
   char* p = reinterpret_cast<char*>(base);
   size_t o = 0;
@@ -380,25 +680,31 @@ SeedWs seed_ws(int b, int n, void* base) {
   w.bbox = reinterpret_cast<float*>(take(sizeof(float) * 8 * b));
   w.roff = reinterpret_cast<int*>(take(sizeof(int) * (size_t)b * (kCells + 1)));
   w.rs = reinterpret_cast<float4*>(take(sizeof(float4) * (size_t)b * n));
+  w.ri = reinterpret_cast<int*>(take(sizeof(int) * (size_t)b * n));
+  w.cbox = reinterpret_cast<float4*>(take(sizeof(float4) * 2 * (size_t)b * divup(n, kWave)));
+  w.qrec = reinterpret_cast<float4*>(take(sizeof(float4) * (size_t)b * s));
+  w.qwin = reinterpret_cast<int*>(take(sizeof(int) * (size_t)b * s));
   w.bytes = o;
   return w;
 }
 
 // The seed costs one sort launch (~10-20 us) and a 256-ref window per query; it pays once
 // the plain scan's insertion work dominates, i.e. thousands of refs.
+#ifndef KNN_QW
+#define KNN_QW 4
+#endif
 inline bool use_seed(int b, int n, int s) { return n >= 2048 && (long long)b * s >= 8192; }
 
-template <bool SEED>
 void launch_knn(int b, int n, int s, int k, const float* xyz, const float* new_xyz, int* idx,
-                float* dist, const SeedWs& w, hipStream_t st) {
+                float* dist, hipStream_t st) {
   // Large reference sets amortise the per-chunk scalar branch over 8 queries per wave; at
   // the model's sizes (N <= 8192) 4 per wave measured faster.
   if (n >= 32768)
-    hipLaunchKernelGGL((knn_kernel<8, SEED>), dim3(divup(s, 32), b), dim3(256), 0, st, n, s, k,
-                       xyz, new_xyz, idx, dist, w.rs, w.bbox, w.roff);
+    hipLaunchKernelGGL(knn_kernel<8>, dim3(divup(s, 32), b), dim3(256), 0, st, n, s, k, xyz,
+                       new_xyz, idx, dist);
   else
-    hipLaunchKernelGGL((knn_kernel<4, SEED>), dim3(divup(s, 16), b), dim3(256), 0, st, n, s, k,
-                       xyz, new_xyz, idx, dist, w.rs, w.bbox, w.roff);
+    hipLaunchKernelGGL(knn_kernel<4>, dim3(divup(s, 16), b), dim3(256), 0, st, n, s, k, xyz,
+                       new_xyz, idx, dist);
 }
 
 }  // namespace
@@ -411,7 +717,7 @@ KDPC_API int kdpc_knn_point(int b, int n, int s, int k, const float* xyz, const 
   KDPC_CHECK_ARG(b >= 0 && n > 0 && s >= 0 && k >= 1 && k <= 64 && k <= n && b <= 65535);
   if ((long long)b * s == 0) return (int)hipSuccess;
   KDPC_CHECK_ARG(xyz && new_xyz && idx);
-  launch_knn<false>(b, n, s, k, xyz, new_xyz, idx, dist, SeedWs{}, (hipStream_t)stream);
+  launch_knn(b, n, s, k, xyz, new_xyz, idx, dist, (hipStream_t)stream);
   KDPC_RETURN_LAUNCH();
 }
 
@@ -419,7 +725,7 @@ KDPC_API int kdpc_knn_point(int b, int n, int s, int k, const float* xyz, const 
 // scan is used (then pass workspace = NULL).
 KDPC_API size_t kdpc_knn_workspace_bytes(int b, int n, int s) {
   if (b <= 0 || n <= 0 || s <= 0 || !use_seed(b, n, s)) return 0;
-  return seed_ws(b, n, nullptr).bytes;
+  return seed_ws(b, n, s, nullptr).bytes;
 }
 
 // kdpc_knn_point with scratch for the seeded threshold (identical results).
@@ -433,9 +739,18 @@ KDPC_API int kdpc_knn_point_ws(int b, int n, int s, int k, const float* xyz,
     return kdpc_knn_point(b, n, s, k, xyz, new_xyz, idx, dist, stream);
   KDPC_CHECK_ARG(xyz && new_xyz && idx && workspace_bytes >= need);
   hipStream_t st = (hipStream_t)stream;
-  const SeedWs w = seed_ws(b, n, workspace);
+  const SeedWs w = seed_ws(b, n, s, workspace);
   hipLaunchKernelGGL(ref_sort_kernel, dim3(b), dim3(kSortThreads), 0, st, n, xyz, w.bbox, w.roff,
-                     w.rs);
-  launch_knn<true>(b, n, s, k, xyz, new_xyz, idx, dist, w, st);
+                     w.rs, w.ri);
+  hipLaunchKernelGGL(chunk_box_kernel, dim3(divup(divup(n, kWave), 4), b), dim3(256), 0, st, n,
+                     w.rs, w.cbox);
+  hipLaunchKernelGGL(query_sort_kernel, dim3(b), dim3(kSortThreads), 0, st, s, n, new_xyz,
+                     w.bbox, w.roff, w.qrec, w.qwin);
+  if (KNN_QW == 8)
+    hipLaunchKernelGGL(knn_cull_kernel<8>, dim3(divup(s, 32), b), dim3(256), 0, st, n, s, k, idx,
+                       dist, w.rs, w.ri, w.cbox, w.qrec, w.qwin);
+  else
+    hipLaunchKernelGGL(knn_cull_kernel<4>, dim3(divup(s, 16), b), dim3(256), 0, st, n, s, k, idx,
+                       dist, w.rs, w.ri, w.cbox, w.qrec, w.qwin);
   KDPC_RETURN_LAUNCH();
 }
