@@ -162,6 +162,36 @@ int kdpc_cost_volume_bwd(int b, int n1, int n2, int k, int din, int dout, const 
                          float *dp2_rows, float *dx1, float *ddir_rows, void *workspace,
                          size_t workspace_bytes, float *dparams, void *stream);
 
+/* ---- wide cost volume (same layers, Din in {64,128,256,512}): the Din -> Dout MLP GEMM
+ *      stays a BLAS GEMM, everything around it is fused (csrc/cost_volume_wide.hip) ------ */
+
+int kdpc_cost_volume_wide_supported(int din, int dout, int k);
+
+/* h0 (B,N1,K,Din) = LeakyReLU((P2[idx] + P1[n]) + (Wpos (x2[idx] - x1[n]) + bpos)) */
+int kdpc_cost_volume_wide_h0(int b, int n1, int n2, int k, int din, const float *x1,
+                             const float *x2, const int *idx, const float *p1, const float *p2,
+                             const float *wpos, const float *bpos, float *h0, void *stream);
+
+/* z1 (B,N1,K,Dout) pre-activation of the MLP -> out (B,N1,Dout) = LeakyReLU(max_k z1),
+ * amax (B,N1,Dout) u8 = first maximal k. */
+int kdpc_cost_volume_wide_max(int b, int n1, int k, int dout, const float *z1, float *out,
+                              unsigned char *amax, void *stream);
+
+/* gout (B,N1,Dout) -> dz1 (B,N1,K,Dout) dense (nonzero only at amax rows),
+ * gsc (B,N1,Dout) = gout * LeakyReLU'(out) (its column sums are db1). */
+int kdpc_cost_volume_wide_max_bwd(int b, int n1, int k, int dout, const float *gout,
+                                  const float *out, const unsigned char *amax, float *dz1,
+                                  float *gsc, void *stream);
+
+/* Rows of the dWpos slab below (each Din*3 floats, summed with kdpc_colsum). */
+int kdpc_cost_volume_wide_slab_rows(void);
+
+/* dz (B,N1,K,Din): dh0 in, dz0 = dh0 * LeakyReLU'(h0) out (in place); dp1 (B,N1,Din) =
+ * sum_k dz0; slab (slab_rows, Din*3) partial sums of dWpos[c][a] = sum dz0[.,c] dir[.,a]. */
+int kdpc_cost_volume_wide_h0_bwd(int b, int n1, int n2, int k, int din, const float *x1,
+                                 const float *x2, const int *idx, const float *h0, float *dz,
+                                 float *dp1, float *slab, void *stream);
+
 /* ---- fused PointConv neighbourhood contraction (pointconv_util.py:217-258, 401-446) ---- */
 
 /* out[b,s, c*16+w] = sum_k G[b,s,k,c] * wt[b,s,k,w],  G = cat(xyz[idx]-center, feats[idx]).

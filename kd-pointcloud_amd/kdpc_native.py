@@ -27,6 +27,12 @@ _SIGNATURES = {
     "kdpc_three_interpolate_grad": [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
     "kdpc_knn_point": [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
     "kdpc_knn_workspace_bytes": [_c_int] * 3,
+    "kdpc_cost_volume_wide_supported": [_c_int] * 3,
+    "kdpc_cost_volume_wide_h0": [_c_int] * 5 + [_vp] * 9,
+    "kdpc_cost_volume_wide_max": [_c_int] * 4 + [_vp] * 4,
+    "kdpc_cost_volume_wide_max_bwd": [_c_int] * 4 + [_vp] * 6,
+    "kdpc_cost_volume_wide_slab_rows": [],
+    "kdpc_cost_volume_wide_h0_bwd": [_c_int] * 5 + [_vp] * 8,
     "kdpc_knn_point_ws": [_c_int] * 4 + [_vp] * 5 + [_c_size, _vp],
     "kdpc_group_rows": [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp],
     "kdpc_csr_workspace_bytes": [_c_int, _c_int, _c_int],
@@ -390,6 +396,61 @@ def cost_volume_bwd(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout):
           _dev(dp2_rows, f, "dp2_rows"), _dev(dx1, f, "dx1"), _dev(ddir_rows, f, "ddir_rows"),
           ws.data_ptr(), ws_bytes, _dev(dparams, f, "dparams"), _stream(x1))
     return dp1, dp2_rows, dx1, ddir_rows, dparams
+
+
+# ------------------------------------------------------------------ wide cost volume
+def cost_volume_wide_supported(din, dout, k):
+    return bool(load_library().kdpc_cost_volume_wide_supported(din, dout, k))
+
+
+def cost_volume_wide_h0(x1, x2, idx, p1, p2, wpos, bpos):
+    """-> h0 (B,N1,K,Din) = LeakyReLU(P2[idx] + P1 + Wpos dir + bpos)."""
+    B, N1, _ = x1.shape
+    N2, K, din = x2.shape[1], idx.shape[2], p1.shape[2]
+    f = torch.float32
+    h0 = torch.empty((B, N1, K, din), dtype=f, device=x1.device)
+    _call("kdpc_cost_volume_wide_h0", B, N1, N2, K, din, _dev(x1, f, "x1"), _dev(x2, f, "x2"),
+          _dev(idx, torch.int32, "idx"), _dev(p1, f, "p1"), _dev(p2, f, "p2"),
+          _dev(wpos, f, "wpos"), _dev(bpos, f, "bpos"), _dev(h0, f, "h0"), _stream(x1),
+          work=(4 * B * N1 * (K * (1 + 2 * din + 3) + din + 3), 10.0 * B * N1 * K * din))
+    return h0
+
+
+def cost_volume_wide_max(z1, B, N1, K, dout):
+    """z1 (B*N1*K, Dout) -> out (B,N1,Dout), amax (B,N1,Dout) u8."""
+    f = torch.float32
+    out = torch.empty((B, N1, dout), dtype=f, device=z1.device)
+    amax = torch.empty((B, N1, dout), dtype=torch.uint8, device=z1.device)
+    _call("kdpc_cost_volume_wide_max", B, N1, K, dout, _dev(z1, f, "z1"), _dev(out, f, "out"),
+          _dev(amax, torch.uint8, "amax"), _stream(z1))
+    return out, amax
+
+
+def cost_volume_wide_max_bwd(gout, out, amax, K):
+    """-> dz1 (B*N1*K, Dout) dense, gsc (B*N1, Dout)."""
+    B, N1, dout = out.shape
+    f = torch.float32
+    dz1 = torch.empty((B * N1 * K, dout), dtype=f, device=out.device)
+    gsc = torch.empty((B * N1, dout), dtype=f, device=out.device)
+    _call("kdpc_cost_volume_wide_max_bwd", B, N1, K, dout, _dev(gout, f, "gout"),
+          _dev(out, f, "out"), _dev(amax, torch.uint8, "amax"), _dev(dz1, f, "dz1"),
+          _dev(gsc, f, "gsc"), _stream(out))
+    return dz1, gsc
+
+
+def cost_volume_wide_h0_bwd(x1, x2, idx, h0, dz):
+    """dz (B*N1*K, Din) dh0 -> dz0 in place; -> dp1 (B,N1,Din), dWpos (Din,3)."""
+    B, N1, _ = x1.shape
+    N2, K, din = x2.shape[1], idx.shape[2], h0.shape[-1]
+    f = torch.float32
+    lib = load_library()
+    rows = lib.kdpc_cost_volume_wide_slab_rows()
+    slab = torch.empty((rows, din * 3), dtype=f, device=x1.device)
+    dp1 = torch.empty((B, N1, din), dtype=f, device=x1.device)
+    _call("kdpc_cost_volume_wide_h0_bwd", B, N1, N2, K, din, _dev(x1, f, "x1"), _dev(x2, f, "x2"),
+          _dev(idx, torch.int32, "idx"), _dev(h0, f, "h0"), _dev(dz, f, "dz"),
+          _dev(dp1, f, "dp1"), _dev(slab, f, "slab"), _stream(x1))
+    return dp1, colsum(slab).view(din, 3)
 
 
 # ------------------------------------------------------------------ PointConv contraction

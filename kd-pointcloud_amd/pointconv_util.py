@@ -508,6 +508,41 @@ class _CostVolume(torch.autograd.Function):
         return dx1, dx2, None, dp1, dp2, dwpos, dbpos, dw1, db1
 
 
+class _CostVolumeWide(torch.autograd.Function):
+    """Wide cost volume (csrc/cost_volume_wide.hip): the Din -> Dout MLP is one BLAS GEMM,
+    the gather / position transform / activations / max around it are fused kernels.
+    Same arguments and result as _CostVolume."""
+
+    @staticmethod
+    def forward(ctx, x1, x2, idx, p1, p2, wpos, bpos, w1, b1):
+        B, N1, K = idx.shape
+        h0 = _nat.cost_volume_wide_h0(x1, x2, idx, p1, p2, wpos, bpos)
+        z1 = torch.addmm(b1, h0.view(-1, h0.shape[-1]), w1.t())
+        out, amax = _nat.cost_volume_wide_max(z1, B, N1, K, w1.shape[0])
+        ctx.save_for_backward(x1, x2, idx, wpos, w1, h0, out, amax)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        x1, x2, idx, wpos, w1, h0, out, amax = ctx.saved_tensors
+        B, N1, K = idx.shape
+        N2, din = x2.shape[1], h0.shape[-1]
+        dz1, gsc = _nat.cost_volume_wide_max_bwd(gout.contiguous(), out, amax, K)
+        h0f = h0.view(-1, din)
+        dw1 = torch.mm(dz1.t(), h0f)
+        db1 = _nat.colsum(gsc)
+        dz = torch.mm(dz1, w1)  # dh0; becomes dz0 in place
+        del dz1
+        dp1, dwpos = _nat.cost_volume_wide_h0_bwd(x1, x2, idx, h0, dz)
+        dbpos = _nat.colsum(dp1.view(-1, din))
+        csr = _nat.csr_of(idx, N2)
+        dp2 = _nat.group_rows_grad(dz.view(B, N1 * K, din), csr, B, N2, din)
+        ddir = torch.mm(dz, wpos)  # (rows, 3)
+        dx2 = _nat.group_rows_grad(ddir.view(B, N1 * K, 3), csr, B, N2, 3)
+        dx1 = -ddir.view(B, N1, K, 3).sum(2)
+        return dx1, dx2, None, dp1, dp2, dwpos, dbpos, dw1, db1
+
+
 _FUSED_COST_VOLUME = True  # test seam: False forces the unfused torch formulation
 
 
@@ -520,7 +555,13 @@ def _fusable(nsample, pos, mlp, act, din):
     if not isinstance(norm, nn.Identity) or not isinstance(a2, nn.LeakyReLU) \
             or a2.negative_slope != LEAKY_RATE or conv.bias is None:
         return False
-    return _nat.cost_volume_supported(din, conv.out_channels, nsample) and pos.bias is not None
+    if pos.bias is None:
+        return False
+    if _nat.cost_volume_supported(din, conv.out_channels, nsample):
+        return _CostVolume
+    if _nat.cost_volume_wide_supported(din, conv.out_channels, nsample):
+        return _CostVolumeWide
+    return False
 
 
 def _cost_volume(nsample, xyz1, xyz2, points1, points2, pos, mlp, act, knn_idx=None):
@@ -540,11 +581,12 @@ def _cost_volume_cl(nsample, x1, x2, p1, p2, pos, mlp, act, knn_idx=None):
     if knn_idx is None:
         knn_idx = knn_point(nsample, x2, x1)
     din = p1.shape[-1]
-    if _fusable(nsample, pos, mlp, act, din):
+    fn = _fusable(nsample, pos, mlp, act, din)
+    if fn:
         conv = mlp[0].composed_module[0]
-        return _CostVolume.apply(x1, x2, knn_idx, p1.contiguous(), p2.contiguous(),
-                                 pos.weight.view(din, 3), pos.bias,
-                                 conv.weight.view(conv.out_channels, din), conv.bias)
+        return fn.apply(x1, x2, _as_idx32(knn_idx).contiguous(), p1.contiguous(), p2.contiguous(),
+                        pos.weight.view(din, 3), pos.bias,
+                        conv.weight.view(conv.out_channels, din), conv.bias)
     direction = index_points_group(x2, knn_idx) - x1.view(B, N1, 1, C)
     grouped_points2 = index_points_group(p2, knn_idx)
     h = act((grouped_points2 + p1.unsqueeze(2)) + _linear_1x1(pos, direction))

@@ -16,7 +16,9 @@ def _scale_close(a, b, rtol=1e-5, name="", floor=1e-6):
 
 
 @pytest.mark.parametrize("din,dout,n1,n2,bsz", [(32, 32, 1000, 900, 2), (64, 64, 513, 700, 3),
-                                                (32, 64, 300, 300, 1), (64, 32, 257, 600, 2)])
+                                                (32, 64, 300, 300, 1), (64, 32, 257, 600, 2),
+                                                (128, 128, 300, 280, 2), (256, 256, 200, 250, 2),
+                                                (128, 256, 130, 140, 1)])
 def test_cost_volume_fused_equals_unfused(din, dout, n1, n2, bsz):
     import pointconv_util as P
     import synthetic
@@ -26,6 +28,10 @@ def test_cost_volume_fused_equals_unfused(din, dout, n1, n2, bsz):
     x2 = torch.from_numpy(synthetic.ft3d_batch(bsz, n2, seed=2)[0]).to(DEV).permute(0, 2, 1)
     f1 = torch.randn(bsz, din, n1, device=DEV)
     f2 = torch.randn(bsz, din, n2, device=DEV)
+    import kdpc_native
+    wide = not kdpc_native.cost_volume_supported(din, dout, 32)
+    assert P._fusable(32, layer.pos1, layer.mlp1, layer._act(layer.bn1), din) is (
+        P._CostVolumeWide if wide else P._CostVolume)
     outs, grads = [], []
     for fused in (True, False):
         P._FUSED_COST_VOLUME = fused
