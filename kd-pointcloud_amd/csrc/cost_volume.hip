@@ -68,12 +68,27 @@ __device__ __forceinline__ void build_h0(int n, int k, const float* __restrict__
   const float p1 = p1b[(long long)n * D_IN + c];
   const float w0 = wpos[c * 3 + 0], w1 = wpos[c * 3 + 1], w2 = wpos[c * 3 + 2];
   const float bp = bpos[c];
+  // row broadcasts by readlane (uniform lane index: SGPR, no LDS round trip); the loop is
+  // unrolled so all of the query's neighbour gathers are in flight together
+#pragma unroll
   for (int r0 = 0; r0 < kRows; r0 += RPP) {
     const int r = r0 + sub;
-    const int j = __shfl(my_j, r, kWave);
-    const float dx = __shfl(my_dx, r, kWave);
-    const float dy = __shfl(my_dy, r, kWave);
-    const float dz = __shfl(my_dz, r, kWave);
+    const int ja = __builtin_amdgcn_readlane(my_j, r0);
+    const float dxa = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_dx), r0));
+    const float dya = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_dy), r0));
+    const float dza = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_dz), r0));
+    int j = ja;
+    float dx = dxa, dy = dya, dz = dza;
+    if (RPP == 2) {
+      const int jb = __builtin_amdgcn_readlane(my_j, r0 + 1);
+      const float dxb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_dx), r0 + 1));
+      const float dyb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_dy), r0 + 1));
+      const float dzb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_dz), r0 + 1));
+      j = sub ? jb : ja;
+      dx = sub ? dxb : dxa;
+      dy = sub ? dyb : dya;
+      dz = sub ? dzb : dza;
+    }
     float h = 0.f;
     if (r < k) {
       const float g2 = p2b[(long long)j * D_IN + c];
@@ -269,9 +284,9 @@ __global__ __launch_bounds__(256) void cost_volume_bwd_kernel(
     // channel sums over rows in ascending order (every lane runs the loop so the row
     // broadcasts are wave-uniform; only sub==0 lanes own a channel)
     for (int r = 0; r < k; ++r) {
-      const float rdx = __shfl(dx, r, kWave);
-      const float rdy = __shfl(dy, r, kWave);
-      const float rdz = __shfl(dz, r, kWave);
+      const float rdx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dx), r));
+      const float rdy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dy), r));
+      const float rdz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dz), r));
       const float dzv = lds_d[r * LD + c];
       dp1_acc = __fadd_rn(dp1_acc, dzv);
       gwp0 = __builtin_fmaf(dzv, rdx, gwp0);
@@ -297,9 +312,9 @@ __global__ __launch_bounds__(256) void cost_volume_bwd_kernel(
     // dx1[n] = -sum_r d(dir_r), ascending r (uniform broadcasts, lane 0 stores)
     float s0 = 0.f, s1 = 0.f, s2 = 0.f;
     for (int r = 0; r < k; ++r) {
-      s0 = __fadd_rn(s0, __shfl(g0, r, kWave));
-      s1 = __fadd_rn(s1, __shfl(g1, r, kWave));
-      s2 = __fadd_rn(s2, __shfl(g2, r, kWave));
+      s0 = __fadd_rn(s0, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(g0), r)));
+      s1 = __fadd_rn(s1, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(g1), r)));
+      s2 = __fadd_rn(s2, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(g2), r)));
     }
     if (lane == 0) {
       float* o = dx1 + ((long long)b * n1 + n) * 3;
