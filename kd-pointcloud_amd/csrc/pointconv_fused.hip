@@ -47,6 +47,7 @@ constexpr int kBlk = 32 * 4 + 16;   // floats per 4-column block of a 32-row MFM
 constexpr int kTS = 32 + 4;         // row stride of transposed (inner = row) 32-row tiles
 constexpr int kDaS = kNC + 4;       // row stride of the dA chunk
 constexpr int kTargetWG = 512;      // grid size the split heuristics aim for
+constexpr int kCUs = 256;           // MI355X compute units
 
 struct Geo {
   int n, s, k, d, c, r, nch, c8;  // c = 3 + d, r = B*S rows, nch = ceil(c/8), c8 = 8*nch
@@ -339,7 +340,7 @@ __global__ __launch_bounds__(256) void pc_slab_sum_kernel(int nslabs, long long 
 // pairs t and t+256.  dgr: dG rows [R*K][C8].
 template <int O, int KM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
-void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float* __restrict__ wl,
+void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float* __restrict__ wlt,
                         const float* __restrict__ dy, float* __restrict__ dgr,
                         float* __restrict__ dwt, float* __restrict__ dcenter,
                         int chunks_per_split) {
@@ -394,27 +395,31 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float* __rest
     for (int q = 0; q < PP; ++q)
 #pragma unroll
       for (int c = 0; c < kCC; ++c) gv[q][c] = g_fetch(g, src, pn[q], row0 + pr[q], c0 + c);
+    // B operand = the Linear weight column colg over the O outputs: one contiguous row of
+    // the transposed weight, read as float4 (4 inner indices per lane and MFMA block)
+    // branch-free (clamped address + select) and PF blocks ahead of its MFMAs (one block
+    // ahead left every step waiting on an L2 round trip)
     const int colg = c0 * kW + n0 + l32;
     const bool ok = (colg >> 4) < g.c;
-    const float* wcol = wl + colg;
+    const float4* wrow = reinterpret_cast<const float4*>(wlt + (long long)(ok ? colg : 0) * O);
+    constexpr int NOG = O / 8;
+    constexpr int PF = NOG < 4 ? NOG : 4;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 bq[PF];
+#pragma unroll
+    for (int p2 = 0; p2 < PF; ++p2) {
+      const float4 v = wrow[2 * p2 + half];
+      bq[p2] = ok ? v : z4;
+    }
     f32x16 acc = zero16();
-    float4 bcur, bnxt = make_float4(0.f, 0.f, 0.f, 0.f);
-    bcur.x = ok ? wcol[(4 * half + 0) * c16] : 0.f;
-    bcur.y = ok ? wcol[(4 * half + 1) * c16] : 0.f;
-    bcur.z = ok ? wcol[(4 * half + 2) * c16] : 0.f;
-    bcur.w = ok ? wcol[(4 * half + 3) * c16] : 0.f;
-#pragma unroll 4
-    for (int og = 0; og < O / 8; ++og) {
-      if (og + 1 < O / 8) {
-        const int ob = 8 * (og + 1) + 4 * half;
-        bnxt.x = ok ? wcol[(ob + 0) * c16] : 0.f;
-        bnxt.y = ok ? wcol[(ob + 1) * c16] : 0.f;
-        bnxt.z = ok ? wcol[(ob + 2) * c16] : 0.f;
-        bnxt.w = ok ? wcol[(ob + 3) * c16] : 0.f;
-      }
+#pragma unroll
+    for (int og = 0; og < NOG; ++og) {
       const float4 av = *reinterpret_cast<const float4*>(dyl + (2 * og + half) * kBlk + l32 * 4);
-      acc = mfma4(av, bcur, acc);
-      bcur = bnxt;
+      acc = mfma4(av, bq[og % PF], acc);
+      if (og + PF < NOG) {
+        const float4 v = wrow[2 * (og + PF) + half];
+        bq[og % PF] = ok ? v : z4;
+      }
     }
 #pragma unroll
     for (int e = 0; e < 16; ++e)
@@ -467,6 +472,24 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float* __rest
 #pragma unroll
     for (int v = 0; v < kW / 4; ++v)
       dst[v] = make_float4(dw[q][4 * v], dw[q][4 * v + 1], dw[q][4 * v + 2], dw[q][4 * v + 3]);
+  }
+}
+
+// wlt (16C, O) = wl (O, 16C)^T, 32x32 tiles through LDS
+__global__ __launch_bounds__(256) void pc_transpose_kernel(int rows, int cols,
+                                                           const float* __restrict__ src,
+                                                           float* __restrict__ dst) {
+  __shared__ float tile[32][33];
+  const int bx = blockIdx.x * 32, by = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int i = ty; i < 32; i += 8) {
+    const int r = by + i, c = bx + tx;
+    tile[i][tx] = (r < rows && c < cols) ? src[(long long)r * cols + c] : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int c = bx + i, r = by + tx;
+    if (c < cols && r < rows) dst[(long long)c * rows + r] = tile[tx][i];
   }
 }
 
@@ -625,7 +648,7 @@ struct Plan {
   int ks, cps;                 // fwd channel splits / chunks per split
   int bks, bcps;               // bwd-data channel splits (32-row tiles)
   int rs, rps, xcd, wgs;       // bwd-weight row splits, rows per split, XCD map, grid
-  size_t fwd_slab, dgr, dwt_slab, dwl_slab;  // bytes
+  size_t fwd_slab, dgr, dwt_slab, dwl_slab, wlt;  // bytes
 };
 
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -657,18 +680,42 @@ bool plan_of(int b, int s, int k, int d, int o, Plan* p) {
   p->rt = divup(p->r, p->tm);
   channel_split(p->nch, p->rt, &p->ks, &p->cps);
   channel_split(p->nch, divup(p->r, 32), &p->bks, &p->bcps);
+  // bwd-weight row splits: every (chunk, split) workgroup carries the same MFMA work and
+  // all of them are resident at once, so the kernel takes (most workgroups on one CU) x
+  // (rows per split) / efficiency; pick the split count minimising that (the old fixed
+  // target of 512 made 520 workgroups: 3 on a few CUs, 2 on the rest).  Multiples of 8 keep
+  // the XCD mapping (a split's chunks share its dy / wt rows in one L2) unless >6% slower.
   const int t32 = std::max(1, divup(p->r, 32));
-  int rs = std::max(1, std::min(t32, divup(kTargetWG, p->nch)));
+  const int per_cu = o == 256 ? 2 : 3;  // resident 512-thread workgroups (LDS)
+  const int cap = std::max(1, std::min(t32, kCUs * per_cu / p->nch));
+  // measured (level-0 estimator, O = 128, 15 chunks): 255 workgroups (1 per CU) 477 us,
+  // 520 (2-3 per CU) 597 us, 765 (3 per CU) 777 us -- co-resident workgroups slow each
+  // other down (L2 / LDS contention) more than they overlap: fewer, longer splits
+  auto cost = [&](int rs) {
+    const int rps = divup(t32, rs);
+    const int per = divup(p->nch * divup(t32, rps), kCUs);
+    // O = 64 has half the MFMA work per gathered row: there the gathers dominate and more
+    // co-resident workgroups hide them (252 workgroups 300 us vs 486: 206 us)
+    const double eff = o >= 128 ? (per >= 3 ? 0.6 : (per == 2 ? 0.8 : 1.0))
+                                : (per >= 3 ? 1.0 : (per == 2 ? 0.9 : 0.65));
+    return per * rps / eff;
+  };
+  int best = 1, best8 = 0;
+  for (int rs = 1; rs <= cap; ++rs) {
+    if (cost(rs) < cost(best)) best = rs;
+    if (rs % 8 == 0 && (best8 == 0 || cost(rs) < cost(best8))) best8 = rs;
+  }
+  const int rs = (best8 > 0 && cost(best8) <= 1.06 * cost(best)) ? best8 : best;
   p->rps = divup(t32, rs) * 32;
   p->rs = std::max(1, divup(p->r, p->rps));
-  p->xcd = p->rs >= 8 ? 1 : 0;
-  const int rs_pad = p->xcd ? divup(p->rs, 8) * 8 : p->rs;
-  p->wgs = p->nch * rs_pad;
+  p->xcd = (p->rs >= 8 && p->rs % 8 == 0) ? 1 : 0;
+  p->wgs = p->nch * p->rs;
   const size_t c16 = (size_t)p->c * kW;
   p->fwd_slab = p->ks > 1 ? align256((size_t)p->ks * p->r * o * 4) : 0;
   p->dgr = align256((size_t)p->r * k * p->c8 * 4);
   p->dwt_slab = p->bks > 1 ? align256((size_t)p->bks * p->r * k * kW * 4) : 0;
   p->dwl_slab = p->rs > 1 ? align256((size_t)p->rs * o * c16 * 4) : 0;
+  p->wlt = align256((size_t)o * c16 * 4);
   return true;
 }
 
@@ -702,10 +749,16 @@ hipError_t bwd_launch(const Geo& g, const Plan& p, int b, const float* wt, const
   float* dgr = reinterpret_cast<float*>(ws);
   float* dwt_slab = reinterpret_cast<float*>(ws + p.dgr);
   float* dwl_slab = reinterpret_cast<float*>(ws + p.dgr + p.dwt_slab);
+  float* wlt = reinterpret_cast<float*>(ws + p.dgr + p.dwt_slab + p.dwl_slab);
   const long long rk = (long long)p.r * g.k;
-  hipLaunchKernelGGL((pc_bwd_data_kernel<O, KM>), dim3(divup(p.r, 32), p.bks), dim3(256), 0, st,
-                     g, wt, wl, dy, dgr, p.bks > 1 ? dwt_slab : dwt, dcenter, p.bcps);
+  const int c16 = g.c * kW;
+  hipLaunchKernelGGL(pc_transpose_kernel, dim3(divup(c16, 32), divup(O, 32)), dim3(256), 0, st,
+                     O, c16, wl, wlt);
   hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((pc_bwd_data_kernel<O, KM>), dim3(divup(p.r, 32), p.bks), dim3(256), 0, st,
+                     g, wt, wlt, dy, dgr, p.bks > 1 ? dwt_slab : dwt, dcenter, p.bcps);
+  e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (p.bks > 1 && (e = slab_sum(p.bks, rk * kW, dwt_slab, nullptr, 1, dwt, st)) != hipSuccess)
     return e;
@@ -781,7 +834,7 @@ KDPC_API int kdpc_pointconv_fwd(int b, int n, int s, int k, int d, int o, const 
 
 KDPC_API size_t kdpc_pointconv_bwd_workspace_bytes(int b, int s, int k, int d, int o) {
   Plan p;
-  return plan_of(b, s, k, d, o, &p) ? p.dgr + p.dwt_slab + p.dwl_slab : 0;
+  return plan_of(b, s, k, d, o, &p) ? p.dgr + p.dwt_slab + p.dwl_slab + p.wlt : 0;
 }
 
 KDPC_API int kdpc_pointconv_bwd(int b, int n, int s, int k, int d, int o, const float* xyz,
@@ -802,7 +855,7 @@ KDPC_API int kdpc_pointconv_bwd(int b, int n, int s, int k, int d, int o, const 
   }
   KDPC_CHECK_ARG(xyz && center && idx && wt && wl && dy && offsets && perm && dcenter && dwt &&
                  dwl && (d == 0 || (feats && dfeats)));
-  KDPC_CHECK_ARG(workspace && workspace_bytes >= p.dgr + p.dwt_slab + p.dwl_slab);
+  KDPC_CHECK_ARG(workspace && workspace_bytes >= p.dgr + p.dwt_slab + p.dwl_slab + p.wlt);
   const Geo g = geo_of(b, n, s, k, d, p, xyz, center, feats, idx);
   char* ws = reinterpret_cast<char*>(workspace);
   return (int)KDPC_PC_DISPATCH(bwd_launch, g, p, b, wt, wl, dy, offsets, perm, dxyz, dfeats,
