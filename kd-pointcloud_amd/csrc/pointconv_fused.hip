@@ -336,19 +336,25 @@ __global__ __launch_bounds__(256) void pc_slab_sum_kernel(int nslabs, long long 
 }
 
 // -------------------------------------------------------------------- backward: data
-// grid (32-row tiles, channel splits), 256 threads; each thread owns (row, neighbour)
-// pairs t and t+256.  dgr: dG rows [R*K][C8].
+// grid (TR-row tiles, channel splits), 256 threads; each thread owns (row, neighbour)
+// pairs t and t+256.  dgr: dG rows [R*K][C8].  (28-row tiles for K = 9 -- one pair per
+// thread instead of a second VALU pass for 32 lanes -- measured slower, 934 vs 854 us at
+// level 0: the kernel is bound by its MFMA / B-operand stream, not by the VALU phase.)
+template <int KM>
+constexpr int bwd_tile_rows() { return 32; }
+
 template <int O, int KM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float* __restrict__ wlt,
                         const float* __restrict__ dy, float* __restrict__ dgr,
                         float* __restrict__ dwt, float* __restrict__ dcenter,
                         int chunks_per_split) {
-  constexpr int PP = (32 * KM + 255) / 256;  // pairs per thread
+  constexpr int TR = bwd_tile_rows<KM>();
+  constexpr int PP = (TR * KM + 255) / 256;  // pairs per thread
   __shared__ __attribute__((aligned(16))) float dyl[(O / 4) * kBlk];
   __shared__ __attribute__((aligned(16))) float dal[32 * kDaS];
-  __shared__ float dcl[32 * KM * 3];
-  const int row0 = blockIdx.x * 32;
+  __shared__ float dcl[TR * KM * 3];
+  const int row0 = blockIdx.x * TR;
   const int split = blockIdx.y;
   const int ch0 = split * chunks_per_split;
   const int ch1 = min(g.nch, ch0 + chunks_per_split);
@@ -360,7 +366,8 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float* __rest
   for (int e = t; e < 32 * O; e += 256) {
     const int r = e / O, o = e % O;
     const int row = row0 + r;
-    dyl[(o >> 2) * kBlk + r * 4 + (o & 3)] = row < g.r ? dy[(long long)row * O + o] : 0.f;
+    dyl[(o >> 2) * kBlk + r * 4 + (o & 3)] =
+        (r < TR && row < g.r) ? dy[(long long)row * O + o] : 0.f;
   }
   float wp[PP][kW], dw[PP][kW];
   int pr[PP], pk[PP], pn[PP];
@@ -369,7 +376,7 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float* __rest
     const int p = t + 256 * q;
     pr[q] = p / g.k;
     pk[q] = p - pr[q] * g.k;
-    const bool ok = p < 32 * g.k && row0 + pr[q] < g.r;
+    const bool ok = p < TR * g.k && row0 + pr[q] < g.r;
     pn[q] = ok ? nbr_of(g, row0 + pr[q], pk[q]) : -1;
     const long long pos = (long long)(row0 + pr[q]) * g.k + pk[q];
 #pragma unroll
@@ -387,30 +394,43 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float* __rest
   __syncthreads();
 
   const int n0 = wv * 32;  // this wave's 32 dA columns of the chunk
-  for (int ch = ch0; ch < ch1; ++ch) {
-    const int c0 = ch * kCC;
-    // this chunk's neighbour channels, in flight during the MFMAs
-    float gv[PP][kCC];
+  // Load order matters: loads and stores retire in issue order (vmcnt), so an MFMA waiting
+  // on a B fragment also waits for every older gather and dG store.  Per chunk: the first
+  // PF B blocks and the neighbour gathers of chunk ch+1 are issued right after chunk ch's
+  // MFMAs -- before ch's dG stores -- so ch+1's first MFMAs wait only on those, and the
+  // gathers land during ch's VALU phase (they are used in ch+1's VALU phase).
+  // B operand = the Linear weight column over the O outputs: one contiguous row of the
+  // transposed weight, float4 per lane and block, branch-free (clamped address + select).
+  constexpr int NOG = O / 8;
+  constexpr int PF = NOG < 4 ? NOG : 4;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto brow = [&](int ch) {
+    const int colg = ch * kCC * kW + n0 + l32;
+    return reinterpret_cast<const float4*>(wlt + (long long)((colg >> 4) < g.c ? colg : 0) * O);
+  };
+  auto bok = [&](int ch) { return ((ch * kCC * kW + n0 + l32) >> 4) < g.c; };
+  float4 bq[PF];
+  float gv[PP][kCC], gn[PP][kCC];
+  auto gather = [&](int ch, float (&dst)[PP][kCC]) {
 #pragma unroll
     for (int q = 0; q < PP; ++q)
 #pragma unroll
-      for (int c = 0; c < kCC; ++c) gv[q][c] = g_fetch(g, src, pn[q], row0 + pr[q], c0 + c);
-    // B operand = the Linear weight column colg over the O outputs: one contiguous row of
-    // the transposed weight, read as float4 (4 inner indices per lane and MFMA block)
-    // branch-free (clamped address + select) and PF blocks ahead of its MFMAs (one block
-    // ahead left every step waiting on an L2 round trip)
-    const int colg = c0 * kW + n0 + l32;
-    const bool ok = (colg >> 4) < g.c;
-    const float4* wrow = reinterpret_cast<const float4*>(wlt + (long long)(ok ? colg : 0) * O);
-    constexpr int NOG = O / 8;
-    constexpr int PF = NOG < 4 ? NOG : 4;
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 bq[PF];
+      for (int c = 0; c < kCC; ++c) dst[q][c] = g_fetch(g, src, pn[q], row0 + pr[q], ch * kCC + c);
+  };
+  if (ch0 < ch1) {
+    const float4* wr0 = brow(ch0);
+    const bool ok0 = bok(ch0);
 #pragma unroll
     for (int p2 = 0; p2 < PF; ++p2) {
-      const float4 v = wrow[2 * p2 + half];
-      bq[p2] = ok ? v : z4;
+      const float4 v = wr0[2 * p2 + half];
+      bq[p2] = ok0 ? v : z4;
     }
+    gather(ch0, gv);
+  }
+  for (int ch = ch0; ch < ch1; ++ch) {
+    const int c0 = ch * kCC;
+    const float4* wrow = brow(ch);
+    const bool ok = bok(ch);
     f32x16 acc = zero16();
 #pragma unroll
     for (int og = 0; og < NOG; ++og) {
@@ -420,6 +440,16 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float* __rest
         const float4 v = wrow[2 * (og + PF) + half];
         bq[og % PF] = ok ? v : z4;
       }
+    }
+    if (ch + 1 < ch1) {
+      const float4* wr1 = brow(ch + 1);
+      const bool ok1 = bok(ch + 1);
+#pragma unroll
+      for (int p2 = 0; p2 < PF; ++p2) {
+        const float4 v = wr1[2 * p2 + half];
+        bq[p2] = ok1 ? v : z4;
+      }
+      gather(ch + 1, gn);
     }
 #pragma unroll
     for (int e = 0; e < 16; ++e)
@@ -453,8 +483,12 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float* __rest
       }
     }
     __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PP; ++q)
+#pragma unroll
+      for (int c = 0; c < kCC; ++c) gv[q][c] = gn[q][c];
   }
-  if (ch0 == 0 && t < 32 * 3) {
+  if (ch0 == 0 && t < TR * 3) {
     const int r = t / 3, i = t - (t / 3) * 3;
     const int row = row0 + r;
     if (row < g.r) {
@@ -756,7 +790,8 @@ hipError_t bwd_launch(const Geo& g, const Plan& p, int b, const float* wt, const
                      O, c16, wl, wlt);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((pc_bwd_data_kernel<O, KM>), dim3(divup(p.r, 32), p.bks), dim3(256), 0, st,
+  hipLaunchKernelGGL((pc_bwd_data_kernel<O, KM>), dim3(divup(p.r, bwd_tile_rows<KM>()), p.bks),
+                     dim3(256), 0, st,
                      g, wt, wlt, dy, dgr, p.bks > 1 ? dwt_slab : dwt, dcenter, p.bcps);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
