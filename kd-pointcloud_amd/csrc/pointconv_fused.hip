@@ -742,6 +742,8 @@ bool plan_of(int b, int s, int k, int d, int o, Plan* p) {
   const int rs = (best8 > 0 && cost(best8) <= 1.06 * cost(best)) ? best8 : best;
   p->rps = divup(t32, rs) * 32;
   p->rs = std::max(1, divup(p->r, p->rps));
+  // (padding the split count up to a multiple of 8 for the XCD mapping was tried: 272
+  // workgroups put 2 on some CUs, 661 vs 477 us at level 0 -- balance beats L2 locality)
   p->xcd = (p->rs >= 8 && p->rs % 8 == 0) ? 1 : 0;
   p->wgs = p->nch * p->rs;
   const size_t c16 = (size_t)p->c * kW;
