@@ -544,6 +544,7 @@ class _CostVolumeWide(torch.autograd.Function):
 
 
 _FUSED_COST_VOLUME = True  # test seam: False forces the unfused torch formulation
+_WIDE_MIN_DIN = 128  # Din=64 through the wide path measured within noise (311.8 vs 309.9 pairs/s)
 
 
 def _fusable(nsample, pos, mlp, act, din):
@@ -557,6 +558,8 @@ def _fusable(nsample, pos, mlp, act, din):
         return False
     if pos.bias is None:
         return False
+    if din >= _WIDE_MIN_DIN and _nat.cost_volume_wide_supported(din, conv.out_channels, nsample):
+        return _CostVolumeWide
     if _nat.cost_volume_supported(din, conv.out_channels, nsample):
         return _CostVolume
     if _nat.cost_volume_wide_supported(din, conv.out_channels, nsample):
