@@ -38,6 +38,7 @@ using namespace kdpc;
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kW = 16;              // WeightNet width (weightnet=16 in every model layer)
 constexpr int kCC = 8;              // channels per chunk
@@ -402,7 +403,7 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float* __rest
   // B operand = the Linear weight column over the O outputs: one contiguous row of the
   // transposed weight, float4 per lane and block, branch-free (clamped address + select).
   constexpr int NOG = O / 8;
-  constexpr int PF = NOG < 4 ? NOG : 4;
+  constexpr int PF = NOG < 4 ? NOG : 4;  // (16 ahead measured slower: 949 vs 854 us)
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   auto brow = [&](int ch) {
     const int colg = ch * kCC * kW + n0 + l32;
@@ -411,11 +412,30 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float* __rest
   auto bok = [&](int ch) { return ((ch * kCC * kW + n0 + l32) >> 4) < g.c; };
   float4 bq[PF];
   float gv[PP][kCC], gn[PP][kCC];
+  // a pair's 8 channels of a feature chunk are 32 contiguous bytes of its neighbour's row:
+  // two 16-byte buffer loads (dword-aligned; past-the-row lanes masked, past-the-buffer
+  // reads 0) instead of eight 4-byte ones; chunk 0 (xyz - center) stays per channel
   auto gather = [&](int ch, float (&dst)[PP][kCC]) {
+    if (ch == 0) {
 #pragma unroll
-    for (int q = 0; q < PP; ++q)
+      for (int q = 0; q < PP; ++q)
 #pragma unroll
-      for (int c = 0; c < kCC; ++c) dst[q][c] = g_fetch(g, src, pn[q], row0 + pr[q], ch * kCC + c);
+        for (int c = 0; c < kCC; ++c) dst[q][c] = g_fetch(g, src, pn[q], row0 + pr[q], c);
+      return;
+    }
+#pragma unroll
+    for (int q = 0; q < PP; ++q) {
+      const unsigned off = pn[q] < 0 ? kOOB : feat_off(g, pn[q]) + (unsigned)(ch * kCC - 3) * 4u;
+      const f32x4 lo = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     src.feats, (int)off, 0, 0));
+      const f32x4 hi = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     src.feats, (int)(off + 16u), 0, 0));
+#pragma unroll
+      for (int c = 0; c < kCC; ++c) {
+        const float v = c < 4 ? lo[c] : hi[c - 4];
+        dst[q][c] = ch * kCC + c < g.c ? v : 0.f;
+      }
+    }
   };
   if (ch0 < ch1) {
     const float4* wr0 = brow(ch0);
@@ -460,26 +480,34 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float* __rest
       if (pn[q] < 0) continue;
       const int r = pr[q];
       const long long pos = (long long)(row0 + r) * g.k + pk[q];
-      float* dgo = dgr + pos * g.c8 + c0;
-#pragma unroll 2
-      for (int cl = 0; cl < kCC; ++cl) {
-        float da[kW];
+      // the pair's 8 dG values are 32 contiguous (32-byte aligned) bytes: one 16-byte store
+      // per half-chunk of 4 channels (a fully unrolled 8-channel body spilled)
+      float4* dgo = reinterpret_cast<float4*>(dgr + pos * g.c8 + c0);
+#pragma unroll 1
+      for (int hc = 0; hc < 2; ++hc) {
+        float sv[4];
 #pragma unroll
-        for (int v = 0; v < kW / 4; ++v) {
-          const float4 x = *reinterpret_cast<const float4*>(dal + r * kDaS + cl * kW + 4 * v);
-          da[4 * v + 0] = x.x;
-          da[4 * v + 1] = x.y;
-          da[4 * v + 2] = x.z;
-          da[4 * v + 3] = x.w;
+        for (int c4 = 0; c4 < 4; ++c4) {
+          const int cl = 4 * hc + c4;
+          float da[kW];
+#pragma unroll
+          for (int v = 0; v < kW / 4; ++v) {
+            const float4 x = *reinterpret_cast<const float4*>(dal + r * kDaS + cl * kW + 4 * v);
+            da[4 * v + 0] = x.x;
+            da[4 * v + 1] = x.y;
+            da[4 * v + 2] = x.z;
+            da[4 * v + 3] = x.w;
+          }
+          float s = 0.f;
+#pragma unroll
+          for (int w = 0; w < kW; ++w) s = __builtin_fmaf(da[w], wp[q][w], s);
+          sv[c4] = s;
+          if (c0 == 0 && cl < 3) dcl[(r * g.k + pk[q]) * 3 + cl] = s;
+          const float gc = hc ? gv[q][4 + c4] : gv[q][c4];
+#pragma unroll
+          for (int w = 0; w < kW; ++w) dw[q][w] = __builtin_fmaf(da[w], gc, dw[q][w]);
         }
-        float s = 0.f;
-#pragma unroll
-        for (int w = 0; w < kW; ++w) s = __builtin_fmaf(da[w], wp[q][w], s);
-        dgo[cl] = s;
-        if (c0 == 0 && cl < 3) dcl[(r * g.k + pk[q]) * 3 + cl] = s;
-        const float gc = gv[q][cl];
-#pragma unroll
-        for (int w = 0; w < kW; ++w) dw[q][w] = __builtin_fmaf(da[w], gc, dw[q][w]);
+        dgo[hc] = make_float4(sv[0], sv[1], sv[2], sv[3]);
       }
     }
     __syncthreads();
