@@ -593,19 +593,27 @@ __global__ __launch_bounds__(256) void pc_csr_sum_kernel(long long npts, int c, 
 
 // ------------------------------------------------------------------ backward: weight
 // 1-D grid of nch x splits workgroups (512 threads); each owns the O x 128 tile of dwl for
-// one chunk over one split's rows.  With >= 8 splits, the chunks of split s all run on XCD
-// s % 8 (workgroups are dealt to the XCDs round-robin by linear id).
+// one chunk over one split's rows, walked in tiles of TR rows (the MFMA inner dimension).
+// TR = 64 for O = 128: twice the MFMA work per gather / build / barrier round of the
+// 32-row tile (one workgroup per CU either way: the grid model below).  With >= 8 splits,
+// the chunks of split s all run on XCD s % 8 (workgroups are dealt round-robin by id).
+template <int O>
+constexpr int wgt_tile_rows() { return O == 128 ? 64 : 32; }  // O = 256 at 64 rows spilled
+
 template <int O, int KM, bool EX>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
 void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __restrict__ dy,
                           float* __restrict__ dwl, int rows_per_split, int nsplit, int xcd_map) {
+  constexpr int TR = wgt_tile_rows<O>();
+  constexpr int TS = TR + 4;               // row stride of the transposed tiles
+  constexpr int RP = TR / 32;              // build passes (rows rb, rb + 32, ...)
   constexpr int MT = O / 32;
   constexpr int MPW = MT / 2;              // 8 waves: 4 column tiles x 2 row-tile groups
-  constexpr int GS = (32 * KM + 63) / 64;  // gather slots per thread
-  constexpr int DS = O / 16;               // dy slots per thread
-  __shared__ __attribute__((aligned(16))) float gl[32 * KM * kCC];
-  __shared__ __attribute__((aligned(16))) float dyt[O * kTS];
-  __shared__ __attribute__((aligned(16))) float at[kNC * kTS];
+  constexpr int GS = (TR * KM + 63) / 64;  // gather slots per thread
+  constexpr int DS = TR * O / 512;         // dy slots per thread
+  __shared__ __attribute__((aligned(16))) float gl[TR * KM * kCC];
+  __shared__ __attribute__((aligned(16))) float dyt[O * TS];
+  __shared__ __attribute__((aligned(16))) float at[kNC * TS];
 
   const int L = blockIdx.x;
   int ch, split;
@@ -627,16 +635,19 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
   const int nt = wv & 3;
   const int m0 = (wv >> 2) * MPW;
   const long long c16 = (long long)g.c * kW;
-  const int tk = 32 * kk;
+  const int tk = TR * kk;
   const Srcs src = srcs_of(g);
 
   // registers prefetched one tile ahead
-  float wr[KM], gr[GS], dr[DS];
+  float wr[RP][KM], gr[GS], dr[DS];
   auto fetch = [&](int row0) {
-    const int row = row0 + rb;
 #pragma unroll
-    for (int k = 0; k < KM; ++k)
-      wr[k] = (row < rend && k < kk) ? wt[((long long)row * kk + k) * kW + w] : 0.f;
+    for (int p2 = 0; p2 < RP; ++p2) {
+      const int row = row0 + rb + 32 * p2;
+#pragma unroll
+      for (int k = 0; k < KM; ++k)
+        wr[p2][k] = (row < rend && k < kk) ? wt[((long long)row * kk + k) * kW + w] : 0.f;
+    }
 #pragma unroll
     for (int i = 0; i < GS; ++i) {
       const int rk = (t >> 3) + 64 * i;
@@ -657,7 +668,7 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
 #pragma unroll
   for (int i = 0; i < MPW; ++i) acc[i] = zero16();
   fetch(rbeg);
-  for (int row0 = rbeg; row0 < rend; row0 += 32) {
+  for (int row0 = rbeg; row0 < rend; row0 += TR) {
     __syncthreads();  // previous tile's MFMAs are done with dyt / at
 #pragma unroll
     for (int i = 0; i < GS; ++i) {
@@ -667,27 +678,30 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
 #pragma unroll
     for (int i = 0; i < DS; ++i) {
       const int e = t + 512 * i;
-      dyt[(e % O) * kTS + e / O] = dr[i];
+      dyt[(e % O) * TS + e / O] = dr[i];
     }
-    float wc[KM];
+    float wc[RP][KM];
 #pragma unroll
-    for (int k = 0; k < KM; ++k) wc[k] = wr[k];
+    for (int p2 = 0; p2 < RP; ++p2)
+#pragma unroll
+      for (int k = 0; k < KM; ++k) wc[p2][k] = wr[p2][k];
     __syncthreads();
-    if (row0 + 32 < rend) fetch(row0 + 32);
-    {
+    if (row0 + TR < rend) fetch(row0 + TR);
+#pragma unroll
+    for (int p2 = 0; p2 < RP; ++p2) {
       float a[kCC];
-      build_row<KM>(gl, rb, kk, wc, a);
+      build_row<KM>(gl, rb + 32 * p2, kk, wc[p2], a);
 #pragma unroll
-      for (int c = 0; c < kCC; ++c) at[(c * kW + w) * kTS + rb] = a[c];
+      for (int c = 0; c < kCC; ++c) at[(c * kW + w) * TS + rb + 32 * p2] = a[c];
     }
     __syncthreads();
 #pragma unroll
-    for (int gb = 0; gb < 4; ++gb) {
-      const float4 bv = *reinterpret_cast<const float4*>(at + (nt * 32 + l32) * kTS + 8 * gb + 4 * half);
+    for (int gb = 0; gb < TR / 8; ++gb) {
+      const float4 bv = *reinterpret_cast<const float4*>(at + (nt * 32 + l32) * TS + 8 * gb + 4 * half);
 #pragma unroll
       for (int i = 0; i < MPW; ++i) {
         const float4 av =
-            *reinterpret_cast<const float4*>(dyt + ((m0 + i) * 32 + l32) * kTS + 8 * gb + 4 * half);
+            *reinterpret_cast<const float4*>(dyt + ((m0 + i) * 32 + l32) * TS + 8 * gb + 4 * half);
         acc[i] = mfma4(av, bv, acc[i]);
       }
     }
@@ -748,7 +762,7 @@ bool plan_of(int b, int s, int k, int d, int o, Plan* p) {
   // target of 512 made 520 workgroups: 3 on a few CUs, 2 on the rest).  Multiples of 8 keep
   // the XCD mapping (a split's chunks share its dy / wt rows in one L2) unless >6% slower.
   const int t32 = std::max(1, divup(p->r, 32));
-  const int per_cu = o == 256 ? 2 : 3;  // resident 512-thread workgroups (LDS)
+  const int per_cu = o == 128 ? 1 : (o == 256 ? 2 : 3);  // resident 512-thread workgroups (LDS)
   const int cap = std::max(1, std::min(t32, kCUs * per_cu / p->nch));
   // measured (level-0 estimator, O = 128, 15 chunks): 255 workgroups (1 per CU) 477 us,
   // 520 (2-3 per CU) 597 us, 765 (3 per CU) 777 us -- co-resident workgroups slow each
