@@ -51,22 +51,33 @@ def splitk_tn(a, b):
 
 
 class _Linear(Function):
-    """2-D only: callers reshape outside, so no view is created inside the Function (a view
-    returned from a custom Function may not be modified in place, e.g. by LeakyReLU)."""
+    """y (..., out) = x (..., in) W^T + b.  The N-d output is allocated by the Function itself
+    (the GEMM writes through a 2-D view of it), so it is not a view: callers apply in-place
+    LeakyReLU to it.  Returning a reshape of a 2-D result made every such activation an
+    in-place op on a view -- autograd then recorded CopySlices / AsStrided nodes (21 zero-
+    fills, 42 copies and 21 clones per training step)."""
 
     @staticmethod
-    def forward(ctx, x2, weight, bias):
-        y = torch.addmm(bias, x2, weight.t()) if bias is not None else x2.mm(weight.t())
+    def forward(ctx, x, weight, bias):
+        x2 = x.reshape(-1, x.shape[-1])
+        y = torch.empty((*x.shape[:-1], weight.shape[0]), dtype=x.dtype, device=x.device)
+        y2 = y.view(-1, weight.shape[0])
+        if bias is not None:
+            torch.addmm(bias, x2, weight.t(), out=y2)
+        else:
+            torch.mm(x2, weight.t(), out=y2)
         ctx.save_for_backward(x2, weight)
         ctx.has_bias = bias is not None
+        ctx.xshape = x.shape
         return y
 
     @staticmethod
-    def backward(ctx, g2):
+    def backward(ctx, g):
         x2, weight = ctx.saved_tensors
+        g2 = g.reshape(-1, g.shape[-1])
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
-            gx = g2.mm(weight)
+            gx = g2.mm(weight).view(ctx.xshape)
         if ctx.needs_input_grad[1]:
             gw = splitk_tn(g2.contiguous(), x2)
         if ctx.has_bias and ctx.needs_input_grad[2]:
@@ -76,8 +87,7 @@ class _Linear(Function):
 
 def linear(x, weight, bias=None):
     """F.linear on (..., in) with the split-K weight gradient."""
-    y = _Linear.apply(x.reshape(-1, x.shape[-1]), weight, bias)
-    return y.view(*x.shape[:-1], weight.shape[0])
+    return _Linear.apply(x, weight, bias)
 
 
 class _Conv1x1(Function):
