@@ -159,7 +159,7 @@ void pc_fwd_kernel(Geo g, const float* __restrict__ wt, const float* __restrict_
   constexpr int MPW = (MT == 2 && !SPLIT_M) ? 2 : 1;
   constexpr int NPW = KG > 1 ? 1 : (MT * NT / 4) / MPW;
   constexpr int RPT = TM / 16;                    // builder rows per thread
-  constexpr int GS = TM * KM / 32;                // gather slots per thread
+  constexpr int GS = (TM * KM + 127) / 128;       // gather slots (float4) per thread
   __shared__ __attribute__((aligned(16))) float gl[TM * KM * kCC];
   __shared__ __attribute__((aligned(16))) float al[MT][(kNC / 4) * kBlk];
 
@@ -187,15 +187,21 @@ void pc_fwd_kernel(Geo g, const float* __restrict__ wt, const float* __restrict_
       wr[q][k] = (row < g.r && k < kk) ? wt[((long long)row * kk + k) * kW + w] : 0.f;
   }
   const Srcs src = srcs_of(g);
+  // gather slots: (row, neighbour) rk = (t >> 1) + 128 i, channels 4*h4 .. 4*h4+3 of the
+  // chunk -- one 16-byte buffer load per slot (two lanes cover a neighbour's 8 channels)
+  const int h4 = t & 1;
   unsigned nbf[GS];  // byte offsets of the slots' neighbour feature rows
-  float gr[GS];
+  float4 gr[GS];
 #pragma unroll
   for (int i = 0; i < GS; ++i) {
-    const int rk = (t >> 3) + 32 * i;
+    const int rk = (t >> 1) + 128 * i;
     const int r = rk / kk;
     const int nb = rk < tk ? nbr_of(g, row0 + r, rk - r * kk) : -1;
     nbf[i] = feat_off(g, nb);
-    gr[i] = g_fetch(g, src, nb, row0 + r, ch0 * kCC + cs);
+    float v[4];
+#pragma unroll
+    for (int e2 = 0; e2 < 4; ++e2) v[e2] = g_fetch(g, src, nb, row0 + r, ch0 * kCC + 4 * h4 + e2);
+    gr[i] = make_float4(v[0], v[1], v[2], v[3]);
   }
   f32x16 acc[MPW][NPW];
 #pragma unroll
@@ -208,8 +214,8 @@ void pc_fwd_kernel(Geo g, const float* __restrict__ wt, const float* __restrict_
     __syncthreads();  // previous chunk's MFMAs are done with al; gl is free
 #pragma unroll
     for (int i = 0; i < GS; ++i) {
-      const int rk = (t >> 3) + 32 * i;
-      if (rk < tk) gl[rk * kCC + cs] = gr[i];
+      const int rk = (t >> 1) + 128 * i;
+      if (rk < tk) *reinterpret_cast<float4*>(gl + rk * kCC + 4 * h4) = gr[i];
     }
     __syncthreads();
     // The chunk's Linear-weight fragments (MFMA B operand, served from L2): the first PF
@@ -238,12 +244,15 @@ void pc_fwd_kernel(Geo g, const float* __restrict__ wt, const float* __restrict_
     // (issued on the last chunk too -- the values are unused there -- so the loop body is
     // straight-line code and the compiler's load counting stays exact)
     {
-      const int cg = c0 + kCC + cs;
+      const int cg = c0 + kCC + 4 * h4;  // first of the slot's 4 channels (>= 8: features)
       const unsigned co = (unsigned)(cg - 3) * 4u;
 #pragma unroll
       for (int i = 0; i < GS; ++i) {
-        const float v = bload(src.feats, nbf[i] + co);  // out-of-range offsets read 0
-        gr[i] = cg < g.c ? v : 0.f;
+        // out-of-range offsets read 0; channels past the row are masked
+        const f32x4 v = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(src.feats, (int)(nbf[i] + co), 0, 0));
+        gr[i] = make_float4(cg < g.c ? v[0] : 0.f, cg + 1 < g.c ? v[1] : 0.f,
+                            cg + 2 < g.c ? v[2] : 0.f, cg + 3 < g.c ? v[3] : 0.f);
       }
     }
 #pragma unroll
