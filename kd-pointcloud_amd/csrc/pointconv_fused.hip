@@ -618,7 +618,7 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
   constexpr int RP = TR / 32;              // build passes (rows rb, rb + 32, ...)
   constexpr int MT = O / 32;
   constexpr int MPW = MT / 2;              // 8 waves: 4 column tiles x 2 row-tile groups
-  constexpr int GS = (TR * KM + 63) / 64;  // gather slots per thread
+  constexpr int GS = (TR * KM + 255) / 256;  // gather slots (float4) per thread
   constexpr int DS = TR * O / 512;         // dy slots per thread
   __shared__ __attribute__((aligned(16))) float gl[TR * KM * kCC];
   __shared__ __attribute__((aligned(16))) float dyt[O * TS];
@@ -648,7 +648,10 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
   const Srcs src = srcs_of(g);
 
   // registers prefetched one tile ahead
-  float wr[RP][KM], gr[GS], dr[DS];
+  // gather slots: (row, neighbour) rk = (t >> 1) + 256 i, channels 4*h4 .. +3 of the chunk
+  const int h4 = t & 1;
+  float wr[RP][KM], dr[DS];
+  float4 gr[GS];
   auto fetch = [&](int row0) {
 #pragma unroll
     for (int p2 = 0; p2 < RP; ++p2) {
@@ -659,11 +662,23 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
     }
 #pragma unroll
     for (int i = 0; i < GS; ++i) {
-      const int rk = (t >> 3) + 64 * i;
+      const int rk = (t >> 1) + 256 * i;
       const int r = rk / kk;
       const int rw = row0 + r;
       const int nb = (rk < tk && rw < rend) ? nbr_of(g, rw, rk - r * kk) : -1;
-      gr[i] = g_fetch(g, src, nb, rw, c0 + cs);
+      if (c0 == 0) {  // xyz - center channels: per element
+        float v[4];
+#pragma unroll
+        for (int e2 = 0; e2 < 4; ++e2) v[e2] = g_fetch(g, src, nb, rw, 4 * h4 + e2);
+        gr[i] = make_float4(v[0], v[1], v[2], v[3]);
+      } else {  // 16 contiguous bytes of the neighbour's feature row; past-the-row masked
+        const int cg = c0 + 4 * h4;
+        const unsigned off = nb < 0 ? kOOB : feat_off(g, nb) + (unsigned)(cg - 3) * 4u;
+        const f32x4 v = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(src.feats, (int)off, 0, 0));
+        gr[i] = make_float4(cg < g.c ? v[0] : 0.f, cg + 1 < g.c ? v[1] : 0.f,
+                            cg + 2 < g.c ? v[2] : 0.f, cg + 3 < g.c ? v[3] : 0.f);
+      }
     }
 #pragma unroll
     for (int i = 0; i < DS; ++i) {
@@ -681,8 +696,8 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
     __syncthreads();  // previous tile's MFMAs are done with dyt / at
 #pragma unroll
     for (int i = 0; i < GS; ++i) {
-      const int rk = (t >> 3) + 64 * i;
-      if (rk < tk) gl[rk * kCC + cs] = gr[i];
+      const int rk = (t >> 1) + 256 * i;
+      if (rk < tk) *reinterpret_cast<float4*>(gl + rk * kCC + 4 * h4) = gr[i];
     }
 #pragma unroll
     for (int i = 0; i < DS; ++i) {
