@@ -8,7 +8,8 @@
  *   - float = f32, int = int32; layouts are the reference's (contiguous, row-major);
  *   - `stream` is a hipStream_t (NULL = default stream); every call is asynchronous on it,
  *     never synchronises the host, and allocates nothing (except the reference-shaped
- *     *_grad entry points, see below);
+ *     *_grad entry points, which take a stream-ordered temporary; their *_ws variants
+ *     take a caller workspace instead);
  *   - return value is a hipError_t code (0 = hipSuccess).  Invalid sizes/pointers return
  *     hipErrorInvalidValue (1) without launching.  The reference instead printed and
  *     called exit(-1) on launch failure (e.g. sampling_gpu.cu:39-43).
@@ -26,6 +27,10 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+
+/* sha256 (hex) of the sources this library was built from (kd-pointcloud_amd/build_native.py
+ * embeds it; the Python loader refuses a library whose id does not match its sources). */
+const char *kdpc_build_id(void);
 
 /* ---- sampling -------------------------------------------------------------------------- */
 
@@ -46,9 +51,26 @@ int kdpc_gather_points(int b, int c, int n, int npoints, const float *points, co
                        float *out, void *stream);
 
 /* Replaces gather_points_grad_wrapper(b, c, n, npoints, grad_out, idx, grad_points)
- * (sampling.cpp:25-35; kernel sampling_gpu.cu:46-63).  Overwrites grad_points (B,C,N). */
+ * (sampling.cpp:25-35; kernel sampling_gpu.cu:46-63).  Overwrites grad_points (B,C,N) with a
+ * deterministic sum.  Scratch: a stream-ordered temporary (hipMallocAsync on `stream`). */
 int kdpc_gather_points_grad(int b, int c, int n, int npoints, const float *grad_out,
                             const int *idx, float *grad_points, void *stream);
+
+/* Scratch bytes of the *_grad_ws entry points for an index of B x P values in [0, N)
+ * (gather: P = npoints; group: P = npoints*nsample; three_interpolate: P = 3N, N -> M). */
+size_t kdpc_grad_workspace_bytes(int b, int n, int p);
+
+/* The three reference-shaped backward entry points with a caller-owned workspace (no
+ * allocation at all: graph-capture safe). */
+int kdpc_gather_points_grad_ws(int b, int c, int n, int npoints, const float *grad_out,
+                               const int *idx, float *grad_points, void *workspace,
+                               size_t workspace_bytes, void *stream);
+int kdpc_group_points_grad_ws(int b, int c, int n, int npoints, int nsample,
+                              const float *grad_out, const int *idx, float *grad_points,
+                              void *workspace, size_t workspace_bytes, void *stream);
+int kdpc_three_interpolate_grad_ws(int b, int c, int n, int m, const float *grad_out,
+                                   const int *idx, const float *weight, float *grad_points,
+                                   void *workspace, size_t workspace_bytes, void *stream);
 
 /* ---- grouping -------------------------------------------------------------------------- */
 
@@ -66,8 +88,7 @@ int kdpc_group_points(int b, int c, int n, int npoints, int nsample, const float
 
 /* Replaces group_points_grad_wrapper(b, c, n, npoints, nsample, grad_out, idx, grad_points)
  * (group_points.cpp:11-24; kernel group_points_gpu.cu:8-25).  Overwrites grad_points (B,C,N).
- * Uses a library-owned workspace grown with hipMalloc on first use (not capture-safe on
- * that first call); the *_csr entry points below take caller-owned buffers instead. */
+ * Scratch: a stream-ordered temporary; kdpc_group_points_grad_ws takes a caller buffer. */
 int kdpc_group_points_grad(int b, int c, int n, int npoints, int nsample, const float *grad_out,
                            const int *idx, float *grad_points, void *stream);
 
@@ -86,7 +107,8 @@ int kdpc_three_interpolate(int b, int c, int m, int n, const float *points, cons
                            const float *weight, float *out, void *stream);
 
 /* Replaces three_interpolate_grad_wrapper(b, c, n, m, grad_out, idx, weight, grad_points)
- * (interpolate.cpp:43-57; kernel interpolate_gpu.cu:120-142).  Overwrites grad_points (B,C,M). */
+ * (interpolate.cpp:43-57; kernel interpolate_gpu.cu:120-142).  Overwrites grad_points (B,C,M).
+ * Scratch: a stream-ordered temporary; kdpc_three_interpolate_grad_ws takes a caller buffer. */
 int kdpc_three_interpolate_grad(int b, int c, int n, int m, const float *grad_out,
                                 const int *idx, const float *weight, float *grad_points,
                                 void *stream);

@@ -3,10 +3,16 @@
     python kd-pointcloud_amd/build_native.py        # -> kd-pointcloud_amd/lib/libkdpc_hip.so
 
 Plain hipcc (no torch headers): each csrc/*.hip is compiled to an object in parallel and
-linked into one shared library.  Objects are rebuilt only when a source or header is newer.
+linked into one shared library.  Objects are keyed by a hash of everything that determines
+them (the source, every header, the flags and the hipcc version), never by file times, so a
+build reuses an object only if it would compile to the same thing.  The library exports
+kdpc_build_id() = the hash of the sources it was built from (source_id() below);
+kdpc_native refuses to load a library whose id does not match the sources next to it, so a
+run can never use a stale binary.
 """
 import concurrent.futures
 import glob
+import hashlib
 import os
 import subprocess
 import sys
@@ -28,21 +34,44 @@ CFLAGS = [
 ]
 
 
-def _newer(target, deps):
-    if not os.path.exists(target):
-        return True
-    t = os.path.getmtime(target)
-    return any(os.path.getmtime(d) > t for d in deps)
+def source_files(csrc=CSRC, root=ROOT):
+    """Every file the library is built from, in a fixed order."""
+    return (sorted(glob.glob(os.path.join(csrc, "*.hip"))) +
+            sorted(glob.glob(os.path.join(csrc, "*.h"))) + [os.path.join(root, "include", "kdpc.h")])
 
 
-def _compile(src):
-    obj = os.path.join(OBJ, os.path.basename(src) + ".o")
-    deps = [src] + glob.glob(os.path.join(CSRC, "*.h")) + [os.path.join(ROOT, "include", "kdpc.h")]
-    if _newer(obj, deps):
-        cmd = [HIPCC] + CFLAGS + ["-c", src, "-o", obj]
-        r = subprocess.run(cmd, capture_output=True, text=True)
+def source_id(csrc=CSRC, root=ROOT):
+    """sha256 over the names and contents of the library's sources (what kdpc_build_id()
+    of a library built from them returns)."""
+    h = hashlib.sha256()
+    for p in source_files(csrc, root):
+        h.update(os.path.basename(p).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    return h.hexdigest()
+
+
+def _hipcc_version():
+    r = subprocess.run([HIPCC, "--version"], capture_output=True, text=True)
+    return r.stdout
+
+
+def _compile(src, headers_digest, tool):
+    h = hashlib.sha256()
+    with open(src, "rb") as f:
+        h.update(f.read())
+    h.update(headers_digest.encode())
+    h.update(" ".join(CFLAGS).encode())
+    h.update(tool.encode())
+    obj = os.path.join(OBJ, f"{os.path.basename(src)}.{h.hexdigest()[:16]}.o")
+    if not os.path.exists(obj):
+        tmp = obj + ".tmp"
+        r = subprocess.run([HIPCC] + CFLAGS + ["-c", src, "-o", tmp], capture_output=True,
+                           text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
+        os.replace(tmp, obj)
     return obj
 
 
@@ -50,15 +79,37 @@ def build(verbose=True):
     os.makedirs(OBJ, exist_ok=True)
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    hd = hashlib.sha256()
+    for p in source_files()[len(srcs):]:
+        with open(p, "rb") as f:
+            hd.update(f.read())
+    tool = _hipcc_version()
+    sid = source_id()
     with concurrent.futures.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        objs = list(ex.map(_compile, srcs))
-    if _newer(LIB, objs):
-        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-fPIC", "-o", LIB] + objs
+        objs = list(ex.map(lambda s: _compile(s, hd.hexdigest(), tool), srcs))
+    # the build id: a one-function host object naming the sources' hash
+    idsrc = os.path.join(OBJ, "kdpc_build_id.cpp")
+    with open(idsrc, "w") as f:
+        f.write('extern "C" __attribute__((visibility("default"))) const char* '
+                f'kdpc_build_id(void) {{ return "{sid}"; }}\n')
+    idobj = _compile(idsrc, hd.hexdigest(), tool)
+    stamp = LIB + ".inputs"
+    link_key = "\n".join(objs + [idobj])
+    old = open(stamp).read() if os.path.exists(stamp) else None
+    if old != link_key or not os.path.exists(LIB):
+        tmp = LIB + ".tmp"
+        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-fPIC", "-o", tmp] + objs + [idobj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr}")
+        os.replace(tmp, LIB)
+        with open(stamp, "w") as f:
+            f.write(link_key)
+    for o in glob.glob(os.path.join(OBJ, "*.o")):  # objects of superseded sources
+        if o not in objs and o != idobj:
+            os.remove(o)
     if verbose:
-        print(f"built {LIB}")
+        print(f"built {LIB} (sources {sid[:12]})")
     return LIB
 
 

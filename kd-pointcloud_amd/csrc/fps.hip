@@ -206,11 +206,10 @@ hipError_t launch_reg(int b, int n, int m, int T, int log2T, const float* xyz, f
   const size_t lds = slot_bytes + (size_t)n * 3 * sizeof(float);
   if (lds <= 160 * 1024) {
     auto k = fps_kernel<BLOCK, PPT, true>;
-    static bool attr_set = false;
-    if (!attr_set) {
-      hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      attr_set = true;
-    }
+    // once per process and instantiation (thread-safe static initialisation)
+    static const hipError_t attr =
+        hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (attr != hipSuccess) return attr;
     hipLaunchKernelGGL(k, dim3(b), dim3(BLOCK), lds, st, n, m, T, log2T, xyz, temp, idx);
   } else {
     hipLaunchKernelGGL((fps_kernel<BLOCK, PPT, false>), dim3(b), dim3(BLOCK), slot_bytes, st, n,

@@ -266,12 +266,10 @@ hipError_t launch_group_lds(dim3 grid, size_t lds, hipStream_t st, int c, int n,
                             int p_slice, int nslice, int groups, int xcd_units,
                             const float* points, const int* idx, float* out) {
   auto k = group_points_lds_kernel<CG>;
-  static bool attr_set = false;  // one process per GPU: set once
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              kRowLdsBytes);
-    attr_set = true;
-  }
+  // once per process and instantiation (thread-safe static initialisation)
+  static const hipError_t attr = hipFuncSetAttribute(
+      (const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, kRowLdsBytes);
+  if (attr != hipSuccess) return attr;
   hipLaunchKernelGGL(k, grid, dim3(256), lds, st, c, n, p_total, p_slice, nslice, groups,
                      xcd_units, points, idx, out);
   return hipGetLastError();

@@ -236,45 +236,36 @@ __global__ __launch_bounds__(256) void csr_sum_rows_kernel(int b, int n, int c,
   }
 }
 
-// Lazily grown internal workspace for the reference-shaped grad entry points, which have
-// no workspace argument.  Not graph-capture safe on first growth; the *_csr entry points
-// (caller-owned buffers) are what the torch path uses.
-struct InternalWs {
-  void* ptr = nullptr;
-  size_t bytes = 0;
+// Workspace of the reference-shaped grad entry points: [CSR build scratch | offsets (B*N+1)
+// | perm (B*P)].  The *_ws variants take it from the caller; the reference-signature ones
+// (no workspace argument) take it from the stream-ordered allocator on their own stream
+// (hipMallocAsync / hipFreeAsync): no library-global state, safe across threads and
+// streams, and the allocation is ordered with the kernels that use it.
+struct GradWs {
+  size_t csr, off, perm, total;
 };
-InternalWs g_ws;
 
-hipError_t internal_ws(size_t bytes, void** out) {
-  if (g_ws.bytes < bytes) {
-    if (g_ws.ptr) {
-      hipError_t e = hipFree(g_ws.ptr);
-      if (e != hipSuccess) return e;
-      g_ws.ptr = nullptr;
-      g_ws.bytes = 0;
-    }
-    hipError_t e = hipMalloc(&g_ws.ptr, bytes);
-    if (e != hipSuccess) return e;
-    g_ws.bytes = bytes;
-  }
-  *out = g_ws.ptr;
+hipError_t grad_ws_layout(int b, int n, int p, GradWs* L) {
+  CsrLayout C;
+  hipError_t e = csr_layout(b, n, p, &C);
+  if (e != hipSuccess) return e;
+  L->csr = C.total;
+  L->off = align256(sizeof(int) * ((size_t)b * n + 1));
+  L->perm = align256(sizeof(int) * (size_t)b * p);
+  L->total = L->csr + L->off + L->perm;
   return hipSuccess;
 }
 
-// internal CSR: [workspace | offsets (B*N+1) | perm (B*P)]
-hipError_t internal_csr(int b, int n, int p, const int* idx, hipStream_t st, int** offsets,
-                        int** perm) {
-  CsrLayout L;
-  hipError_t e = csr_layout(b, n, p, &L);
+// builds the CSR of idx (B,P) over [0,N) inside ws; -> offsets / perm pointers into ws
+hipError_t ws_csr(int b, int n, int p, const int* idx, void* ws, size_t ws_bytes, hipStream_t st,
+                  int** offsets, int** perm) {
+  GradWs L;
+  hipError_t e = grad_ws_layout(b, n, p, &L);
   if (e != hipSuccess) return e;
-  const size_t off_bytes = align256(sizeof(int) * ((size_t)b * n + 1));
-  const size_t perm_bytes = align256(sizeof(int) * (size_t)b * p);
-  void* ws = nullptr;
-  e = internal_ws(L.total + off_bytes + perm_bytes, &ws);
-  if (e != hipSuccess) return e;
-  *offsets = (int*)((char*)ws + L.total);
-  *perm = (int*)((char*)ws + L.total + off_bytes);
-  return csr_build(b, n, p, idx, ws, L.total, *offsets, *perm, st);
+  if (!ws || ws_bytes < L.total) return hipErrorInvalidValue;
+  *offsets = (int*)((char*)ws + L.csr);
+  *perm = (int*)((char*)ws + L.csr + L.off);
+  return csr_build(b, n, p, idx, ws, L.csr, *offsets, *perm, st);
 }
 
 }  // namespace
@@ -305,12 +296,11 @@ KDPC_API int kdpc_csr_sum_channels(int b, int c, int n, int p, const float* src,
   if (total == 0) return (int)hipSuccess;
   KDPC_CHECK_ARG(dst && offsets && (p == 0 || (src && perm)));
   if (p > 0 && (size_t)p * sizeof(float) <= kSumRowLdsBytes && c <= 65535 && b <= 65535) {
-    static bool attr = false;
-    if (!attr) {
-      hipFuncSetAttribute((const void*)csr_sum_cm_lds_kernel,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, kSumRowLdsBytes);
-      attr = true;
-    }
+    // once per process (thread-safe static initialisation)
+    static const hipError_t attr = hipFuncSetAttribute(
+        (const void*)csr_sum_cm_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+        kSumRowLdsBytes);
+    if (attr != hipSuccess) return (int)attr;
     hipLaunchKernelGGL(csr_sum_cm_lds_kernel, dim3(c, b), dim3(256), (size_t)p * sizeof(float),
                        (hipStream_t)stream, c, n, p, src, offsets, perm, dst);
     KDPC_RETURN_LAUNCH();
@@ -376,17 +366,82 @@ KDPC_API int kdpc_group_rows_grad_csr(int b, int n, int c, const float* grad_out
 }
 
 // ------------------------------------------- reference-shaped grad entry points (no CSR arg)
-// Reference: gather_points_grad_wrapper(b, c, n, npoints, grad_out, idx, grad_points)
-KDPC_API int kdpc_gather_points_grad(int b, int c, int n, int npoints, const float* grad_out,
-                                     const int* idx, float* grad_points, void* stream) {
+KDPC_API size_t kdpc_grad_workspace_bytes(int b, int n, int p) {
+  if (b <= 0 || n <= 0 || p <= 0) return 0;
+  GradWs L;
+  return grad_ws_layout(b, n, p, &L) == hipSuccess ? L.total : 0;
+}
+
+KDPC_API int kdpc_gather_points_grad_ws(int b, int c, int n, int npoints, const float* grad_out,
+                                        const int* idx, float* grad_points, void* workspace,
+                                        size_t workspace_bytes, void* stream) {
   KDPC_CHECK_ARG(b >= 0 && c >= 0 && n > 0 && npoints >= 0);
   if ((long long)b * c * n == 0) return (int)hipSuccess;
   hipStream_t st = (hipStream_t)stream;
   if (npoints == 0) return (int)hipMemsetAsync(grad_points, 0, sizeof(float) * b * c * n, st);
+  KDPC_CHECK_ARG(grad_out && idx && grad_points);
   int *offsets, *perm;
-  hipError_t e = internal_csr(b, n, npoints, idx, st, &offsets, &perm);
+  hipError_t e = ws_csr(b, n, npoints, idx, workspace, workspace_bytes, st, &offsets, &perm);
   if (e != hipSuccess) return (int)e;
   return kdpc_csr_sum_channels(b, c, n, npoints, grad_out, offsets, perm, grad_points, stream);
+}
+
+KDPC_API int kdpc_group_points_grad_ws(int b, int c, int n, int npoints, int nsample,
+                                       const float* grad_out, const int* idx, float* grad_points,
+                                       void* workspace, size_t workspace_bytes, void* stream) {
+  KDPC_CHECK_ARG(b >= 0 && c >= 0 && n > 0 && npoints >= 0 && nsample >= 0);
+  if ((long long)b * c * n == 0) return (int)hipSuccess;
+  hipStream_t st = (hipStream_t)stream;
+  const int p = npoints * nsample;
+  if (p == 0) return (int)hipMemsetAsync(grad_points, 0, sizeof(float) * b * c * n, st);
+  KDPC_CHECK_ARG(grad_out && idx && grad_points);
+  int *offsets, *perm;
+  hipError_t e = ws_csr(b, n, p, idx, workspace, workspace_bytes, st, &offsets, &perm);
+  if (e != hipSuccess) return (int)e;
+  return kdpc_csr_sum_channels(b, c, n, p, grad_out, offsets, perm, grad_points, stream);
+}
+
+KDPC_API int kdpc_three_interpolate_grad_ws(int b, int c, int n, int m, const float* grad_out,
+                                            const int* idx, const float* weight,
+                                            float* grad_points, void* workspace,
+                                            size_t workspace_bytes, void* stream) {
+  KDPC_CHECK_ARG(b >= 0 && c >= 0 && n >= 0 && m > 0);
+  if ((long long)b * c * m == 0) return (int)hipSuccess;
+  hipStream_t st = (hipStream_t)stream;
+  if (n == 0) return (int)hipMemsetAsync(grad_points, 0, sizeof(float) * b * c * m, st);
+  KDPC_CHECK_ARG(grad_out && idx && weight && grad_points);
+  int *offsets, *perm;
+  hipError_t e = ws_csr(b, m, n * 3, idx, workspace, workspace_bytes, st, &offsets, &perm);
+  if (e != hipSuccess) return (int)e;
+  return kdpc_three_interpolate_grad_csr(b, c, n, m, grad_out, weight, offsets, perm, grad_points,
+                                         stream);
+}
+
+namespace {
+// run fn(workspace, bytes) with a stream-ordered temporary of `bytes` on st
+template <class F>
+int with_stream_ws(size_t bytes, hipStream_t st, F fn) {
+  void* ws = nullptr;
+  hipError_t e = hipMallocAsync(&ws, bytes, st);
+  if (e != hipSuccess) return (int)e;
+  const int r = fn(ws, bytes);
+  e = hipFreeAsync(ws, st);
+  return r != 0 ? r : (int)e;
+}
+}  // namespace
+
+// Reference: gather_points_grad_wrapper(b, c, n, npoints, grad_out, idx, grad_points)
+KDPC_API int kdpc_gather_points_grad(int b, int c, int n, int npoints, const float* grad_out,
+                                     const int* idx, float* grad_points, void* stream) {
+  KDPC_CHECK_ARG(b >= 0 && c >= 0 && n > 0 && npoints >= 0);
+  if ((long long)b * c * n * npoints == 0)
+    return kdpc_gather_points_grad_ws(b, c, n, npoints, grad_out, idx, grad_points, nullptr, 0,
+                                      stream);
+  return with_stream_ws(kdpc_grad_workspace_bytes(b, n, npoints), (hipStream_t)stream,
+                        [&](void* ws, size_t nb) {
+                          return kdpc_gather_points_grad_ws(b, c, n, npoints, grad_out, idx,
+                                                            grad_points, ws, nb, stream);
+                        });
 }
 
 // Reference: group_points_grad_wrapper(b, c, n, npoints, nsample, grad_out, idx, grad_points)
@@ -394,14 +449,15 @@ KDPC_API int kdpc_group_points_grad(int b, int c, int n, int npoints, int nsampl
                                     const float* grad_out, const int* idx, float* grad_points,
                                     void* stream) {
   KDPC_CHECK_ARG(b >= 0 && c >= 0 && n > 0 && npoints >= 0 && nsample >= 0);
-  if ((long long)b * c * n == 0) return (int)hipSuccess;
-  hipStream_t st = (hipStream_t)stream;
-  const int p = npoints * nsample;
-  if (p == 0) return (int)hipMemsetAsync(grad_points, 0, sizeof(float) * b * c * n, st);
-  int *offsets, *perm;
-  hipError_t e = internal_csr(b, n, p, idx, st, &offsets, &perm);
-  if (e != hipSuccess) return (int)e;
-  return kdpc_csr_sum_channels(b, c, n, p, grad_out, offsets, perm, grad_points, stream);
+  const long long p = (long long)npoints * nsample;
+  if ((long long)b * c * n * p == 0)
+    return kdpc_group_points_grad_ws(b, c, n, npoints, nsample, grad_out, idx, grad_points,
+                                     nullptr, 0, stream);
+  return with_stream_ws(kdpc_grad_workspace_bytes(b, n, (int)p), (hipStream_t)stream,
+                        [&](void* ws, size_t nb) {
+                          return kdpc_group_points_grad_ws(b, c, n, npoints, nsample, grad_out,
+                                                           idx, grad_points, ws, nb, stream);
+                        });
 }
 
 // Reference: three_interpolate_grad_wrapper(b, c, n, m, grad_out, idx, weight, grad_points)
@@ -409,12 +465,12 @@ KDPC_API int kdpc_three_interpolate_grad(int b, int c, int n, int m, const float
                                          const int* idx, const float* weight, float* grad_points,
                                          void* stream) {
   KDPC_CHECK_ARG(b >= 0 && c >= 0 && n >= 0 && m > 0);
-  if ((long long)b * c * m == 0) return (int)hipSuccess;
-  hipStream_t st = (hipStream_t)stream;
-  if (n == 0) return (int)hipMemsetAsync(grad_points, 0, sizeof(float) * b * c * m, st);
-  int *offsets, *perm;
-  hipError_t e = internal_csr(b, m, n * 3, idx, st, &offsets, &perm);
-  if (e != hipSuccess) return (int)e;
-  return kdpc_three_interpolate_grad_csr(b, c, n, m, grad_out, weight, offsets, perm, grad_points,
-                                         stream);
+  if ((long long)b * c * m * n == 0)
+    return kdpc_three_interpolate_grad_ws(b, c, n, m, grad_out, idx, weight, grad_points,
+                                          nullptr, 0, stream);
+  return with_stream_ws(kdpc_grad_workspace_bytes(b, m, n * 3), (hipStream_t)stream,
+                        [&](void* ws, size_t nb) {
+                          return kdpc_three_interpolate_grad_ws(b, c, n, m, grad_out, idx, weight,
+                                                                grad_points, ws, nb, stream);
+                        });
 }

@@ -61,13 +61,13 @@ class FpsPrefetch:
 
     def __init__(self):
         self.stream = None
-        self.key = None
+        self.inputs = None  # strong references: identity, not a reusable address, is the key
         self.fps = None
         self.event = None
 
     @staticmethod
-    def _key(pos1, pos2):
-        return (pos1.data_ptr(), pos2.data_ptr(), tuple(pos1.shape), pos1._version, pos2._version)
+    def _versions(pos1, pos2):
+        return (pos1._version, pos2._version)
 
     def launch(self, model, pos1, pos2):
         if not pos1.is_cuda:
@@ -79,17 +79,25 @@ class FpsPrefetch:
             self.fps = _core(model).precompute_fps(pos1, pos2)
             self.event = torch.cuda.Event()
             self.event.record(self.stream)
-        self.key = self._key(pos1, pos2)
+        # the side stream reads pos1/pos2: keep the caching allocator from handing their
+        # blocks to the main stream before the FPS chain has finished with them
+        pos1.record_stream(self.stream)
+        pos2.record_stream(self.stream)
+        self.inputs = (pos1, pos2, self._versions(pos1, pos2))
 
     def take(self, pos1, pos2):
-        """The prefetched indices if they were computed for exactly these inputs."""
-        if self.fps is None or self.key != self._key(pos1, pos2):
+        """The prefetched indices if they were computed for exactly these (unmodified)
+        tensor objects."""
+        if self.fps is None or self.inputs is None:
+            return None
+        p1, p2, ver = self.inputs
+        if p1 is not pos1 or p2 is not pos2 or ver != self._versions(pos1, pos2):
             return None
         cur = torch.cuda.current_stream(pos1.device)
         cur.wait_event(self.event)
         for t in self.fps:
             t.record_stream(cur)
-        fps, self.fps, self.key = self.fps, None, None
+        fps, self.fps, self.inputs = self.fps, None, None
         return fps
 
 
@@ -182,6 +190,9 @@ class GraphedStep:
     copied into static buffers before each replay.  Warm-up iterations run eagerly on a side
     stream (they allocate lazily-initialised state: optimizer moments, cached attributes)."""
 
+    drop_warmup_graph = True  # diagnostics seam (tools/graph_diag.py)
+    capture_on_side_stream = False
+
     def __init__(self, loss_fn, params, optimizer, example_inputs, warmup=3):
         self.loss_fn = loss_fn
         self.opt = optimizer
@@ -191,25 +202,31 @@ class GraphedStep:
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
+            loss = None
             for _ in range(warmup):
                 self.opt.zero_grad(set_to_none=True)
                 loss = self.loss_fn(*self.static)
                 loss.backward()
                 self._allreduce_eager()
                 self.opt.step()
+            # drop the last warm-up graph: while it lives, the parameters' AccumulateGrad
+            # nodes (created on this side stream) would be reused by the captured backward
+            if self.drop_warmup_graph:
+                del loss
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         # graph A: forward + backward; .grad tensors are allocated inside (static addresses)
         self.opt.zero_grad(set_to_none=True)
         self.graph_a = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph_a):
+        kw = {"stream": side} if self.capture_on_side_stream else {}
+        with torch.cuda.graph(self.graph_a, **kw):
             self.loss = self.loss_fn(*self.static)
             self.loss.backward()
             self.grads = [p.grad for p in self.params if p.grad is not None]
             self.flat = torch.cat([g.reshape(-1) for g in self.grads]) if self.world > 1 else None
         # graph B: unpack + optimizer step
         self.graph_b = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph_b, pool=self.graph_a.pool()):
+        with torch.cuda.graph(self.graph_b, pool=self.graph_a.pool(), **kw):
             if self.world > 1:
                 self._unpack()
             self.opt.step()

@@ -19,6 +19,11 @@ _SIGNATURES = {
     "kdpc_opt_n_threads": [_c_int],
     "kdpc_gather_points": [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp],
     "kdpc_gather_points_grad": [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp],
+    "kdpc_grad_workspace_bytes": [_c_int, _c_int, _c_int],
+    "kdpc_gather_points_grad_ws": [_c_int] * 4 + [_vp] * 4 + [_c_size, _vp],
+    "kdpc_group_points_grad_ws": [_c_int] * 5 + [_vp] * 4 + [_c_size, _vp],
+    "kdpc_three_interpolate_grad_ws": [_c_int] * 4 + [_vp] * 5 + [_c_size, _vp],
+    "kdpc_build_id": [],
     "kdpc_ball_query": [_c_int, _c_int, _c_int, _c_float, _c_int, _vp, _vp, _vp, _vp],
     "kdpc_group_points": [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp],
     "kdpc_group_points_grad": [_c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp],
@@ -64,7 +69,8 @@ _SIGNATURES = {
     "kdpc_weightnet_bwd_workspace_bytes": [],
     "kdpc_weightnet_bwd": [_c_int] * 4 + [_vp] * 13 + [_c_size, _vp],
 }
-_RESTYPES = {"kdpc_csr_workspace_bytes": _c_size, "kdpc_cost_volume_bwd_workspace_bytes": _c_size,
+_RESTYPES = {"kdpc_build_id": ctypes.c_char_p, "kdpc_grad_workspace_bytes": _c_size,
+             "kdpc_csr_workspace_bytes": _c_size, "kdpc_cost_volume_bwd_workspace_bytes": _c_size,
              "kdpc_pointconv_fwd_workspace_bytes": _c_size,
              "kdpc_pointconv_bwd_workspace_bytes": _c_size,
              "kdpc_weightnet_bwd_workspace_bytes": _c_size,
@@ -94,8 +100,23 @@ def load_library(path=LIB_PATH):
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = _RESTYPES.get(name, _c_int)
+    _check_build_id(lib, path)
     _lib = lib
     return lib
+
+
+def _check_build_id(lib, path):
+    """The library must have been built from the sources next to it (build_native.py embeds
+    their hash): a stale binary is refused, so no run uses kernels its tree does not hold.
+    Skipped when the sources are not shipped (KDPC_LIB pointing at an installed library)."""
+    if not os.path.isdir(os.path.join(_HERE, "csrc")) or os.environ.get("KDPC_LIB"):
+        return
+    import build_native
+    want = build_native.source_id()
+    got = lib.kdpc_build_id().decode()
+    if got != want:
+        raise KdpcError(f"{path} was built from other sources (build id {got[:12]}, sources "
+                        f"{want[:12]}); rebuild with `python kd-pointcloud_amd/build_native.py`")
 
 
 def _check(status, name):

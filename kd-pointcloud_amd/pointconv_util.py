@@ -370,7 +370,9 @@ class _PointConvLayer(torch.autograd.Function):
         dxyz, dfeats, dcenter, dwt, dwl = _nat.pointconv_bwd(
             xyz, center, feats, idx, wt, wl, gy, _nat.csr_of(idx, xyz.shape[1]),
             need_xyz=ctx.needs_input_grad[0])
-        dbias = gy.view(-1, gy.shape[-1]).sum(0) if ctx.needs_input_grad[6] else None
+        # fixed-order HIP column sum (torch's tall dim-0 reduction gave wrong sums when
+        # replayed from a captured graph, tools/graph_diag.py)
+        dbias = _nat.colsum(gy.view(-1, gy.shape[-1])) if ctx.needs_input_grad[6] else None
         return (dxyz, dcenter if ctx.needs_input_grad[1] else None, dfeats, None, dwt, dwl, dbias)
 
 

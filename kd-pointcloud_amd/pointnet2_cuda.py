@@ -4,7 +4,8 @@ The nine `*_wrapper` functions keep the reference's argument lists and in-place 
 (caller-allocated GPU tensors), so the reference's own pointnet2_utils.py runs unchanged on
 top of them.  Each forwards to the matching C-ABI entry point in include/kdpc.h.
 Deterministic backward: *_grad_wrapper overwrites grad_points (the reference accumulated
-into a caller-zeroed buffer with atomics; the result for a zeroed buffer is the same sum).
+into a caller-zeroed buffer with atomics; the result for a zeroed buffer is the same sum);
+their scratch comes from the torch caching allocator (the C ABI's *_grad_ws entry points).
 """
 import kdpc_native as _nat
 
@@ -35,9 +36,19 @@ def group_points_wrapper(b, c, n, npoints, nsample, points, idx, out):
     return 1
 
 
+def _ws(n, p, like):
+    """Scratch of a *_grad_ws call from the torch caching allocator (stream-ordered with the
+    op, graph-capture safe)."""
+    import torch
+    nbytes = _nat.load_library().kdpc_grad_workspace_bytes(n[0], n[1], p)
+    ws = torch.empty((max(int(nbytes), 1),), dtype=torch.uint8, device=like.device)
+    return ws.data_ptr(), nbytes
+
+
 def group_points_grad_wrapper(b, c, n, npoints, nsample, grad_out, idx, grad_points):
-    _nat._call("kdpc_group_points_grad", b, c, n, npoints, nsample, _f(grad_out, "grad_out"),
-               _i(idx, "idx"), _f(grad_points, "grad_points"), _nat._stream(grad_out))
+    ws, nb = _ws((b, n), npoints * nsample, grad_out)
+    _nat._call("kdpc_group_points_grad_ws", b, c, n, npoints, nsample, _f(grad_out, "grad_out"),
+               _i(idx, "idx"), _f(grad_points, "grad_points"), ws, nb, _nat._stream(grad_out))
     return 1
 
 
@@ -48,8 +59,9 @@ def gather_points_wrapper(b, c, n, npoints, points, idx, out):
 
 
 def gather_points_grad_wrapper(b, c, n, npoints, grad_out, idx, grad_points):
-    _nat._call("kdpc_gather_points_grad", b, c, n, npoints, _f(grad_out, "grad_out"),
-               _i(idx, "idx"), _f(grad_points, "grad_points"), _nat._stream(grad_out))
+    ws, nb = _ws((b, n), npoints, grad_out)
+    _nat._call("kdpc_gather_points_grad_ws", b, c, n, npoints, _f(grad_out, "grad_out"),
+               _i(idx, "idx"), _f(grad_points, "grad_points"), ws, nb, _nat._stream(grad_out))
     return 1
 
 
@@ -70,6 +82,7 @@ def three_interpolate_wrapper(b, c, m, n, points, idx, weight, out):
 
 
 def three_interpolate_grad_wrapper(b, c, n, m, grad_out, idx, weight, grad_points):
-    _nat._call("kdpc_three_interpolate_grad", b, c, n, m, _f(grad_out, "grad_out"),
-               _i(idx, "idx"), _f(weight, "weight"), _f(grad_points, "grad_points"),
+    ws, nb = _ws((b, m), 3 * n, grad_out)
+    _nat._call("kdpc_three_interpolate_grad_ws", b, c, n, m, _f(grad_out, "grad_out"),
+               _i(idx, "idx"), _f(weight, "weight"), _f(grad_points, "grad_points"), ws, nb,
                _nat._stream(grad_out))

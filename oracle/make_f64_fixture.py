@@ -11,8 +11,9 @@ restatement on the (exactly gathered) fp32 coordinates, and stores the float64 g
 sums: the test then allows the GPU build the reference's own fp32 error |g32 - g64| per
 parameter.
 
-    python oracle/make_f64_fixture.py    -> tests/golden/model_knntrace_n2048_f64.npz
+    python oracle/make_f64_fixture.py [--n 8192]  -> tests/golden/model_knntrace_n{n}_f64.npz
 """
+import argparse
 import os
 import sys
 
@@ -22,9 +23,10 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 import make_fixtures as MF  # noqa: E402
+from gradproj import projection  # noqa: E402
 
 
-def main(n=2048):
+def main(n=2048, full_grads=None, dtype=torch.float64):
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     R = MF.setup_reference()
     g = np.load(os.path.join(MF.GOLDEN, f"model_knntrace_n{n}.npz"))
@@ -52,13 +54,13 @@ def main(n=2048):
     mods = (R.pcu, sys.modules["pointconv_util2"])
     orig = {m: m.knn_point for m in mods}
     f32 = torch.cuda.FloatTensor
-    torch.cuda.FloatTensor = lambda *s: torch.empty(*s, dtype=torch.float64)
+    torch.cuda.FloatTensor = lambda *s: torch.empty(*s, dtype=dtype)
     for m in mods:
         m.knn_point = replay
     try:
-        pos1, pos2, flow = (torch.from_numpy(g[k]).double() for k in ("pos1", "pos2", "flow"))
-        teacher = MF._synth(R.teacher.PointConvBidirection(), seed=1).double().eval()
-        student = MF._synth(R.student.PointConvBidirection(), seed=2).double().train()
+        pos1, pos2, flow = (torch.from_numpy(g[k]).to(dtype) for k in ("pos1", "pos2", "flow"))
+        teacher = MF._synth(R.teacher.PointConvBidirection(), seed=1).to(dtype).eval()
+        student = MF._synth(R.student.PointConvBidirection(), seed=2).to(dtype).train()
         with torch.no_grad():
             t_out = teacher(pos1, pos2, pos1, pos2)
         s_out = student(pos1, pos2, pos1, pos2)
@@ -72,14 +74,25 @@ def main(n=2048):
         torch.cuda.FloatTensor = f32
         stub.furthest_point_sampling_wrapper = fps32
     assert pos["i"] == len(calls), (pos["i"], len(calls))
+    named = [(k, p) for k, p in student.named_parameters()]
+    proj = [projection(k, p.grad) for k, p in named]
     out = {
         "grad_sum_f64": np.array([float(p.grad.sum()) if p.grad is not None else 0.0
-                                  for _, p in student.named_parameters()]),
+                                  for _, p in named]),
+        # two fixed random projections per parameter: sensitive to elementwise errors that
+        # cancel in the plain sum (tests compare sum_i g_i r_i against sum_i |g_i r_i|)
+        "grad_proj_f64": np.array([p[0] for p in proj]),
+        "grad_absproj_f64": np.array([p[1] for p in proj]),
         "kd_f64": kd.detach().numpy(),
         "replay_worst": np.array(pos["worst"]),
     }
     for i in range(4):
         out[f"s_flow{i}_f64"] = flows[i].detach().numpy()
+    if full_grads:  # every gradient element (diagnostics: tools/grad_gap.py), not committed
+        np.savez_compressed(full_grads, **{k: p.grad.numpy() for k, p in student.named_parameters()
+                                           if p.grad is not None})
+        print("wrote", full_grads)
+        return
     path = os.path.join(MF.GOLDEN, f"model_knntrace_n{n}_f64.npz")
     np.savez_compressed(path, **out)
     d = np.abs(out["grad_sum_f64"] - g["grad_sum"]) / (g["grad_abs"] + 1e-12)
@@ -89,4 +102,9 @@ def main(n=2048):
 
 
 if __name__ == "__main__":
-    main()
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=2048)
+    ap.add_argument("--full-grads", default=None, help="dump every gradient element here")
+    ap.add_argument("--f32", action="store_true", help="run the reference in float32 instead")
+    a = ap.parse_args()
+    main(a.n, a.full_grads, torch.float32 if a.f32 else torch.float64)

@@ -224,3 +224,31 @@ def test_pointnet2_utils_autograd(nat):
     d, i = U.three_nn(_t(_cloud(1, 200, 1)), _t(_cloud(1, 50, 2)))
     d2, i2 = O.three_nn(_cloud(1, 200, 1), _cloud(1, 50, 2))
     np.testing.assert_allclose(d.cpu().numpy(), np.sqrt(d2), rtol=1e-6)
+
+
+def test_knn_config5_sampled_vs_oracle(nat):
+    """BASELINE configs[4]: K=32, N=65536 references per frame, B=4, queries = a second
+    65536-point frame.  The full result is computed on the GPU (seeded culled scan); ~512
+    queries per frame are checked bit-exactly (indices and distances) against the oracle's
+    brute-force expanded-form scan."""
+    b, n, k = 4, 65536, 32
+    ref = _cloud(b, n, seed=505)
+    qry = _cloud(b, n, seed=506)
+    assert nat.load_library().kdpc_knn_workspace_bytes(b, n, n) > 0  # the culled scan
+    idx, dist = nat.knn_point(k, _t(ref), _t(qry), return_dist=True)
+    idx, dist = idx.cpu().numpy(), dist.cpu().numpy()
+    rng = np.random.default_rng(5)
+    rows = np.sort(rng.choice(n, 512, replace=False))
+    idx_ref, dist_ref = O.knn(k, ref, qry[:, rows])
+    np.testing.assert_array_equal(idx[:, rows], idx_ref)
+    np.testing.assert_array_equal(dist[:, rows].view(np.int32), dist_ref.view(np.int32))
+
+
+def test_ball_query_config2_size(nat):
+    """BASELINE configs[1] sizes: B=8, N=8192 points, M=2048 FPS centres, r=0.5, K=16 --
+    bit-exact vs the oracle (first K hits by index, padded with the first hit)."""
+    xyz = _cloud(8, 8192, seed=808)
+    fidx, _ = O.furthest_point_sample(xyz, 2048)
+    centres = np.take_along_axis(xyz, fidx[..., None].astype(np.int64), 1)
+    out = nat.ball_query(0.5, 16, _t(xyz), _t(centres)).cpu().numpy()
+    np.testing.assert_array_equal(out, O.ball_query(0.5, 16, xyz, centres))

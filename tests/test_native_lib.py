@@ -81,3 +81,24 @@ def test_ctypes_signatures_match_header():
                 assert t is ctypes.c_float, (name, p)
             else:
                 assert t is ctypes.c_int, (name, p)
+
+
+def test_library_built_from_these_sources():
+    """kdpc_build_id() is the hash of the sources next to the library: the loader refuses a
+    stale binary (a changed kernel source without a rebuild)."""
+    import build_native
+    lib = kdpc_native.load_library()
+    assert lib.kdpc_build_id().decode() == build_native.source_id()
+
+
+def test_stale_library_is_refused(tmp_path):
+    import build_native
+    import shutil
+    csrc = tmp_path / "csrc"
+    shutil.copytree(build_native.CSRC, csrc)
+    (tmp_path / "include").mkdir()
+    shutil.copy(os.path.join(ROOT, "include", "kdpc.h"), tmp_path / "include")
+    assert build_native.source_id(str(csrc), str(tmp_path)) == build_native.source_id()
+    with open(csrc / "fps.hip", "a") as f:
+        f.write("\n// edited\n")
+    assert build_native.source_id(str(csrc), str(tmp_path)) != build_native.source_id()
