@@ -22,6 +22,8 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "build")
 LIB = os.path.join(HERE, "lib", "libkdpc_hip.so")
+TORCH_OPS_SRC = os.path.join(HERE, "torch_ops", "kdpc_torch_ops.cpp")
+TORCH_OPS_LIB = os.path.join(HERE, "lib", "libkdpc_torch.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("KDPC_ARCH", "gfx950")
 
@@ -75,6 +77,51 @@ def _compile(src, headers_digest, tool):
     return obj
 
 
+def _torch_flags():
+    """Compile / link flags for a host-only op library against this torch-ROCm install."""
+    import torch
+    tdir = os.path.dirname(torch.__file__)
+    inc = [os.path.join(tdir, "include"), os.path.join(tdir, "include", "torch", "csrc", "api",
+                                                       "include")]
+    abi = int(torch.compiled_with_cxx11_abi())
+    cflags = ["-O2", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall",
+              "-Wno-unused-variable", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+              f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-I", os.path.join(ROOT, "include"),
+              "-I", "/opt/rocm/include"] + [f for i in inc for f in ("-isystem", i)]
+    ldflags = ["-shared", "-L", os.path.join(tdir, "lib"), "-lc10", "-lc10_hip", "-ltorch",
+               "-ltorch_cpu", "-ltorch_hip", "-lamdhip64",
+               "-L", os.path.dirname(LIB), "-lkdpc_hip",
+               "-Wl,-rpath,$ORIGIN", "-Wl,-rpath," + os.path.join(tdir, "lib")]
+    return cflags, ldflags, torch.__version__
+
+
+def build_torch_ops(verbose=True):
+    """torch.ops.kdpc (torch_ops/kdpc_torch_ops.cpp) -> lib/libkdpc_torch.so, linked to
+    libkdpc_hip.so.  Rebuilt when the op source, the C ABI header, the flags, the torch
+    version or the HIP library's sources change."""
+    cflags, ldflags, tv = _torch_flags()
+    h = hashlib.sha256()
+    for p in (TORCH_OPS_SRC, os.path.join(ROOT, "include", "kdpc.h")):
+        with open(p, "rb") as f:
+            h.update(f.read())
+    h.update(" ".join(cflags + ldflags).encode() + tv.encode() + source_id().encode())
+    key = h.hexdigest()
+    stamp = TORCH_OPS_LIB + ".inputs"
+    if os.path.exists(TORCH_OPS_LIB) and os.path.exists(stamp) and open(stamp).read() == key:
+        return TORCH_OPS_LIB
+    tmp = TORCH_OPS_LIB + ".tmp"
+    r = subprocess.run(["g++"] + cflags + [TORCH_OPS_SRC, "-o", tmp] + ldflags,
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"torch op library failed to build:\n{r.stderr[-6000:]}")
+    os.replace(tmp, TORCH_OPS_LIB)
+    with open(stamp, "w") as f:
+        f.write(key)
+    if verbose:
+        print(f"built {TORCH_OPS_LIB}")
+    return TORCH_OPS_LIB
+
+
 def build(verbose=True):
     os.makedirs(OBJ, exist_ok=True)
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
@@ -110,6 +157,7 @@ def build(verbose=True):
             os.remove(o)
     if verbose:
         print(f"built {LIB} (sources {sid[:12]})")
+    build_torch_ops(verbose)
     return LIB
 
 

@@ -35,6 +35,37 @@ def _chunks(rows, out_elems):
     return c
 
 
+class _FixedSum(Function):
+    """x.sum(dim) with the HIP fixed-order column sum (csrc/colsum.hip): bitwise
+    reproducible, and safe inside a captured HIP graph.  torch's multi-block ("global")
+    reductions -- a few large outputs over many elements, e.g. a loss summed over all points
+    -- returned wrong values when replayed from a captured graph on this ROCm torch build
+    (tools/graph_diag.py, round 2), so the step's large loss reductions use this."""
+
+    @staticmethod
+    def forward(ctx, x, dim):
+        ctx.shape, ctx.dim = x.shape, dim
+        xt = x.movedim(dim, 0)
+        rest = xt.shape[1:]
+        return _colsum(xt.reshape(xt.shape[0], -1).contiguous()).view(rest)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.unsqueeze(ctx.dim).expand(ctx.shape), None
+
+
+def fixed_sum(x, dim=None):
+    """Deterministic sum over `dim` (all elements when None) of a GPU tensor; torch's sum
+    elsewhere.  Same value up to summation order."""
+    if not x.is_cuda or x.dtype != torch.float32:
+        return x.sum() if dim is None else x.sum(dim)
+    if dim is None:
+        n = x.numel()
+        cols = 64 if n % 64 == 0 and n >= 4096 else 1
+        return _FixedSum.apply(x.reshape(-1, cols), 0).sum()
+    return _FixedSum.apply(x, dim % x.dim())
+
+
 def splitk_tn(a, b):
     """a (R,O), b (R,I) -> a^T b (O,I) with the R reduction split over chunks."""
     R, O = a.shape

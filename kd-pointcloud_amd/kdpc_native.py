@@ -1,15 +1,23 @@
-"""ctypes binding of libkdpc_hip.so (the C ABI in include/kdpc.h) for torch-ROCm tensors.
+"""Python face of the gfx950 HIP kernels for torch-ROCm tensors.
 
-Every op here runs the gfx950 HIP kernels on the tensors' device and the current torch
-stream.  There is no CPU path: a missing library, a CPU tensor or a wrong dtype raises.
+Two layers over libkdpc_hip.so (the C ABI in include/kdpc.h):
+  * torch.ops.kdpc (lib/libkdpc_torch.so, torch_ops/kdpc_torch_ops.cpp): every C entry
+    point registered as a torch operator with a schema, TORCH_CHECKed inputs, outputs and
+    scratch from the caching allocator, launched on the current torch stream.  Every op
+    function below goes through it;
+  * a ctypes binding of the bare C ABI (load_library, _SIGNATURES), used by the C-ABI
+    tests (export / arity / argument validation) and by build-id verification.
+There is no CPU path: a missing library or a CPU tensor raises.
 """
 import ctypes
+import functools
 import os
 
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KDPC_LIB", os.path.join(_HERE, "lib", "libkdpc_hip.so"))
+OPS_PATH = os.path.join(os.path.dirname(LIB_PATH), "libkdpc_torch.so")
 
 _c_int, _c_float, _c_size, _vp = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 
@@ -170,7 +178,7 @@ def set_launch_timer(timer):
 
 
 def _call(name, *args, work=None):
-    """Invoke a C entry point; `work` = (algorithmic bytes, flops) for the launch timer."""
+    """Invoke a C entry point through ctypes (C-ABI tests); `work` as for _op."""
     lib = load_library()
     t = _timer
     if t is not None and name in t.names:
@@ -185,104 +193,111 @@ def _call(name, *args, work=None):
     _check(getattr(lib, name)(*args), name)
 
 
+_ops = None
+
+
+def load_ops():
+    """torch.ops.kdpc, loaded once (after the C library's build-id check)."""
+    global _ops
+    if _ops is None:
+        load_library()
+        if not os.path.exists(OPS_PATH):
+            raise KdpcError(f"kd-pointcloud_amd torch op library not found at {OPS_PATH}; build "
+                            "it with `python kd-pointcloud_amd/build_native.py`")
+        torch.ops.load_library(OPS_PATH)
+        _ops = torch.ops.kdpc
+    return _ops
+
+
+def _gpu(t, name):
+    if not t.is_cuda:
+        raise KdpcError(f"{name} must be a GPU (HIP) tensor: kd-pointcloud_amd has no CPU path")
+    return t
+
+
+def _op(entry, op, *args, work=None):
+    """Run torch.ops.kdpc.<op>; `entry` is the C entry point it launches (the unit the
+    bench's live roofline brackets), `work` = (algorithmic bytes, flops) of the launch."""
+    fn = getattr(_ops or load_ops(), op)
+    t = _timer
+    if t is not None and entry in t.names:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = fn(*args)
+        e1.record()
+        nb, fl = work if work is not None else (0.0, 0.0)
+        t.records.append((entry, e0, e1, float(nb), float(fl)))
+        return out
+    return fn(*args)
+
+
 # ------------------------------------------------------------------------------ ops
 def furthest_point_sampling(xyz, npoint, temp=None):
-    """xyz (B,N,3) f32 -> idx (B,npoint) i32.  temp: optional (B,N) scratch (1e10-filled)."""
-    B, N, _ = xyz.shape
-    idx = torch.empty((B, npoint), dtype=torch.int32, device=xyz.device)
+    """xyz (B,N,3) f32 -> idx (B,npoint) i32.  temp: optional (B,N) scratch (1e10-filled),
+    left holding the final min-distances (the reference wrapper's in-place contract)."""
+    B, N, _ = _gpu(xyz, "xyz").shape
+    work = (B * (12 * N + 8 * N + 4 * npoint), B * N * npoint * 8)
     if temp is None:
-        temp = torch.full((B, N), 1e10, dtype=torch.float32, device=xyz.device)
-    _call("kdpc_furthest_point_sampling", B, N, npoint, _dev(xyz, torch.float32, "xyz"),
-          _dev(temp, torch.float32, "temp"), _dev(idx, torch.int32, "idx"), _stream(xyz),
-          work=(B * (12 * N + 8 * N + 4 * npoint), B * N * npoint * 8))
+        return _op("kdpc_furthest_point_sampling", "furthest_point_sample", xyz, npoint,
+                   work=work)
+    idx = torch.empty((B, npoint), dtype=torch.int32, device=xyz.device)
+    _op("kdpc_furthest_point_sampling", "furthest_point_sampling_wrapper", B, N, npoint, xyz,
+        temp, idx, work=work)
     return idx
 
 
 def gather_points(points, idx):
     """points (B,C,N), idx (B,M) i32 -> (B,C,M)."""
-    B, C, N = points.shape
-    M = idx.shape[1]
-    out = torch.empty((B, C, M), dtype=torch.float32, device=points.device)
-    _call("kdpc_gather_points", B, C, N, M, _dev(points, torch.float32, "points"),
-          _dev(idx, torch.int32, "idx"), _dev(out, torch.float32, "out"), _stream(points))
-    return out
+    return _op("kdpc_gather_points", "gather_points", _gpu(points, "points"), idx)
 
 
 def ball_query(radius, nsample, xyz, new_xyz):
-    B, N, _ = xyz.shape
-    M = new_xyz.shape[1]
-    idx = torch.empty((B, M, nsample), dtype=torch.int32, device=xyz.device)
-    _call("kdpc_ball_query", B, N, M, float(radius), int(nsample),
-          _dev(new_xyz, torch.float32, "new_xyz"), _dev(xyz, torch.float32, "xyz"),
-          _dev(idx, torch.int32, "idx"), _stream(xyz))
-    return idx
+    return _op("kdpc_ball_query", "ball_query", float(radius), int(nsample), _gpu(xyz, "xyz"),
+               new_xyz)
 
 
 def group_points(points, idx):
     """points (B,C,N), idx (B,S,K) i32 -> (B,C,S,K)."""
-    B, C, N = points.shape
+    B, C, N = _gpu(points, "points").shape
     _, S, K = idx.shape
-    out = torch.empty((B, C, S, K), dtype=torch.float32, device=points.device)
     # SURVEY §8d algorithmic bytes: B*(4CN + 4SK + 4CSK)
-    _call("kdpc_group_points", B, C, N, S, K, _dev(points, torch.float32, "points"),
-          _dev(idx, torch.int32, "idx"), _dev(out, torch.float32, "out"), _stream(points),
-          work=(B * (4 * C * N + 4 * S * K + 4 * C * S * K), 0))
-    return out
+    return _op("kdpc_group_points", "group_points", points, idx,
+               work=(B * (4 * C * N + 4 * S * K + 4 * C * S * K), 0))
 
 
 def three_nn(unknown, known):
     """-> (dist2 (B,N,3) squared, idx (B,N,3) i32)."""
-    B, N, _ = unknown.shape
-    M = known.shape[1]
-    dist2 = torch.empty((B, N, 3), dtype=torch.float32, device=unknown.device)
-    idx = torch.empty((B, N, 3), dtype=torch.int32, device=unknown.device)
-    _call("kdpc_three_nn", B, N, M, _dev(unknown, torch.float32, "unknown"),
-          _dev(known, torch.float32, "known"), _dev(dist2, torch.float32, "dist2"),
-          _dev(idx, torch.int32, "idx"), _stream(unknown))
-    return dist2, idx
+    return _op("kdpc_three_nn", "three_nn", _gpu(unknown, "unknown"), known)
 
 
 def three_interpolate(points, idx, weight):
-    B, C, M = points.shape
-    N = idx.shape[1]
-    out = torch.empty((B, C, N), dtype=torch.float32, device=points.device)
-    _call("kdpc_three_interpolate", B, C, M, N, _dev(points, torch.float32, "points"),
-          _dev(idx, torch.int32, "idx"), _dev(weight, torch.float32, "weight"),
-          _dev(out, torch.float32, "out"), _stream(points))
-    return out
+    return _op("kdpc_three_interpolate", "three_interpolate", _gpu(points, "points"), idx,
+               weight)
 
 
 def knn_point(nsample, xyz, new_xyz, return_dist=False, seeded=True):
     """xyz (B,N,3) refs, new_xyz (B,S,3) queries -> idx (B,S,K) i32 ascending (dist, idx).
     seeded: allow the seeded-threshold scan where it pays (identical results; False forces
     the unseeded scan, for tests)."""
-    B, N, _ = xyz.shape
+    B, N, _ = _gpu(xyz, "xyz").shape
     S = new_xyz.shape[1]
     if nsample > N:
         raise ValueError(f"knn_point: nsample={nsample} > number of points {N}")
-    idx = torch.empty((B, S, nsample), dtype=torch.int32, device=xyz.device)
-    dist = torch.empty((B, S, nsample), dtype=torch.float32, device=xyz.device) if return_dist else None
-    ws_bytes = load_library().kdpc_knn_workspace_bytes(B, N, S) if seeded else 0
-    ws = torch.empty((ws_bytes,), dtype=torch.uint8, device=xyz.device) if ws_bytes else None
-    _call("kdpc_knn_point_ws", B, N, S, int(nsample), _dev(xyz, torch.float32, "xyz"),
-          _dev(new_xyz, torch.float32, "new_xyz"), _dev(idx, torch.int32, "idx"),
-          _dev(dist, torch.float32, "dist") if dist is not None else None,
-          ws.data_ptr() if ws is not None else None, ws_bytes, _stream(xyz),
-          work=(B * (12 * N + 12 * S + 4 * S * nsample * (2 if return_dist else 1)),
-                B * S * N * 8))
-    return (idx, dist) if return_dist else idx
+    work = (B * (12 * N + 12 * S + 4 * S * nsample * (2 if return_dist else 1)), B * S * N * 8)
+    if return_dist:
+        return _op("kdpc_knn_point", "knn_point_dist", int(nsample), xyz, new_xyz, seeded,
+                   work=work)
+    return _op("kdpc_knn_point", "knn_point", int(nsample), xyz, new_xyz, seeded, work=work)
 
 
 def group_rows(points, idx):
     """points (B,N,C), idx (B,P) i32 -> (B,P,C) (point-major row gather)."""
-    B, N, C = points.shape
+    B, N, C = _gpu(points, "points").shape
     P = idx.shape[1]
-    out = torch.empty((B, P, C), dtype=torch.float32, device=points.device)
     # algorithmic bytes (SURVEY §8d): table read once + idx read + rows written
-    _call("kdpc_group_rows", B, N, C, P, _dev(points, torch.float32, "points"),
-          _dev(idx, torch.int32, "idx"), _dev(out, torch.float32, "out"), _stream(points),
-          work=(B * (4 * N * C + 4 * P + 4 * P * C), 0))
-    return out
+    return _op("kdpc_group_rows", "group_rows", points, idx,
+               work=(B * (4 * N * C + 4 * P + 4 * P * C), 0))
 
 
 class Csr:
@@ -290,18 +305,8 @@ class Csr:
     __slots__ = ("offsets", "perm", "n", "p")
 
     def __init__(self, idx2d, n):
-        B, P = idx2d.shape
-        lib = load_library()
-        ws_bytes = lib.kdpc_csr_workspace_bytes(B, n, P)
-        if ws_bytes == 0:
-            raise KdpcError("kdpc_csr_workspace_bytes returned 0 (invalid sizes?)")
-        dev = idx2d.device
-        ws = torch.empty((ws_bytes,), dtype=torch.uint8, device=dev)
-        self.offsets = torch.empty((B * n + 1,), dtype=torch.int32, device=dev)
-        self.perm = torch.empty((B * P,), dtype=torch.int32, device=dev)
-        self.n, self.p = n, P
-        _call("kdpc_csr_build", B, n, P, _dev(idx2d, torch.int32, "idx"), ws.data_ptr(), ws_bytes,
-              self.offsets.data_ptr(), self.perm.data_ptr(), _stream(idx2d))
+        self.offsets, self.perm = _op("kdpc_csr_build", "csr_build", _gpu(idx2d, "idx"), n)
+        self.n, self.p = n, idx2d.shape[1]
 
 
 def batch_prefix(idx, b):
@@ -340,35 +345,22 @@ def csr_of(idx, n):
 def group_rows_grad(grad_out, csr, B, N, C):
     """grad_out (B,P,C) -> (B,N,C) deterministic scatter-add through csr."""
     grad_out = grad_out.contiguous()
-    out = torch.empty((B, N, C), dtype=torch.float32, device=grad_out.device)
     P = grad_out.shape[1]
-    _call("kdpc_group_rows_grad_csr", B, N, C, _dev(grad_out, torch.float32, "grad_out"),
-          csr.offsets.data_ptr(), csr.perm.data_ptr(), _dev(out, torch.float32, "grad_points"),
-          _stream(grad_out), work=(B * (4 * P * C + 4 * P + 4 * N + 4 * N * C), 0))
-    return out
+    return _op("kdpc_group_rows_grad_csr", "group_rows_grad", grad_out.view(B, P, C),
+               csr.offsets, csr.perm, N, work=(B * (4 * P * C + 4 * P + 4 * N + 4 * N * C), 0))
 
 
 def csr_sum_channels(src, csr, B, C, N):
     """src (B,C,P) -> (B,C,N): the backward of gather_points/group_points."""
-    src = src.contiguous()
-    P = src.numel() // max(1, B * C)
-    out = torch.empty((B, C, N), dtype=torch.float32, device=src.device)
-    _call("kdpc_csr_sum_channels", B, C, N, P, _dev(src, torch.float32, "src"),
-          csr.offsets.data_ptr(), csr.perm.data_ptr(), _dev(out, torch.float32, "dst"),
-          _stream(src))
-    return out
+    return _op("kdpc_csr_sum_channels", "csr_sum_channels", src.contiguous(), csr.offsets,
+               csr.perm, B, C, N)
 
 
 def three_interpolate_grad(grad_out, idx, weight, m):
     """grad_out (B,C,N) -> (B,C,M) deterministic."""
-    grad_out = grad_out.contiguous()
-    B, C, N = grad_out.shape
     csr = csr_of(idx, m)
-    out = torch.empty((B, C, m), dtype=torch.float32, device=grad_out.device)
-    _call("kdpc_three_interpolate_grad_csr", B, C, N, m, _dev(grad_out, torch.float32, "grad_out"),
-          _dev(weight, torch.float32, "weight"), csr.offsets.data_ptr(), csr.perm.data_ptr(),
-          _dev(out, torch.float32, "grad_points"), _stream(grad_out))
-    return out
+    return _op("kdpc_three_interpolate_grad_csr", "three_interpolate_grad_csr",
+               grad_out.contiguous(), weight, csr.offsets, csr.perm, m)
 
 
 # ------------------------------------------------------------------ fused cost volume
@@ -378,137 +370,73 @@ def cost_volume_supported(din, dout, k):
 
 def cost_volume_fwd(x1, x2, idx, p1, p2, wpos, bpos, w1, b1):
     """-> out (B,N1,Dout) f32, amax (B,N1,Dout) u8.  See include/kdpc.h."""
-    B, N1, _ = x1.shape
-    N2 = x2.shape[1]
+    B, N1, _ = _gpu(x1, "x1").shape
     K = idx.shape[2]
     din, dout = p1.shape[2], w1.shape[0]
-    out = torch.empty((B, N1, dout), dtype=torch.float32, device=x1.device)
-    amax = torch.empty((B, N1, dout), dtype=torch.uint8, device=x1.device)
-    f = torch.float32
-    _call("kdpc_cost_volume_fwd", B, N1, N2, K, din, dout, _dev(x1, f, "x1"), _dev(x2, f, "x2"),
-          _dev(idx, torch.int32, "idx"), _dev(p1, f, "p1"), _dev(p2, f, "p2"),
-          _dev(wpos, f, "wpos"), _dev(bpos, f, "bpos"), _dev(w1, f, "w1"), _dev(b1, f, "b1"),
-          _dev(out, f, "out"), _dev(amax, torch.uint8, "amax"), _stream(x1),
-          work=(4 * B * N1 * (3 + K + din + K * din + 2 * dout) + B * N1 * dout,
-                2.0 * B * N1 * K * din * dout))
-    return out, amax
+    return _op("kdpc_cost_volume_fwd", "cost_volume_fwd", x1, x2, idx, p1, p2, wpos, bpos, w1,
+               b1, work=(4 * B * N1 * (3 + K + din + K * din + 2 * dout) + B * N1 * dout,
+                         2.0 * B * N1 * K * din * dout))
 
 
 def cost_volume_bwd(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout):
     """-> dp1 (B,N1,Din), dp2_rows (B,N1,K,Din), dx1 (B,N1,3), ddir_rows (B,N1,K,3), dparams."""
-    B, N1, _ = x1.shape
-    N2 = x2.shape[1]
-    K = idx.shape[2]
-    din, dout = p1.shape[2], w1.shape[0]
-    dev = x1.device
-    f = torch.float32
-    dp1 = torch.empty((B, N1, din), dtype=f, device=dev)
-    dp2_rows = torch.empty((B, N1, K, din), dtype=f, device=dev)
-    dx1 = torch.empty((B, N1, 3), dtype=f, device=dev)
-    ddir_rows = torch.empty((B, N1, K, 3), dtype=f, device=dev)
-    dparams = torch.empty((dout * din + dout + 4 * din,), dtype=f, device=dev)
-    lib = load_library()
-    ws_bytes = lib.kdpc_cost_volume_bwd_workspace_bytes(B, N1, din, dout)
-    ws = torch.empty((max(ws_bytes, 4),), dtype=torch.uint8, device=dev)
-    _call("kdpc_cost_volume_bwd", B, N1, N2, K, din, dout, _dev(x1, f, "x1"), _dev(x2, f, "x2"),
-          _dev(idx, torch.int32, "idx"), _dev(p1, f, "p1"), _dev(p2, f, "p2"),
-          _dev(wpos, f, "wpos"), _dev(bpos, f, "bpos"), _dev(w1, f, "w1"), _dev(out, f, "out"),
-          _dev(amax, torch.uint8, "amax"), _dev(gout, f, "dout"), _dev(dp1, f, "dp1"),
-          _dev(dp2_rows, f, "dp2_rows"), _dev(dx1, f, "dx1"), _dev(ddir_rows, f, "ddir_rows"),
-          ws.data_ptr(), ws_bytes, _dev(dparams, f, "dparams"), _stream(x1))
-    return dp1, dp2_rows, dx1, ddir_rows, dparams
+    return _op("kdpc_cost_volume_bwd", "cost_volume_bwd", _gpu(x1, "x1"), x2, idx, p1, p2,
+               wpos, bpos, w1, out, amax, gout)
 
 
 # ------------------------------------------------------------------ wide cost volume
+@functools.lru_cache(maxsize=None)
 def cost_volume_wide_supported(din, dout, k):
     return bool(load_library().kdpc_cost_volume_wide_supported(din, dout, k))
 
 
 def cost_volume_wide_h0(x1, x2, idx, p1, p2, wpos, bpos):
     """-> h0 (B,N1,K,Din) = LeakyReLU(P2[idx] + P1 + Wpos dir + bpos)."""
-    B, N1, _ = x1.shape
-    N2, K, din = x2.shape[1], idx.shape[2], p1.shape[2]
-    f = torch.float32
-    h0 = torch.empty((B, N1, K, din), dtype=f, device=x1.device)
-    _call("kdpc_cost_volume_wide_h0", B, N1, N2, K, din, _dev(x1, f, "x1"), _dev(x2, f, "x2"),
-          _dev(idx, torch.int32, "idx"), _dev(p1, f, "p1"), _dev(p2, f, "p2"),
-          _dev(wpos, f, "wpos"), _dev(bpos, f, "bpos"), _dev(h0, f, "h0"), _stream(x1),
-          work=(4 * B * N1 * (K * (1 + 2 * din + 3) + din + 3), 10.0 * B * N1 * K * din))
-    return h0
+    B, N1, _ = _gpu(x1, "x1").shape
+    K, din = idx.shape[2], p1.shape[2]
+    return _op("kdpc_cost_volume_wide_h0", "cost_volume_wide_h0", x1, x2, idx, p1, p2, wpos,
+               bpos, work=(4 * B * N1 * (K * (1 + 2 * din + 3) + din + 3),
+                           10.0 * B * N1 * K * din))
 
 
 def cost_volume_wide_max(z1, B, N1, K, dout):
     """z1 (B*N1*K, Dout) -> out (B,N1,Dout), amax (B,N1,Dout) u8."""
-    f = torch.float32
-    out = torch.empty((B, N1, dout), dtype=f, device=z1.device)
-    amax = torch.empty((B, N1, dout), dtype=torch.uint8, device=z1.device)
-    _call("kdpc_cost_volume_wide_max", B, N1, K, dout, _dev(z1, f, "z1"), _dev(out, f, "out"),
-          _dev(amax, torch.uint8, "amax"), _stream(z1))
-    return out, amax
+    return _op("kdpc_cost_volume_wide_max", "cost_volume_wide_max", _gpu(z1, "z1"), B, N1, K,
+               dout)
 
 
 def cost_volume_wide_max_bwd(gout, out, amax, K):
     """-> dz1 (B*N1*K, Dout) dense, gsc (B*N1, Dout)."""
-    B, N1, dout = out.shape
-    f = torch.float32
-    dz1 = torch.empty((B * N1 * K, dout), dtype=f, device=out.device)
-    gsc = torch.empty((B * N1, dout), dtype=f, device=out.device)
-    _call("kdpc_cost_volume_wide_max_bwd", B, N1, K, dout, _dev(gout, f, "gout"),
-          _dev(out, f, "out"), _dev(amax, torch.uint8, "amax"), _dev(dz1, f, "dz1"),
-          _dev(gsc, f, "gsc"), _stream(out))
-    return dz1, gsc
+    return _op("kdpc_cost_volume_wide_max_bwd", "cost_volume_wide_max_bwd",
+               _gpu(gout, "gout"), out, amax, K)
 
 
 def cost_volume_wide_h0_bwd(x1, x2, idx, h0, dz):
     """dz (B*N1*K, Din) dh0 -> dz0 in place; -> dp1 (B,N1,Din), dWpos (Din,3)."""
-    B, N1, _ = x1.shape
-    N2, K, din = x2.shape[1], idx.shape[2], h0.shape[-1]
-    f = torch.float32
-    lib = load_library()
-    rows = lib.kdpc_cost_volume_wide_slab_rows()
-    slab = torch.empty((rows, din * 3), dtype=f, device=x1.device)
-    dp1 = torch.empty((B, N1, din), dtype=f, device=x1.device)
-    _call("kdpc_cost_volume_wide_h0_bwd", B, N1, N2, K, din, _dev(x1, f, "x1"), _dev(x2, f, "x2"),
-          _dev(idx, torch.int32, "idx"), _dev(h0, f, "h0"), _dev(dz, f, "dz"),
-          _dev(dp1, f, "dp1"), _dev(slab, f, "slab"), _stream(x1))
+    din = h0.shape[-1]
+    dp1, slab = _op("kdpc_cost_volume_wide_h0_bwd", "cost_volume_wide_h0_bwd", _gpu(x1, "x1"),
+                    x2, idx, h0, dz)
     return dp1, colsum(slab).view(din, 3)
 
 
 # ------------------------------------------------------------------ PointConv contraction
 def pointconv_contract_fwd(xyz, center, feats, idx, wt):
     """-> A (B,S,16*(3+D)), c-major (the reference's .view(B,S,-1) of (B,S,C,16))."""
-    B, N, _ = xyz.shape
+    B, N, _ = _gpu(xyz, "xyz").shape
     S, K = idx.shape[1], idx.shape[2]
-    D = feats.shape[2]
-    C = 3 + D
-    out = torch.empty((B, S, 16 * C), dtype=torch.float32, device=xyz.device)
-    f = torch.float32
-    _call("kdpc_pointconv_contract_fwd", B, N, S, K, D, _dev(xyz, f, "xyz"),
-          _dev(center, f, "center"), _dev(feats, f, "feats"), _dev(idx, torch.int32, "idx"),
-          _dev(wt, f, "wt"), _dev(out, f, "out"), _stream(xyz),
-          work=(4 * B * S * (K + K * C + 16 * K + 16 * C), 2.0 * B * S * K * C * 16))
-    return out
+    C = 3 + feats.shape[2]
+    return _op("kdpc_pointconv_contract_fwd", "pointconv_contract_fwd", xyz, center, feats, idx,
+               wt, work=(4 * B * S * (K + K * C + 16 * K + 16 * C), 2.0 * B * S * K * C * 16))
 
 
 def pointconv_contract_bwd(xyz, center, feats, idx, wt, dout):
     """-> dg_rows (B,S,K,3+D), dwt (B,S,K,16), dcenter (B,S,3)."""
-    B, N, _ = xyz.shape
-    S, K = idx.shape[1], idx.shape[2]
-    D = feats.shape[2]
-    C = 3 + D
-    dev = xyz.device
-    f = torch.float32
-    dg_rows = torch.empty((B, S, K, C), dtype=f, device=dev)
-    dwt = torch.empty((B, S, K, 16), dtype=f, device=dev)
-    dcenter = torch.empty((B, S, 3), dtype=f, device=dev)
-    _call("kdpc_pointconv_contract_bwd", B, N, S, K, D, _dev(xyz, f, "xyz"),
-          _dev(center, f, "center"), _dev(feats, f, "feats"), _dev(idx, torch.int32, "idx"),
-          _dev(wt, f, "wt"), _dev(dout, f, "dout"), _dev(dg_rows, f, "dg_rows"),
-          _dev(dwt, f, "dwt"), _dev(dcenter, f, "dcenter"), _stream(xyz))
-    return dg_rows, dwt, dcenter
+    return _op("kdpc_pointconv_contract_bwd", "pointconv_contract_bwd", _gpu(xyz, "xyz"),
+               center, feats, idx, wt, dout)
 
 
 # ------------------------------------------------------------------ fused PointConv layer
+@functools.lru_cache(maxsize=None)
 def pointconv_supported(k, d, o):
     return bool(load_library().kdpc_pointconv_supported(k, d, o))
 
@@ -520,146 +448,63 @@ def _workspace(nbytes, device):
 def pointconv_fwd(xyz, center, feats, idx, wt, wl, bias):
     """Fused gather + contraction + Linear: -> y (B,S,O) = A wl^T + bias, A never stored.
     xyz (B,N,3), center (B,S,3), feats (B,N,D), idx (B,S,K) i32, wt (B,S,K,16), wl (O,16C)."""
-    B, N, _ = xyz.shape
+    B, N, _ = _gpu(xyz, "xyz").shape
     S, K = idx.shape[1], idx.shape[2]
-    D = feats.shape[2]
-    O = wl.shape[0]
-    C = 3 + D
-    f = torch.float32
-    lib = load_library()
-    ws_bytes = lib.kdpc_pointconv_fwd_workspace_bytes(B, S, K, D, O)
-    ws = _workspace(ws_bytes, xyz.device)
-    y = torch.empty((B, S, O), dtype=f, device=xyz.device)
+    O, C = wl.shape[0], 3 + feats.shape[2]
     R = B * S
-    _call("kdpc_pointconv_fwd", B, N, S, K, D, O, _dev(xyz, f, "xyz"), _dev(center, f, "center"),
-          _dev(feats, f, "feats"), _dev(idx, torch.int32, "idx"), _dev(wt, f, "wt"),
-          _dev(wl, f, "wl"), _dev(bias, f, "bias"), _dev(y, f, "y"), ws.data_ptr(), ws_bytes,
-          _stream(xyz),
-          work=(4 * R * (K + K * C + 16 * K + O) + 4 * O * 16 * C,
-                2.0 * R * K * C * 16 + 2.0 * R * 16 * C * O))
-    return y
+    return _op("kdpc_pointconv_fwd", "pointconv_fwd", xyz, center, feats, idx, wt, wl, bias,
+               work=(4 * R * (K + K * C + 16 * K + O) + 4 * O * 16 * C,
+                     2.0 * R * K * C * 16 + 2.0 * R * 16 * C * O))
 
 
 def pointconv_bwd(xyz, center, feats, idx, wt, wl, dy, csr, need_xyz=True):
     """Backward of pointconv_fwd for dy (B,S,O) -> (dxyz|None, dfeats, dcenter, dwt, dwl)."""
-    B, N, _ = xyz.shape
+    B, N, _ = _gpu(xyz, "xyz").shape
     S, K = idx.shape[1], idx.shape[2]
-    D = feats.shape[2]
-    O = wl.shape[0]
-    C = 3 + D
-    f = torch.float32
-    dev = xyz.device
-    lib = load_library()
-    ws_bytes = lib.kdpc_pointconv_bwd_workspace_bytes(B, S, K, D, O)
-    if ws_bytes == 0:
-        raise KdpcError("kdpc_pointconv_bwd_workspace_bytes returned 0 (invalid sizes?)")
-    ws = _workspace(ws_bytes, dev)
-    dxyz = torch.empty((B, N, 3), dtype=f, device=dev) if need_xyz else None
-    dfeats = torch.empty((B, N, D), dtype=f, device=dev)
-    dcenter = torch.empty((B, S, 3), dtype=f, device=dev)
-    dwt = torch.empty((B, S, K, 16), dtype=f, device=dev)
-    dwl = torch.empty((O, 16 * C), dtype=f, device=dev)
+    O, C = wl.shape[0], 3 + feats.shape[2]
     R = B * S
-    _call("kdpc_pointconv_bwd", B, N, S, K, D, O, _dev(xyz, f, "xyz"), _dev(center, f, "center"),
-          _dev(feats, f, "feats"), _dev(idx, torch.int32, "idx"), _dev(wt, f, "wt"),
-          _dev(wl, f, "wl"), _dev(dy, f, "dy"), csr.offsets.data_ptr(), csr.perm.data_ptr(),
-          dxyz.data_ptr() if need_xyz else None, _dev(dfeats, f, "dfeats"),
-          _dev(dcenter, f, "dcenter"), _dev(dwt, f, "dwt"), _dev(dwl, f, "dwl"), ws.data_ptr(),
-          ws_bytes, _stream(xyz),
-          work=(4 * R * (2 * K * C + 32 * K + 2 * O) + 8 * O * 16 * C,
-                4.0 * R * K * C * 16 + 4.0 * R * 16 * C * O))
-    return dxyz, dfeats, dcenter, dwt, dwl
+    return _op("kdpc_pointconv_bwd", "pointconv_bwd", xyz, center, feats, idx, wt, wl, dy,
+               csr.offsets, csr.perm, bool(need_xyz),
+               work=(4 * R * (2 * K * C + 32 * K + 2 * O) + 8 * O * 16 * C,
+                     4.0 * R * K * C * 16 + 4.0 * R * 16 * C * O))
 
 
 # ------------------------------------------------------------------- fused WeightNet
 def weightnet_fwd(xyz, center, idx, params):
     """wt (B,S,K,16) from xyz (B,N,3), center (B,S,3), idx (B,S,K) i32 and the six WeightNet
     tensors params = (W0 (8,3[,1,1]), b0, W1 (8,8), b1, W2 (16,8), b2)."""
-    B, N, _ = xyz.shape
+    B, N, _ = _gpu(xyz, "xyz").shape
     S, K = idx.shape[1], idx.shape[2]
-    f = torch.float32
-    wt = torch.empty((B, S, K, 16), dtype=f, device=xyz.device)
-    ptrs = [_dev(p, f, f"weightnet param {i}") for i, p in enumerate(params)]
-    _call("kdpc_weightnet_fwd", B, N, S, K, _dev(xyz, f, "xyz"), _dev(center, f, "center"),
-          _dev(idx, torch.int32, "idx"), *ptrs, _dev(wt, f, "wt"), _stream(xyz),
-          work=(B * (12 * N + 12 * S + S * K * (4 + 64)), 2.0 * B * S * K * (24 + 64 + 128)))
-    return wt
+    return _op("kdpc_weightnet_fwd", "weightnet_fwd", xyz, center, idx, *params,
+               work=(B * (12 * N + 12 * S + S * K * (4 + 64)), 2.0 * B * S * K * (24 + 64 + 128)))
 
 
 def weightnet_bwd(xyz, center, idx, params, dwt, need_rel=False):
     """-> (drel (B,S,K,3) | None, dparams (248,): dW0 | db0 | dW1 | db1 | dW2 | db2)."""
-    B, N, _ = xyz.shape
-    S, K = idx.shape[1], idx.shape[2]
-    f = torch.float32
-    dev = xyz.device
-    lib = load_library()
-    ws_bytes = lib.kdpc_weightnet_bwd_workspace_bytes()
-    ws = torch.empty((ws_bytes,), dtype=torch.uint8, device=dev)
-    dparams = torch.empty((lib.kdpc_weightnet_param_count(),), dtype=f, device=dev)
-    drel = torch.empty((B, S, K, 3), dtype=f, device=dev) if need_rel else None
-    ptrs = [_dev(p, f, f"weightnet param {i}") for i, p in enumerate(params)]
-    _call("kdpc_weightnet_bwd", B, N, S, K, _dev(xyz, f, "xyz"), _dev(center, f, "center"),
-          _dev(idx, torch.int32, "idx"), *ptrs, _dev(dwt, f, "dwt"),
-          drel.data_ptr() if need_rel else None, dparams.data_ptr(), ws.data_ptr(), ws_bytes,
-          _stream(xyz))
-    return drel, dparams
+    return _op("kdpc_weightnet_bwd", "weightnet_bwd", _gpu(xyz, "xyz"), center, idx, *params,
+               dwt, bool(need_rel))
 
 
 # ------------------------------------------------------- BatchNorm1d + LeakyReLU (rows)
 def batchnorm_lrelu_fwd(x2, weight, bias, eps, momentum, slope, run_mean, run_var):
     """Train mode over x2 (R, C): -> (y, mean, invstd); running stats updated in place."""
-    R, C = x2.shape
-    f = torch.float32
-    dev = x2.device
-    lib = load_library()
-    ws = _workspace(lib.kdpc_batchnorm_workspace_bytes(R, C), dev)
-    y = torch.empty_like(x2)
-    mean = torch.empty((C,), dtype=f, device=dev)
-    invstd = torch.empty((C,), dtype=f, device=dev)
-    _call("kdpc_batchnorm_lrelu_fwd", R, C, _dev(x2, f, "x"), _dev(weight, f, "weight"),
-          _dev(bias, f, "bias"), float(eps), float(momentum), float(slope),
-          None if run_mean is None else _dev(run_mean, f, "running_mean"),
-          None if run_var is None else _dev(run_var, f, "running_var"),
-          mean.data_ptr(), invstd.data_ptr(), y.data_ptr(), ws.data_ptr(), ws.numel(),
-          _stream(x2), work=(12 * R * C, 0))
-    return y, mean, invstd
+    R, C = _gpu(x2, "x").shape
+    return _op("kdpc_batchnorm_lrelu_fwd", "batchnorm_lrelu_fwd", x2, weight, bias, float(eps),
+               float(momentum), float(slope), run_mean, run_var, work=(12 * R * C, 0))
 
 
 def batchnorm_lrelu_apply(x2, mean, invstd, weight, bias, slope):
-    R, C = x2.shape
-    f = torch.float32
-    y = torch.empty_like(x2)
-    _call("kdpc_batchnorm_lrelu_apply", R, C, _dev(x2, f, "x"), _dev(mean, f, "mean"),
-          _dev(invstd, f, "invstd"), _dev(weight, f, "weight"), _dev(bias, f, "bias"),
-          float(slope), y.data_ptr(), _stream(x2))
-    return y
+    return _op("kdpc_batchnorm_lrelu_apply", "batchnorm_lrelu_apply", _gpu(x2, "x"), mean,
+               invstd, weight, bias, float(slope))
 
 
 def batchnorm_lrelu_bwd(dy, y, x2, weight, mean, invstd, slope):
     """-> (dx, dweight, dbias)."""
-    R, C = x2.shape
-    f = torch.float32
-    dev = x2.device
-    lib = load_library()
-    ws = _workspace(lib.kdpc_batchnorm_workspace_bytes(R, C), dev)
-    dx = torch.empty_like(x2)
-    dw = torch.empty((C,), dtype=f, device=dev)
-    db = torch.empty((C,), dtype=f, device=dev)
-    _call("kdpc_batchnorm_lrelu_bwd", R, C, _dev(dy, f, "dy"), _dev(y, f, "y"), _dev(x2, f, "x"),
-          _dev(weight, f, "weight"), _dev(mean, f, "mean"), _dev(invstd, f, "invstd"),
-          float(slope), dx.data_ptr(), dw.data_ptr(), db.data_ptr(), ws.data_ptr(), ws.numel(),
-          _stream(x2), work=(20 * R * C, 0))
-    return dx, dw, db
+    R, C = _gpu(x2, "x").shape
+    return _op("kdpc_batchnorm_lrelu_bwd", "batchnorm_lrelu_bwd", dy, y, x2, weight, mean,
+               invstd, float(slope), work=(20 * R * C, 0))
 
 
 def colsum(x2):
     """Column sums of a row-major (R, L) tensor, deterministic fixed-order: -> (L,)."""
-    R, L = x2.shape
-    f = torch.float32
-    lib = load_library()
-    nb = lib.kdpc_colsum_workspace_bytes(R, L)
-    ws = _workspace(nb, x2.device)
-    out = torch.empty((L,), dtype=f, device=x2.device)
-    _call("kdpc_colsum", R, L, _dev(x2, f, "src"), out.data_ptr(), ws.data_ptr(), nb,
-          _stream(x2))
-    return out
+    return _op("kdpc_colsum", "colsum", _gpu(x2, "src"))

@@ -1,12 +1,15 @@
 """Scene-flow and knowledge-distillation losses (drop-in for the reference's loss_functions.py).
 
 Same names, arguments and arithmetic as the reference (loss_functions.py:6-235); the only
-change is that accumulators are created on the inputs' device instead of via
-`torch.zeros(1).cuda()`, and the GT pyramid is gathered with the HIP row gather.
+changes are that accumulators are created on the inputs' device instead of via
+`torch.zeros(1).cuda()`, the GT pyramid is gathered with the HIP row gather, and the large
+sums of the training objective (over all points / all hint features) are fixed-order HIP
+column sums (dense.fixed_sum: reproducible, and correct inside a captured HIP graph).
 The iterative/bridge variants (att_*, bridge_*) belong to models outside this build's scope.
 """
 import torch
 
+from dense import fixed_sum
 from pointconv_util import index_points_gather as index_points
 
 scale = 1.0
@@ -33,7 +36,7 @@ def multiScaleLoss(pred_flows, gt_flow, fps_idxs, alpha=[0.02, 0.04, 0.08, 0.16]
     total_loss = _zero(gt_flow)
     for i in range(num_scale):
         diff_flow = pred_flows[i].permute(0, 2, 1) - gt_flows[i + offset]
-        total_loss += alpha[i] * torch.norm(diff_flow, dim=2).sum(dim=1).mean()
+        total_loss += alpha[i] * fixed_sum(torch.norm(diff_flow, dim=2), 1).mean()
     return total_loss
 
 
@@ -92,8 +95,8 @@ def biDirection_loss_ht(outputs, feat1s, feat2s, fps_idxs1, fps_idxs2, gt_flow, 
     src_hint_loss = ((feat1s[layer] - t_feat1s[layer]) ** 2) / 2
     target_hint_loss = ((feat2s[layer] - t_feat2s[layer]) ** 2) / 2
     return _zero(gt_flow) + (beta * (gamma * loss1 + (1 - gamma) * loss2)
-                             + (1 - beta) * (0.5 * src_hint_loss.sum()
-                                             + 0.5 * target_hint_loss.sum()))
+                             + (1 - beta) * (0.5 * fixed_sum(src_hint_loss)
+                                             + 0.5 * fixed_sum(target_hint_loss)))
 
 
 # flow_loss_ht (reference loss_functions.py:98-121) reads the undefined names `fps_idxs`

@@ -486,8 +486,10 @@ class _CostVolume(torch.autograd.Function):
     p1 (B,N1,D), p2 (B,N2,D) channel-last -> (B,N1,Dout) channel-last."""
 
     @staticmethod
-    def forward(ctx, x1, x2, idx, p1, p2, wpos, bpos, w1, b1):
+    def forward(ctx, x1, x2, idx, p1, p2, wpos, bpos, w1, b1, amax_override=None):
         out, amax = _nat.cost_volume_fwd(x1, x2, idx, p1, p2, wpos, bpos, w1, b1)
+        if amax_override is not None:
+            amax = amax_override(amax)
         ctx.save_for_backward(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax)
         return out
 
@@ -507,7 +509,7 @@ class _CostVolume(torch.autograd.Function):
         db1 = dpar[o:o + dout]
         dwpos = dpar[o + dout:o + dout + 3 * din].view(3, din).t()
         dbpos = dpar[o + dout + 3 * din:]
-        return dx1, dx2, None, dp1, dp2, dwpos, dbpos, dw1, db1
+        return dx1, dx2, None, dp1, dp2, dwpos, dbpos, dw1, db1, None
 
 
 class _CostVolumeWide(torch.autograd.Function):
@@ -516,11 +518,13 @@ class _CostVolumeWide(torch.autograd.Function):
     Same arguments and result as _CostVolume."""
 
     @staticmethod
-    def forward(ctx, x1, x2, idx, p1, p2, wpos, bpos, w1, b1):
+    def forward(ctx, x1, x2, idx, p1, p2, wpos, bpos, w1, b1, amax_override=None):
         B, N1, K = idx.shape
         h0 = _nat.cost_volume_wide_h0(x1, x2, idx, p1, p2, wpos, bpos)
         z1 = torch.addmm(b1, h0.view(-1, h0.shape[-1]), w1.t())
         out, amax = _nat.cost_volume_wide_max(z1, B, N1, K, w1.shape[0])
+        if amax_override is not None:
+            amax = amax_override(amax)
         ctx.save_for_backward(x1, x2, idx, wpos, w1, h0, out, amax)
         return out
 
@@ -542,10 +546,22 @@ class _CostVolumeWide(torch.autograd.Function):
         ddir = torch.mm(dz, wpos)  # (rows, 3)
         dx2 = _nat.group_rows_grad(ddir.view(B, N1 * K, 3), csr, B, N2, 3)
         dx1 = -ddir.view(B, N1, K, 3).sum(2)
-        return dx1, dx2, None, dp1, dp2, dwpos, dbpos, dw1, db1
+        return dx1, dx2, None, dp1, dp2, dwpos, dbpos, dw1, db1, None
 
 
 _FUSED_COST_VOLUME = True  # test seam: False forces the unfused torch formulation
+_amax_override = None
+
+
+def set_amax_override(fn):
+    """Test seam: `fn(amax) -> amax` replaces the max-over-K routing (which neighbour each
+    (point, channel) maximum came from, (B,N1,Dout) uint8) that the fused cost volume's
+    backward uses, for every call made with gradients enabled -- the parity tests replay
+    the float64 reference's routing with it, as set_knn_override replays its neighbours.
+    None restores the computed routing.  Returns the previous override."""
+    global _amax_override
+    prev, _amax_override = _amax_override, fn
+    return prev
 _WIDE_MIN_DIN = 128  # Din=64 through the wide path measured within noise (311.8 vs 309.9 pairs/s)
 
 
@@ -589,9 +605,10 @@ def _cost_volume_cl(nsample, x1, x2, p1, p2, pos, mlp, act, knn_idx=None):
     fn = _fusable(nsample, pos, mlp, act, din)
     if fn:
         conv = mlp[0].composed_module[0]
+        ovr = _amax_override if torch.is_grad_enabled() else None
         return fn.apply(x1, x2, _as_idx32(knn_idx).contiguous(), p1.contiguous(), p2.contiguous(),
                         pos.weight.view(din, 3), pos.bias,
-                        conv.weight.view(conv.out_channels, din), conv.bias)
+                        conv.weight.view(conv.out_channels, din), conv.bias, ovr)
     direction = index_points_group(x2, knn_idx) - x1.view(B, N1, 1, C)
     grouped_points2 = index_points_group(p2, knn_idx)
     h = act((grouped_points2 + p1.unsqueeze(2)) + _linear_1x1(pos, direction))

@@ -57,13 +57,30 @@ def main(n=2048, full_grads=None, dtype=torch.float64):
     torch.cuda.FloatTensor = lambda *s: torch.empty(*s, dtype=dtype)
     for m in mods:
         m.knn_point = replay
+    # the cost volumes' max over K (CrossLayerLight.cross, pointconv_util.py:1848): record
+    # the student's routing -- which neighbour each (point, channel) maximum came from -- in
+    # call order, so the GPU test can replay it (a float64 near-tie may route differently
+    # from any fp32 evaluation)
+    amax = []
+    import torch.nn.functional as TF
+    pool = TF.max_pool2d
+
+    def recording_pool(x, kernel_size, *a, **k):
+        out, ind = pool(x, kernel_size, *a, return_indices=True, **k)
+        n = x.shape[3]
+        amax.append((ind[:, :, 0, :] // n).permute(0, 2, 1).to(torch.uint8).numpy())
+        return out
     try:
         pos1, pos2, flow = (torch.from_numpy(g[k]).to(dtype) for k in ("pos1", "pos2", "flow"))
         teacher = MF._synth(R.teacher.PointConvBidirection(), seed=1).to(dtype).eval()
         student = MF._synth(R.student.PointConvBidirection(), seed=2).to(dtype).train()
         with torch.no_grad():
             t_out = teacher(pos1, pos2, pos1, pos2)
-        s_out = student(pos1, pos2, pos1, pos2)
+        TF.max_pool2d = recording_pool
+        try:
+            s_out = student(pos1, pos2, pos1, pos2)
+        finally:
+            TF.max_pool2d = pool
         flows, f1i, f2i, _, _, feat1s, feat2s, _ = s_out
         kd = R.loss.biDirection_loss_ht(flows, feat1s, feat2s, f1i, f2i, flow, t_out[0],
                                         t_out[5], t_out[6], t_out[1], t_out[2], 0.3, 0.8, layer=3)
@@ -88,6 +105,9 @@ def main(n=2048, full_grads=None, dtype=torch.float64):
     }
     for i in range(4):
         out[f"s_flow{i}_f64"] = flows[i].detach().numpy()
+    out["n_amax"] = np.array(len(amax))
+    for j, a in enumerate(amax):
+        out[f"amax{j}"] = a
     if full_grads:  # every gradient element (diagnostics: tools/grad_gap.py), not committed
         np.savez_compressed(full_grads, **{k: p.grad.numpy() for k, p in student.named_parameters()
                                            if p.grad is not None})

@@ -258,11 +258,25 @@ def make_model_knn_trace(R, n=2048):
             m.knn_point = fn
     out = dict(pos1=p1[None], pos2=p2[None], flow=fl[None], msl=_np(msl), kd=_np(kd),
                n_calls=np.array(len(calls)))
+    clouds = {}  # every distinct input cloud once (float32 bytes -> id)
+
+    def cloud_id(a):
+        a32 = np.ascontiguousarray(a.astype(np.float32))
+        key = a32.tobytes()
+        if key not in clouds:
+            clouds[key] = len(clouds)
+            out[f"cloud{clouds[key]}"] = a32
+        return clouds[key]
+
     for i, (k, xyz, q, idx) in enumerate(calls):
         out[f"knn{i}_k"] = np.array(k)
         out[f"knn{i}_rsum"] = np.concatenate([xyz[0].sum(0), (xyz[0] ** 2).sum(0)])
         out[f"knn{i}_qsum"] = np.concatenate([q[0].sum(0), (q[0] ** 2).sum(0)])
         out[f"knn{i}_idx"] = idx[0].astype(np.int16)
+        # the call's own coordinates: certifies each free-running neighbour difference as a
+        # near-tie of the reference's distances or as moved inputs (tests/test_gpu_model.py)
+        out[f"knn{i}_rcloud"] = np.array(cloud_id(xyz[0]))
+        out[f"knn{i}_qcloud"] = np.array(cloud_id(q[0]))
     for tag, o in (("t", t_out), ("s", s_out)):
         for i, f in enumerate(o[0]):
             out[f"{tag}_flow{i}"] = _np(f)

@@ -252,3 +252,37 @@ def test_ball_query_config2_size(nat):
     centres = np.take_along_axis(xyz, fidx[..., None].astype(np.int64), 1)
     out = nat.ball_query(0.5, 16, _t(xyz), _t(centres)).cpu().numpy()
     np.testing.assert_array_equal(out, O.ball_query(0.5, 16, xyz, centres))
+
+
+def test_c_abi_direct_equals_torch_ops(nat):
+    """The bare C ABI (ctypes, no torch in the call path) and torch.ops.kdpc give identical
+    results on the same inputs: the torch operators add checks and allocation only."""
+    ops = nat.load_ops()
+    xyz = _t(_cloud(2, 1500, seed=21))
+    q = _t(_cloud(2, 300, seed=22))
+    st = torch.cuda.current_stream().cuda_stream
+    idx_c = torch.empty((2, 300, 16), dtype=torch.int32, device=DEV)
+    nat._call("kdpc_ball_query", 2, 1500, 300, 0.5, 16, q.data_ptr(), xyz.data_ptr(),
+              idx_c.data_ptr(), st)
+    assert torch.equal(idx_c, ops.ball_query(0.5, 16, xyz, q))
+    kidx = torch.empty((2, 300, 9), dtype=torch.int32, device=DEV)
+    nat._call("kdpc_knn_point", 2, 1500, 300, 9, xyz.data_ptr(), q.data_ptr(), kidx.data_ptr(),
+              None, st)
+    assert torch.equal(kidx, ops.knn_point(9, xyz, q))
+    feats = torch.randn(2, 1500, 24, device=DEV)
+    rows = torch.empty((2, 300 * 9, 24), device=DEV)
+    nat._call("kdpc_group_rows", 2, 1500, 24, 300 * 9, feats.data_ptr(), kidx.data_ptr(),
+              rows.data_ptr(), st)
+    assert torch.equal(rows, ops.group_rows(feats, kidx.view(2, -1)))
+    temp = torch.full((2, 1500), 1e10, device=DEV)
+    fidx = torch.empty((2, 100), dtype=torch.int32, device=DEV)
+    nat._call("kdpc_furthest_point_sampling", 2, 1500, 100, xyz.data_ptr(), temp.data_ptr(),
+              fidx.data_ptr(), st)
+    assert torch.equal(fidx, ops.furthest_point_sample(xyz, 100))
+    g = torch.randn(2, 24, 300, 9, device=DEV)
+    gp = torch.empty((2, 24, 1500), device=DEV)
+    nat._call("kdpc_group_points_grad", 2, 24, 1500, 300, 9, g.data_ptr(), kidx.data_ptr(),
+              gp.data_ptr(), st)  # reference-shaped entry: stream-ordered scratch
+    gp2 = torch.zeros_like(gp)
+    ops.group_points_grad_wrapper(2, 24, 1500, 300, 9, g, kidx, gp2)
+    assert torch.equal(gp, gp2)
