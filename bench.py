@@ -242,6 +242,17 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
+    # host enqueue time of one eager step: the Python/torch.ops time to issue it, measured
+    # from an idle device (the step is GPU-bound while this stays below ms_per_step)
+    host = []
+    for i in range(2):
+        torch.cuda.synchronize()
+        h0 = time.perf_counter()
+        eager(*batches[i % nb])
+        host.append(time.perf_counter() - h0)
+        torch.cuda.synchronize()
+    host_ms = round(min(host) * 1e3, 3)
+
     # per-kernel roofline: HIP events around every launch of the named C entry points, over
     # eager replays of the same step after the timed region (a graph replay has no
     # per-launch host hook); kernel durations do not depend on how the launch was issued
@@ -271,6 +282,7 @@ def main():
                    "batch_per_gpu": args.batch, "global_batch": world * args.batch,
                    "npoints": args.npoints, "parallelism": f"dp{world}",
                    "step": "hip-graph" if args.graph else "eager"},
+        "host_enqueue_ms": host_ms,
         "roofline": roof,
         "roofline_gather": roof_gather,
     }

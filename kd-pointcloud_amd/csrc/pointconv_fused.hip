@@ -35,6 +35,13 @@
 
 using namespace kdpc;
 
+// diagnostic builds only (tools/build_variants.sh): 0 = the real kernel; weight-gradient
+// kernel with 2 no build, 3 no loads in the loop, 4 no staging, 5 MFMAs only,
+// 6 / 7 / 8 no WeightNet-weight / dy / gathered-feature loads
+#ifndef KDPC_WGT_MODE
+#define KDPC_WGT_MODE 0
+#endif
+
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -603,33 +610,48 @@ __global__ __launch_bounds__(256) void pc_csr_sum_kernel(long long npts, int c, 
 // ------------------------------------------------------------------ backward: weight
 // 1-D grid of nch x splits workgroups (512 threads); each owns the O x 128 tile of dwl for
 // one chunk over one split's rows, walked in tiles of TR rows (the MFMA inner dimension).
-// TR = 64 for O = 128: twice the MFMA work per gather / build / barrier round of the
-// 32-row tile (one workgroup per CU either way: the grid model below).  With >= 8 splits,
-// the chunks of split s all run on XCD s % 8 (workgroups are dealt round-robin by id).
-template <int O>
-constexpr int wgt_tile_rows() { return O == 128 ? 64 : 32; }  // O = 256 at 64 rows spilled
+// With >= 8 splits, the chunks of split s all run on XCD s % 8 (workgroups are dealt
+// round-robin by id): they share that split's dy / wt rows in one L2.
+//
+// Software pipeline over the row tiles, two LDS buffers for the MFMA operands: while the
+// matrix cores run tile t's MFMAs (dy^T from dyt[t&1], A from at[t&1]), the same waves build
+// tile t+1's block of A on the VALU (gathered G in gl, WeightNet weights in registers) into
+// at[(t+1)&1]; tile t+2's loads, issued at the top of the step, land meanwhile (staged to LDS
+// after the barrier, so no load latency sits between barriers).  The phases are independent
+// within one basic block, so the MFMAs' 64-cycle shadows carry the build (the unpipelined
+// kernel serialised them behind barriers: ~27 % MFMA busy, profiles/round02).
+template <int O, int KM>
+constexpr int wgt_tile_rows() { return O == 256 || (O == 128 && KM > 9) ? 32 : 64; }
 
 template <int O, int KM, bool EX>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
 void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __restrict__ dy,
                           float* __restrict__ dwl, int rows_per_split, int nsplit, int xcd_map) {
-  constexpr int TR = wgt_tile_rows<O>();
+  constexpr int TR = wgt_tile_rows<O, KM>();
   constexpr int TS = TR + 4;               // row stride of the transposed tiles
   constexpr int RP = TR / 32;              // build passes (rows rb, rb + 32, ...)
   constexpr int MT = O / 32;
-  constexpr int MPW = MT / 2;              // 8 waves: 4 column tiles x 2 row-tile groups
-  constexpr int GS = (TR * KM + 255) / 256;  // gather slots (float4) per thread
-  constexpr int DS = TR * O / 512;         // dy slots per thread
+  constexpr int MPW = MT / 2 > 0 ? MT / 2 : 1;  // 8 waves: 4 column tiles x 2 row-tile groups
+  constexpr int GS = (TR * KM + 255) / 256;     // gather slots (float4) per thread
+  constexpr int DV = TR * O / (512 * 4);        // dy float4 slots per thread
+  static_assert(DV >= 1 && TR * O % 2048 == 0, "dy tile must split into float4 slots");
+  static_assert(MT >= 2, "O >= 64");
   __shared__ __attribute__((aligned(16))) float gl[TR * KM * kCC];
-  __shared__ __attribute__((aligned(16))) float dyt[O * TS];
-  __shared__ __attribute__((aligned(16))) float at[kNC * TS];
+  __shared__ __attribute__((aligned(16))) float dyt[2][O * TS];
+  __shared__ __attribute__((aligned(16))) float at[2][kNC * TS];
 
+  // XCD fill: workgroups are dealt to the 8 XCDs round-robin by id, so block L runs on XCD
+  // L % 8; give each XCD a contiguous run of (split, chunk) pairs (split-major), so the
+  // chunks of one split -- which all read that split's dy / wt rows -- share at most two
+  // L2s (a plain split-major order spreads them over all eight).  Speed only: any
+  // placement computes the same result.
   const int L = blockIdx.x;
   int ch, split;
   if (xcd_map) {
-    const int q = L >> 3;
-    split = (L & 7) + 8 * (q / g.nch);
-    ch = q % g.nch;
+    const int per_xcd = (int)gridDim.x >> 3;
+    const int pidx = (L & 7) * per_xcd + (L >> 3);
+    split = pidx / g.nch;
+    ch = pidx % g.nch;
   } else {
     ch = L % g.nch;
     split = L / g.nch;
@@ -639,96 +661,181 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
   const int kk = EX ? KM : g.k;  // exact-K instantiation: constant trip counts
   const int rbeg = split * rows_per_split;
   const int rend = min(g.r, rbeg + rows_per_split);
+  const int ntiles = (rend - rbeg + TR - 1) / TR;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, half = lane >> 5, l32 = lane & 31;
-  const int w = t & (kW - 1), rb = t >> 4, cs = t & (kCC - 1);
+  const int w = t & (kW - 1), rb = t >> 4;
   const int nt = wv & 3;
   const int m0 = (wv >> 2) * MPW;
   const long long c16 = (long long)g.c * kW;
   const int tk = TR * kk;
   const Srcs src = srcs_of(g);
 
-  // registers prefetched one tile ahead
-  // gather slots: (row, neighbour) rk = (t >> 1) + 256 i, channels 4*h4 .. +3 of the chunk
+  // tile registers: WeightNet weights (row rb + 32 p2, all K, column w), gathered G
+  // (row-neighbour rk = (t >> 1) + 256 i, channels 4*h4 .. +3), dy (float4 slots).  The
+  // gathers' neighbour indices are loaded one fetch AHEAD (nbi): a gather issued right
+  // behind its own index load would stall the wave on that load (vmcnt retires in order).
   const int h4 = t & 1;
-  float wr[RP][KM], dr[DS];
-  float4 gr[GS];
-  auto fetch = [&](int row0) {
-#pragma unroll
-    for (int p2 = 0; p2 < RP; ++p2) {
-      const int row = row0 + rb + 32 * p2;
-#pragma unroll
-      for (int k = 0; k < KM; ++k)
-        wr[p2][k] = (row < rend && k < kk) ? wt[((long long)row * kk + k) * kW + w] : 0.f;
-    }
+  float wr[RP][KM], wc[RP][KM];
+  float4 gr[GS], dr[DV];
+  int nbi[GS];  // global neighbour row (b*N + idx) of each gather slot, >= b*n for none
+  // Every load of the tile is unconditional (a load under a branch -- or under a select the
+  // compiler turns into one -- makes it drain the whole load queue right behind it): rows past
+  // the split read through an out-of-range buffer offset, which returns 0 without touching
+  // memory.  Neighbour slots past the tile get the index kNoNbr (>= b*n: gathers read 0).
+  constexpr int kNoNbr = 1 << 30;
+  const __amdgpu_buffer_rsrc_t idx_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<int*>(g.idx), (short)0, (int)((long long)g.r * g.k * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wt_rs = rsrc(wt, (long long)g.r * kk * kW);
+  const __amdgpu_buffer_rsrc_t dy_rs = rsrc(dy, (long long)g.r * O);
+  // batch base (b * n) of a row: one integer division per tile; a row x = rr + r rows past
+  // the tile's first cloud start (x < s + TR) lies in cloud b0 + x / s, taken from a float
+  // quotient corrected by one step either way (its error is below 1) -- branch-free, so the
+  // loads stay in one scheduling region with the MFMAs
+  const float inv_s = 1.f / (float)g.s;
+  auto fetch_idx = [&](int tile) {
+    const int row0 = rbeg + tile * TR;
+    const int b0 = row0 / g.s;
+    const int rr = row0 - b0 * g.s;
 #pragma unroll
     for (int i = 0; i < GS; ++i) {
       const int rk = (t >> 1) + 256 * i;
       const int r = rk / kk;
       const int rw = row0 + r;
-      const int nb = (rk < tk && rw < rend) ? nbr_of(g, rw, rk - r * kk) : -1;
-      if (c0 == 0) {  // xyz - center channels: per element
-        float v[4];
+      const bool ok = rk < tk && rw < rend;
+      const int x = rr + r;
+      int q = (int)((float)x * inv_s);
+      q += ((q + 1) * g.s <= x ? 1 : 0) - (q * g.s > x ? 1 : 0);
+      const int bb = b0 + q;
+      const int base = ok ? bb * g.n : kNoNbr;
+      const unsigned off = ok ? ((unsigned)rw * (unsigned)g.k + (unsigned)(rk - r * kk)) * 4u : kOOB;
+      nbi[i] = base + (int)__builtin_amdgcn_raw_buffer_load_b32(idx_rs, (int)off, 0, 0);
+    }
+  };
+  auto fetch = [&](int tile) {
+    const int row0 = rbeg + tile * TR;
 #pragma unroll
-        for (int e2 = 0; e2 < 4; ++e2) v[e2] = g_fetch(g, src, nb, rw, 4 * h4 + e2);
-        gr[i] = make_float4(v[0], v[1], v[2], v[3]);
-      } else {  // 16 contiguous bytes of the neighbour's feature row; past-the-row masked
-        const int cg = c0 + 4 * h4;
-        const unsigned off = nb < 0 ? kOOB : feat_off(g, nb) + (unsigned)(cg - 3) * 4u;
-        const f32x4 v = __builtin_bit_cast(
-            f32x4, __builtin_amdgcn_raw_buffer_load_b128(src.feats, (int)off, 0, 0));
-        gr[i] = make_float4(cg < g.c ? v[0] : 0.f, cg + 1 < g.c ? v[1] : 0.f,
-                            cg + 2 < g.c ? v[2] : 0.f, cg + 3 < g.c ? v[3] : 0.f);
+    for (int p2 = 0; p2 < RP; ++p2) {
+      const int row = row0 + rb + 32 * p2;
+      const unsigned base = row < rend ? ((unsigned)row * (unsigned)kk * kW + w) * 4u : kOOB;
+#pragma unroll
+      for (int k = 0; k < KM; ++k) {
+        const unsigned off = k < kk ? base + (unsigned)(k * kW * 4) : kOOB;
+        wr[p2][k] = KDPC_WGT_MODE == 6 ? 0.5f : __builtin_bit_cast(
+            float, __builtin_amdgcn_raw_buffer_load_b32(wt_rs, (int)off, 0, 0));
       }
     }
+    // Branch-free gathers (a load under a branch makes the compiler drain the whole load
+    // queue right behind it): every slot issues the same three 16-byte buffer loads, with
+    // out-of-range offsets (which read 0 without touching memory) for what it does not need.
+    // Slot channels 4*h4 .. +3 of the chunk: for chunk 0, lane half 0 holds xyz - center and
+    // feature 0, lane half 1 features 1..4; otherwise 4 consecutive features.
 #pragma unroll
-    for (int i = 0; i < DS; ++i) {
-      const int e = t + 512 * i;
-      const int rw = row0 + e / O;
-      dr[i] = rw < rend ? dy[(long long)rw * O + (e % O)] : 0.f;
+    for (int i = 0; i < GS; ++i) {
+      const int rk = (t >> 1) + 256 * i;
+      const int rw = row0 + rk / kk;
+      const int nb = nbi[i];
+      const bool live = (unsigned)nb < (unsigned)g.bn;
+      const bool xyz = c0 == 0 && h4 == 0;
+      const int vch = c0 == 0 ? (h4 ? 1 : 0) : c0 - 3 + 4 * h4;  // first feature of the load
+      const unsigned voff = live ? (unsigned)nb * (unsigned)g.d * 4u + (unsigned)vch * 4u : kOOB;
+      const unsigned xoff = (xyz && live) ? (unsigned)nb * 12u : kOOB;
+      const unsigned coff = (xyz && live) ? (unsigned)rw * 12u : kOOB;
+      const f32x4 v = KDPC_WGT_MODE == 8 ? f32x4{(float)voff, 1.f, 2.f, 3.f} :
+          __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(src.feats, (int)voff, 0, 0));
+      const f32x4 x = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(src.xyz, (int)xoff, 0, 0));
+      const f32x4 cc = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(src.center, (int)coff, 0, 0));
+      // The xyz - center terms are added unconditionally (they are 0 - 0 outside the xyz
+      // slots): a select on them would let the compiler sink their loads under a branch.
+      const int cg = c0 + 4 * h4;  // first chunk channel of the slot
+      const float a0 = xyz ? 0.f : (cg < g.c ? v[0] : 0.f);
+      const float a1 = xyz ? 0.f : (cg + 1 < g.c ? v[1] : 0.f);
+      const float a2 = xyz ? 0.f : (cg + 2 < g.c ? v[2] : 0.f);
+      const float a3 = xyz ? (3 < g.c ? v[0] : 0.f) : (cg + 3 < g.c ? v[3] : 0.f);
+      gr[i] = make_float4(a0 + (x[0] - cc[0]), a1 + (x[1] - cc[1]), a2 + (x[2] - cc[2]), a3);
+    }
+    fetch_idx(tile + 1);
+    // dy slot q = t + 512 i: row q % TR (consecutive lanes: consecutive rows, so the
+    // transposed LDS writes below hit consecutive banks), columns 4 (q / TR) .. +3
+#pragma unroll
+    for (int i = 0; i < DV; ++i) {
+      const int q = t + 512 * i;
+      const int rw = row0 + q % TR;
+      const unsigned off = rw < rend ? ((unsigned)rw * O + 4u * (unsigned)(q / TR)) * 4u : kOOB;
+      dr[i] = KDPC_WGT_MODE == 7 ? make_float4(1.f, 2.f, 3.f, (float)q) : __builtin_bit_cast(
+          float4, __builtin_amdgcn_raw_buffer_load_b128(dy_rs, (int)off, 0, 0));
+    }
+  };
+  // registers -> LDS: gathered G into gl, dy transposed into dyt[buf], weights into wc
+  auto stage = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < GS; ++i) {
+      const int rk = (t >> 1) + 256 * i;
+      if (rk < tk) *reinterpret_cast<float4*>(gl + rk * kCC + 4 * h4) = gr[i];
+    }
+    float* dt = dyt[buf];
+#pragma unroll
+    for (int i = 0; i < DV; ++i) {
+      const int q = t + 512 * i;
+      const int r = q % TR, o = 4 * (q / TR);
+      dt[(o + 0) * TS + r] = dr[i].x;
+      dt[(o + 1) * TS + r] = dr[i].y;
+      dt[(o + 2) * TS + r] = dr[i].z;
+      dt[(o + 3) * TS + r] = dr[i].w;
+    }
+#pragma unroll
+    for (int p2 = 0; p2 < RP; ++p2)
+#pragma unroll
+      for (int k = 0; k < KM; ++k) wc[p2][k] = wr[p2][k];
+  };
+  // A block of the tile staged in gl / wc -> at[buf] (transposed: column-major rows)
+  auto build = [&](int buf) {
+    float* ab = at[buf];
+#pragma unroll
+    for (int p2 = 0; p2 < RP; ++p2) {
+      float a[kCC];
+      build_row<KM>(gl, rb + 32 * p2, kk, wc[p2], a);
+#pragma unroll
+      for (int c = 0; c < kCC; ++c) ab[(c * kW + w) * TS + rb + 32 * p2] = a[c];
     }
   };
 
   f32x16 acc[MPW];
 #pragma unroll
   for (int i = 0; i < MPW; ++i) acc[i] = zero16();
-  fetch(rbeg);
-  for (int row0 = rbeg; row0 < rend; row0 += TR) {
-    __syncthreads();  // previous tile's MFMAs are done with dyt / at
+  if (ntiles <= 0) return;
+  // prologue: tile 0 staged and built, tile 1 staged
+  fetch_idx(0);
+  fetch(0);
+  stage(0);
+  __syncthreads();
+  build(0);
+  fetch(1);
+  __syncthreads();
+  stage(1);
+  __syncthreads();
+  for (int tile = 0; tile < ntiles; ++tile) {
+    const int cur = tile & 1;
+    // tile+2's loads are issued first and land under this tile's MFMAs; tile's MFMAs || tile+1's
+    // build (independent: at[cur] / dyt[cur] vs gl, wc -> at[!cur])
+    if (KDPC_WGT_MODE != 3 && KDPC_WGT_MODE != 5) fetch(tile + 2);
+    const float* dt = dyt[cur];
+    const float* ab = at[cur];
 #pragma unroll
-    for (int i = 0; i < GS; ++i) {
-      const int rk = (t >> 1) + 256 * i;
-      if (rk < tk) *reinterpret_cast<float4*>(gl + rk * kCC + 4 * h4) = gr[i];
-    }
-#pragma unroll
-    for (int i = 0; i < DS; ++i) {
-      const int e = t + 512 * i;
-      dyt[(e % O) * TS + e / O] = dr[i];
-    }
-    float wc[RP][KM];
-#pragma unroll
-    for (int p2 = 0; p2 < RP; ++p2)
-#pragma unroll
-      for (int k = 0; k < KM; ++k) wc[p2][k] = wr[p2][k];
-    __syncthreads();
-    if (row0 + TR < rend) fetch(row0 + TR);
-#pragma unroll
-    for (int p2 = 0; p2 < RP; ++p2) {
-      float a[kCC];
-      build_row<KM>(gl, rb + 32 * p2, kk, wc[p2], a);
-#pragma unroll
-      for (int c = 0; c < kCC; ++c) at[(c * kW + w) * TS + rb + 32 * p2] = a[c];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int gb = 0; gb < TR / 8; ++gb) {
-      const float4 bv = *reinterpret_cast<const float4*>(at + (nt * 32 + l32) * TS + 8 * gb + 4 * half);
+    for (int gb = 0; gb < TR / 8 && KDPC_WGT_MODE != 1; ++gb) {
+      const float4 bv = *reinterpret_cast<const float4*>(ab + (nt * 32 + l32) * TS + 8 * gb + 4 * half);
 #pragma unroll
       for (int i = 0; i < MPW; ++i) {
         const float4 av =
-            *reinterpret_cast<const float4*>(dyt + ((m0 + i) * 32 + l32) * TS + 8 * gb + 4 * half);
+            *reinterpret_cast<const float4*>(dt + ((m0 + i) * 32 + l32) * TS + 8 * gb + 4 * half);
         acc[i] = mfma4(av, bv, acc[i]);
       }
     }
+    if (KDPC_WGT_MODE != 2 && KDPC_WGT_MODE != 5) build(cur ^ 1);
+    __syncthreads();  // at[cur] / dyt[cur] / gl consumed; at[cur ^ 1] complete
+    if (KDPC_WGT_MODE != 4 && KDPC_WGT_MODE != 5) stage(cur);  // tile + 2
+    __syncthreads();
   }
   const long long col = (long long)c0 * kW + nt * 32 + l32;
   if (col >= c16) return;
@@ -781,24 +888,18 @@ bool plan_of(int b, int s, int k, int d, int o, Plan* p) {
   channel_split(p->nch, p->rt, &p->ks, &p->cps);
   channel_split(p->nch, divup(p->r, 32), &p->bks, &p->bcps);
   // bwd-weight row splits: every (chunk, split) workgroup carries the same MFMA work and
-  // all of them are resident at once, so the kernel takes (most workgroups on one CU) x
-  // (rows per split) / efficiency; pick the split count minimising that (the old fixed
-  // target of 512 made 520 workgroups: 3 on a few CUs, 2 on the rest).  Multiples of 8 keep
-  // the XCD mapping (a split's chunks share its dy / wt rows in one L2) unless >6% slower.
-  const int t32 = std::max(1, divup(p->r, 32));
-  const int per_cu = o == 128 ? 1 : (o == 256 ? 2 : 3);  // resident 512-thread workgroups (LDS)
-  const int cap = std::max(1, std::min(t32, kCUs * per_cu / p->nch));
-  // measured (level-0 estimator, O = 128, 15 chunks): 255 workgroups (1 per CU) 477 us,
-  // 520 (2-3 per CU) 597 us, 765 (3 per CU) 777 us -- co-resident workgroups slow each
-  // other down (L2 / LDS contention) more than they overlap: fewer, longer splits
+  // all of them are resident at once (one 512-thread workgroup per CU: the pipelined kernel
+  // double-buffers its operands in 90-158 KB of LDS), so the kernel takes (workgroups on the
+  // busiest CU) x (tiles per split); pick the split count minimising that.  Multiples of 8
+  // keep the XCD mapping (a split's chunks share its dy / wt rows in one L2) unless >6%
+  // slower.  (round 1, unpipelined: 2-3 co-resident workgroups per CU ran slower than one.)
+  const int trw = km_of(k) <= 9 ? (o == 256 ? 32 : 64) : (o == 64 ? 64 : 32);
+  const int t32 = std::max(1, divup(p->r, trw));
+  const int cap = std::max(1, std::min(t32, kCUs / p->nch));
   auto cost = [&](int rs) {
     const int rps = divup(t32, rs);
     const int per = divup(p->nch * divup(t32, rps), kCUs);
-    // O = 64 has half the MFMA work per gathered row: there the gathers dominate and more
-    // co-resident workgroups hide them (252 workgroups 300 us vs 486: 206 us)
-    const double eff = o >= 128 ? (per >= 3 ? 0.6 : (per == 2 ? 0.8 : 1.0))
-                                : (per >= 3 ? 1.0 : (per == 2 ? 0.9 : 0.65));
-    return per * rps / eff;
+    return (double)per * (rps + 2);  // + the pipeline's prologue
   };
   int best = 1, best8 = 0;
   for (int rs = 1; rs <= cap; ++rs) {
@@ -806,12 +907,10 @@ bool plan_of(int b, int s, int k, int d, int o, Plan* p) {
     if (rs % 8 == 0 && (best8 == 0 || cost(rs) < cost(best8))) best8 = rs;
   }
   const int rs = (best8 > 0 && cost(best8) <= 1.06 * cost(best)) ? best8 : best;
-  p->rps = divup(t32, rs) * 32;
+  p->rps = divup(t32, rs) * trw;
   p->rs = std::max(1, divup(p->r, p->rps));
-  // (padding the split count up to a multiple of 8 for the XCD mapping was tried: 272
-  // workgroups put 2 on some CUs, 661 vs 477 us at level 0 -- balance beats L2 locality)
-  p->xcd = (p->rs >= 8 && p->rs % 8 == 0) ? 1 : 0;
-  p->wgs = p->nch * p->rs;
+  p->xcd = 1;
+  p->wgs = divup(p->nch * p->rs, 8) * 8;  // XCD fill: a multiple of 8 workgroups
   const size_t c16 = (size_t)p->c * kW;
   p->fwd_slab = p->ks > 1 ? align256((size_t)p->ks * p->r * o * 4) : 0;
   p->dgr = align256((size_t)p->r * k * p->c8 * 4);

@@ -41,10 +41,14 @@ def timeit(fn, iters=10, warmup=2):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default=None)
+    ap.add_argument("--only", default=None, help="substring of the shape names to run")
+    ap.add_argument("--iters", type=int, default=10)
     args = ap.parse_args()
     res = {}
     g = torch.Generator(device="cpu").manual_seed(0)
     for name, (B, N, S, Kn, D, O) in SHAPES.items():
+        if args.only and args.only not in name:
+            continue
         xyz = torch.randn(B, N, 3, generator=g).to(DEV)
         center = xyz[:, :S].contiguous()
         feats = torch.randn(B, N, D, generator=g).to(DEV)
@@ -55,8 +59,9 @@ def main():
         bias = torch.randn(O, generator=g).to(DEV)
         dy = torch.randn(B, S, O, generator=g).to(DEV)
         csr = K.csr_of(idx, N)
-        fwd = timeit(lambda: K.pointconv_fwd(xyz, center, feats, idx, wt, wl, bias))
-        bwd = timeit(lambda: K.pointconv_bwd(xyz, center, feats, idx, wt, wl, dy, csr, need_xyz=False))
+        fwd = timeit(lambda: K.pointconv_fwd(xyz, center, feats, idx, wt, wl, bias), args.iters)
+        bwd = timeit(lambda: K.pointconv_bwd(xyz, center, feats, idx, wt, wl, dy, csr,
+                                             need_xyz=False), args.iters)
         R = B * S
         gemm = 2.0 * R * 16 * C * O
         build = 2.0 * R * Kn * C * 16
