@@ -36,6 +36,12 @@ CFLAGS = [
 ]
 
 
+# per-source extra flags.  cost_volume.hip: no SLP packing (v_pk_fma pairs of independent
+# accumulators force their LDS operands into adjacent registers, hoisted in bulk: the
+# backward kernel went from 182 to >256 VGPRs with it)
+EXTRA_FLAGS = {"cost_volume.hip": ["-fno-slp-vectorize"]}
+
+
 def source_files(csrc=CSRC, root=ROOT):
     """Every file the library is built from, in a fixed order."""
     return (sorted(glob.glob(os.path.join(csrc, "*.hip"))) +
@@ -64,12 +70,13 @@ def _compile(src, headers_digest, tool):
     with open(src, "rb") as f:
         h.update(f.read())
     h.update(headers_digest.encode())
-    h.update(" ".join(CFLAGS).encode())
+    flags = CFLAGS + EXTRA_FLAGS.get(os.path.basename(src), [])
+    h.update(" ".join(flags).encode())
     h.update(tool.encode())
     obj = os.path.join(OBJ, f"{os.path.basename(src)}.{h.hexdigest()[:16]}.o")
     if not os.path.exists(obj):
         tmp = obj + ".tmp"
-        r = subprocess.run([HIPCC] + CFLAGS + ["-c", src, "-o", tmp], capture_output=True,
+        r = subprocess.run([HIPCC] + flags + ["-c", src, "-o", tmp], capture_output=True,
                            text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")

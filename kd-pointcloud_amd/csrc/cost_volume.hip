@@ -25,6 +25,8 @@
 //                                       fixed order by a second kernel)
 // Supported: D_IN, D_OUT in {32, 64}, K <= 32 (the K=32 levels 0-1 of the models; the
 // small levels 2-3 with D >= 128 keep the unfused path).
+#include <algorithm>
+
 #include "kdpc_common.h"
 
 using namespace kdpc;
@@ -179,8 +181,27 @@ __global__ __launch_bounds__(256) void cost_volume_fwd_kernel(
 }
 
 // ------------------------------------------------------------------------------ backward
+// One wave per query, queries walked in a software pipeline: the next query's loads (its
+// neighbour indices one query further ahead, then its P2 rows, directions, P1 row, output,
+// output gradient and argmax) are issued as soon as the current query's h0 is built, so
+// they land under the current query's MFMAs and channel loops.  One LDS tile per wave
+// holds h0 and is overwritten in place by dz0 (h0 is last read by the dW1 update).
+//
+// Lane layouts.  L (gathers, row passes): lane = (sub, c), c = lane % D_IN, rows RPP*i + sub.
+// MFMA accumulator: lane (half, l32), tile t: column 32t + l32, rows (e&3) + 8(e>>2) + 4 half.
+// Row-per-lane (direction gradients): lane l32 = neighbour row, the two halves split the
+// channels.  D_IN = 32: the halves of L split the rows and the dW1 rows, nothing idles.
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+constexpr unsigned kOOB = 0x80000000u;  // out-of-range byte offset: loads read 0, stores drop
+
 template <int D_IN, int D_OUT>
-__global__ __launch_bounds__(256) void cost_volume_bwd_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D_IN == 32 ? 2 : 1)))
+void cost_volume_bwd_kernel(
     int n1, int n2, int k, int queries_per_wave, const float* __restrict__ x1,
     const float* __restrict__ x2, const int* __restrict__ idx, const float* __restrict__ p1,
     const float* __restrict__ p2, const float* __restrict__ wpos, const float* __restrict__ bpos,
@@ -188,133 +209,199 @@ __global__ __launch_bounds__(256) void cost_volume_bwd_kernel(
     const unsigned char* __restrict__ amax, const float* __restrict__ dout,
     float* __restrict__ dp1, float* __restrict__ dp2_rows, float* __restrict__ dx1,
     float* __restrict__ ddir_rows, float* __restrict__ slab) {
-  constexpr int LD = D_IN + 1;
-  constexpr int RPP = 64 / D_IN;
-  constexpr int TI = D_IN / 32;  // 32-column tiles of dh0
+  constexpr int LD = D_IN + 1;            // odd row stride: row-per-lane reads hit 32 banks
+  constexpr int RPP = 64 / D_IN;          // layout-L rows per pass
+  constexpr int RT = kRows / RPP;         // layout-L passes
+  constexpr int TI = D_IN / 32;           // 32-column tiles of dh0
+  constexpr int DPL = RPP == 2 ? D_OUT / 2 : D_OUT;  // dW1 rows per lane
+  constexpr int CPH = D_IN / 2;           // channels per half in the row-per-lane pass
   constexpr int SLAB = D_OUT * D_IN + D_OUT + 4 * D_IN;
-  constexpr int PER_WAVE = 2 * kRows * LD;
-  // the per-wave h0 / dh0 tiles and, after the query loop, the workgroup's partial-sum
-  // buffer share one LDS block (2 workgroups per CU instead of 1)
-  constexpr int LDS_FLOATS = kWaves * (PER_WAVE > SLAB ? PER_WAVE : SLAB);
-  __shared__ float lds_all[LDS_FLOATS];
+  constexpr int TILE = kRows * LD;
+  constexpr int PER_WAVE = TILE + 4 * kRows + 2 * D_OUT;  // h0/dz0, directions, (g', argmax)
+  constexpr int SHARED = 4 * D_IN;                         // Wpos rows (x, y, z, 0)
+  constexpr int BODY = SHARED + kWaves * PER_WAVE;
+  constexpr int LDS_FLOATS = BODY > SLAB ? BODY : SLAB;
+  static_assert(TILE % 4 == 0 && PER_WAVE % 4 == 0, "16-byte aligned LDS tables");
+  __shared__ __attribute__((aligned(16))) float lds_all[LDS_FLOATS];
   const int b = blockIdx.y;
   const int wave = threadIdx.x >> 6;
   const int lane = lane_id();
   const int half = lane >> 5, l32 = lane & 31;
-  float* lds_h = lds_all + wave * PER_WAVE;
-  float* lds_d = lds_h + kRows * LD;
-  // B fragments of W1 for dh0 = M W1 (inner index d = output channel): lane l supplies
-  // W1[2s + half][32t + l32]
+  const int c = lane % D_IN, sub = lane / D_IN;
+  const int dl = lane % D_OUT;
+  float4* wposT = reinterpret_cast<float4*>(lds_all);
+  float* T = lds_all + SHARED + wave * PER_WAVE;
+  float4* dirT = reinterpret_cast<float4*>(T + TILE);
+  float2* gdam = reinterpret_cast<float2*>(T + TILE + 4 * kRows);
+  for (int e = threadIdx.x; e < D_IN; e += blockDim.x)
+    wposT[e] = make_float4(wpos[e * 3 + 0], wpos[e * 3 + 1], wpos[e * 3 + 2], 0.f);
+  __syncthreads();
+
+  // B fragments of W1 for dh0 = M W1 (inner index d): lane supplies W1[2s + half][32t + l32]
   float bwt[TI][D_OUT / 2];
 #pragma unroll
   for (int t = 0; t < TI; ++t)
 #pragma unroll
     for (int s2 = 0; s2 < D_OUT / 2; ++s2) bwt[t][s2] = w1[(2 * s2 + half) * D_IN + 32 * t + l32];
+  const float w0 = wpos[c * 3 + 0], wy = wpos[c * 3 + 1], wz = wpos[c * 3 + 2], bp = bpos[c];
+
   const float* x1b = x1 + (long long)b * n1 * 3;
-  const float* x2b = x2 + (long long)b * n2 * 3;
-  const int* idxb = idx + (long long)b * n1 * k;
-  const float* p1b = p1 + (long long)b * n1 * D_IN;
-  const float* p2b = p2 + (long long)b * n2 * D_IN;
-  const int c = lane % D_IN;
-  const int sub = lane / D_IN;
-  // per-lane parameter-gradient accumulators (lane c < D_IN; lanes >= D_IN of the D_IN=32
-  // case duplicate and are ignored at the end)
-  float gw1[D_OUT];
+  const __amdgpu_buffer_rsrc_t x2r = rsrc_of(x2 + (long long)b * n2 * 3, (long long)n2 * 12);
+  const __amdgpu_buffer_rsrc_t ixr = rsrc_of(idx + (long long)b * n1 * k, (long long)n1 * k * 4);
+  const __amdgpu_buffer_rsrc_t p1r = rsrc_of(p1 + (long long)b * n1 * D_IN, (long long)n1 * D_IN * 4);
+  const __amdgpu_buffer_rsrc_t p2r = rsrc_of(p2 + (long long)b * n2 * D_IN, (long long)n2 * D_IN * 4);
+  const long long ob0 = (long long)b * n1 * D_OUT;
+  const __amdgpu_buffer_rsrc_t outr = rsrc_of(out + ob0, (long long)n1 * D_OUT * 4);
+  const __amdgpu_buffer_rsrc_t dor = rsrc_of(dout + ob0, (long long)n1 * D_OUT * 4);
+  const __amdgpu_buffer_rsrc_t amr = rsrc_of(amax + ob0, (long long)n1 * D_OUT);
+
+  // parameter-gradient accumulators: gw1[i] = dW1[d0 + i][c]; gwp / gbp per (c, row parity)
+  const int d0 = RPP == 2 ? sub * (D_OUT / 2) : 0;
+  float gw1[DPL];
 #pragma unroll
-  for (int d = 0; d < D_OUT; ++d) gw1[d] = 0.f;
+  for (int i = 0; i < DPL; ++i) gw1[i] = 0.f;
   float gb1 = 0.f, gwp0 = 0.f, gwp1 = 0.f, gwp2 = 0.f, gbp = 0.f;
 
   const int q0 = (blockIdx.x * kWaves + wave) * queries_per_wave;
-  for (int qi = 0; qi < queries_per_wave; ++qi) {
-    const int n = q0 + qi;
-    if (n >= n1) break;
-    int j;
-    float dx, dy, dz;
-    build_h0<D_IN>(n, k, x1b, x2b, idxb, p1b, p2b, wpos, bpos, lds_h, j, dx, dy, dz);
-    // g'[d] = dout[d] * LeakyReLU'(z1[am[d], d]); sign(z1) at the argmax == sign(out[d])
-    const long long ob = ((long long)b * n1 + n) * D_OUT;
-    const int dl = lane % D_OUT;
-    const float od = out[ob + dl];
-    const float gd_l = dout[ob + dl] * (od > 0.f ? 1.f : kSlope);
-    const int am_l = amax[ob + dl];
-    // dh0 = M W1 on the matrix cores, M[r][d] = g'[d] [am[d] == r] (one nonzero per column):
-    // the MFMA's f32 accumulation is the fma chain over ascending d, i.e. the same sums as
-    // scattering g'[d] W1[d, :] into row am[d] in ascending d
+  const int q1 = min(n1, q0 + queries_per_wave);
+  // prefetched state of the next query
+  int jn = 0;                 // lane r: its neighbour index (query n + 1 during query n)
+  float pv[RT];               // layout L: P2[j_r][c]
+  float xv0, xv1, xv2;        // lane r: x2[j_r]
+  float p1v, outv, doutv;
+  unsigned amv;
+  // No per-row masks on the load offsets (they would be hoisted out of the query loop as
+  // per-row registers): past-the-end offsets read 0 through the buffers' bounds, and the
+  // neighbour slots r >= k read some valid row (the next query's indices, or row 0) whose
+  // h0 row only ever meets zeros (no argmax points there; its dz0 row is dh0 = 0).
+  auto load_idx = [&](int n) {
+    jn = (int)__builtin_amdgcn_raw_buffer_load_b32(ixr, (int)(((unsigned)n * (unsigned)k + lane) * 4u), 0, 0);
+  };
+  auto issue = [&](int n) {  // loads of query n (jn = its indices)
+    const unsigned xo = (unsigned)jn * 12u;
+    xv0 = bload(x2r, xo);
+    xv1 = bload(x2r, xo + 4u);
+    xv2 = bload(x2r, xo + 8u);
+#pragma unroll
+    for (int i = 0; i < RT; ++i) {
+      int j;
+      if (RPP == 1) {
+        j = __builtin_amdgcn_readlane(jn, i);
+      } else {
+        const int ja = __builtin_amdgcn_readlane(jn, 2 * i), jb = __builtin_amdgcn_readlane(jn, 2 * i + 1);
+        j = sub ? jb : ja;
+      }
+      pv[i] = bload(p2r, ((unsigned)j * D_IN + c) * 4u);
+    }
+    p1v = bload(p1r, ((unsigned)n * D_IN + c) * 4u);
+    const unsigned oo = (unsigned)n * D_OUT + dl;
+    outv = bload(outr, oo * 4u);
+    doutv = bload(dor, oo * 4u);
+    amv = __builtin_amdgcn_raw_buffer_load_b8(amr, (int)oo, 0, 0);
+  };
+  load_idx(q0);
+  issue(q0);
+  load_idx(q0 + 1);
+
+  for (int n = q0; n < q1; ++n) {
+    // ---- h0 of query n into T (layout L), directions into dirT, (g', argmax) into gdam
+    const float qx = x1b[n * 3 + 0], qy = x1b[n * 3 + 1], qz = x1b[n * 3 + 2];
+    if (lane < kRows) dirT[lane] = make_float4(xv0 - qx, xv1 - qy, xv2 - qz, 0.f);
+    if (lane < D_OUT)
+      gdam[lane] = make_float2(doutv * (outv > 0.f ? 1.f : kSlope), __int_as_float((int)amv));
+    const float gd_l = doutv * (outv > 0.f ? 1.f : kSlope);
+#pragma unroll
+    for (int i = 0; i < RT; ++i) {
+      const int r = RPP * i + sub;
+      const float4 dr = dirT[r];
+      const float pos = __fadd_rn(__builtin_fmaf(wz, dr.z, __builtin_fmaf(wy, dr.y, __fmul_rn(w0, dr.x))), bp);
+      T[r * LD + c] = lrelu(__fadd_rn(__fadd_rn(pv[i], p1v), pos));
+      if (i % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- the next query's loads, in flight during this query's compute
+    issue(n + 1);
+    load_idx(n + 2);
+    __builtin_amdgcn_sched_barrier(0);
+
+    // ---- dh0 = M W1 on the matrix cores, M[r][d] = g'[d] [am[d] == r]: the MFMA's f32
+    // accumulation is the fma chain over ascending d, i.e. the same sums as scattering
+    // g'[d] W1[d, :] into row am[d] in ascending d
     f32x16 dacc[TI];
 #pragma unroll
     for (int t = 0; t < TI; ++t) dacc[t] = f32x16{0};
 #pragma unroll
     for (int s2 = 0; s2 < D_OUT / 2; ++s2) {
-      const float g_lo = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gd_l), 2 * s2));
-      const float g_hi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gd_l), 2 * s2 + 1));
-      const int r_lo = __builtin_amdgcn_readlane(am_l, 2 * s2);
-      const int r_hi = __builtin_amdgcn_readlane(am_l, 2 * s2 + 1);
-      const float a = half ? (r_hi == l32 ? g_hi : 0.f) : (r_lo == l32 ? g_lo : 0.f);
+      const float2 ga = gdam[2 * s2 + half];
+      const float a = __float_as_int(ga.y) == l32 ? ga.x : 0.f;
 #pragma unroll
       for (int t = 0; t < TI; ++t)
         dacc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bwt[t][s2], dacc[t], 0, 0, 0);
     }
+    // ---- dW1[d, c] += g'[d] h0[am[d], c] (reads h0 before dz0 overwrites it)
+#pragma unroll
+    for (int i = 0; i < DPL; ++i) {
+      const float2 ga = gdam[d0 + i];
+      gw1[i] = __builtin_fmaf(ga.x, T[__float_as_int(ga.y) * LD + c], gw1[i]);
+      if (i % 8 == 7) __builtin_amdgcn_sched_barrier(0);  // bound the hoisted LDS reads
+    }
+    if (lane < D_OUT) gb1 += gd_l;
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- dz0 = dh0 * LeakyReLU'(h0), in place (accumulator layout)
 #pragma unroll
     for (int t = 0; t < TI; ++t)
 #pragma unroll
-      for (int e = 0; e < 16; ++e)
-        lds_d[((e & 3) + 8 * (e >> 2) + 4 * half) * LD + 32 * t + l32] = dacc[t][e];
-    // dW1[d, :] += g'[d] * h0[am[d], :]
-#pragma unroll
-    for (int d = 0; d < D_OUT; ++d) {
-      const float gd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gd_l), d));
-      const int r = __builtin_amdgcn_readlane(am_l, d);
-      gw1[d] = __builtin_fmaf(gd, lds_h[r * LD + c], gw1[d]);
-    }
-    __builtin_amdgcn_wave_barrier();
-    if (lane < D_OUT) gb1 += gd_l;
-    __builtin_amdgcn_wave_barrier();
-    // dz0 = dh0 * LeakyReLU'(h0) in place; rows written out; per-lane channel sums
+      for (int e = 0; e < 16; ++e) {
+        const int a = ((e & 3) + 8 * (e >> 2) + 4 * half) * LD + 32 * t + l32;
+        const float hv = T[a];
+        T[a] = dacc[t][e] * (hv > 0.f ? 1.f : kSlope);
+        if (e % 8 == 7) __builtin_amdgcn_sched_barrier(0);
+      }
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- row pass (layout L): dP2 rows out; dP1, dWpos, dbpos channel sums
     float dp1_acc = 0.f;
-    for (int r0 = 0; r0 < kRows; r0 += RPP) {
-      const int r = r0 + sub;
-      if (r < k) {
-        const float hv = lds_h[r * LD + c];
-        const float dz0 = lds_d[r * LD + c] * (hv > 0.f ? 1.f : kSlope);
-        lds_d[r * LD + c] = dz0;
-        dp2_rows[(((long long)b * n1 + n) * k + r) * D_IN + c] = dz0;
-      }
+    float* dp2n = dp2_rows + (((long long)b * n1 + n) * k) * D_IN + c;
+#pragma unroll 4
+    for (int r = sub; r < k; r += RPP) {  // rows >= k are zero
+      const float v = T[r * LD + c];
+      const float4 dr = dirT[r];
+      dp2n[r * D_IN] = v;
+      dp1_acc = __fadd_rn(dp1_acc, v);
+      gwp0 = __builtin_fmaf(v, dr.x, gwp0);
+      gwp1 = __builtin_fmaf(v, dr.y, gwp1);
+      gwp2 = __builtin_fmaf(v, dr.z, gwp2);
+      gbp = __fadd_rn(gbp, v);
     }
-    __builtin_amdgcn_wave_barrier();
-    // channel sums over rows in ascending order (every lane runs the loop so the row
-    // broadcasts are wave-uniform; only sub==0 lanes own a channel)
-    for (int r = 0; r < k; ++r) {
-      const float rdx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dx), r));
-      const float rdy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dy), r));
-      const float rdz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dz), r));
-      const float dzv = lds_d[r * LD + c];
-      dp1_acc = __fadd_rn(dp1_acc, dzv);
-      gwp0 = __builtin_fmaf(dzv, rdx, gwp0);
-      gwp1 = __builtin_fmaf(dzv, rdy, gwp1);
-      gwp2 = __builtin_fmaf(dzv, rdz, gwp2);
-      gbp = __fadd_rn(gbp, dzv);
-    }
+    if (RPP == 2) dp1_acc = __fadd_rn(dp1_acc, __shfl_xor(dp1_acc, 32, kWave));
     if (sub == 0) dp1[((long long)b * n1 + n) * D_IN + c] = dp1_acc;
-    // d(dir_r) = Wpos^T dz0[r]   (lane r owns row r; ascending channel order)
+    // ---- d(dir_r) = Wpos^T dz0[r] (lane l32 = row, halves split the channels)
     float g0 = 0.f, g1 = 0.f, g2 = 0.f;
-    if (lane < k) {
-      for (int cc = 0; cc < D_IN; ++cc) {
-        const float dzv = lds_d[lane * LD + cc];
-        g0 = __builtin_fmaf(wpos[cc * 3 + 0], dzv, g0);
-        g1 = __builtin_fmaf(wpos[cc * 3 + 1], dzv, g1);
-        g2 = __builtin_fmaf(wpos[cc * 3 + 2], dzv, g2);
-      }
+#pragma unroll
+    for (int i = 0; i < CPH; ++i) {
+      const int cc = half * CPH + i;
+      const float v = T[l32 * LD + cc];
+      const float4 wp = wposT[cc];
+      g0 = __builtin_fmaf(wp.x, v, g0);
+      g1 = __builtin_fmaf(wp.y, v, g1);
+      g2 = __builtin_fmaf(wp.z, v, g2);
+      if (i % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+    g0 = __fadd_rn(g0, __shfl_xor(g0, 32, kWave));
+    g1 = __fadd_rn(g1, __shfl_xor(g1, 32, kWave));
+    g2 = __fadd_rn(g2, __shfl_xor(g2, 32, kWave));
+    const bool row = lane < k;  // lanes >= 32 never (k <= 32)
+    if (row) {
       float* dd = ddir_rows + (((long long)b * n1 + n) * k + lane) * 3;
       dd[0] = g0;
       dd[1] = g1;
       dd[2] = g2;
     }
-    // dx1[n] = -sum_r d(dir_r), ascending r (uniform broadcasts, lane 0 stores)
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-    for (int r = 0; r < k; ++r) {
-      s0 = __fadd_rn(s0, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(g0), r)));
-      s1 = __fadd_rn(s1, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(g1), r)));
-      s2 = __fadd_rn(s2, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(g2), r)));
+    // ---- dx1[n] = -sum_r d(dir_r) (butterfly over the 32 row lanes)
+    float s0 = row ? g0 : 0.f, s1 = row ? g1 : 0.f, s2 = row ? g2 : 0.f;
+#pragma unroll
+    for (int m = 16; m >= 1; m >>= 1) {
+      s0 = __fadd_rn(s0, __shfl_xor(s0, m, kWave));
+      s1 = __fadd_rn(s1, __shfl_xor(s1, m, kWave));
+      s2 = __fadd_rn(s2, __shfl_xor(s2, m, kWave));
     }
     if (lane == 0) {
       float* o = dx1 + ((long long)b * n1 + n) * 3;
@@ -322,31 +409,46 @@ __global__ __launch_bounds__(256) void cost_volume_bwd_kernel(
       o[1] = -s1;
       o[2] = -s2;
     }
-    __builtin_amdgcn_wave_barrier();
   }
-  // workgroup partials: waves write their accumulators, wave 0 sums them in wave order
-  __syncthreads();  // every wave is done with its h0/dh0 tiles (the buffer is reused)
-  float* rw = lds_all + wave * SLAB;
-  if (sub == 0) {
+  // ---- workgroup partials: waves add their accumulators into one LDS slab in wave order
+  if (RPP == 2) {  // fold the row-parity halves of the channel sums
+    gwp0 = __fadd_rn(gwp0, __shfl_xor(gwp0, 32, kWave));
+    gwp1 = __fadd_rn(gwp1, __shfl_xor(gwp1, 32, kWave));
+    gwp2 = __fadd_rn(gwp2, __shfl_xor(gwp2, 32, kWave));
+    gbp = __fadd_rn(gbp, __shfl_xor(gbp, 32, kWave));
+  }
+  __syncthreads();  // every wave is done with its tiles (the buffer is reused)
+  float* rw = lds_all;
+  for (int w = 0; w < kWaves; ++w) {
+    if (wave == w) {
 #pragma unroll
-    for (int d = 0; d < D_OUT; ++d) rw[d * D_IN + c] = gw1[d];
-    rw[D_OUT * D_IN + D_OUT + 0 * D_IN + c] = gwp0;
-    rw[D_OUT * D_IN + D_OUT + 1 * D_IN + c] = gwp1;
-    rw[D_OUT * D_IN + D_OUT + 2 * D_IN + c] = gwp2;
-    rw[D_OUT * D_IN + D_OUT + 3 * D_IN + c] = gbp;
+      for (int i = 0; i < DPL; ++i) {
+        float* e = rw + (d0 + i) * D_IN + c;
+        *e = w ? __fadd_rn(*e, gw1[i]) : gw1[i];
+      }
+      if (lane < D_OUT) {
+        float* e = rw + D_OUT * D_IN + lane;
+        *e = w ? __fadd_rn(*e, gb1) : gb1;
+      }
+      if (sub == 0) {
+        const float v4[4] = {gwp0, gwp1, gwp2, gbp};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float* e = rw + D_OUT * D_IN + D_OUT + q * D_IN + c;
+          *e = w ? __fadd_rn(*e, v4[q]) : v4[q];
+        }
+      }
+    }
+    __syncthreads();
   }
-  if (lane < D_OUT) rw[D_OUT * D_IN + lane] = gb1;
-  __syncthreads();
   float* sb = slab + ((long long)blockIdx.y * gridDim.x + blockIdx.x) * SLAB;
-  for (int e = threadIdx.x; e < SLAB; e += blockDim.x) {
-    float v = lds_all[e];
-    for (int w = 1; w < kWaves; ++w) v = __fadd_rn(v, lds_all[w * SLAB + e]);
-    sb[e] = v;
-  }
+  for (int e = threadIdx.x; e < SLAB; e += blockDim.x) sb[e] = rw[e];
 }
 
 constexpr int kFwdQPW = 8;
-constexpr int kBwdQPW = 32;
+// backward queries per wave: enough waves for ~8 per SIMD over the launch (the workgroups'
+// partial slabs grow with the wave count; the pipeline amortises its prologue over the rest)
+inline int bwd_qpw(int b, int n1) { return std::max(2, (int)divupll((long long)b * n1, 8192)); }
 
 inline int slab_len(int din, int dout) { return dout * din + dout + 4 * din; }
 
@@ -368,9 +470,10 @@ hipError_t bwd_launch(int b, int n1, int n2, int k, const float* x1, const float
                       const unsigned char* amax, const float* dout, float* dp1, float* dp2_rows,
                       float* dx1, float* ddir_rows, float* slab, float* dparams,
                       hipStream_t st) {
-  dim3 grid(divup(n1, kWaves * kBwdQPW), b);
+  const int qpw = bwd_qpw(b, n1);
+  dim3 grid(divup(n1, kWaves * qpw), b);
   hipLaunchKernelGGL((cost_volume_bwd_kernel<DI, DO>), grid, dim3(256), 0, st, n1, n2, k,
-                     kBwdQPW, x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, dout, dp1,
+                     qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, dout, dp1,
                      dp2_rows, dx1, ddir_rows, slab);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -412,7 +515,7 @@ KDPC_API int kdpc_cost_volume_fwd(int b, int n1, int n2, int k, int din, int dou
 // Scratch for the backward's per-workgroup parameter-gradient slabs.
 KDPC_API size_t kdpc_cost_volume_bwd_workspace_bytes(int b, int n1, int din, int dout) {
   if (b <= 0 || n1 <= 0 || !supported(din, dout, 1)) return 0;
-  const long long nslabs = (long long)divup(n1, kWaves * kBwdQPW) * b;
+  const long long nslabs = (long long)divup(n1, kWaves * bwd_qpw(b, n1)) * b;
   const int len = slab_len(din, dout);
   return (size_t)(nslabs * len + colsum_scratch_floats((int)nslabs, len)) * sizeof(float);
 }
