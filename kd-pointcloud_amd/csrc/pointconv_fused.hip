@@ -38,6 +38,9 @@ using namespace kdpc;
 // diagnostic builds only (tools/build_variants.sh): 0 = the real kernel; weight-gradient
 // kernel with 2 no build, 3 no loads in the loop, 4 no staging, 5 MFMAs only,
 // 6 / 7 / 8 no WeightNet-weight / dy / gathered-feature loads
+#ifndef KDPC_DAT_MODE  // diagnostic variants of the data kernel (0 = the real kernel)
+#define KDPC_DAT_MODE 0
+#endif
 #ifndef KDPC_WGT_MODE
 #define KDPC_WGT_MODE 0
 #endif
@@ -354,20 +357,24 @@ __global__ __launch_bounds__(256) void pc_slab_sum_kernel(int nslabs, long long 
 
 // -------------------------------------------------------------------- backward: data
 // grid (TR-row tiles, channel splits), 256 threads; each thread owns (row, neighbour)
-// pairs t and t+256.  dgr: dG rows [R*K][C8].  (28-row tiles for K = 9 -- one pair per
-// thread instead of a second VALU pass for 32 lanes -- measured slower, 934 vs 854 us at
-// level 0: the kernel is bound by its MFMA / B-operand stream, not by the VALU phase.)
+// pairs t and t+256.  dgr: dG rows [R*K][C8].  Measured alternatives for K = 9 (flow0):
+// 28-row tiles, one pair per thread (934 vs 854 us, round 1); 320 threads, one pair each,
+// a fifth wave with no MFMA tile (931 us at 3 waves/SIMD with spills, 761 us at 2, vs 622):
+// the second pair pass of wave 0 is cheaper than the lost occupancy.
 template <int KM>
 constexpr int bwd_tile_rows() { return 32; }
+template <int KM>
+constexpr int bwd_threads() { return 256; }
 
 template <int O, int KM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
-void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float* __restrict__ wlt,
+__global__ __launch_bounds__(bwd_threads<KM>()) __attribute__((amdgpu_waves_per_eu(2)))
+void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __restrict__ wsw,
                         const float* __restrict__ dy, float* __restrict__ dgr,
                         float* __restrict__ dwt, float* __restrict__ dcenter,
                         int chunks_per_split) {
   constexpr int TR = bwd_tile_rows<KM>();
-  constexpr int PP = (TR * KM + 255) / 256;  // pairs per thread
+  constexpr int NT = bwd_threads<KM>();
+  constexpr int PP = (TR * KM + NT - 1) / NT;  // pairs per thread
   __shared__ __attribute__((aligned(16))) float dyl[(O / 4) * kBlk];
   __shared__ __attribute__((aligned(16))) float dal[32 * kDaS];
   __shared__ float dcl[TR * KM * 3];
@@ -380,7 +387,7 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float* __rest
   const long long rk_total = (long long)g.r * g.k;
   const Srcs src = srcs_of(g);
 
-  for (int e = t; e < 32 * O; e += 256) {
+  for (int e = t; e < 32 * O; e += NT) {
     const int r = e / O, o = e % O;
     const int row = row0 + r;
     dyl[(o >> 2) * kBlk + r * 4 + (o & 3)] =
@@ -390,7 +397,7 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float* __rest
   int pr[PP], pk[PP], pn[PP];
 #pragma unroll
   for (int q = 0; q < PP; ++q) {
-    const int p = t + 256 * q;
+    const int p = t + NT * q;
     pr[q] = p / g.k;
     pk[q] = p - pr[q] * g.k;
     const bool ok = p < TR * g.k && row0 + pr[q] < g.r;
@@ -410,120 +417,132 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float* __rest
   }
   __syncthreads();
 
-  const int n0 = wv * 32;  // this wave's 32 dA columns of the chunk
+  const bool mw = wv < 4;            // the MFMA waves (wave 4 of a 320-thread group: none)
+  const int n0 = (mw ? wv : 3) * 32;  // this wave's 32 dA columns of the chunk
   // Load order matters: loads and stores retire in issue order (vmcnt), so an MFMA waiting
   // on a B fragment also waits for every older gather and dG store.  Per chunk: the first
   // PF B blocks and the neighbour gathers of chunk ch+1 are issued right after chunk ch's
   // MFMAs -- before ch's dG stores -- so ch+1's first MFMAs wait only on those, and the
   // gathers land during ch's VALU phase (they are used in ch+1's VALU phase).
-  // B operand = the Linear weight column over the O outputs: one contiguous row of the
-  // transposed weight, float4 per lane and block, branch-free (clamped address + select).
+  // B operand = the Linear weight columns of the chunk over the O outputs, pre-swizzled by
+  // pc_swizzle_bwd_kernel into the order the waves read them: one wave's fragment of one
+  // 8-output group is 1 KiB contiguous (a transposed (16C, O) copy, read a float4 per lane
+  // from 32 different rows, fetched 2x its bytes from L2); zero past the last column.
   constexpr int NOG = O / 8;
   constexpr int PF = NOG < 4 ? NOG : 4;  // (16 ahead measured slower: 949 vs 854 us)
-  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   auto brow = [&](int ch) {
-    const int colg = ch * kCC * kW + n0 + l32;
-    return reinterpret_cast<const float4*>(wlt + (long long)((colg >> 4) < g.c ? colg : 0) * O);
+    return KDPC_DAT_MODE == 3 ? wsw + lane : wsw + (long long)((ch * 4 + n0 / 32) * NOG) * 64 + lane;
   };
-  auto bok = [&](int ch) { return ((ch * kCC * kW + n0 + l32) >> 4) < g.c; };
   float4 bq[PF];
   float gv[PP][kCC], gn[PP][kCC];
-  // a pair's 8 channels of a feature chunk are 32 contiguous bytes of its neighbour's row:
-  // two 16-byte buffer loads (dword-aligned; past-the-row lanes masked, past-the-buffer
-  // reads 0) instead of eight 4-byte ones; chunk 0 (xyz - center) stays per channel
+  // a pair's 8 channels of a chunk: two 16-byte buffer loads of its neighbour's feature row
+  // (dword-aligned; past-the-row lanes masked, past-the-buffer reads 0), plus, for chunk 0,
+  // xyz - center.  Branch-free: every chunk issues the same four loads (the xyz / center
+  // ones out of range except in chunk 0) and adds the xyz terms unconditionally, so no load
+  // sits under a branch (which would drain the load queue right behind it).
   auto gather = [&](int ch, float (&dst)[PP][kCC]) {
-    if (ch == 0) {
-#pragma unroll
-      for (int q = 0; q < PP; ++q)
-#pragma unroll
-        for (int c = 0; c < kCC; ++c) dst[q][c] = g_fetch(g, src, pn[q], row0 + pr[q], c);
-      return;
-    }
+    const bool c0 = ch == 0;
+    const unsigned lo_ch = c0 ? 0u : (unsigned)(ch * kCC - 3) * 4u;
+    const unsigned hi_ch = c0 ? 4u : lo_ch + 16u;
 #pragma unroll
     for (int q = 0; q < PP; ++q) {
-      const unsigned off = pn[q] < 0 ? kOOB : feat_off(g, pn[q]) + (unsigned)(ch * kCC - 3) * 4u;
+      const int nb = pn[q];
+      const bool live = nb >= 0;
+      const unsigned fo = (live && KDPC_DAT_MODE != 4) ? (unsigned)nb * (unsigned)g.d * 4u : kOOB;
       const f32x4 lo = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                     src.feats, (int)off, 0, 0));
+                                                     src.feats, (int)(fo + lo_ch), 0, 0));
       const f32x4 hi = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                     src.feats, (int)(off + 16u), 0, 0));
+                                                     src.feats, (int)(fo + hi_ch), 0, 0));
+      const unsigned xo = (c0 && live && KDPC_DAT_MODE != 4) ? (unsigned)nb * 12u : kOOB;
+      const unsigned co = (c0 && live) ? (unsigned)(row0 + pr[q]) * 12u : kOOB;
+      const f32x4 x = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                    src.xyz, (int)xo, 0, 0));
+      const f32x4 cc = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     src.center, (int)co, 0, 0));
+      float v[kCC];
 #pragma unroll
-      for (int c = 0; c < kCC; ++c) {
-        const float v = c < 4 ? lo[c] : hi[c - 4];
-        dst[q][c] = ch * kCC + c < g.c ? v : 0.f;
-      }
+      for (int c = 0; c < 3; ++c) v[c] = (c0 ? 0.f : lo[c]) + (x[c] - cc[c]);
+      v[3] = c0 ? lo[0] : lo[3];
+#pragma unroll
+      for (int c = 4; c < kCC; ++c) v[c] = hi[c - 4];
+#pragma unroll
+      for (int c = 0; c < kCC; ++c) dst[q][c] = ch * kCC + c < g.c ? v[c] : 0.f;
     }
   };
   if (ch0 < ch1) {
     const float4* wr0 = brow(ch0);
-    const bool ok0 = bok(ch0);
 #pragma unroll
-    for (int p2 = 0; p2 < PF; ++p2) {
-      const float4 v = wr0[2 * p2 + half];
-      bq[p2] = ok0 ? v : z4;
-    }
+    for (int p2 = 0; p2 < PF; ++p2) bq[p2] = wr0[p2 * 64];
     gather(ch0, gv);
   }
   for (int ch = ch0; ch < ch1; ++ch) {
     const int c0 = ch * kCC;
     const float4* wrow = brow(ch);
-    const bool ok = bok(ch);
     f32x16 acc = zero16();
+    if (mw) {  // wave-uniform
 #pragma unroll
-    for (int og = 0; og < NOG; ++og) {
-      const float4 av = *reinterpret_cast<const float4*>(dyl + (2 * og + half) * kBlk + l32 * 4);
-      acc = mfma4(av, bq[og % PF], acc);
-      if (og + PF < NOG) {
-        const float4 v = wrow[2 * (og + PF) + half];
-        bq[og % PF] = ok ? v : z4;
+      for (int og = 0; og < NOG; ++og) {
+        const float4 av = *reinterpret_cast<const float4*>(dyl + (2 * og + half) * kBlk + l32 * 4);
+        if (KDPC_DAT_MODE != 1) acc = mfma4(av, bq[og % PF], acc);
+        else acc[og & 15] += av.x * bq[og % PF].y;
+        if (og + PF < NOG) bq[og % PF] = wrow[(og + PF) * 64];
       }
     }
     if (ch + 1 < ch1) {
       const float4* wr1 = brow(ch + 1);
-      const bool ok1 = bok(ch + 1);
 #pragma unroll
-      for (int p2 = 0; p2 < PF; ++p2) {
-        const float4 v = wr1[2 * p2 + half];
-        bq[p2] = ok1 ? v : z4;
-      }
+      for (int p2 = 0; p2 < PF; ++p2) bq[p2] = wr1[p2 * 64];
       gather(ch + 1, gn);
     }
+    if (mw) {
 #pragma unroll
-    for (int e = 0; e < 16; ++e)
-      dal[((e & 3) + 8 * (e >> 2) + 4 * half) * kDaS + n0 + l32] = acc[e];
+      for (int e = 0; e < 16; ++e)
+        dal[((e & 3) + 8 * (e >> 2) + 4 * half) * kDaS + n0 + l32] = acc[e];
+    }
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < PP; ++q) {
+    for (int q = 0; q < PP && KDPC_DAT_MODE != 2; ++q) {
       if (pn[q] < 0) continue;
       const int r = pr[q];
       const long long pos = (long long)(row0 + r) * g.k + pk[q];
-      // the pair's 8 dG values are 32 contiguous (32-byte aligned) bytes: one 16-byte store
-      // per half-chunk of 4 channels (a fully unrolled 8-channel body spilled)
+      // the pair's 8 dG values are 32 contiguous (32-byte aligned) bytes: two 16-byte stores.
+      // Channel cl + 1's dA row is read from LDS while channel cl computes (the scheduling
+      // barrier keeps the compiler from hoisting further reads, which spilled).
       float4* dgo = reinterpret_cast<float4*>(dgr + pos * g.c8 + c0);
-#pragma unroll 1
-      for (int hc = 0; hc < 2; ++hc) {
-        float sv[4];
+      const float4* drow = reinterpret_cast<const float4*>(dal + r * kDaS);
+      float4 cur[kW / 4], nxt[kW / 4];
 #pragma unroll
-        for (int c4 = 0; c4 < 4; ++c4) {
-          const int cl = 4 * hc + c4;
-          float da[kW];
+      for (int v = 0; v < kW / 4; ++v) cur[v] = drow[v];
+      float sv[kCC];
 #pragma unroll
-          for (int v = 0; v < kW / 4; ++v) {
-            const float4 x = *reinterpret_cast<const float4*>(dal + r * kDaS + cl * kW + 4 * v);
-            da[4 * v + 0] = x.x;
-            da[4 * v + 1] = x.y;
-            da[4 * v + 2] = x.z;
-            da[4 * v + 3] = x.w;
-          }
-          float s = 0.f;
+      for (int cl = 0; cl < kCC; ++cl) {
+        if (cl + 1 < kCC) {
 #pragma unroll
-          for (int w = 0; w < kW; ++w) s = __builtin_fmaf(da[w], wp[q][w], s);
-          sv[c4] = s;
-          if (c0 == 0 && cl < 3) dcl[(r * g.k + pk[q]) * 3 + cl] = s;
-          const float gc = hc ? gv[q][4 + c4] : gv[q][c4];
-#pragma unroll
-          for (int w = 0; w < kW; ++w) dw[q][w] = __builtin_fmaf(da[w], gc, dw[q][w]);
+          for (int v = 0; v < kW / 4; ++v) nxt[v] = drow[(cl + 1) * (kW / 4) + v];
         }
-        dgo[hc] = make_float4(sv[0], sv[1], sv[2], sv[3]);
+        float da[kW];
+#pragma unroll
+        for (int v = 0; v < kW / 4; ++v) {
+          da[4 * v + 0] = cur[v].x;
+          da[4 * v + 1] = cur[v].y;
+          da[4 * v + 2] = cur[v].z;
+          da[4 * v + 3] = cur[v].w;
+        }
+        float sacc = 0.f;
+#pragma unroll
+        for (int w = 0; w < kW; ++w) sacc = __builtin_fmaf(da[w], wp[q][w], sacc);
+        sv[cl] = sacc;
+        if (c0 == 0 && cl < 3) dcl[(r * g.k + pk[q]) * 3 + cl] = sacc;
+        const float gc = gv[q][cl];
+#pragma unroll
+        for (int w = 0; w < kW; ++w) dw[q][w] = __builtin_fmaf(da[w], gc, dw[q][w]);
+#pragma unroll
+        for (int v = 0; v < kW / 4; ++v) cur[v] = nxt[v];
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (KDPC_DAT_MODE != 5) {
+        dgo[0] = make_float4(sv[0], sv[1], sv[2], sv[3]);
+        dgo[1] = make_float4(sv[4], sv[5], sv[6], sv[7]);
       }
     }
     __syncthreads();
@@ -553,21 +572,30 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float* __rest
   }
 }
 
-// wlt (16C, O) = wl (O, 16C)^T, 32x32 tiles through LDS
-__global__ __launch_bounds__(256) void pc_transpose_kernel(int rows, int cols,
-                                                           const float* __restrict__ src,
-                                                           float* __restrict__ dst) {
-  __shared__ float tile[32][33];
-  const int bx = blockIdx.x * 32, by = blockIdx.y * 32;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  for (int i = ty; i < 32; i += 8) {
-    const int r = by + i, c = bx + tx;
-    tile[i][tx] = (r < rows && c < cols) ? src[(long long)r * cols + c] : 0.f;
-  }
-  __syncthreads();
-  for (int i = ty; i < 32; i += 8) {
-    const int c = bx + i, r = by + tx;
-    if (c < cols && r < rows) dst[(long long)c * rows + r] = tile[tx][i];
+// wl (O, 16C) -> the data kernel's B operand order: float4 (ch, wave, og, lane) =
+// wl[8 og + 4 (lane >> 5) + 0..3][ch * 128 + 32 wave + (lane & 31)], zero past column 16C.
+// One thread per float4; a wave reads 32 consecutive columns of 4 rows (coalesced).
+__global__ __launch_bounds__(256) void pc_swizzle_bwd_kernel(int o, int c16, int nch,
+                                                             const float* __restrict__ wl,
+                                                             float4* __restrict__ wsw) {
+  const int nog = o / 8;
+  const long long total = (long long)nch * 4 * nog * 64;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int lane = (int)(e & 63);
+    const long long q = e >> 6;
+    const int og = (int)(q % nog);
+    const long long cw = q / nog;  // ch * 4 + wave
+    const int col = (int)(cw * 32) + (lane & 31);
+    const int o0 = 8 * og + 4 * (lane >> 5);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (col < c16) {
+      v.x = wl[(long long)(o0 + 0) * c16 + col];
+      v.y = wl[(long long)(o0 + 1) * c16 + col];
+      v.z = wl[(long long)(o0 + 2) * c16 + col];
+      v.w = wl[(long long)(o0 + 3) * c16 + col];
+    }
+    wsw[e] = v;
   }
 }
 
@@ -916,7 +944,7 @@ bool plan_of(int b, int s, int k, int d, int o, Plan* p) {
   p->dgr = align256((size_t)p->r * k * p->c8 * 4);
   p->dwt_slab = p->bks > 1 ? align256((size_t)p->bks * p->r * k * kW * 4) : 0;
   p->dwl_slab = p->rs > 1 ? align256((size_t)p->rs * o * c16 * 4) : 0;
-  p->wlt = align256((size_t)o * c16 * 4);
+  p->wlt = align256((size_t)p->nch * kNC * o * 4);  // swizzled B, padded to whole chunks
   return true;
 }
 
@@ -950,16 +978,17 @@ hipError_t bwd_launch(const Geo& g, const Plan& p, int b, const float* wt, const
   float* dgr = reinterpret_cast<float*>(ws);
   float* dwt_slab = reinterpret_cast<float*>(ws + p.dgr);
   float* dwl_slab = reinterpret_cast<float*>(ws + p.dgr + p.dwt_slab);
-  float* wlt = reinterpret_cast<float*>(ws + p.dgr + p.dwt_slab + p.dwl_slab);
+  float4* wsw = reinterpret_cast<float4*>(ws + p.dgr + p.dwt_slab + p.dwl_slab);
   const long long rk = (long long)p.r * g.k;
   const int c16 = g.c * kW;
-  hipLaunchKernelGGL(pc_transpose_kernel, dim3(divup(c16, 32), divup(O, 32)), dim3(256), 0, st,
-                     O, c16, wl, wlt);
+  const long long nsw = (long long)g.nch * 4 * (O / 8) * 64;
+  hipLaunchKernelGGL(pc_swizzle_bwd_kernel, dim3((unsigned)divupll(nsw, 256)), dim3(256), 0, st,
+                     O, c16, g.nch, wl, wsw);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((pc_bwd_data_kernel<O, KM>), dim3(divup(p.r, bwd_tile_rows<KM>()), p.bks),
-                     dim3(256), 0, st,
-                     g, wt, wlt, dy, dgr, p.bks > 1 ? dwt_slab : dwt, dcenter, p.bcps);
+                     dim3(bwd_threads<KM>()), 0, st,
+                     g, wt, wsw, dy, dgr, p.bks > 1 ? dwt_slab : dwt, dcenter, p.bcps);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (p.bks > 1 && (e = slab_sum(p.bks, rk * kW, dwt_slab, nullptr, 1, dwt, st)) != hipSuccess)
