@@ -23,3 +23,10 @@ def projection(name, grad):
     g = grad.detach().double().reshape(-1).cpu().numpy()
     r = projection_vectors(name, g.size)
     return list(r @ g), list(np.abs(r) @ np.abs(g))
+
+
+def flow_layer_weight(name, shape):
+    """The fixed output weighting of the flow-layer fixtures (make_fixtures.make_flow_layers;
+    the GPU test regenerates it): loss = sum(out * weight)."""
+    rng = np.random.default_rng([77, zlib.crc32(name.encode())])
+    return rng.normal(size=shape).astype(np.float32)

@@ -6,8 +6,8 @@ reference so CPU results are bitwise comparable with the reference run on CPU:
   * index_points via torch.gather            (reference: pointnet2 gather/group ext)
   * FPS: the C restatement (oracle/pointnet2_oracle.c) or, for the CPU baseline the
     north star names, a random subsample (the PointConvDRand pattern, pointconv_util.py:621)
-  * layers                                   pointconv_util.py:17-258,401-446,1791-1868,
-                                             2114-2256
+  * layers                                   pointconv_util.py:17-258,401-446,1474-1517,
+                                             1791-1868,2039-2256
   * PointConvBidirection                     models_bid_pointconv.py:14-207 (two clouds
                                              run separately, in reference order)
   * multiScaleLoss, biDirection_loss_ht      loss_functions.py:6-25, 83-96
@@ -207,6 +207,76 @@ class CrossLayerLight(nn.Module):
         f1 = self.cross_t1(f1)
         f2 = self.cross_t2(f2)
         return f1, f2, self.cross(pc1, pc2, f1, f2, self.pos2, self.mlp2, self.bn2)
+
+
+class FlowEmbeddingLayer(nn.Module):
+    """pointconv_util.py:1474-1517: the cross() cost volume with its own t11/t22/pos."""
+
+    def __init__(self, nsample, cin, mlp, bn=False, use_leaky=True):
+        super().__init__()
+        self.nsample = nsample
+        self.mlp = nn.ModuleList()
+        self.pos = nn.Conv2d(3, mlp[0], 1)
+        self.t11 = nn.Conv1d(cin, mlp[0], 1)
+        self.t22 = nn.Conv1d(cin, mlp[0], 1)
+        self.bias = nn.Parameter(torch.randn((1, mlp[0], 1, 1)))
+        self.bn = nn.Identity()
+        for a, b in zip(mlp[:-1], mlp[1:]):
+            self.mlp.append(Conv2d(a, b, use_leaky=use_leaky))
+        self.relu = _act(use_leaky)
+
+    def forward(self, xyz1, xyz2, points1, points2):
+        B, C, N1 = xyz1.shape
+        xyz1, xyz2 = xyz1.permute(0, 2, 1), xyz2.permute(0, 2, 1)
+        points1 = self.t11(points1).permute(0, 2, 1)
+        points2 = self.t22(points2).permute(0, 2, 1)
+        D1 = points1.shape[-1]
+        idx = knn_point(self.nsample, xyz2, xyz1)
+        direction = index_points_group(xyz2, idx) - xyz1.view(B, N1, 1, C)
+        g2 = index_points_group(points2, idx).permute(0, 3, 2, 1)
+        g1 = points1.view(B, N1, 1, D1).repeat(1, 1, self.nsample, 1).permute(0, 3, 2, 1)
+        h = self.relu(self.bn(g2 + g1 + self.pos(direction.permute(0, 3, 2, 1))))
+        for conv in self.mlp:
+            h = conv(h)
+        return F.max_pool2d(h, (h.size(2), 1)).squeeze(2)
+
+
+class PointConvFlow(nn.Module):
+    """pointconv_util.py:2039-2112: point-to-patch cost (MLP over [p1, p2[idx], dir], summed
+    with WeightNet weights over K) then patch-to-patch (the cost grouped over cloud 1's own
+    kNN, summed with a second WeightNet)."""
+
+    def __init__(self, nsample, cin, mlp, bn=False, use_leaky=True):
+        super().__init__()
+        self.nsample, self.bn = nsample, bn
+        self.mlp_convs = nn.ModuleList()
+        last = cin
+        for c in mlp:
+            self.mlp_convs.append(nn.Conv2d(last, c, 1))
+            last = c
+        self.weightnet1 = WeightNet(3, last)
+        self.weightnet2 = WeightNet(3, last)
+        self.relu = _act(use_leaky)
+
+    def forward(self, xyz1, xyz2, points1, points2):
+        B, C, N1 = xyz1.shape
+        D1 = points1.shape[1]
+        xyz1, xyz2 = xyz1.permute(0, 2, 1), xyz2.permute(0, 2, 1)
+        points1, points2 = points1.permute(0, 2, 1), points2.permute(0, 2, 1)
+        idx = knn_point(self.nsample, xyz2, xyz1)
+        direction = index_points_group(xyz2, idx) - xyz1.view(B, N1, 1, C)
+        g2 = index_points_group(points2, idx)
+        g1 = points1.view(B, N1, 1, D1).repeat(1, 1, self.nsample, 1)
+        h = torch.cat([g1, g2, direction], dim=-1).permute(0, 3, 2, 1)
+        for conv in self.mlp_convs:
+            h = self.relu(conv(h))
+        w = self.weightnet1(direction.permute(0, 3, 2, 1))
+        p2p = torch.sum(w * h, dim=2)
+        idx = knn_point(self.nsample, xyz1, xyz1)
+        direction = index_points_group(xyz1, idx) - xyz1.view(B, N1, 1, C)
+        w = self.weightnet2(direction.permute(0, 3, 2, 1))
+        grouped = index_points_group(p2p.permute(0, 2, 1), idx)
+        return torch.sum(w * grouped.permute(0, 3, 2, 1), dim=2)
 
 
 def _idw(grouped_xyz_norm, grouped_vals, B, N):

@@ -70,6 +70,61 @@ def test_layers_match_reference(golden):
     _close(flo, g["est_out_flow"], rtol=2e-5, name="estimator flow")
 
 
+@pytest.mark.parametrize("name", ["fe32", "fe64", "fe128", "pcf"])
+def test_flow_layers_match_reference(golden, name):
+    """FlowEmbeddingLayer (D 32 / 64: fused cost volume; 128: the wide path) and
+    PointConvFlow vs the reference at B=2, N=512: the output at 1e-5 of its scale, every input
+    and parameter gradient of sum(out * weight) at 1e-4 of its scale (the reference's CPU GEMMs
+    and the max-over-K routing accumulate in other orders)."""
+    import pointconv_util as P
+    from gradproj import flow_layer_weight
+    g = golden("flow_layers_ref.npz")
+    make = {"fe32": lambda: P.FlowEmbeddingLayer(32, 64, [32, 32]),
+            "fe64": lambda: P.FlowEmbeddingLayer(32, 64, [64, 64]),
+            "fe128": lambda: P.FlowEmbeddingLayer(16, 64, [128, 128]),
+            "pcf": lambda: P.PointConvFlow(16, 64 + 64 + 3, [64, 64])}[name]
+    seed = {"fe32": 51, "fe64": 52, "fe128": 53, "pcf": 54}[name]
+    layer = load_synthetic(make(), seed=seed).to(DEV)
+    x1 = _t(g["x1"].transpose(0, 2, 1)).permute(0, 2, 1)
+    x2 = _t(g["x2"].transpose(0, 2, 1)).permute(0, 2, 1)
+    ins = [t.detach().clone().requires_grad_(True) for t in (x1, x2, _t(g["f1"]), _t(g["f2"]))]
+    # the reference's neighbours, replayed in call order; the build's own kNN may differ from
+    # them only on near-tied rows (checked: every differing row is a near-tie of the
+    # reference's fp32 distances)
+    ref_idx = [g[f"{name}_knn{i}"].astype(np.int32) for i in range(2) if f"{name}_knn{i}" in g]
+    calls = []
+
+    def replay(nsample, xyz, new_xyz):
+        i = len(calls)
+        calls.append(1)
+        own = P._nat.knn_point(nsample, xyz.contiguous(), new_xyz.contiguous()).cpu().numpy()
+        ref = ref_idx[i]
+        assert ref.shape == own.shape, (ref.shape, own.shape)
+        xr = xyz.detach().double().cpu().numpy()
+        xq = new_xyz.detach().double().cpu().numpy()
+        for b, s_ in zip(*np.nonzero((np.sort(own, -1) != np.sort(ref, -1)).any(-1))):
+            q = xq[b, s_]
+            d = ((xr[b] - q) ** 2).sum(-1)
+            lost = np.setdiff1d(ref[b, s_], own[b, s_])
+            got = np.setdiff1d(own[b, s_], ref[b, s_])
+            gap = abs(d[lost].max() - d[got].min())
+            assert gap <= _tie_tol(q, xr[b]), (name, i, b, s_, gap)
+        return _t(ref)
+    prev = P.set_knn_override(replay)
+    try:
+        out = layer(*ins)
+    finally:
+        P.set_knn_override(prev)
+    assert len(calls) == len(ref_idx)
+    _close(out, g[name + "_out"], name=name + " out")
+    (out * _t(flow_layer_weight(name, tuple(out.shape)))).sum().backward()
+    for k, t in zip(("dx1", "dx2", "df1", "df2"), ins):
+        _close(t.grad, g[f"{name}_{k}"], rtol=1e-4, name=f"{name} {k}")
+    for k, prm in layer.named_parameters():
+        if prm.grad is not None:
+            _close(prm.grad, g[f"{name}_grad_{k}"], rtol=1e-4, name=f"{name} {k}")
+
+
 def test_multiscale_loss_matches_reference(golden):
     """BASELINE configs[0]: the product multiScaleLoss (HIP row gather for the GT pyramid) on
     the reference's own B=2, N=2048 four-level pyramid."""

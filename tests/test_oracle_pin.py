@@ -53,6 +53,32 @@ def test_layer_oracle_matches_reference(golden):
     _close(M.PointWarping()(x1, x2, flow), g["warp_out"])
 
 
+@pytest.mark.parametrize("name", ["fe32", "fe64", "fe128", "pcf"])
+def test_flow_layer_oracle_matches_reference(golden, name):
+    """FlowEmbeddingLayer / PointConvFlow restatements vs the reference (B=2, N=512): output
+    and every input / parameter gradient of sum(out * weight)."""
+    from gradproj import flow_layer_weight
+    g = golden("flow_layers_ref.npz")
+    make = {"fe32": lambda: M.FlowEmbeddingLayer(32, 64, [32, 32]),
+            "fe64": lambda: M.FlowEmbeddingLayer(32, 64, [64, 64]),
+            "fe128": lambda: M.FlowEmbeddingLayer(16, 64, [128, 128]),
+            "pcf": lambda: M.PointConvFlow(16, 64 + 64 + 3, [64, 64])}[name]
+    seed = {"fe32": 51, "fe64": 52, "fe128": 53, "pcf": 54}[name]
+    layer = load_synthetic(make(), seed=seed)
+    x1 = torch.from_numpy(g["x1"].transpose(0, 2, 1).copy()).permute(0, 2, 1)
+    x2 = torch.from_numpy(g["x2"].transpose(0, 2, 1).copy()).permute(0, 2, 1)
+    ins = [t.detach().clone().requires_grad_(True)
+           for t in (x1, x2, torch.from_numpy(g["f1"]), torch.from_numpy(g["f2"]))]
+    out = layer(*ins)
+    _close(out, g[name + "_out"])
+    (out * torch.from_numpy(flow_layer_weight(name, tuple(out.shape)))).sum().backward()
+    for k, t in zip(("dx1", "dx2", "df1", "df2"), ins):
+        _close(t.grad, g[f"{name}_{k}"], rtol=1e-4)
+    for k, prm in layer.named_parameters():
+        if prm.grad is not None:
+            _close(prm.grad, g[f"{name}_grad_{k}"], rtol=1e-4)
+
+
 @pytest.fixture(scope="module")
 def oracle_model_run(golden):
     g = golden("model_ref_n4096.npz")
