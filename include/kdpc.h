@@ -285,6 +285,35 @@ int kdpc_weightnet_bwd(int b, int n, int s, int k, const float *xyz, const float
                        float *drel, float *dparams, void *workspace, size_t workspace_bytes,
                        void *stream);
 
+/* ---- WeightNet-weighted neighbour sums: PointConvFlow's point-to-patch and patch-to-patch
+ *      cost sums (pointconv_util.py:2039-2112) ----------------------------------------- */
+
+/* Floats of kdpc_wn_wsum_bwd's dparams for C output channels: dW0 (8,3) | db0 (8) |
+ * dW1 (8,8) | db1 (8) | dW2 (C,8) | db2 (C) = 104 + 9C. */
+int kdpc_wn_wsum_param_count(int c);
+
+/* out[b,q,c] = sum_k w[b,q,k,c] * v(b,q,k,c), w = ReLU(W2 ReLU(W1 ReLU(W0 dir + b0) + b1) + b2)
+ * of dir (B,N,K,3); v(b,q,k,c) = v[b,q,k,c] for idx == NULL (v (B,N,K,C)), else
+ * v[b, idx[b,q,k], c] (v (B,M,C), idx (B,N,K) int32 in [0,M)).  W0 (8,3) b0 (8) W1 (8,8)
+ * b1 (8) W2 (C,8) b2 (C) row-major (nn.Conv2d).  1 <= K <= 64, 1 <= C <= 256.
+ * Replaces the reference's weightnet1/2(direction) + torch.sum(weights * points, dim=2)
+ * (and index_points_group of the point-to-patch cost). */
+int kdpc_wn_wsum_fwd(int b, int n, int m, int k, int c, const float *dir, const int *idx,
+                     const float *v, const float *w0, const float *b0, const float *w1,
+                     const float *b1, const float *w2, const float *b2, float *out, void *stream);
+
+/* Scratch bytes of kdpc_wn_wsum_bwd. */
+size_t kdpc_wn_wsum_bwd_workspace_bytes(int b, int n, int c);
+
+/* Backward for dout (B,N,C): dv_rows (B,N,K,C) = w * dout (v's gradient when idx == NULL;
+ * otherwise the per-(q,k) rows the caller sums per point through the CSR of idx),
+ * ddir (B,N,K,3), dparams (layout above), deterministic fixed-order sums. */
+int kdpc_wn_wsum_bwd(int b, int n, int m, int k, int c, const float *dir, const int *idx,
+                     const float *v, const float *w0, const float *b0, const float *w1,
+                     const float *b1, const float *w2, const float *b2, const float *dout,
+                     float *dv_rows, float *ddir, float *dparams, void *workspace,
+                     size_t workspace_bytes, void *stream);
+
 /* ---- BatchNorm1d + LeakyReLU over point-major rows (pointconv_util.py:217-258, bn=True
  *      estimator PointConvs: Linear -> BatchNorm1d -> LeakyReLU(0.1)) ------------------- */
 

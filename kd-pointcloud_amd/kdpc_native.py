@@ -76,12 +76,17 @@ _SIGNATURES = {
     "kdpc_weightnet_fwd": [_c_int] * 4 + [_vp] * 11,
     "kdpc_weightnet_bwd_workspace_bytes": [],
     "kdpc_weightnet_bwd": [_c_int] * 4 + [_vp] * 13 + [_c_size, _vp],
+    "kdpc_wn_wsum_param_count": [_c_int],
+    "kdpc_wn_wsum_fwd": [_c_int] * 5 + [_vp] * 11,
+    "kdpc_wn_wsum_bwd_workspace_bytes": [_c_int] * 3,
+    "kdpc_wn_wsum_bwd": [_c_int] * 5 + [_vp] * 14 + [_c_size, _vp],
 }
 _RESTYPES = {"kdpc_build_id": ctypes.c_char_p, "kdpc_grad_workspace_bytes": _c_size,
              "kdpc_csr_workspace_bytes": _c_size, "kdpc_cost_volume_bwd_workspace_bytes": _c_size,
              "kdpc_pointconv_fwd_workspace_bytes": _c_size,
              "kdpc_pointconv_bwd_workspace_bytes": _c_size,
              "kdpc_weightnet_bwd_workspace_bytes": _c_size,
+             "kdpc_wn_wsum_bwd_workspace_bytes": _c_size,
              "kdpc_batchnorm_workspace_bytes": _c_size,
              "kdpc_colsum_workspace_bytes": _c_size, "kdpc_knn_workspace_bytes": _c_size}
 
@@ -483,6 +488,24 @@ def weightnet_bwd(xyz, center, idx, params, dwt, need_rel=False):
     """-> (drel (B,S,K,3) | None, dparams (248,): dW0 | db0 | dW1 | db1 | dW2 | db2)."""
     return _op("kdpc_weightnet_bwd", "weightnet_bwd", _gpu(xyz, "xyz"), center, idx, *params,
                dwt, bool(need_rel))
+
+
+# ---------------------------------------------- WeightNet-weighted neighbour sums
+def wn_wsum_fwd(dir_, idx, v, params):
+    """out (B,N,C) = sum_k WeightNet(dir)[b,q,k,c] * v(b,q,k,c): v (B,N,K,C) for idx None,
+    else v[b, idx[b,q,k], c] of v (B,M,C).  params = (W0, b0, W1, b1, W2 (C,8), b2)."""
+    B, N, K, _ = _gpu(dir_, "dir").shape
+    C = params[4].shape[0]
+    vbytes = 4 * (B * N * K * C if idx is None else v.shape[1] * B * C + B * N * K)
+    return _op("kdpc_wn_wsum_fwd", "wn_wsum_fwd", dir_, idx, v, *params,
+               work=(12 * B * N * K + vbytes + 4 * B * N * C,
+                     2.0 * B * N * K * (24 + 64 + 9 * C)))
+
+
+def wn_wsum_bwd(dir_, idx, v, params, dout):
+    """-> dv_rows (B,N,K,C) = w * dout, ddir (B,N,K,3), dparams (104 + 9C)."""
+    return _op("kdpc_wn_wsum_bwd", "wn_wsum_bwd", _gpu(dir_, "dir"), idx, v, *params,
+               dout.contiguous())
 
 
 # ------------------------------------------------------- BatchNorm1d + LeakyReLU (rows)

@@ -768,14 +768,56 @@ class PointConvFlow(nn.Module):
                 shp = h.shape
                 h = self.mlp_bns[i](h.reshape(-1, shp[-1], 1, 1)).view(shp)
             h = self.relu(h)
-        w1 = self.weightnet1.channel_last(direction)
-        point_to_patch = torch.sum(w1 * h, dim=2)  # (B,N1,C')
+        point_to_patch = _weighted_sum(self.weightnet1, direction, None, h)  # (B,N1,C')
         # patch-to-patch
         knn_idx = knn_point(K, x1, x1)
         direction = index_points_group(x1, knn_idx) - x1.view(B, N1, 1, C)
-        w2 = self.weightnet2.channel_last(direction)
-        grouped_cost = index_points_group(point_to_patch, knn_idx)
-        return torch.sum(w2 * grouped_cost, dim=2).permute(0, 2, 1)
+        return _weighted_sum(self.weightnet2, direction, knn_idx, point_to_patch).permute(0, 2, 1)
+
+
+_FUSED_WSUM = True  # test seam: False forces the WeightNet + broadcast-multiply + sum path
+
+
+def _weighted_sum(weightnet, direction, idx, v):
+    """sum_k weightnet(direction)[b,q,k,:] * v(b,q,k,:) -> (B,N,C): v (B,N,K,C) for idx None
+    (point-to-patch), else v[b, idx[b,q,k], :] of v (B,M,C) (patch-to-patch).  One fused HIP
+    kernel each way (csrc/weightnet_wsum.hip) for the reference's 3 -> 8 -> 8 -> C ReLU
+    WeightNet without BN; reference: pointconv_util.py:2098-2112."""
+    widths = [c.in_channels for c in weightnet.mlp_convs] + [weightnet.mlp_convs[-1].out_channels]
+    C = widths[-1]
+    if (_FUSED_WSUM and not weightnet.bn and widths[:3] == [3, 8, 8] and len(widths) == 4
+            and C <= 256 and direction.shape[2] <= 64):
+        params = [t for c in weightnet.mlp_convs for t in (c.weight, c.bias)]
+        return _WnWeightedSum.apply(direction.contiguous(),
+                                    None if idx is None else _as_idx32(idx).contiguous(),
+                                    v.contiguous(), *params)
+    w = weightnet.channel_last(direction)
+    vals = v if idx is None else index_points_group(v, idx)
+    return torch.sum(w * vals, dim=2)
+
+
+class _WnWeightedSum(torch.autograd.Function):
+    """Fused WeightNet-weighted neighbour sum (csrc/weightnet_wsum.hip)."""
+
+    @staticmethod
+    def forward(ctx, direction, idx, v, *params):
+        ctx.save_for_backward(direction, idx, v, *params)
+        return _nat.wn_wsum_fwd(direction, idx, v, params)
+
+    @staticmethod
+    def backward(ctx, dout):
+        direction, idx, v, *params = ctx.saved_tensors
+        dv_rows, ddir, dflat = _nat.wn_wsum_bwd(direction, idx, v, params, dout)
+        dparams = [g.view_as(p) for g, p in zip(dflat.split([p.numel() for p in params]), params)]
+        dv = None
+        if ctx.needs_input_grad[2]:
+            if idx is None:
+                dv = dv_rows
+            else:  # per-(q,k) rows summed per point through the kNN CSR (deterministic)
+                B, N, K, C = dv_rows.shape
+                M = v.shape[1]
+                dv = _nat.group_rows_grad(dv_rows.view(B, N * K, C), _nat.csr_of(idx, M), B, M, C)
+        return (ddir if ctx.needs_input_grad[0] else None, None, dv, *dparams)
 
 
 def _inverse_distance_blend(grouped_xyz_norm, grouped_values):

@@ -514,6 +514,39 @@ std::tuple<c10::optional<Tensor>, Tensor> weightnet_bwd(Tensor xyz, Tensor cente
   return {need_rel ? c10::optional<Tensor>(drel) : c10::nullopt, dparams};
 }
 
+// ---------------------------------------------------- WeightNet-weighted neighbour sums
+Tensor wn_wsum_fwd(Tensor dir, c10::optional<Tensor> idx, Tensor v, Tensor w0, Tensor b0,
+                   Tensor w1, Tensor b1, Tensor w2, Tensor b2) {
+  for (auto* t : {&dir, &v, &w0, &b0, &w1, &b1, &w2, &b2}) dev(*t, kF, "wn_wsum input");
+  if (idx) dev(*idx, kI, "idx");
+  GUARD(dir);
+  const int64_t b = dir.size(0), n = dir.size(1), k = dir.size(2), c = w2.size(0);
+  const int64_t m = idx ? v.size(1) : 1;
+  Tensor out = empty_f({b, n, c}, dir);
+  check(kdpc_wn_wsum_fwd(b, n, m, k, c, F(dir), idx ? I(*idx) : nullptr, F(v), F(w0), F(b0),
+                         F(w1), F(b1), F(w2), F(b2), F(out), stream_of(dir)), "wn_wsum_fwd");
+  return out;
+}
+
+std::tuple<Tensor, Tensor, Tensor> wn_wsum_bwd(Tensor dir, c10::optional<Tensor> idx, Tensor v,
+                                               Tensor w0, Tensor b0, Tensor w1, Tensor b1,
+                                               Tensor w2, Tensor b2, Tensor dout) {
+  for (auto* t : {&dir, &v, &w0, &b0, &w1, &b1, &w2, &b2, &dout}) dev(*t, kF, "wn_wsum input");
+  if (idx) dev(*idx, kI, "idx");
+  GUARD(dir);
+  const int64_t b = dir.size(0), n = dir.size(1), k = dir.size(2), c = w2.size(0);
+  const int64_t m = idx ? v.size(1) : 1;
+  const size_t nb = kdpc_wn_wsum_bwd_workspace_bytes(b, n, c);
+  Tensor ws = workspace(nb, dir);
+  Tensor dv_rows = empty_f({b, n, k, c}, dir);
+  Tensor ddir = empty_f({b, n, k, 3}, dir);
+  Tensor dparams = empty_f({kdpc_wn_wsum_param_count(c)}, dir);
+  check(kdpc_wn_wsum_bwd(b, n, m, k, c, F(dir), idx ? I(*idx) : nullptr, F(v), F(w0), F(b0),
+                         F(w1), F(b1), F(w2), F(b2), F(dout), F(dv_rows), F(ddir), F(dparams),
+                         ws.data_ptr(), nb, stream_of(dir)), "wn_wsum_bwd");
+  return {dv_rows, ddir, dparams};
+}
+
 // ------------------------------------------------------- BatchNorm1d + LeakyReLU, colsum
 std::tuple<Tensor, Tensor, Tensor> batchnorm_lrelu_fwd(Tensor x, Tensor weight, Tensor bias,
                                                        double eps, double momentum,
@@ -638,6 +671,10 @@ TORCH_LIBRARY(kdpc, m) {
         "Tensor b1, Tensor w2, Tensor b2) -> Tensor");
   m.def("weightnet_bwd(Tensor xyz, Tensor center, Tensor idx, Tensor w0, Tensor b0, Tensor w1, "
         "Tensor b1, Tensor w2, Tensor b2, Tensor dwt, bool need_rel) -> (Tensor?, Tensor)");
+  m.def("wn_wsum_fwd(Tensor dir, Tensor? idx, Tensor v, Tensor w0, Tensor b0, Tensor w1, "
+        "Tensor b1, Tensor w2, Tensor b2) -> Tensor");
+  m.def("wn_wsum_bwd(Tensor dir, Tensor? idx, Tensor v, Tensor w0, Tensor b0, Tensor w1, "
+        "Tensor b1, Tensor w2, Tensor b2, Tensor dout) -> (Tensor, Tensor, Tensor)");
   m.def("batchnorm_lrelu_fwd(Tensor x, Tensor weight, Tensor bias, float eps, float momentum, "
         "float slope, Tensor(a!)? run_mean, Tensor(b!)? run_var) -> (Tensor, Tensor, Tensor)");
   m.def("batchnorm_lrelu_apply(Tensor x, Tensor mean, Tensor invstd, Tensor weight, "
@@ -682,6 +719,8 @@ TORCH_LIBRARY_IMPL(kdpc, CUDA, m) {
   m.impl("pointconv_contract_bwd", pointconv_contract_bwd);
   m.impl("weightnet_fwd", weightnet_fwd);
   m.impl("weightnet_bwd", weightnet_bwd);
+  m.impl("wn_wsum_fwd", wn_wsum_fwd);
+  m.impl("wn_wsum_bwd", wn_wsum_bwd);
   m.impl("batchnorm_lrelu_fwd", batchnorm_lrelu_fwd);
   m.impl("batchnorm_lrelu_apply", batchnorm_lrelu_apply);
   m.impl("batchnorm_lrelu_bwd", batchnorm_lrelu_bwd);

@@ -209,3 +209,38 @@ def test_batchnorm_lrelu_vs_torch(r, c):
             (x.double() - bn.running_mean.double()) / torch.sqrt(bn.running_var.double() + bn.eps)
             * bn.weight.double() + bn.bias.double(), 0.1)
     _scale_close(ye, ref, rtol=1e-5, name="eval")
+
+
+@pytest.mark.parametrize("k,d,mlp,n1,n2,bsz", [(16, 64, [64, 64], 512, 600, 2),
+                                               (9, 32, [32, 48], 300, 257, 3),
+                                               (32, 40, [128], 200, 300, 1),
+                                               (64, 16, [256], 129, 140, 1)])
+def test_pointconv_flow_fused_equals_unfused(k, d, mlp, n1, n2, bsz):
+    """PointConvFlow's WeightNet-weighted sums (csrc/weightnet_wsum.hip, dense and gathered)
+    equal the WeightNet + broadcast-multiply + torch.sum path: output and every gradient."""
+    import pointconv_util as P
+    import synthetic
+    torch.manual_seed(k + d)
+    layer = P.PointConvFlow(k, 2 * d + 3, mlp).to(DEV)
+    x1 = torch.from_numpy(synthetic.ft3d_batch(bsz, n1, seed=5)[0]).to(DEV).permute(0, 2, 1)
+    x2 = torch.from_numpy(synthetic.ft3d_batch(bsz, n2, seed=6)[0]).to(DEV).permute(0, 2, 1)
+    f1 = torch.randn(bsz, d, n1, device=DEV)
+    f2 = torch.randn(bsz, d, n2, device=DEV)
+    outs, grads = [], []
+    for fused in (True, False):
+        P._FUSED_WSUM = fused
+        try:
+            ins = [t.detach().clone().requires_grad_(True) for t in (x1, x2, f1, f2)]
+            layer.zero_grad()
+            o = layer(*ins)
+            torch.manual_seed(11)
+            (o * torch.randn_like(o)).sum().backward()
+            outs.append(o.detach())
+            grads.append([t.grad for t in ins] + [p.grad for p in layer.parameters()])
+        finally:
+            P._FUSED_WSUM = True
+    _scale_close(outs[0], outs[1], name="out")
+    for i, (a, b) in enumerate(zip(grads[0], grads[1])):
+        assert (a is None) == (b is None), i
+        if a is not None:  # (the WeightNets' unused BatchNorm modules have none)
+            _scale_close(a, b, rtol=2e-5, name=f"grad {i}")
