@@ -131,6 +131,16 @@ int kdpc_knn_point_ws(int b, int n, int s, int k, const float *xyz, const float 
                       int *idx, float *dist, void *workspace, size_t workspace_bytes,
                       void *stream);
 
+/* kNN in feature space (CrossLayerLightFG's knn_point over (B,N,D) features,
+ * pointconv_util.py:1871-1957 with square_distance + topk :73-107): ref (B,N,D),
+ * query (B,S,D) -> idx (B,S,K) int32 ascending by (dist, index), dist (B,S,K) if non-null,
+ * dist = (-2 q.r + |q|^2) + |r|^2; the dot products run on the f32 matrix cores.
+ * 1 <= D <= 128, 1 <= K <= min(32, N).  Workspace: the row norms. */
+size_t kdpc_knn_feature_workspace_bytes(int b, int n, int s);
+int kdpc_knn_feature(int b, int n, int s, int d, int k, const float *ref, const float *query,
+                     int *idx, float *dist, void *workspace, size_t workspace_bytes,
+                     void *stream);
+
 /* ---- point-major grouping + deterministic scatter (no reference counterpart: these
  *      replace index_points_group's permute/grouping_operation/permute chain,
  *      pointconv_util.py:122-133, and its atomicAdd backward) ------------------------- */

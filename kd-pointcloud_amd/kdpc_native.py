@@ -76,6 +76,8 @@ _SIGNATURES = {
     "kdpc_weightnet_fwd": [_c_int] * 4 + [_vp] * 11,
     "kdpc_weightnet_bwd_workspace_bytes": [],
     "kdpc_weightnet_bwd": [_c_int] * 4 + [_vp] * 13 + [_c_size, _vp],
+    "kdpc_knn_feature_workspace_bytes": [_c_int] * 3,
+    "kdpc_knn_feature": [_c_int] * 5 + [_vp] * 5 + [_c_size, _vp],
     "kdpc_wn_wsum_param_count": [_c_int],
     "kdpc_wn_wsum_fwd": [_c_int] * 5 + [_vp] * 11,
     "kdpc_wn_wsum_bwd_workspace_bytes": [_c_int] * 3,
@@ -87,6 +89,7 @@ _RESTYPES = {"kdpc_build_id": ctypes.c_char_p, "kdpc_grad_workspace_bytes": _c_s
              "kdpc_pointconv_bwd_workspace_bytes": _c_size,
              "kdpc_weightnet_bwd_workspace_bytes": _c_size,
              "kdpc_wn_wsum_bwd_workspace_bytes": _c_size,
+             "kdpc_knn_feature_workspace_bytes": _c_size,
              "kdpc_batchnorm_workspace_bytes": _c_size,
              "kdpc_colsum_workspace_bytes": _c_size, "kdpc_knn_workspace_bytes": _c_size}
 
@@ -294,6 +297,22 @@ def knn_point(nsample, xyz, new_xyz, return_dist=False, seeded=True):
         return _op("kdpc_knn_point", "knn_point_dist", int(nsample), xyz, new_xyz, seeded,
                    work=work)
     return _op("kdpc_knn_point", "knn_point", int(nsample), xyz, new_xyz, seeded, work=work)
+
+
+def knn_feature(nsample, ref, query, return_dist=False):
+    """kNN in feature space: ref (B,N,D), query (B,S,D), D <= 128 -> idx (B,S,K) i32
+    ascending (dist, idx) [, dist]; the distance GEMM runs on the f32 matrix cores."""
+    B, N, D = _gpu(ref, "ref").shape
+    S = query.shape[1]
+    if nsample > N:
+        raise ValueError(f"knn_feature: nsample={nsample} > number of points {N}")
+    work = (B * 4 * (N * D + S * D + S * nsample * (2 if return_dist else 1)),
+            2.0 * B * S * N * D)
+    if return_dist:
+        return _op("kdpc_knn_feature", "knn_feature_dist", int(nsample), ref.contiguous(),
+                   query.contiguous(), work=work)
+    return _op("kdpc_knn_feature", "knn_feature", int(nsample), ref.contiguous(),
+               query.contiguous(), work=work)
 
 
 def group_rows(points, idx):

@@ -180,9 +180,12 @@ def set_knn_override(fn):
 
 def knn_point(nsample, xyz, new_xyz):
     """Reference: pointconv_util.py:96-107.  xyz (B,N,C) refs, new_xyz (B,S,C) queries ->
-    (B,S,nsample) int32, ascending by (distance, index)."""
+    (B,S,nsample) int32, ascending by (distance, index).  C = 3: csrc/knn.hip; other C
+    (feature-space neighbours, C <= 128): csrc/knn_feature.hip."""
     if _knn_override is not None:
         return _knn_override(nsample, xyz, new_xyz)
+    if xyz.shape[-1] != 3:  # feature space (CrossLayerLightFG): distance GEMM on MFMA
+        return _nat.knn_feature(nsample, xyz, new_xyz)
     return _nat.knn_point(nsample, xyz.contiguous(), new_xyz.contiguous())
 
 
@@ -698,6 +701,55 @@ class CrossLayerLight(nn.Module):
         feat1_final = _cost_volume_cl(self.nsample, xa1, xa2, feat1_new, feat2_new,
                                       self.pos2, self.mlp2, self._act(self.bn2),
                                       _nat.batch_prefix(idx, B))
+        return feat1_new, feat2_new, feat1_final
+
+
+class CrossLayerLightFG(CrossLayerLight):
+    """Feature-grouping cost volume.  Reference: pointconv_util.py:1871-1957: CrossLayerLight
+    whose neighbourhood of a point is nsample // 2 nearest neighbours in FEATURE space
+    (knn1 / knn2, (B,D,N)) followed by nsample // 2 nearest in coordinates -- the two index
+    sets concatenated along K (duplicates kept, as in the reference).  Same parameters and
+    state_dict keys as CrossLayerLight; mlp2 is required (the reference's forward always
+    applies cross_t1 / cross_t2)."""
+
+    def cross(self, xyz1, xyz2, points1, points2, knn1, knn2, pos, mlp, bn, nsample=None):
+        """Reference layout in and out: xyz* (B,3,N), points* / knn* (B,C,N) -> (B,D,N)."""
+        x1, x2 = _cl(xyz1), _cl(xyz2)
+        idx = self._neighbours(x1, x2, _cl(knn1), _cl(knn2), nsample or self.nsample)
+        return _cost_volume_cl(idx.shape[-1], x1, x2, _cl(points1), _cl(points2), pos, mlp,
+                               self._act(bn), idx).permute(0, 2, 1)
+
+    @staticmethod
+    def _neighbours(x1, x2, f1, f2, nsample):
+        """(B,N1,2*(nsample//2)) = cat(feature kNN of f1 in f2, coordinate kNN of x1 in x2)."""
+        half = nsample // 2
+        return torch.cat([_as_idx32(knn_point(half, f2, f1)), _as_idx32(knn_point(half, x2, x1))],
+                         dim=-1)
+
+    def forward(self, pc1, pc2, feat1, feat2, knn1, knn2):
+        out = self.forward_cl(_cl(pc1), _cl(pc2), _cl(feat1), _cl(feat2), _cl(knn1), _cl(knn2))
+        return tuple(t.permute(0, 2, 1) for t in out)
+
+    def forward_cl(self, pc1, pc2, feat1, feat2, knn1, knn2):
+        """Point-major.  Both directions of the first cost volume run as one batch of 2B; the
+        refinement cross(pc1, pc2) reuses the pc1 half of that batch's neighbour sets (the
+        same two searches the reference repeats)."""
+        B = pc1.shape[0]
+        xa, xb = torch.cat([pc1, pc2], 0), torch.cat([pc2, pc1], 0)
+        idx = self._neighbours(xa, xb, torch.cat([knn1, knn2], 0), torch.cat([knn2, knn1], 0),
+                               self.nsample)
+        fa = torch.cat([feat1, feat2], 0)
+        ta = _linear_1x1(self.cross_t11, fa)
+        tb = _linear_1x1(self.cross_t22, fa)
+        tb1, tb2 = tb.split(B)
+        tb = torch.cat([tb2, tb1], 0)
+        k = idx.shape[-1]
+        both = _cost_volume_cl(k, xa, xb, ta, tb, self.pos1, self.mlp1, self._act(self.bn1), idx)
+        feat1_new, feat2_new = both.split(B)
+        feat1_new = _linear_1x1(self.cross_t1, feat1_new)
+        feat2_new = _linear_1x1(self.cross_t2, feat2_new)
+        feat1_final = _cost_volume_cl(k, pc1, pc2, feat1_new, feat2_new, self.pos2, self.mlp2,
+                                      self._act(self.bn2), _nat.batch_prefix(idx, B))
         return feat1_new, feat2_new, feat1_final
 
 

@@ -264,6 +264,31 @@ TT knn_point_dist(int64_t nsample, Tensor xyz, Tensor new_xyz, bool seeded) {
   return knn_point_impl(nsample, xyz, new_xyz, true, seeded);
 }
 
+TT knn_feature_impl(int64_t nsample, Tensor ref, Tensor query, bool want_dist) {
+  dev(ref, kF, "ref"), dev(query, kF, "query"), same_device(ref, query, "query");
+  TORCH_CHECK(ref.dim() == 3 && query.dim() == 3 && ref.size(0) == query.size(0) &&
+                  ref.size(2) == query.size(2),
+              "kdpc: knn_feature expects ref (B,N,D), query (B,S,D)");
+  GUARD(ref);
+  const int64_t b = ref.size(0), n = ref.size(1), d = ref.size(2), s = query.size(1);
+  Tensor idx = at::empty({b, s, nsample}, ref.options().dtype(at::kInt));
+  Tensor dist = want_dist ? empty_f({b, s, nsample}, ref) : Tensor();
+  const size_t nb = kdpc_knn_feature_workspace_bytes(b, n, s);
+  Tensor ws = workspace(nb, ref);
+  check(kdpc_knn_feature(b, n, s, d, nsample, F(ref), F(query), I(idx),
+                         want_dist ? F(dist) : nullptr, ws.data_ptr(), nb, stream_of(ref)),
+        "knn_feature");
+  return {idx, dist};
+}
+
+Tensor knn_feature(int64_t nsample, Tensor ref, Tensor query) {
+  return std::get<0>(knn_feature_impl(nsample, ref, query, false));
+}
+
+TT knn_feature_dist(int64_t nsample, Tensor ref, Tensor query) {
+  return knn_feature_impl(nsample, ref, query, true);
+}
+
 // ------------------------------------------------------- point-major rows and the CSR
 Tensor group_rows(Tensor points, Tensor idx) {
   dev(points, kF, "points"), dev(idx, kI, "idx"), same_device(points, idx, "idx");
@@ -639,6 +664,8 @@ TORCH_LIBRARY(kdpc, m) {
   m.def("knn_point(int nsample, Tensor xyz, Tensor new_xyz, bool seeded=True) -> Tensor");
   m.def("knn_point_dist(int nsample, Tensor xyz, Tensor new_xyz, bool seeded=True) "
         "-> (Tensor, Tensor)");
+  m.def("knn_feature(int nsample, Tensor ref, Tensor query) -> Tensor");
+  m.def("knn_feature_dist(int nsample, Tensor ref, Tensor query) -> (Tensor, Tensor)");
   m.def("group_rows(Tensor points, Tensor idx) -> Tensor");
   m.def("csr_build(Tensor idx, int n) -> (Tensor, Tensor)");
   m.def("group_rows_grad(Tensor grad_out, Tensor offsets, Tensor perm, int n) -> Tensor");
@@ -719,6 +746,8 @@ TORCH_LIBRARY_IMPL(kdpc, CUDA, m) {
   m.impl("pointconv_contract_bwd", pointconv_contract_bwd);
   m.impl("weightnet_fwd", weightnet_fwd);
   m.impl("weightnet_bwd", weightnet_bwd);
+  m.impl("knn_feature", knn_feature);
+  m.impl("knn_feature_dist", knn_feature_dist);
   m.impl("wn_wsum_fwd", wn_wsum_fwd);
   m.impl("wn_wsum_bwd", wn_wsum_bwd);
   m.impl("batchnorm_lrelu_fwd", batchnorm_lrelu_fwd);

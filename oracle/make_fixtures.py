@@ -235,6 +235,49 @@ def make_flow_layers(R):
     np.savez_compressed(os.path.join(GOLDEN, "flow_layers_ref.npz"), **out)
 
 
+def make_fg(R):
+    """CrossLayerLightFG (ref pointconv_util.py:1871-1957) at B=2, N=512: its three outputs,
+    every input / parameter gradient of sum_i sum(out_i * weight_i) and the reference's
+    neighbour indices in call order (feature-space and coordinate kNN)."""
+    torch.manual_seed(0)
+    out = {}
+    n = 512
+    pairs = [synthetic.ft3d_pair(n, seed=45, pair=i) for i in range(2)]
+    x1 = torch.from_numpy(np.stack([p[0] for p in pairs])).permute(0, 2, 1)
+    x2 = torch.from_numpy(np.stack([p[1] for p in pairs])).permute(0, 2, 1)
+    rng = np.random.default_rng(47)
+    f32 = lambda *s: torch.from_numpy(rng.normal(size=s).astype(np.float32))  # noqa: E731
+    f1, f2, k1, k2 = f32(2, 64, n), f32(2, 64, n), f32(2, 32, n), f32(2, 32, n)
+    out.update(x1=_np(x1), x2=_np(x2), f1=_np(f1), f2=_np(f2), k1=_np(k1), k2=_np(k2))
+    layer = _synth(R.pcu.CrossLayerLightFG(32, 64, [32, 32], [32, 32]), seed=55)
+    ins = [t.detach().clone().requires_grad_(True) for t in (x1, x2, f1, f2, k1, k2)]
+    knn = R.pcu.knn_point
+    calls = []
+
+    def rec(nsample, xyz, new_xyz):
+        idx = knn(nsample, xyz, new_xyz)
+        calls.append(_np(idx).astype(np.int16))
+        return idx
+    R.pcu.knn_point = rec
+    try:
+        outs = layer(*ins)
+    finally:
+        R.pcu.knn_point = knn
+    loss = 0
+    for i, o in enumerate(outs):
+        out[f"out{i}"] = _np(o)
+        loss = loss + (o * torch.from_numpy(flow_layer_weight(f"fg{i}", tuple(o.shape)))).sum()
+    loss.backward()
+    for k, t in zip(("dx1", "dx2", "df1", "df2", "dk1", "dk2"), ins):
+        out[k] = _np(t.grad) if t.grad is not None else np.zeros(0, np.float32)
+    for k, prm in layer.named_parameters():
+        if prm.grad is not None:
+            out[f"grad_{k}"] = _np(prm.grad)
+    for i, c in enumerate(calls):
+        out[f"knn{i}"] = c
+    np.savez_compressed(os.path.join(GOLDEN, "fg_ref.npz"), **out)
+
+
 def make_model(R, n=4096):
     """Teacher (eval) + student (train) at B=1, N=n; MSL and KD losses and grad summaries."""
     p1, p2, fl = synthetic.ft3d_pair(n, seed=7, pair=0)
@@ -354,7 +397,7 @@ def main(which=None):
     R = setup_reference()
     steps = {"knn": lambda: make_knn(R), "losses": lambda: make_losses(R),
              "layers": lambda: make_layers(R), "model": lambda: make_model(R),
-             "flowlayers": lambda: make_flow_layers(R),
+             "flowlayers": lambda: make_flow_layers(R), "fg": lambda: make_fg(R),
              "trace2048": lambda: make_model_knn_trace(R),
              # BASELINE configs[2]'s point count (the metric's size), B=1
              "trace8192": lambda: make_model_knn_trace(R, n=8192)}

@@ -7,7 +7,7 @@ reference so CPU results are bitwise comparable with the reference run on CPU:
   * FPS: the C restatement (oracle/pointnet2_oracle.c) or, for the CPU baseline the
     north star names, a random subsample (the PointConvDRand pattern, pointconv_util.py:621)
   * layers                                   pointconv_util.py:17-258,401-446,1474-1517,
-                                             1791-1868,2039-2256
+                                             1791-1957,2039-2256
   * PointConvBidirection                     models_bid_pointconv.py:14-207 (two clouds
                                              run separately, in reference order)
   * multiScaleLoss, biDirection_loss_ht      loss_functions.py:6-25, 83-96
@@ -207,6 +207,37 @@ class CrossLayerLight(nn.Module):
         f1 = self.cross_t1(f1)
         f2 = self.cross_t2(f2)
         return f1, f2, self.cross(pc1, pc2, f1, f2, self.pos2, self.mlp2, self.bn2)
+
+
+class CrossLayerLightFG(CrossLayerLight):
+    """pointconv_util.py:1871-1957: neighbourhoods = nsample//2 feature-space kNN (knn1/knn2)
+    concatenated with nsample//2 coordinate kNN."""
+
+    def cross(self, xyz1, xyz2, points1, points2, knn1, knn2, pos, mlp, bn, nsample=None):
+        nsample = nsample or self.nsample
+        B, C, N1 = xyz1.shape
+        D1 = points1.shape[1]
+        xyz1, xyz2 = xyz1.permute(0, 2, 1), xyz2.permute(0, 2, 1)
+        points1, points2 = points1.permute(0, 2, 1), points2.permute(0, 2, 1)
+        knn1, knn2 = knn1.permute(0, 2, 1), knn2.permute(0, 2, 1)
+        idx_f = knn_point(nsample // 2, knn2, knn1)
+        idx_p = knn_point(nsample // 2, xyz2, xyz1)
+        nbr = torch.cat((index_points_group(xyz2, idx_f), index_points_group(xyz2, idx_p)), -2)
+        direction = nbr - xyz1.view(B, N1, 1, C)
+        g2 = torch.cat((index_points_group(points2, idx_f).permute(0, 3, 2, 1),
+                        index_points_group(points2, idx_p).permute(0, 3, 2, 1)), -2)
+        g1 = points1.view(B, N1, 1, D1).repeat(1, 1, nsample, 1).permute(0, 3, 2, 1)
+        h = self.relu(bn(g2 + g1 + pos(direction.permute(0, 3, 2, 1))))
+        for conv in mlp:
+            h = conv(h)
+        return F.max_pool2d(h, (h.size(2), 1)).squeeze(2)
+
+    def forward(self, pc1, pc2, feat1, feat2, knn1, knn2):
+        f1 = self.cross_t1(self.cross(pc1, pc2, self.cross_t11(feat1), self.cross_t22(feat2), knn1,
+                                      knn2, self.pos1, self.mlp1, self.bn1))
+        f2 = self.cross_t2(self.cross(pc2, pc1, self.cross_t11(feat2), self.cross_t22(feat1), knn2,
+                                      knn1, self.pos1, self.mlp1, self.bn1))
+        return f1, f2, self.cross(pc1, pc2, f1, f2, knn1, knn2, self.pos2, self.mlp2, self.bn2)
 
 
 class FlowEmbeddingLayer(nn.Module):

@@ -286,3 +286,52 @@ def test_c_abi_direct_equals_torch_ops(nat):
     gp2 = torch.zeros_like(gp)
     ops.group_points_grad_wrapper(2, 24, 1500, 300, 9, g, kidx, gp2)
     assert torch.equal(gp, gp2)
+
+
+def _feature_tie_tol(q, r, d):
+    """Rounding bound of dist = (-2 q.r + |q|^2) + |r|^2 in fp32 when the D-term dot product
+    and the norms accumulate in different orders (matrix core vs CPU GEMM / float64): a few
+    ulp per term of |q|^2 + |r|^2, D terms, twice over."""
+    return 8 * d * 2.0 ** -24 * ((q ** 2).sum() + (r ** 2).sum(-1).max())
+
+
+@pytest.mark.parametrize("b,n,s,d,k", [(2, 1000, 700, 32, 16), (1, 512, 512, 64, 32),
+                                       (3, 300, 257, 5, 7), (1, 2048, 100, 128, 1),
+                                       (2, 777, 333, 100, 9)])
+def test_knn_feature_matches_float64(nat, b, n, s, d, k):
+    """Feature-space kNN (MFMA distance GEMM + per-lane top-K) vs a float64 brute force:
+    every query's neighbour set equals the exact one except where the swapped neighbours are
+    a near-tie within fp32 rounding; distances within that rounding; ascending order."""
+    rng = np.random.default_rng(b * 1000 + d)
+    ref = rng.normal(size=(b, n, d)).astype(np.float32)
+    qry = rng.normal(size=(b, s, d)).astype(np.float32)
+    idx, dist = nat.knn_feature(k, _t(ref), _t(qry), return_dist=True)
+    idx, dist = idx.cpu().numpy(), dist.cpu().numpy()
+    assert idx.shape == (b, s, k) and idx.min() >= 0 and idx.max() < n
+    assert np.all(np.diff(dist, axis=-1) >= 0)
+    r64, q64 = ref.astype(np.float64), qry.astype(np.float64)
+    flips = 0
+    for bb in range(b):
+        full = ((q64[bb, :, None, :] - r64[bb, None, :, :]) ** 2).sum(-1)  # (s, n)
+        exact = np.argsort(full, axis=1, kind="stable")[:, :k]
+        for q in range(s):
+            tol = _feature_tie_tol(q64[bb, q], r64[bb], d)
+            np.testing.assert_allclose(dist[bb, q], full[q, idx[bb, q]], atol=tol)
+            got, want = set(idx[bb, q]), set(exact[q])
+            if got != want:
+                flips += 1
+                lost = full[q, sorted(want - got)].max()
+                extra = full[q, sorted(got - want)].min()
+                assert abs(lost - extra) <= tol, (bb, q, lost, extra, tol)
+    assert flips <= max(2, s * b // 100), flips
+
+
+def test_knn_point_dispatches_feature_space(nat):
+    """pointconv_util.knn_point over D != 3 rows runs the feature kernel (the reference's
+    knn_point is dimension-agnostic, CrossLayerLightFG calls it on (B,N,D) features)."""
+    import pointconv_util as P
+    rng = np.random.default_rng(4)
+    ref = _t(rng.normal(size=(2, 300, 16)).astype(np.float32))
+    qry = _t(rng.normal(size=(2, 200, 16)).astype(np.float32))
+    np.testing.assert_array_equal(P.knn_point(8, ref, qry).cpu().numpy(),
+                                  nat.knn_feature(8, ref, qry).cpu().numpy())

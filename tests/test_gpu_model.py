@@ -125,6 +125,60 @@ def test_flow_layers_match_reference(golden, name):
             _close(prm.grad, g[f"{name}_grad_{k}"], rtol=1e-4, name=f"{name} {k}")
 
 
+def test_cross_layer_fg_matches_reference(golden):
+    """CrossLayerLightFG (feature-space + coordinate neighbourhoods) vs the reference at B=2,
+    N=512 with the reference's neighbours replayed (the build's own feature kNN agrees with
+    them except on near-ties, checked): the three outputs at 1e-5 of their scale, every input
+    and parameter gradient at 1e-4."""
+    import pointconv_util as P
+    from gradproj import flow_layer_weight
+    g = golden("fg_ref.npz")
+    layer = load_synthetic(P.CrossLayerLightFG(32, 64, [32, 32], [32, 32]), seed=55).to(DEV)
+    x1 = _t(g["x1"].transpose(0, 2, 1)).permute(0, 2, 1)
+    x2 = _t(g["x2"].transpose(0, 2, 1)).permute(0, 2, 1)
+    ins = [t.detach().clone().requires_grad_(True) for t in (x1, x2, _t(g["f1"]), _t(g["f2"]))]
+    # reference calls: cross(1,2): feature knn0, coords knn1; cross(2,1): knn2, knn3; the
+    # build batches both directions: feature = cat(knn0, knn2), coords = cat(knn1, knn3)
+    want = [np.concatenate([g["knn0"], g["knn2"]]), np.concatenate([g["knn1"], g["knn3"]])]
+    np.testing.assert_array_equal(g["knn4"], g["knn0"])  # the refinement repeats cross(1,2)'s
+    np.testing.assert_array_equal(g["knn5"], g["knn1"])
+    calls = []
+
+    def replay(nsample, xyz, new_xyz):
+        ref = want[len(calls)].astype(np.int32)
+        calls.append(xyz.shape[-1])
+        own = (P._nat.knn_feature(nsample, xyz, new_xyz) if xyz.shape[-1] != 3 else
+               P._nat.knn_point(nsample, xyz.contiguous(), new_xyz.contiguous())).cpu().numpy()
+        assert own.shape == ref.shape
+        xr = xyz.detach().double().cpu().numpy()
+        xq = new_xyz.detach().double().cpu().numpy()
+        d = xr.shape[-1]
+        for b, s_ in zip(*np.nonzero((np.sort(own, -1) != np.sort(ref, -1)).any(-1))):
+            q = xq[b, s_]
+            dd = ((xr[b] - q) ** 2).sum(-1)
+            lost = dd[np.setdiff1d(ref[b, s_], own[b, s_])].max()
+            got = dd[np.setdiff1d(own[b, s_], ref[b, s_])].min()
+            tol = 8 * d * 2.0 ** -24 * ((q ** 2).sum() + (xr[b] ** 2).sum(-1).max())
+            assert abs(lost - got) <= tol, (len(calls), b, s_, lost, got)
+        return _t(ref)
+    prev = P.set_knn_override(replay)
+    try:
+        outs = layer(*ins, _t(g["k1"]), _t(g["k2"]))
+    finally:
+        P.set_knn_override(prev)
+    assert calls == [32, 3]
+    loss = 0
+    for i, o in enumerate(outs):
+        _close(o, g[f"out{i}"], name=f"fg out{i}")
+        loss = loss + (o * _t(flow_layer_weight(f"fg{i}", tuple(o.shape)))).sum()
+    loss.backward()
+    for k, t in zip(("dx1", "dx2", "df1", "df2"), ins):
+        _close(t.grad, g[k], rtol=1e-4, name=f"fg {k}")
+    for k, prm in layer.named_parameters():
+        if prm.grad is not None:
+            _close(prm.grad, g[f"grad_{k}"], rtol=1e-4, name=f"fg {k}")
+
+
 def test_multiscale_loss_matches_reference(golden):
     """BASELINE configs[0]: the product multiScaleLoss (HIP row gather for the GT pyramid) on
     the reference's own B=2, N=2048 four-level pyramid."""

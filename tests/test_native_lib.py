@@ -117,6 +117,7 @@ TORCH_OPS = {
     "ball_query": "kdpc_ball_query", "group_points": "kdpc_group_points",
     "three_nn": "kdpc_three_nn", "three_interpolate": "kdpc_three_interpolate",
     "knn_point": "kdpc_knn_point_ws", "knn_point_dist": "kdpc_knn_point_ws",
+    "knn_feature": "kdpc_knn_feature", "knn_feature_dist": "kdpc_knn_feature",
     "group_rows": "kdpc_group_rows", "csr_build": "kdpc_csr_build",
     "group_rows_grad": "kdpc_group_rows_grad_csr", "csr_sum_channels": "kdpc_csr_sum_channels",
     "three_interpolate_grad_csr": "kdpc_three_interpolate_grad_csr",

@@ -79,6 +79,28 @@ def test_flow_layer_oracle_matches_reference(golden, name):
             _close(prm.grad, g[f"{name}_grad_{k}"], rtol=1e-4)
 
 
+def test_fg_oracle_matches_reference(golden):
+    """CrossLayerLightFG restatement (feature-space + coordinate kNN) vs the reference."""
+    from gradproj import flow_layer_weight
+    g = golden("fg_ref.npz")
+    layer = load_synthetic(M.CrossLayerLightFG(32, 64, [32, 32], [32, 32]), seed=55)
+    x1 = torch.from_numpy(g["x1"].transpose(0, 2, 1).copy()).permute(0, 2, 1)
+    x2 = torch.from_numpy(g["x2"].transpose(0, 2, 1).copy()).permute(0, 2, 1)
+    ins = [t.detach().clone().requires_grad_(True)
+           for t in (x1, x2, torch.from_numpy(g["f1"]), torch.from_numpy(g["f2"]))]
+    outs = layer(*ins, torch.from_numpy(g["k1"]), torch.from_numpy(g["k2"]))
+    loss = 0
+    for i, o in enumerate(outs):
+        _close(o, g[f"out{i}"])
+        loss = loss + (o * torch.from_numpy(flow_layer_weight(f"fg{i}", tuple(o.shape)))).sum()
+    loss.backward()
+    for k, t in zip(("dx1", "dx2", "df1", "df2"), ins):
+        _close(t.grad, g[k], rtol=1e-4)
+    for k, prm in layer.named_parameters():
+        if prm.grad is not None:
+            _close(prm.grad, g[f"grad_{k}"], rtol=1e-4)
+
+
 @pytest.fixture(scope="module")
 def oracle_model_run(golden):
     g = golden("model_ref_n4096.npz")
