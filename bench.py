@@ -224,7 +224,8 @@ def main():
         eager = step
 
     # the eager steps issue the next batch's FPS chain on a side stream (distill.FpsPrefetch)
-    nxt = (lambda i: {"next_batch": batches[(i + 1) % nb]}) if not args.graph else (lambda i: {})
+    # (the graphed step does the same inside graph A, on a forked stream)
+    nxt = lambda i: {"next_batch": batches[(i + 1) % nb]}  # noqa: E731
     for i in range(args.warmup):
         step(*batches[i % nb], **nxt(i))
     if world > 1:

@@ -178,9 +178,10 @@ def epe3d(model, pos1, pos2, flow):
 
 class GraphedStep:
     """One training step replayed from HIP graphs (MI355X: the eager step issues ~2000
-    launches per iteration from Python, ~27 ms of host time, more than the GPU needs).
+    launches per iteration from Python, ~21 ms of host time, about as much as the GPU needs).
 
-        graph A: forward + loss + backward (+ packing the gradients into one flat buffer)
+        graph A: [FPS of the NEXT batch on a forked stream] + forward + loss + backward
+                 (+ packing the gradients into one flat buffer)
         eager:   one all_reduce of the flat gradient buffer (world > 1; RCCL over xGMI)
         graph B: unpack the averaged gradients + optimizer step (Adam, capturable=True)
 
@@ -188,24 +189,36 @@ class GraphedStep:
     step, and keeping it eager avoids depending on collective capture.  `loss_fn(*inputs)`
     must run the whole forward (model call(s) and loss) and return the loss; the inputs are
     copied into static buffers before each replay.  Warm-up iterations run eagerly on a side
-    stream (they allocate lazily-initialised state: optimizer moments, cached attributes)."""
+    stream (they allocate lazily-initialised state: optimizer moments, cached attributes).
+
+    prefetch_fn (optional, e.g. PointConvBidirection.precompute_fps): a function of the first
+    `n_prefetch` inputs whose result loss_fn takes as `fps=`.  Graph A then runs it for the
+    next batch on a forked stream, beside this batch's forward/backward (FpsPrefetch inside
+    the graph: FPS is ~2.4 ms of latency-bound work on 16 CUs), into buffers the next replay
+    reads.  A call whose batch is not the previous call's `next_batch` recomputes it eagerly
+    first, so results never depend on what was prefetched."""
 
     drop_warmup_graph = True  # diagnostics seam (tools/graph_diag.py)
     capture_on_side_stream = False
 
-    def __init__(self, loss_fn, params, optimizer, example_inputs, warmup=3):
+    def __init__(self, loss_fn, params, optimizer, example_inputs, warmup=3, prefetch_fn=None,
+                 n_prefetch=2):
         self.loss_fn = loss_fn
         self.opt = optimizer
         self.params = [p for p in params if p.requires_grad]
         self.static = [t.detach().clone() for t in example_inputs]
         self.world = dist.get_world_size() if is_dist() else 1
+        self.prefetch_fn = prefetch_fn
+        self.n_prefetch = n_prefetch
+        self.static_next = [t.detach().clone() for t in example_inputs[:n_prefetch]]
+        self._pending = None  # (tensors, versions) the buffered prefetch was computed for
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             loss = None
             for _ in range(warmup):
                 self.opt.zero_grad(set_to_none=True)
-                loss = self.loss_fn(*self.static)
+                loss = self.loss_fn(*self.static, **self._fps_kw(self._eager_prefetch()))
                 loss.backward()
                 self._allreduce_eager()
                 self.opt.step()
@@ -213,24 +226,52 @@ class GraphedStep:
             # nodes (created on this side stream) would be reused by the captured backward
             if self.drop_warmup_graph:
                 del loss
+            self.fps_cur = self._eager_prefetch()
+            if self.fps_cur is not None:
+                self.fps_cur = [t.clone() for t in self.fps_cur]
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         # graph A: forward + backward; .grad tensors are allocated inside (static addresses)
         self.opt.zero_grad(set_to_none=True)
         self.graph_a = torch.cuda.CUDAGraph()
         kw = {"stream": side} if self.capture_on_side_stream else {}
+        fork = torch.cuda.Stream() if prefetch_fn is not None else None
         with torch.cuda.graph(self.graph_a, **kw):
-            self.loss = self.loss_fn(*self.static)
+            cap = torch.cuda.current_stream()
+            if fork is not None:
+                # graph B of the previous replay copied its fps_next into fps_cur
+                fork.wait_stream(cap)
+                with torch.cuda.stream(fork):
+                    self.fps_next = list(prefetch_fn(*self.static_next))
+            self.loss = self.loss_fn(*self.static, **self._fps_kw(self.fps_cur))
             self.loss.backward()
             self.grads = [p.grad for p in self.params if p.grad is not None]
             self.flat = torch.cat([g.reshape(-1) for g in self.grads]) if self.world > 1 else None
-        # graph B: unpack + optimizer step
+            if fork is not None:
+                cap.wait_stream(fork)
+        # graph B: unpack + optimizer step (+ hand the prefetched FPS to the next replay)
         self.graph_b = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph_b, pool=self.graph_a.pool(), **kw):
             if self.world > 1:
                 self._unpack()
             self.opt.step()
+            if fork is not None:
+                for c, n in zip(self.fps_cur, self.fps_next):
+                    c.copy_(n)
         torch.cuda.synchronize()
+        self._pending = None
+
+    def _fps_kw(self, fps):
+        return {} if self.prefetch_fn is None else {"fps": fps}
+
+    def _eager_prefetch(self):
+        if self.prefetch_fn is None:
+            return None
+        return list(self.prefetch_fn(*self.static[:self.n_prefetch]))
+
+    @staticmethod
+    def _key(ts):
+        return tuple(ts), tuple(t._version for t in ts)
 
     def _unpack(self):
         off = 0
@@ -253,9 +294,24 @@ class GraphedStep:
             off += g.numel()
         torch._foreach_div_(grads, float(self.world))
 
-    def __call__(self, *inputs):
+    def __call__(self, *inputs, next_batch=None):
         for s, t in zip(self.static, inputs):
             s.copy_(t, non_blocking=True)
+        if self.prefetch_fn is not None:
+            cur = inputs[:self.n_prefetch]
+            hit = False
+            if self._pending is not None:
+                ts, ver = self._pending
+                hit = (len(ts) == len(cur) and all(a is b for a, b in zip(ts, cur))
+                       and ver == tuple(t._version for t in cur))
+            if not hit:  # not prefetched by the previous replay: compute it now
+                for c, n in zip(self.fps_cur, self._eager_prefetch()):
+                    c.copy_(n)
+            nxt = inputs if next_batch is None else next_batch
+            for s, t in zip(self.static_next, nxt[:self.n_prefetch]):
+                s.copy_(t, non_blocking=True)
+            self._pending = (self._key(nxt[:self.n_prefetch]) if next_batch is not None
+                             else None)
         self.graph_a.replay()
         if self.world > 1:
             dist.all_reduce(self.flat)
@@ -263,30 +319,37 @@ class GraphedStep:
         return self.loss.detach()
 
 
-def graphed_flow_step(model, optimizer, example_inputs, loss_fn=None, warmup=3):
-    """FlowTrainStep as a GraphedStep (model: the bare module, not DDP-wrapped)."""
+def graphed_flow_step(model, optimizer, example_inputs, loss_fn=None, warmup=3, prefetch=True):
+    """FlowTrainStep as a GraphedStep (model: the bare module, not DDP-wrapped).  prefetch:
+    the next batch's FPS chain runs inside graph A on a forked stream (see GraphedStep)."""
     loss_fn = loss_fn or loss_functions.multiScaleLoss
     model.train()
 
-    def run(pos1, pos2, flow):
-        flows, fps1, _, _, _, _, _, _ = model(pos1, pos2, pos1, pos2)
+    def run(pos1, pos2, flow, fps=None):
+        kw = {} if fps is None else {"fps_idx": fps}
+        flows, fps1, _, _, _, _, _, _ = model(pos1, pos2, pos1, pos2, **kw)
         return loss_fn(flows, flow, fps1)
-    return GraphedStep(run, model.parameters(), optimizer, example_inputs, warmup)
+    return GraphedStep(run, model.parameters(), optimizer, example_inputs, warmup,
+                       prefetch_fn=model.precompute_fps if prefetch else None)
 
 
 def graphed_kd_step(teacher, student, optimizer, example_inputs, gamma=0.3, beta=0.8, layer=3,
-                    warmup=3):
-    """KDTrainStep (distilTrain.py:164-182) as a GraphedStep."""
+                    warmup=3, prefetch=True):
+    """KDTrainStep (distilTrain.py:164-182) as a GraphedStep; teacher and student share the
+    (prefetched) FPS chain, as KDTrainStep does."""
     for p in teacher.parameters():
         p.requires_grad_(False)
     teacher.eval()
     student.train()
 
-    def run(pos1, pos2, flow):
+    def run(pos1, pos2, flow, fps=None):
+        kw = {} if fps is None else {"fps_idx": fps}
         with torch.no_grad():
-            t_flows, t_fps1, t_fps2, _, _, t_feat1s, t_feat2s, _ = teacher(pos1, pos2, pos1, pos2)
-        flows, fps1, fps2, _, _, feat1s, feat2s, _ = student(pos1, pos2, pos1, pos2)
+            t_flows, t_fps1, t_fps2, _, _, t_feat1s, t_feat2s, _ = teacher(pos1, pos2, pos1, pos2,
+                                                                           **kw)
+        flows, fps1, fps2, _, _, feat1s, feat2s, _ = student(pos1, pos2, pos1, pos2, **kw)
         return loss_functions.biDirection_loss_ht(
             flows, feat1s, feat2s, fps1, fps2, flow, t_flows, t_feat1s, t_feat2s, t_fps1, t_fps2,
             gamma, beta, layer=layer)
-    return GraphedStep(run, student.parameters(), optimizer, example_inputs, warmup)
+    return GraphedStep(run, student.parameters(), optimizer, example_inputs, warmup,
+                       prefetch_fn=student.precompute_fps if prefetch else None)

@@ -44,9 +44,13 @@ def test_graphed_step_equals_eager(mode):
     # the graphed step's constructor ran one eager warm-up step on batches[0]
     eager(*batches[0])
     losses = []
-    for b in batches[1:]:
+    # batches[1] -> batches[2] prefetched inside graph A; then batches[1] again, which the
+    # previous replay did not prefetch (batches[2] was announced as next: eager recompute)
+    seq = [(batches[1], batches[2]), (batches[2], batches[0]), (batches[1], None),
+           (batches[2], None)]
+    for b, nxt in seq:
         le = eager(*b)
-        lg = graphed(*b)
+        lg = graphed(*b, next_batch=nxt)
         losses.append((float(le), float(lg)))
     torch.cuda.synchronize()
     for le, lg in losses:
