@@ -66,8 +66,31 @@ def _stub_pointnet2_cuda():
         grad_points.scatter_add_(2, flat, grad_out.reshape(b, c, -1))
         return 1
 
+    def ball_query_wrapper(b, n, m, radius, nsample, new_xyz, xyz, idx):
+        idx.copy_(torch.from_numpy(C.ball_query(radius, nsample, xyz.numpy(), new_xyz.numpy())))
+        return 1
+
+    def three_nn_wrapper(b, n, m, unknown, known, dist2, idx):
+        d, i = C.three_nn(unknown.numpy(), known.numpy())
+        dist2.copy_(torch.from_numpy(d))
+        idx.copy_(torch.from_numpy(i))
+        return 1
+
+    def three_interpolate_wrapper(b, c, m, n, points, idx, weight, out):
+        g = torch.gather(points, 2, idx.long().view(b, 1, n * 3).expand(-1, c, -1)).view(b, c, n, 3)
+        w = weight.view(b, 1, n, 3)
+        out.copy_(g[..., 0] * w[..., 0] + g[..., 1] * w[..., 1] + g[..., 2] * w[..., 2])
+        return 1
+
+    def three_interpolate_grad_wrapper(b, c, n, m, grad_out, idx, weight, grad_points):
+        for j in range(3):
+            grad_points.scatter_add_(2, idx[..., j].long().view(b, 1, n).expand(-1, c, -1),
+                                     grad_out * weight[..., j].view(b, 1, n))
+        return 1
+
     for f in (furthest_point_sampling_wrapper, gather_points_wrapper, gather_points_grad_wrapper,
-              group_points_wrapper, group_points_grad_wrapper):
+              group_points_wrapper, group_points_grad_wrapper, ball_query_wrapper,
+              three_nn_wrapper, three_interpolate_wrapper, three_interpolate_grad_wrapper):
         setattr(m, f.__name__, f)
     return m
 
@@ -278,6 +301,169 @@ def make_fg(R):
     np.savez_compressed(os.path.join(GOLDEN, "fg_ref.npz"), **out)
 
 
+def make_sa_fp(R):
+    """PointNet++ modules (ref pointnet2/pointnet2_modules.py:10-156) in train mode at B=2,
+    N=1024: a 2-scale MSG set abstraction (FPS 1024->128, r 0.2/0.4, K 16/32, BN), a
+    group-all SA, and a feature-propagation module 1024<-128; outputs, input and parameter
+    gradients of sum(out * fixed weights)."""
+    import importlib
+    mods = importlib.import_module("pointnet2.pointnet2_modules")
+    torch.manual_seed(0)
+    n, b = 1024, 2
+    pairs = [synthetic.ft3d_pair(n, seed=61, pair=i) for i in range(b)]
+    # the scene is ~tens of metres wide: scale to a unit-sized cloud so the radii see
+    # both full and partially filled balls
+    xyz = torch.from_numpy(np.stack([p[0] for p in pairs]) / 10.0).float()
+    rng = np.random.default_rng(63)
+    feats = torch.from_numpy(rng.normal(size=(b, 6, n)).astype(np.float32))
+    sa = _synth(mods.PointnetSAModuleMSG(npoint=128, radii=[0.2, 0.4], nsamples=[16, 32],
+                                         mlps=[[6, 16, 32], [6, 16, 32]], bn=True), seed=65)
+    ga = _synth(mods.PointnetSAModule(mlp=[64, 64, 128], npoint=None, bn=True), seed=66)
+    fp = _synth(mods.PointnetFPModule(mlp=[64 + 6, 64, 32], bn=True), seed=67)
+    for m in (sa, ga, fp):
+        m.train()
+    xi = xyz.clone().requires_grad_(True)
+    fi = feats.clone().requires_grad_(True)
+    new_xyz, f1 = sa(xi, fi)
+    _, f2 = ga(new_xyz, f1)
+    f3 = fp(xi, new_xyz, fi, f1)
+    out = dict(xyz=_np(xyz), feats=_np(feats), new_xyz=_np(new_xyz), sa_out=_np(f1),
+               ga_out=_np(f2), fp_out=_np(f3))
+    loss = 0
+    for k, o in (("sa", f1), ("ga", f2), ("fp", f3)):
+        loss = loss + (o * torch.from_numpy(flow_layer_weight(k, tuple(o.shape)))).sum()
+    loss.backward()
+    out["dxyz"] = _np(xi.grad)
+    out["dfeats"] = _np(fi.grad)
+    for tag, m in (("sa", sa), ("ga", ga), ("fp", fp)):
+        for k, prm in m.named_parameters():
+            if prm.grad is not None:
+                out[f"grad_{tag}.{k}"] = _np(prm.grad)
+        for k, buf in m.named_buffers():
+            out[f"buf_{tag}.{k}"] = _np(buf)
+    np.savez_compressed(os.path.join(GOLDEN, "pointnet2_modules_ref.npz"), **out)
+
+
+def _stub_data_deps():
+    """numba (the reference's unused lattice helpers are @njit-decorated at import) and pptk
+    (imported, unused) are absent here: identity decorators / empty modules."""
+    nb = types.ModuleType("numba")
+
+    class _Ty:
+        def __getitem__(self, k):
+            return self
+
+        def __call__(self, *a, **k):
+            return self
+    nb.int64 = _Ty()
+
+    def njit(*a, **k):
+        if len(a) == 1 and callable(a[0]) and not k:
+            return a[0]
+        return lambda f: f
+    nb.njit = njit
+    sys.modules["numba"] = nb
+    sys.modules["pptk"] = types.ModuleType("pptk")
+    if not hasattr(np, "float"):
+        np.float = float  # evaluation_utils.py:30 (removed from NumPy >= 1.24)
+
+
+def make_data(R, scenes=(1, 2, 3), stride=16):
+    """Data path + metrics through the reference's own code:
+    KITTI.pc_loader (ground removal) and the mapping filter, FlyingThings3DSubset.pc_loader
+    (sign flips), ProcessData / Augmentation under fixed NumPy seeds (both NO_CORR modes,
+    replacement and allow_less fallbacks, DEPTH_THRESHOLD 0), KITTI __getitem__, and
+    evaluate_3d / evaluate_2d / get_batch_2d_flow (KITTI calibration and FT3D intrinsics).
+    Inputs are every `stride`-th point of real KITTI scenes from the reference tree."""
+    import importlib
+    import tempfile
+    _stub_data_deps()
+    T = importlib.import_module("transforms")
+    D = importlib.import_module("datasets")
+    E = importlib.import_module("evaluation_utils")
+    G = importlib.import_module("utils.geometry")
+    out = {}
+    kroot = os.path.join(REF, "datasets", "kitti_processed")
+    with open(os.path.join(REF, "datasets", "KITTI_mapping.txt")) as fd:
+        mapping = [ln.strip() != "" for ln in fd.readlines()]
+    out["mapping_nonempty"] = np.array(mapping, dtype=bool)
+    tmp = tempfile.mkdtemp()
+    for s_ in scenes:
+        name = "%06d" % s_
+        pc1 = np.load(os.path.join(kroot, name, "pc1.npy"))[::stride].copy()
+        pc2 = np.load(os.path.join(kroot, name, "pc2.npy"))[::stride].copy()
+        out[f"k{s_}_pc1"], out[f"k{s_}_pc2"] = pc1, pc2
+        d = os.path.join(tmp, "kitti_processed", name)
+        os.makedirs(d)
+        np.save(os.path.join(d, "pc1.npy"), pc1)
+        np.save(os.path.join(d, "pc2.npy"), pc2)
+        a, b = D.KITTI.pc_loader(types.SimpleNamespace(remove_ground=True), d)
+        out[f"k{s_}_noground_pc1"], out[f"k{s_}_noground_pc2"] = a, b
+        a, b = D.FlyingThings3DSubset.pc_loader(None, d)
+        out[f"k{s_}_ft3d_pc1"], out[f"k{s_}_ft3d_pc2"] = a, b
+    base1, base2 = out["k2_noground_pc1"], out["k2_noground_pc2"]
+    n_avail = int(np.logical_and(base1[:, 2] < 35, base2[:, 2] < 35).sum())
+    cases = {"pd_nocorr": (dict(DEPTH_THRESHOLD=35., NO_CORR=True), 2048, False),
+             "pd_corr": (dict(DEPTH_THRESHOLD=35., NO_CORR=False), 2048, False),
+             "pd_replace": (dict(DEPTH_THRESHOLD=35., NO_CORR=True), n_avail + 100, False),
+             "pd_allowless": (dict(DEPTH_THRESHOLD=35., NO_CORR=True), n_avail + 100, True),
+             "pd_nodepth": (dict(DEPTH_THRESHOLD=0., NO_CORR=True), 1024, False),
+             "pd_all": (dict(DEPTH_THRESHOLD=35., NO_CORR=True), 0, False)}
+    for i, (k, (dp, npts, allow)) in enumerate(cases.items()):
+        np.random.seed(100 + i)
+        r = T.ProcessData(dp, npts, allow)([base1.copy(), base2.copy()])
+        out.update({f"{k}_pc1": r[0], f"{k}_pc2": r[1], f"{k}_sf": r[2]})
+    together = dict(degree_range=0.1745329252, shift_range=1., scale_low=0.95, scale_high=1.05,
+                    jitter_sigma=0.01, jitter_clip=0.00)
+    pc2a = dict(degree_range=0., shift_range=0.3, jitter_sigma=0.01, jitter_clip=0.00)
+    pc2b = dict(degree_range=0.1, shift_range=0.3, jitter_sigma=0.01, jitter_clip=0.05)
+    tog_b = dict(together, jitter_clip=0.02)
+    augs = {"aug_cfg_nocorr": (together, pc2a, True), "aug_clip_corr": (tog_b, pc2b, False)}
+    for i, (k, (ta, pa, nc)) in enumerate(augs.items()):
+        np.random.seed(200 + i)
+        r = T.Augmentation(ta, pa, dict(DEPTH_THRESHOLD=35., NO_CORR=nc), 2048)(
+            [base1.copy(), base2.copy()])
+        out.update({f"{k}_pc1": r[0], f"{k}_pc2": r[1], f"{k}_sf": r[2]})
+    # dataset item through the reference KITTI class (ground removal + mapping + ProcessData)
+    import shutil
+    shutil.copy(os.path.join(REF, "datasets", "KITTI_mapping.txt"), tmp)
+    ds = D.KITTI(train=False, transform=T.ProcessData(dict(DEPTH_THRESHOLD=35., NO_CORR=True),
+                                                      2048, False),
+                 num_points=2048, data_root=tmp)
+    out["ds_len"] = np.array(len(ds))
+    np.random.seed(300)
+    item = ds[len(ds) - 1]
+    for j, k in enumerate(("pos1", "pos2", "norm1", "norm2", "flow")):
+        out[f"ds_{k}"] = item[j]
+    out["ds_scene"] = np.array(os.path.basename(item[5]))
+    # metrics
+    rng = np.random.default_rng(400)
+    gt = out["pd_nocorr_sf"][None].repeat(2, 0).astype(np.float32)
+    pred = (gt + rng.normal(scale=0.08, size=gt.shape)).astype(np.float32)
+    pc1 = out["pd_nocorr_pc1"][None].repeat(2, 0)
+    out.update(m_gt=gt, m_pred=pred, m_pc1=pc1)
+    out["m_3d"] = np.array(E.evaluate_3d(pred, gt), dtype=np.float64)
+    # KITTI intrinsics are (B,1,1) in the reference and broadcast against (B,N) points to
+    # (B,B,N): only B=1 (its evaluation config) is well defined, so one call per scene
+    for j, s_ in enumerate(scenes[-2:]):
+        sl = slice(j, j + 1)
+        fp, fg = G.get_batch_2d_flow(pc1[sl], pc1[sl] + gt[sl], pc1[sl] + pred[sl],
+                                     [os.path.join(kroot, "%06d" % s_)])
+        out[f"m_kitti{j}_flow_pred"], out[f"m_kitti{j}_flow_gt"] = fp, fg
+        out[f"m_kitti{j}_2d"] = np.array(E.evaluate_2d(fp, fg), dtype=np.float64)
+    paths = ["/data/FlyingThings3D_subset_processed_35m/val/0000000",
+             "/data/FlyingThings3D_subset_processed_35m/val/0000001"]
+    fp, fg = G.get_batch_2d_flow(pc1, pc1 + gt, pc1 + pred, paths)
+    out["m_ft3d_flow_pred"], out["m_ft3d_flow_gt"] = fp, fg
+    out["m_ft3d_2d"] = np.array(E.evaluate_2d(fp, fg), dtype=np.float64)
+    for s_ in scenes:
+        with open(os.path.join(REF, "utils", "calib_cam_to_cam", "%06d.txt" % s_)) as fd:
+            line = [ln for ln in fd.readlines() if ln.startswith("P_rect_02")][0]
+        out[f"calib{s_}_p_rect_02"] = np.array(line.strip())
+    shutil.rmtree(tmp)
+    np.savez_compressed(os.path.join(GOLDEN, "data_path_ref.npz"), **out)
+
+
 def make_model(R, n=4096):
     """Teacher (eval) + student (train) at B=1, N=n; MSL and KD losses and grad summaries."""
     p1, p2, fl = synthetic.ft3d_pair(n, seed=7, pair=0)
@@ -398,6 +584,7 @@ def main(which=None):
     steps = {"knn": lambda: make_knn(R), "losses": lambda: make_losses(R),
              "layers": lambda: make_layers(R), "model": lambda: make_model(R),
              "flowlayers": lambda: make_flow_layers(R), "fg": lambda: make_fg(R),
+             "safp": lambda: make_sa_fp(R), "data": lambda: make_data(R),
              "trace2048": lambda: make_model_knn_trace(R),
              # BASELINE configs[2]'s point count (the metric's size), B=1
              "trace8192": lambda: make_model_knn_trace(R, n=8192)}
