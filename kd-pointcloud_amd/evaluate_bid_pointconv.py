@@ -50,8 +50,8 @@ def evaluate(model, loader, calib_dir=None, loss_fn=None):
         m3 = evaluate_3d(full, flow)
         fp, fg = geometry.get_batch_2d_flow(pos1, pos1 + flow, pos1 + full, paths, calib_dir)
         m2 = evaluate_2d(fp, fg)
-        row = torch.stack([(loss * b).double(), (epe * b).double(),
-                           *[v.double() for v in m3], *[v.double() for v in m2]])
+        row = torch.stack([v.reshape(()).double() for v in
+                           (loss * b, epe * b, *m3, *m2)])
         acc = row if acc is None else acc + row
         nb += 1
         seen += b
