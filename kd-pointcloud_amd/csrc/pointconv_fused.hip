@@ -30,6 +30,7 @@
 // indices 8b+j (lanes 0-31) and 8b+4+j (lanes 32-63), so every lane's operands for four
 // steps are one float4 (LDS: ds_read_b128; global: one 16-byte load).
 #include <algorithm>
+#include <type_traits>
 
 #include "kdpc_common.h"
 
@@ -572,6 +573,228 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
   }
 }
 
+// Software-pipelined variant of the data kernel.  The kernel above runs each chunk as an
+// MFMA phase (dA = dy wl for the chunk) then, after a barrier, a VALU phase (dG / dwt from
+// that dA): inside one workgroup the two never overlap, and the matrix cores idle through
+// the VALU phase unless the CU's other workgroup happens to be in its MFMA phase.  Here dA is
+// double-buffered in LDS and iteration ch issues chunk ch+1's MFMAs and chunk ch's VALU work
+// in one loop body (step i: one mfma4 of ch+1, then pair-channel item i of ch), so the VALU
+// and LDS work fills the MFMAs' 64-cycle issue shadows of the same wave.  One barrier per
+// chunk.  Identical arithmetic to pc_bwd_data_kernel (same fma order in every sum), so the
+// two produce bit-identical dG / dwt / dcenter.
+template <int O, int KM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* __restrict__ wsw,
+                             const float* __restrict__ dy, float* __restrict__ dgr,
+                             float* __restrict__ dwt, float* __restrict__ dcenter,
+                             int chunks_per_split) {
+  constexpr int TR = 32;
+  constexpr int NT = 256;
+  constexpr int PP = (TR * KM + NT - 1) / NT;  // pairs per thread
+  constexpr int NOG = O / 8;
+  constexpr int PF = NOG < 4 ? NOG : 4;
+  constexpr int NIT = PP * kCC;                // VALU items per chunk per thread
+  constexpr int STEPS = NOG > NIT ? NOG : NIT;
+  __shared__ __attribute__((aligned(16))) float dyl[(O / 4) * kBlk];
+  __shared__ __attribute__((aligned(16))) float dal[2][32 * kDaS];
+  __shared__ float dcl[NT * PP * 3];  // every pair slot (invalid ones write zeros)
+  const int row0 = blockIdx.x * TR;
+  const int split = blockIdx.y;
+  const int ch0 = split * chunks_per_split;
+  const int ch1 = min(g.nch, ch0 + chunks_per_split);
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, half = lane >> 5, l32 = lane & 31;
+  const long long rk_total = (long long)g.r * g.k;
+  const Srcs src = srcs_of(g);
+
+  for (int e = t; e < 32 * O; e += NT) {
+    const int r = e / O, o = e % O;
+    const int row = row0 + r;
+    dyl[(o >> 2) * kBlk + r * 4 + (o & 3)] = row < g.r ? dy[(long long)row * O + o] : 0.f;
+  }
+  float wp[PP][kW], dw[PP][kW];
+  int pr[PP], pk[PP], pn[PP], prc[PP];
+#pragma unroll
+  for (int q = 0; q < PP; ++q) {
+    const int p = t + NT * q;
+    pr[q] = p / g.k;
+    pk[q] = p - pr[q] * g.k;
+    prc[q] = min(pr[q], TR - 1);  // dA row read by this slot (any row when the pair is dead)
+    const bool ok = p < TR * g.k && row0 + pr[q] < g.r;
+    pn[q] = ok ? nbr_of(g, row0 + pr[q], pk[q]) : -1;
+    const long long pos = (long long)(row0 + pr[q]) * g.k + pk[q];
+#pragma unroll
+    for (int v = 0; v < kW / 4; ++v) {
+      const float4 x = ok ? reinterpret_cast<const float4*>(wt + pos * kW)[v]
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+      wp[q][4 * v + 0] = x.x;
+      wp[q][4 * v + 1] = x.y;
+      wp[q][4 * v + 2] = x.z;
+      wp[q][4 * v + 3] = x.w;
+    }
+#pragma unroll
+    for (int w = 0; w < kW; ++w) dw[q][w] = 0.f;
+  }
+
+  auto brow = [&](int ch) { return wsw + (long long)((ch * 4 + wv) * NOG) * 64 + lane; };
+  auto gather = [&](int ch, float (&dst)[PP][kCC]) {
+    const bool c0 = ch == 0;
+    const unsigned lo_ch = c0 ? 0u : (unsigned)(ch * kCC - 3) * 4u;
+    const unsigned hi_ch = c0 ? 4u : lo_ch + 16u;
+#pragma unroll
+    for (int q = 0; q < PP; ++q) {
+      const int nb = pn[q];
+      const bool live = nb >= 0;
+      const unsigned fo = live ? (unsigned)nb * (unsigned)g.d * 4u : kOOB;
+      const f32x4 lo = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     src.feats, (int)(fo + lo_ch), 0, 0));
+      const f32x4 hi = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     src.feats, (int)(fo + hi_ch), 0, 0));
+      const unsigned xo = (c0 && live) ? (unsigned)nb * 12u : kOOB;
+      const unsigned co = (c0 && live) ? (unsigned)(row0 + pr[q]) * 12u : kOOB;
+      const f32x4 x = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                    src.xyz, (int)xo, 0, 0));
+      const f32x4 cc = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     src.center, (int)co, 0, 0));
+      float v[kCC];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) v[c] = (c0 ? 0.f : lo[c]) + (x[c] - cc[c]);
+      v[3] = c0 ? lo[0] : lo[3];
+#pragma unroll
+      for (int c = 4; c < kCC; ++c) v[c] = hi[c - 4];
+#pragma unroll
+      for (int c = 0; c < kCC; ++c) dst[q][c] = ch * kCC + c < g.c ? v[c] : 0.f;
+    }
+  };
+  auto store_da = [&](const f32x16& acc, int buf) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e)
+      dal[buf][((e & 3) + 8 * (e >> 2) + 4 * half) * kDaS + wv * 32 + l32] = acc[e];
+  };
+
+  float4 bq[PF];
+  float gv[PP][kCC], gn[PP][kCC];
+  if (ch0 < ch1) {
+    const float4* wr0 = brow(ch0);
+#pragma unroll
+    for (int p2 = 0; p2 < PF; ++p2) bq[p2] = wr0[p2 * 64];
+    gather(ch0, gv);
+  }
+  __syncthreads();  // dyl
+  if (ch0 < ch1) {  // prologue: chunk ch0's dA
+    const float4* wrow = brow(ch0);
+    f32x16 acc = zero16();
+#pragma unroll
+    for (int og = 0; og < NOG; ++og) {
+      const float4 av = *reinterpret_cast<const float4*>(dyl + (2 * og + half) * kBlk + l32 * 4);
+      acc = mfma4(av, bq[og % PF], acc);
+      if (og + PF < NOG) bq[og % PF] = wrow[(og + PF) * 64];
+    }
+    store_da(acc, 0);
+    if (ch0 + 1 < ch1) {
+      const float4* wr1 = brow(ch0 + 1);
+#pragma unroll
+      for (int p2 = 0; p2 < PF; ++p2) bq[p2] = wr1[p2 * 64];
+    }
+  }
+  __syncthreads();
+  // one chunk step: chunk ch+1's MFMAs (when MF) interleaved with chunk ch's VALU items.
+  // Branch-free body (dead pair slots compute zeros from zero weights / gathers on a clamped
+  // dA row) so the MFMAs and the VALU work share one basic block for the scheduler.
+  auto step = [&](auto mf, const float* dab, const float4* wr1, f32x16& acc,
+                  float (&sv)[PP][kCC]) {
+#pragma unroll
+    for (int i = 0; i < STEPS; ++i) {
+      if constexpr (decltype(mf)::value) {
+        if (i < NOG) {
+          const float4 av =
+              *reinterpret_cast<const float4*>(dyl + (2 * i + half) * kBlk + l32 * 4);
+          acc = mfma4(av, bq[i % PF], acc);
+          if (i + PF < NOG) bq[i % PF] = wr1[(i + PF) * 64];
+        }
+      }
+      if (i < NIT) {
+        const int q = i / kCC, cl = i % kCC;
+        const float4* drow = reinterpret_cast<const float4*>(dab + prc[q] * kDaS) + cl * (kW / 4);
+        float da[kW];
+#pragma unroll
+        for (int v = 0; v < kW / 4; ++v) {
+          const float4 x = drow[v];
+          da[4 * v + 0] = x.x;
+          da[4 * v + 1] = x.y;
+          da[4 * v + 2] = x.z;
+          da[4 * v + 3] = x.w;
+        }
+        float sacc = 0.f;
+#pragma unroll
+        for (int w = 0; w < kW; ++w) sacc = __builtin_fmaf(da[w], wp[q][w], sacc);
+        sv[q][cl] = sacc;
+        const float gc = gv[q][cl];
+#pragma unroll
+        for (int w = 0; w < kW; ++w) dw[q][w] = __builtin_fmaf(da[w], gc, dw[q][w]);
+      }
+      // keep each step's loads with its own math (hoisting every step's dA reads spilled)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  for (int ch = ch0; ch < ch1; ++ch) {
+    const int buf = (ch - ch0) & 1;
+    const bool more = ch + 1 < ch1;  // uniform
+    const int c0 = ch * kCC;
+    if (more) gather(ch + 1, gn);
+    f32x16 acc = zero16();
+    float sv[PP][kCC];
+    if (more)
+      step(std::true_type{}, dal[buf], brow(ch + 1), acc, sv);
+    else
+      step(std::false_type{}, dal[buf], brow(ch + 1), acc, sv);
+#pragma unroll
+    for (int q = 0; q < PP; ++q) {
+      if (c0 == 0) {
+#pragma unroll
+        for (int cl = 0; cl < 3; ++cl) dcl[(t + NT * q) * 3 + cl] = sv[q][cl];
+      }
+      if (pn[q] >= 0) {
+        const long long pos = (long long)(row0 + pr[q]) * g.k + pk[q];
+        float4* dgo = reinterpret_cast<float4*>(dgr + pos * g.c8 + c0);
+        dgo[0] = make_float4(sv[q][0], sv[q][1], sv[q][2], sv[q][3]);
+        dgo[1] = make_float4(sv[q][4], sv[q][5], sv[q][6], sv[q][7]);
+      }
+    }
+    if (more) {
+      store_da(acc, buf ^ 1);
+      if (ch + 2 < ch1) {
+        const float4* wr2 = brow(ch + 2);
+#pragma unroll
+        for (int p2 = 0; p2 < PF; ++p2) bq[p2] = wr2[p2 * 64];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PP; ++q)
+#pragma unroll
+      for (int c = 0; c < kCC; ++c) gv[q][c] = gn[q][c];
+  }
+  if (ch0 == 0 && t < TR * 3) {
+    const int r = t / 3, i = t - (t / 3) * 3;
+    const int row = row0 + r;
+    if (row < g.r) {
+      float s = 0.f;
+      for (int k = 0; k < g.k; ++k) s = __fadd_rn(s, dcl[(r * g.k + k) * 3 + i]);  // slot p
+      dcenter[(long long)row * 3 + i] = -s;
+    }
+  }
+  float* dwt_dst = dwt + (long long)split * rk_total * kW;
+#pragma unroll
+  for (int q = 0; q < PP; ++q) {
+    if (pn[q] < 0) continue;
+    const long long pos = (long long)(row0 + pr[q]) * g.k + pk[q];
+    float4* dst = reinterpret_cast<float4*>(dwt_dst + pos * kW);
+#pragma unroll
+    for (int v = 0; v < kW / 4; ++v)
+      dst[v] = make_float4(dw[q][4 * v], dw[q][4 * v + 1], dw[q][4 * v + 2], dw[q][4 * v + 3]);
+  }
+}
+
 // wl (O, 16C) -> the data kernel's B operand order: float4 (ch, wave, og, lane) =
 // wl[8 og + 4 (lane >> 5) + 0..3][ch * 128 + 32 wave + (lane & 31)], zero past column 16C.
 // One thread per float4; a wave reads 32 consecutive columns of 4 rows (coalesced).
@@ -970,6 +1193,19 @@ hipError_t fwd_launch(const Geo& g, const Plan& p, const float* wt, const float*
   return slab_sum(p.ks, (long long)p.r * O, slab, bias, O, y, st);
 }
 
+// KDPC_PC_BWD_PIPE=1 selects the software-pipelined data kernel.  Measured round 2 (flow0,
+// B=8, N=8192): bit-identical outputs, 1199 vs 1191 us for the whole backward -- interleaving
+// the phases did not pay (the chunk loop waits on memory: a B-fragment wait also waits for
+// older gathers and dG stores, vmcnt retiring in order), so the unpipelined kernel stays the
+// default.
+inline bool bwd_pipe_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("KDPC_PC_BWD_PIPE");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
+
 template <int O, int KM>
 hipError_t bwd_launch(const Geo& g, const Plan& p, int b, const float* wt, const float* wl,
                       const float* dy, const int* offsets, const int* perm, float* dxyz,
@@ -986,9 +1222,13 @@ hipError_t bwd_launch(const Geo& g, const Plan& p, int b, const float* wt, const
                      O, c16, g.nch, wl, wsw);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((pc_bwd_data_kernel<O, KM>), dim3(divup(p.r, bwd_tile_rows<KM>()), p.bks),
-                     dim3(bwd_threads<KM>()), 0, st,
-                     g, wt, wsw, dy, dgr, p.bks > 1 ? dwt_slab : dwt, dcenter, p.bcps);
+  if (bwd_pipe_enabled())
+    hipLaunchKernelGGL((pc_bwd_data_pipe_kernel<O, KM>), dim3(divup(p.r, 32), p.bks), dim3(256),
+                       0, st, g, wt, wsw, dy, dgr, p.bks > 1 ? dwt_slab : dwt, dcenter, p.bcps);
+  else
+    hipLaunchKernelGGL((pc_bwd_data_kernel<O, KM>), dim3(divup(p.r, bwd_tile_rows<KM>()), p.bks),
+                       dim3(bwd_threads<KM>()), 0, st,
+                       g, wt, wsw, dy, dgr, p.bks > 1 ? dwt_slab : dwt, dcenter, p.bcps);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (p.bks > 1 && (e = slab_sum(p.bks, rk * kW, dwt_slab, nullptr, 1, dwt, st)) != hipSuccess)

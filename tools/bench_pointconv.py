@@ -38,18 +38,36 @@ def timeit(fn, iters=10, warmup=2):
     return s.elapsed_time(e) / iters * 1e3
 
 
+def morton_sort(xyz, bits=10):
+    lo = xyz.amin(1, keepdim=True)
+    hi = xyz.amax(1, keepdim=True)
+    q = ((xyz - lo) / (hi - lo + 1e-9) * (2 ** bits - 1)).long()
+    code = torch.zeros(xyz.shape[:2], dtype=torch.long, device=xyz.device)
+    for b in range(bits):
+        for a in range(3):
+            code |= ((q[..., a] >> b) & 1) << (3 * b + a)
+    order = code.argsort(1)
+    return torch.gather(xyz, 1, order.unsqueeze(-1).expand(-1, -1, 3)).contiguous()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default=None)
     ap.add_argument("--only", default=None, help="substring of the shape names to run")
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--dump", default=None, help="save every backward output here (.npz)")
+    ap.add_argument("--morton", action="store_true",
+                    help="sort each cloud by a Morton code first (spatially coherent rows)")
     args = ap.parse_args()
     res = {}
+    dump = {}
     g = torch.Generator(device="cpu").manual_seed(0)
     for name, (B, N, S, Kn, D, O) in SHAPES.items():
         if args.only and args.only not in name:
             continue
         xyz = torch.randn(B, N, 3, generator=g).to(DEV)
+        if args.morton:
+            xyz = morton_sort(xyz)
         center = xyz[:, :S].contiguous()
         feats = torch.randn(B, N, D, generator=g).to(DEV)
         idx = K.knn_point(Kn, xyz, center)
@@ -62,6 +80,11 @@ def main():
         fwd = timeit(lambda: K.pointconv_fwd(xyz, center, feats, idx, wt, wl, bias), args.iters)
         bwd = timeit(lambda: K.pointconv_bwd(xyz, center, feats, idx, wt, wl, dy, csr,
                                              need_xyz=False), args.iters)
+        if args.dump:
+            outs = K.pointconv_bwd(xyz, center, feats, idx, wt, wl, dy, csr, need_xyz=True)
+            for i, o in enumerate(outs):
+                if torch.is_tensor(o):
+                    dump[f"{name}/{i}"] = o.cpu().numpy()
         R = B * S
         gemm = 2.0 * R * 16 * C * O
         build = 2.0 * R * Kn * C * 16
@@ -69,6 +92,9 @@ def main():
                      "fwd_TFLOPs": round((gemm + build) / (fwd * 1e-6) / 1e12, 1),
                      "bwd_TFLOPs": round((2 * gemm + 3 * build) / (bwd * 1e-6) / 1e12, 1)}
         print(name, res[name], flush=True)
+    if args.dump:
+        import numpy as np
+        np.savez(args.dump, **dump)
     if args.json:
         with open(args.json, "w") as f:
             json.dump(res, f, indent=1)
