@@ -1,33 +1,41 @@
 // Deterministic column sums of per-workgroup partial slabs: dst[i] = sum_s slab[s][i].
 //
-// Every parameter-gradient reduction here ends with such a sum over hundreds to thousands
-// of slab rows.  One thread walking all rows of one column serialises thousands of
-// dependent loads (~110 us for 512 x 248); instead the rows are summed in chunks of 64 by
-// a 2-D grid, and the chunk partials again, each level in a fixed order (ascending rows
-// within a chunk, ascending chunks), so the result depends only on the shape.
+// Every parameter-gradient reduction here ends with such a sum over hundreds to millions
+// of rows.  One thread walking all rows of one column serialises thousands of dependent
+// loads (~110 us for 512 x 248); instead a 2-D grid sums row slabs (level 1: about 1024
+// workgroups over the whole matrix, each 64 columns x one contiguous slab of rows) and one
+// more launch sums the slab partials (level 2); matrices of <= 256 rows take one launch.
+// Inside a workgroup the 4 row groups each sum a contiguous quarter of the slab ascending
+// and the quarters are added in order, so the result depends only on the shape.  (Round 1
+// used fixed 64-row chunks and as many levels as needed: 3-4 launches for the 2^16-2^21
+// row gradients, 215 launches per training step.)
 #include <algorithm>
 
 #include "kdpc_common.h"
 
 namespace {
 
-constexpr int kCols = 64;     // columns per workgroup
-constexpr int kGroups = 4;    // row groups per workgroup (256 threads)
-constexpr int kChunk = 64;    // rows per workgroup
+using kdpc::divupll;
 
-// out[blockIdx.y][c] = sum of rows [blockIdx.y*kChunk, +kChunk) of column c (in order:
-// rows within each of the kGroups interleaved sub-chunks ascending, sub-chunks ascending)
-__global__ __launch_bounds__(256) void colsum_kernel(int nrows, long long len,
+constexpr int kCols = 64;        // columns per workgroup
+constexpr int kGroups = 4;       // row groups per workgroup (256 threads)
+constexpr int kOneLevel = 256;   // rows summed in a single launch
+constexpr int kLevel1WG = 1024;  // level-1 workgroups aimed for
+
+// out[blockIdx.y][c] = sum of rows [blockIdx.y*rpw, +rpw) of column c: row group g sums the
+// g-th contiguous quarter ascending, the quarters are added in order
+__global__ __launch_bounds__(256) void colsum_kernel(int nrows, long long len, int rpw,
                                                      const float* __restrict__ src,
                                                      float* __restrict__ dst) {
   __shared__ float part[kGroups][kCols];
   const int cx = threadIdx.x % kCols, g = threadIdx.x / kCols;
   const long long c = (long long)blockIdx.x * kCols + cx;
-  const int r0 = blockIdx.y * kChunk + g * (kChunk / kGroups);
-  const int r1 = min(nrows, r0 + kChunk / kGroups);
+  const int q = (rpw + kGroups - 1) / kGroups;
+  const int r0 = blockIdx.y * rpw + g * q;
+  const int r1 = min(min(nrows, blockIdx.y * rpw + rpw), r0 + q);
   float a = 0.f;
   if (c < len) {
-#pragma unroll 4
+#pragma unroll 8
     for (int r = r0; r < r1; ++r) a = __fadd_rn(a, src[(long long)r * len + c]);
   }
   part[g][cx] = a;
@@ -35,9 +43,24 @@ __global__ __launch_bounds__(256) void colsum_kernel(int nrows, long long len,
   if (g == 0 && c < len) {
     float s = part[0][cx];
 #pragma unroll
-    for (int q = 1; q < kGroups; ++q) s = __fadd_rn(s, part[q][cx]);
+    for (int k = 1; k < kGroups; ++k) s = __fadd_rn(s, part[k][cx]);
     dst[(long long)blockIdx.y * len + c] = s;
   }
+}
+
+// level-1 slab count and rows per slab for an (nrows, len) matrix (1 slab: single launch)
+inline void colsum_plan(int nrows, long long len, int* slabs, int* rpw) {
+  if (nrows <= kOneLevel) {
+    *slabs = 1;
+    *rpw = nrows;
+    return;
+  }
+  const long long cb = divupll(len, kCols);
+  long long g = std::max(2ll, divupll(kLevel1WG, cb));
+  g = std::min(g, divupll(nrows, 64));
+  g = std::max(1ll, std::min(g, 1024ll));
+  *rpw = (int)divupll(nrows, g);
+  *slabs = (int)divupll(nrows, *rpw);
 }
 
 }  // namespace
@@ -45,30 +68,26 @@ __global__ __launch_bounds__(256) void colsum_kernel(int nrows, long long len,
 namespace kdpc {
 
 size_t colsum_scratch_floats(int nrows, long long len) {
-  size_t total = 0;
-  int n = nrows;
-  while (n > kChunk) {
-    n = divup(n, kChunk);
-    total += (size_t)n * len;
-  }
-  return total;
+  int slabs, rpw;
+  colsum_plan(nrows, len, &slabs, &rpw);
+  return slabs > 1 ? (size_t)slabs * len : 0;
 }
 
 hipError_t colsum(int nrows, long long len, const float* slab, float* dst, float* scratch,
                   hipStream_t st) {
-  const float* src = slab;
-  int n = nrows;
-  while (true) {
-    const int out_rows = divup(n, kChunk);
-    float* out = out_rows == 1 ? dst : scratch;
-    dim3 grid((unsigned)divupll(len, kCols), (unsigned)out_rows);
-    hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, st, n, len, src, out);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess || out_rows == 1) return e;
-    src = out;
-    scratch += (size_t)out_rows * len;
-    n = out_rows;
+  int slabs, rpw;
+  colsum_plan(nrows, len, &slabs, &rpw);
+  const unsigned cb = (unsigned)divupll(len, kCols);
+  if (slabs == 1) {
+    hipLaunchKernelGGL(colsum_kernel, dim3(cb, 1), dim3(256), 0, st, nrows, len, nrows, slab, dst);
+    return hipGetLastError();
   }
+  hipLaunchKernelGGL(colsum_kernel, dim3(cb, (unsigned)slabs), dim3(256), 0, st, nrows, len, rpw,
+                     slab, scratch);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(colsum_kernel, dim3(cb, 1), dim3(256), 0, st, slabs, len, slabs, scratch, dst);
+  return hipGetLastError();
 }
 
 }  // namespace kdpc

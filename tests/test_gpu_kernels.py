@@ -335,3 +335,18 @@ def test_knn_point_dispatches_feature_space(nat):
     qry = _t(rng.normal(size=(2, 200, 16)).astype(np.float32))
     np.testing.assert_array_equal(P.knn_point(8, ref, qry).cpu().numpy(),
                                   nat.knn_feature(8, ref, qry).cpu().numpy())
+
+
+@pytest.mark.parametrize("rows,cols", [(1, 7), (200, 3), (256, 64), (257, 130), (4096, 256),
+                                       (65536, 128), (2359296, 3), (131072, 2048)])
+def test_colsum_fixed_order(nat, rows, cols):
+    """Two-level deterministic column sum (csrc/colsum.hip) vs a float64 sum: within the fp32
+    accumulation bound, and bitwise repeatable."""
+    g = torch.Generator(device="cpu").manual_seed(rows + cols)
+    x = torch.randn(rows, cols, generator=g).to(DEV)
+    a = nat.colsum(x)
+    b = nat.colsum(x)
+    assert torch.equal(a, b)
+    want = x.double().sum(0)
+    bound = 1e-6 * x.double().abs().sum(0) * max(1.0, float(np.log2(rows)))
+    assert ((a.double() - want).abs() <= bound + 1e-6).all()
