@@ -10,6 +10,7 @@
 // so grad[b,..,n] = sum of grad_out over perm[offsets[b*N+n] .. offsets[b*N+n+1]) in
 // ascending position order — bit-identical to a sequential CPU accumulation, independent of
 // scheduling.  One CSR serves every gradient that scatters through the same index.
+
 #include <hipcub/hipcub.hpp>
 
 #include "kdpc_common.h"
@@ -18,26 +19,98 @@ using namespace kdpc;
 
 namespace {
 
-__global__ void csr_keys_kernel(int b, int n, int p, const int* __restrict__ idx,
-                                unsigned* __restrict__ keys, int* __restrict__ vals) {
-  const long long total = (long long)b * p;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int bi = (int)(e / p);
-    keys[e] = (unsigned)bi * (unsigned)n + (unsigned)idx[e];
-    vals[e] = (int)e;
+// CSR build = a counting sort by key (b*N + idx) that keeps ascending position inside a key:
+//   memset (two count arrays) -> count (integer atomics) -> exclusive scan (hipcub,
+//   single-pass decoupled look-back) -> fill (slot = offset + an atomic per-key counter:
+//   every position lands in its key's segment, in arbitrary order) -> segment rank sort
+//   (one wave per key), which restores ascending position order.
+// ~6 launches and ~3 passes over the index, against ~10 launches of rocprim's radix /
+// merge sort (round 1: 19 builds per training step, 1.5 ms).  The result is exactly the
+// stable sort's, so every gather-sum through it is bit-identical to before.  Indices
+// outside [0, N) are left out of every segment (the reference had no bounds check).
+// grid (position blocks, batch): no per-element division
+__global__ __launch_bounds__(256) void csr_count_kernel(int n, int p, const int* __restrict__ idx,
+                                                        int* __restrict__ cnt) {
+  const int b = blockIdx.y;
+  const int* row = idx + (long long)b * p;
+  int* c = cnt + (long long)b * n;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < p; i += gridDim.x * blockDim.x) {
+    const int v = row[i];
+    if ((unsigned)v < (unsigned)n) atomicAdd(&c[v], 1);
   }
 }
 
-// offsets[k] = first sorted slot with key >= k, for k in [0, B*N]
-__global__ void csr_offsets_kernel(long long total, unsigned nkeys,
-                                   const unsigned* __restrict__ keys_sorted,
-                                   int* __restrict__ offsets) {
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i <= total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const long long kprev = i == 0 ? -1 : (long long)keys_sorted[i - 1];
-    const long long kcur = i == total ? (long long)nkeys : (long long)keys_sorted[i];
-    for (long long k = kprev + 1; k <= kcur; ++k) offsets[k] = (int)i;
+__global__ __launch_bounds__(256) void csr_fill_kernel(int n, int p, const int* __restrict__ idx,
+                                                       const int* __restrict__ offsets,
+                                                       int* __restrict__ fill,
+                                                       int* __restrict__ perm) {
+  const int b = blockIdx.y;
+  const int* row = idx + (long long)b * p;
+  const long long kb = (long long)b * n;
+  const int e0 = b * p;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < p; i += gridDim.x * blockDim.x) {
+    const int v = row[i];
+    if ((unsigned)v < (unsigned)n) perm[offsets[kb + v] + atomicAdd(&fill[kb + v], 1)] = e0 + i;
+  }
+}
+
+// one wave per key (grid-stride): put the key's segment of perm in ascending order.
+//  * up to 64 * kHold entries: positions are distinct, so slot(x) = #{y in segment : y < x};
+//    each lane holds up to kHold entries and every entry is broadcast once (readlane): a
+//    segment of L entries costs L steps.  All entries are in registers before any store, so
+//    the segment is rewritten in place.
+//  * longer segments (in-degree > 256: a hub point, or degenerate input such as duplicated
+//    points): the wave scans its batch's index row in order and appends every position that
+//    maps to the key (ballot + popcount), P / 64 steps whatever L is.
+constexpr int kHold = 4;
+__global__ __launch_bounds__(256) void csr_segsort_kernel(long long m, int n, int p,
+                                                          const int* __restrict__ idx,
+                                                          const int* __restrict__ offsets,
+                                                          int* __restrict__ perm) {
+  const int lane = threadIdx.x & 63;
+  const long long wave = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long long nwaves = ((long long)gridDim.x * blockDim.x) >> 6;
+  for (long long key = wave; key < m; key += nwaves) {
+    const int o0 = offsets[key], len = offsets[key + 1] - o0;
+    if (len <= 1) continue;
+    int* seg = perm + o0;
+    if (len <= 64 * kHold) {
+      int x[kHold], rank[kHold];
+#pragma unroll
+      for (int h = 0; h < kHold; ++h) {
+        const int i = lane + 64 * h;
+        x[h] = i < len ? seg[i] : 0x7fffffff;
+        rank[h] = 0;
+      }
+#pragma unroll
+      for (int h2 = 0; h2 < kHold; ++h2) {
+        if (64 * h2 >= len) break;
+        const int lim = min(64, len - 64 * h2);
+        for (int j = 0; j < lim; ++j) {
+          const int y = __builtin_amdgcn_readlane(x[h2], j);
+#pragma unroll
+          for (int h = 0; h < kHold; ++h) rank[h] += y < x[h] ? 1 : 0;
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < kHold; ++h)
+        if (lane + 64 * h < len) seg[rank[h]] = x[h];
+    } else {
+      const long long b = key / n;
+      const int v = (int)(key - b * n);
+      const long long e0 = b * p;
+      int out = 0;
+      for (int i0 = 0; i0 < p; i0 += 64) {
+        const int i = i0 + lane;
+        const bool hit = i < p && idx[e0 + i] == v;
+        const unsigned long long mask = __ballot(hit);
+        if (hit) {
+          const int before = __popcll(mask & ((1ull << lane) - 1ull));
+          seg[out + before] = (int)(e0 + i);
+        }
+        out += __popcll(mask);
+      }
+    }
   }
 }
 
@@ -48,30 +121,24 @@ inline int grid_for(long long total, int block) {
   return (int)g;
 }
 
-inline int bits_for(unsigned long long v) {
-  int bits = 1;
-  while (bits < 32 && (1ull << bits) <= v) ++bits;
-  return bits;
-}
-
 struct CsrLayout {
-  size_t keys_in, keys_out, vals_in, cub, total;
+  size_t cnt, fill, scan, scan_bytes, total;  // byte offsets into the workspace
 };
 
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 hipError_t csr_layout(int b, int n, int p, CsrLayout* L) {
-  const long long items = (long long)b * p;
-  size_t cub_bytes = 0;
-  hipError_t e = hipcub::DeviceRadixSort::SortPairs(
-      nullptr, cub_bytes, (const unsigned*)nullptr, (unsigned*)nullptr, (const int*)nullptr,
-      (int*)nullptr, (int)items, 0, bits_for((unsigned long long)b * n), (hipStream_t)0);
+  (void)p;
+  const long long m = (long long)b * n;
+  size_t scan_bytes = 0;
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, (const int*)nullptr,
+                                                  (int*)nullptr, (int)(m + 1), (hipStream_t)0);
   if (e != hipSuccess) return e;
-  L->keys_in = 0;
-  L->keys_out = align256(sizeof(unsigned) * items);
-  L->vals_in = L->keys_out + align256(sizeof(unsigned) * items);
-  L->cub = L->vals_in + align256(sizeof(int) * items);
-  L->total = L->cub + align256(cub_bytes);
+  L->cnt = 0;                                  // m + 1 counts (the last stays 0)
+  L->fill = (size_t)(m + 1) * sizeof(int);     // m per-key fill counters
+  L->scan = align256(L->fill + (size_t)m * sizeof(int));
+  L->scan_bytes = scan_bytes;
+  L->total = L->scan + align256(scan_bytes);
   return hipSuccess;
 }
 
@@ -81,20 +148,20 @@ hipError_t csr_build(int b, int n, int p, const int* idx, void* ws, size_t ws_by
   hipError_t e = csr_layout(b, n, p, &L);
   if (e != hipSuccess) return e;
   if (ws_bytes < L.total) return hipErrorInvalidValue;
-  char* base = (char*)ws;
-  unsigned* keys_in = (unsigned*)(base + L.keys_in);
-  unsigned* keys_out = (unsigned*)(base + L.keys_out);
-  int* vals_in = (int*)(base + L.vals_in);
-  void* cub_tmp = base + L.cub;
-  size_t cub_bytes = L.total - L.cub;
-  const long long items = (long long)b * p;
-  hipLaunchKernelGGL(csr_keys_kernel, dim3(grid_for(items, 256)), dim3(256), 0, st, b, n, p, idx,
-                     keys_in, vals_in);
-  e = hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, keys_in, keys_out, vals_in, perm,
-                                         (int)items, 0, bits_for((unsigned long long)b * n), st);
+  char* base = reinterpret_cast<char*>(ws);
+  int* cnt = reinterpret_cast<int*>(base + L.cnt);
+  int* fill = reinterpret_cast<int*>(base + L.fill);
+  const long long m = (long long)b * n;
+  if ((e = hipMemsetAsync(cnt, 0, L.fill + sizeof(int) * m, st)) != hipSuccess) return e;
+  const dim3 pgrid((unsigned)std::min(divup(p, 256), std::max(1, 4096 / b)), (unsigned)b);
+  hipLaunchKernelGGL(csr_count_kernel, pgrid, dim3(256), 0, st, n, p, idx, cnt);
+  size_t scan_bytes = L.scan_bytes;
+  e = hipcub::DeviceScan::ExclusiveSum(base + L.scan, scan_bytes, cnt, offsets, (int)(m + 1), st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(csr_offsets_kernel, dim3(grid_for(items + 1, 256)), dim3(256), 0, st, items,
-                     (unsigned)((unsigned long long)b * n), keys_out, offsets);
+  hipLaunchKernelGGL(csr_fill_kernel, pgrid, dim3(256), 0, st, n, p, idx, offsets, fill, perm);
+  const int sgrid = (int)std::min<long long>(divupll(m, 4), 8192);  // 4 waves per workgroup
+  hipLaunchKernelGGL(csr_segsort_kernel, dim3(sgrid), dim3(256), 0, st, m, n, p, idx, offsets,
+                     perm);
   return hipGetLastError();
 }
 
@@ -281,7 +348,7 @@ KDPC_API size_t kdpc_csr_workspace_bytes(int b, int n, int p) {
 // Build the inverted index of idx (B,P) with values in [0,N): offsets (B*N+1), perm (B*P).
 KDPC_API int kdpc_csr_build(int b, int n, int p, const int* idx, void* workspace,
                             size_t workspace_bytes, int* offsets, int* perm, void* stream) {
-  KDPC_CHECK_ARG(b > 0 && n > 0 && p > 0 && idx && workspace && offsets && perm);
+  KDPC_CHECK_ARG(b > 0 && b <= 65535 && n > 0 && p > 0 && idx && workspace && offsets && perm);
   KDPC_CHECK_ARG((unsigned long long)b * n < (1ull << 31) && (long long)b * p < (1ll << 31));
   return (int)csr_build(b, n, p, idx, workspace, workspace_bytes, offsets, perm,
                         (hipStream_t)stream);

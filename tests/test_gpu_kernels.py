@@ -350,3 +350,23 @@ def test_colsum_fixed_order(nat, rows, cols):
     want = x.double().sum(0)
     bound = 1e-6 * x.double().abs().sum(0) * max(1.0, float(np.log2(rows)))
     assert ((a.double() - want).abs() <= bound + 1e-6).all()
+
+
+@pytest.mark.parametrize("b,n,p,hub", [(1, 1, 5, 0), (2, 100, 37, 0), (16, 8192, 32768, 0),
+                                       (16, 8192, 262144, 0), (4, 512, 4096, 1000),
+                                       (2, 64, 20000, 20000)])
+def test_csr_build_is_stable_counting_sort(nat, b, n, p, hub):
+    """kdpc_csr_build (count / scan / atomic fill / segment rank sort) equals a stable sort
+    of the keys b*N + idx: offsets = segment starts, perm = positions in ascending order per
+    key -- including hub keys with long segments (the ballot-scan path) and the degenerate
+    case of every position on one key."""
+    g = np.random.default_rng(b * 7 + n + p)
+    idx = g.integers(0, n, size=(b, p)).astype(np.int32)
+    if hub:
+        idx[:, g.choice(p, size=min(hub, p), replace=False)] = 0
+    csr = nat.Csr(torch.from_numpy(idx).to(DEV), n)
+    keys = (np.arange(b)[:, None] * n + idx).reshape(-1)
+    want_perm = np.argsort(keys, kind="stable")
+    want_off = np.searchsorted(keys[want_perm], np.arange(b * n + 1))
+    np.testing.assert_array_equal(csr.offsets.cpu().numpy(), want_off)
+    np.testing.assert_array_equal(csr.perm.cpu().numpy(), want_perm)
