@@ -66,17 +66,21 @@ def parse():
     ap.add_argument("--roofline-kernel", default=PRIMARY_KERNEL)
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--graph", action="store_true",
-                    help="replay the step from HIP graphs (distill.GraphedStep) instead of the "
-                         "eager step (DDP for N>1); round 1: the eager step is GPU-bound and "
-                         "the graph replay was ~10 %% slower, so eager is the default")
+    ap.add_argument("--eager", action="store_true",
+                    help="issue the step eagerly from Python (DDP for N>1) instead of replaying "
+                         "it from HIP graphs (distill.GraphedStep, the default since round 2: "
+                         "the eager step needs ~21 ms of host time per step, as much as the "
+                         "GPU, and the graph replay carries the next batch's FPS chain on a "
+                         "forked stream like the eager FpsPrefetch)")
+    ap.add_argument("--graph", action="store_true", help="(default; kept for old command lines)")
     ap.add_argument("--measure-steps", type=int, default=2,
                     help="eager steps after the timed region for the per-kernel roofline")
     return ap.parse_args()
 
 
 def cpu_baseline(args):
-    """Oracle CPU path on a bounded sample: B=1 pair, N=npoints, fwd+bwd+Adam."""
+    """Oracle CPU path on a bounded sample: B=1 pair, N=npoints, fwd+bwd+Adam (--mode kd:
+    frozen teacher fwd + student fwd+bwd + biDirection_loss_ht + Adam)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import torch_model as M
     import synthetic
@@ -84,12 +88,19 @@ def cpu_baseline(args):
     M.FPS_MODE["mode"] = "random"
     M.FPS_MODE["generator"] = torch.Generator().manual_seed(0)
     model = M.PointConvBidirection().train()
+    teacher = M.PointConvBidirection().eval() if args.mode == "kd" else None
     opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-4)
     p1, p2, fl = (torch.from_numpy(a) for a in synthetic.ft3d_batch(1, args.npoints, seed=99))
 
     def step():
         out = model(p1, p2, p1, p2)
-        loss = M.multiScaleLoss(out[0], fl, out[1])
+        if teacher is None:
+            loss = M.multiScaleLoss(out[0], fl, out[1])
+        else:
+            with torch.no_grad():
+                t = teacher(p1, p2, p1, p2)
+            loss = M.biDirection_loss_ht(out[0], out[5], out[6], out[1], out[2], fl, t[0], t[5],
+                                         t[6], t[1], t[2], 0.3, 0.8, layer=3)
         loss.backward()
         opt.step()
         opt.zero_grad()
@@ -103,7 +114,9 @@ def cpu_baseline(args):
     med = statistics.median(times)
     return {"value": round(1.0 / med, 4), "unit": "pairs/s", "cores": torch.get_num_threads(),
             "kind": "port",
-            "sample": f"1 pair x N={args.npoints}, fwd+bwd+Adam, median of {args.cpu_steps} "
+            "sample": f"1 pair x N={args.npoints}, "
+                      f"{'KD step (teacher fwd + ' if teacher is not None else ''}"
+                      f"fwd+bwd+Adam{')' if teacher is not None else ''}, median of {args.cpu_steps} "
                       f"steps after 1 warm-up ({med:.2f} s/step); oracle/torch_model.py "
                       f"(square_distance+topk kNN, torch.gather, FPS->randperm); "
                       f"host os.cpu_count()={os.cpu_count()}"}
@@ -206,7 +219,8 @@ def main():
     if args.mode == "kd":
         torch.manual_seed(1)
         teacher = PointConvBidirection().to(dev)
-    if args.graph:
+    graph = not args.eager
+    if graph:
         if world > 1:  # replicas start identical (DDP does this broadcast at construction)
             for t in list(student.parameters()) + list(student.buffers()):
                 dist.broadcast(t.data, 0)
@@ -282,7 +296,7 @@ def main():
                    "model": "models_bid_pointconv.PointConvBidirection",
                    "batch_per_gpu": args.batch, "global_batch": world * args.batch,
                    "npoints": args.npoints, "parallelism": f"dp{world}",
-                   "step": "hip-graph" if args.graph else "eager"},
+                   "step": "hip-graph" if graph else "eager"},
         "host_enqueue_ms": host_ms,
         "roofline": roof,
         "roofline_gather": roof_gather,

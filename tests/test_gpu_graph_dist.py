@@ -1,0 +1,93 @@
+"""GraphedStep with world size 2 (the N>1 path of `bench.py --graph`: graph A -> one flat
+all-reduce of the gradients -> graph B) on ONE GPU: two processes share cuda:0 and talk over
+gloo (which accepts device tensors).  Each rank trains on its own batch; after the steps both
+ranks hold identical parameters, equal to a single-process eager step on the averaged
+gradient of the two batches."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _batches(rank):
+    import synthetic
+    return [tuple(torch.from_numpy(a).cuda() for a in synthetic.ft3d_batch(1, 2048, seed=100 + 10 * s + rank))
+            for s in range(3)]
+
+
+def _worker(rank, port, out_dir):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "kd-pointcloud_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    torch.cuda.set_device(0)
+    from distill import graphed_flow_step, make_optimizer
+    from models_bid_pointconv import PointConvBidirection
+    torch.manual_seed(0)
+    model = PointConvBidirection().cuda()
+    opt = make_optimizer(model, capturable=True)
+    mine = _batches(rank)
+    step = graphed_flow_step(model, opt, mine[0], warmup=1)
+    for i in (1, 2):
+        step(*mine[i], next_batch=mine[i + 1] if i + 1 < len(mine) else None)
+    torch.cuda.synchronize()
+    torch.save({k: v.detach().cpu() for k, v in model.named_parameters()},
+               os.path.join(out_dir, f"rank{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_graphed_step_world2_matches_averaged_eager(tmp_path):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "kd-pointcloud_amd"))
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, port, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=180)
+        assert p.exitcode == 0, p.exitcode
+    p0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
+    p1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
+    for k in p0:
+        assert torch.equal(p0[k], p1[k]), k
+    # the same three steps eagerly in one process, gradients of the two ranks' batches averaged
+    import loss_functions
+    from distill import make_optimizer
+    from models_bid_pointconv import PointConvBidirection
+    torch.manual_seed(0)
+    model = PointConvBidirection().cuda().train()
+    opt = make_optimizer(model, capturable=True)
+    b0, b1 = _batches(0), _batches(1)
+    for i in range(3):
+        opt.zero_grad(set_to_none=True)
+        grads = []
+        for bt in (b0[i], b1[i]):
+            for p in model.parameters():
+                p.grad = None
+            flows, fps1 = model(bt[0], bt[1], bt[0], bt[1])[:2]
+            loss_functions.multiScaleLoss(flows, bt[2], fps1).backward()
+            grads.append([None if p.grad is None else p.grad.clone() for p in model.parameters()])
+        for p, g0, g1 in zip(model.parameters(), *grads):
+            p.grad = None if g0 is None else (g0 + g1) / 2
+        opt.step()
+    torch.cuda.synchronize()
+    worst = 0.0
+    for k, v in model.named_parameters():
+        d = float((v.detach().cpu() - p0[k]).abs().max())
+        scale = float(v.detach().abs().max()) + 1e-12
+        worst = max(worst, d / scale)
+    assert worst <= 1e-5, worst
