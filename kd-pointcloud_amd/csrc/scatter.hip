@@ -12,12 +12,19 @@
 // scheduling.  One CSR serves every gradient that scatters through the same index.
 
 #include <hipcub/hipcub.hpp>
+#include <type_traits>
 
 #include "kdpc_common.h"
 
 using namespace kdpc;
 
 namespace {
+
+__device__ __forceinline__ float vadd(float a, float b) { return __fadd_rn(a, b); }
+__device__ __forceinline__ float4 vadd(float4 a, float4 b) {
+  return make_float4(__fadd_rn(a.x, b.x), __fadd_rn(a.y, b.y), __fadd_rn(a.z, b.z),
+                     __fadd_rn(a.w, b.w));
+}
 
 // CSR build = a counting sort by key (b*N + idx) that keeps ascending position inside a key:
 //   memset (two count arrays) -> count (integer atomics) -> exclusive scan (hipcub,
@@ -272,34 +279,41 @@ __global__ __launch_bounds__(256) void group_rows_kernel(int b, int n, int c, in
 }
 
 // grad_points[b,n,:] = sum over seg(b,n) of grad_out[pos,:]  (rows, ascending position)
+// The segment walk is unrolled kU wide: the kU perm entries, then the kU rows, are loaded
+// before the adds (which stay in ascending order), so a segment of L rows costs ~2 L / kU
+// dependent memory latencies instead of 2 L (round 1: one perm load -> one row load -> add
+// per neighbour, latency-bound at ~40 us for the level-0 gradients).
+constexpr int kU = 8;
+
 template <int V>
 __global__ __launch_bounds__(256) void csr_sum_rows_kernel(int b, int n, int c,
                                                            const float* __restrict__ grad_out,
                                                            const int* __restrict__ offsets,
                                                            const int* __restrict__ perm,
                                                            float* __restrict__ dst) {
+  using vec = typename std::conditional<V == 4, float4, float>::type;
   const int cv = c / V;
   const long long total = (long long)b * n * cv;
+  const vec* src = reinterpret_cast<const vec*>(grad_out);
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (long long)gridDim.x * blockDim.x) {
-    const int ch = (int)(e % cv);
     const long long key = e / cv;  // b*n + ni
+    const int ch = (int)(e - key * cv);
     const int j0 = offsets[key], j1 = offsets[key + 1];
-    if (V == 4) {
-      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int j = j0; j < j1; ++j) {
-        const float4 v = reinterpret_cast<const float4*>(grad_out)[(long long)perm[j] * cv + ch];
-        acc.x = __fadd_rn(acc.x, v.x);
-        acc.y = __fadd_rn(acc.y, v.y);
-        acc.z = __fadd_rn(acc.z, v.z);
-        acc.w = __fadd_rn(acc.w, v.w);
-      }
-      reinterpret_cast<float4*>(dst)[e] = acc;
-    } else {
-      float acc = 0.f;
-      for (int j = j0; j < j1; ++j) acc = __fadd_rn(acc, grad_out[(long long)perm[j] * c + ch]);
-      dst[e] = acc;
+    vec acc{};
+    int j = j0;
+    for (; j + kU <= j1; j += kU) {
+      int pj[kU];
+      vec v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) pj[u] = perm[j + u];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) v[u] = src[(long long)pj[u] * cv + ch];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) acc = vadd(acc, v[u]);
     }
+    for (; j < j1; ++j) acc = vadd(acc, src[(long long)perm[j] * cv + ch]);
+    reinterpret_cast<vec*>(dst)[e] = acc;
   }
 }
 

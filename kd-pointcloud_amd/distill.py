@@ -184,6 +184,8 @@ class GraphedStep:
                  (+ packing the gradients into one flat buffer)
         eager:   one all_reduce of the flat gradient buffer (world > 1; RCCL over xGMI)
         graph B: unpack the averaged gradients + optimizer step (Adam, capturable=True)
+    With one process there is no all-reduce and the optimizer step is captured at the end of
+    graph A (a single graph per step).
 
     The collective stays outside the graphs on purpose: it is one 31.8 MB all-reduce per
     step, and keeping it eager avoids depending on collective capture.  `loss_fn(*inputs)`
@@ -249,17 +251,25 @@ class GraphedStep:
             self.flat = torch.cat([g.reshape(-1) for g in self.grads]) if self.world > 1 else None
             if fork is not None:
                 cap.wait_stream(fork)
-        # graph B: unpack + optimizer step (+ hand the prefetched FPS to the next replay)
-        self.graph_b = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph_b, pool=self.graph_a.pool(), **kw):
-            if self.world > 1:
+            if self.world == 1:  # nothing runs between the halves: one graph, one launch
+                self._tail(fork)
+        # graph B: unpack + optimizer step (+ hand the prefetched FPS to the next replay);
+        # a second graph launch costs ~0.5 ms of idle GPU between the replays (rocprofv3,
+        # round 2), so it exists only when the all-reduce has to run between the two
+        self.graph_b = None
+        if self.world > 1:
+            self.graph_b = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph_b, pool=self.graph_a.pool(), **kw):
                 self._unpack()
-            self.opt.step()
-            if fork is not None:
-                for c, n in zip(self.fps_cur, self.fps_next):
-                    c.copy_(n)
+                self._tail(fork)
         torch.cuda.synchronize()
         self._pending = None
+
+    def _tail(self, fork):
+        self.opt.step()
+        if fork is not None:
+            for c, n in zip(self.fps_cur, self.fps_next):
+                c.copy_(n)
 
     def _fps_kw(self, fps):
         return {} if self.prefetch_fn is None else {"fps": fps}
@@ -313,9 +323,9 @@ class GraphedStep:
             self._pending = (self._key(nxt[:self.n_prefetch]) if next_batch is not None
                              else None)
         self.graph_a.replay()
-        if self.world > 1:
+        if self.graph_b is not None:
             dist.all_reduce(self.flat)
-        self.graph_b.replay()
+            self.graph_b.replay()
         return self.loss.detach()
 
 

@@ -32,14 +32,16 @@ def main(mode):
         g.graph_a.replay()
         torch.cuda.synchronize()
         l1 = float(g.loss)
-        g.graph_b.replay()
+        if g.graph_b is not None:
+            g.graph_b.replay()
         torch.cuda.synchronize()
         l2 = float(g.loss)
         g.graph_a.replay()  # replay A again with the updated parameters? no: same inputs
         torch.cuda.synchronize()
         l3 = float(g.loss)
         print(mode, i, "after A", l1, "after B", l2, "A again", l3, flush=True)
-        g.graph_b.replay()
+        if g.graph_b is not None:
+            g.graph_b.replay()
 
 
 main("kd")
