@@ -48,6 +48,8 @@ ROOFLINE = {
     "kdpc_group_points": ("hbm", "GB/s", HBM_PEAK_GBS, ["group_points_lds_kernel",
                                                          "group_points_kernel"]),
     "kdpc_knn_point": ("valu", "TFLOP/s", FP32_VALU_PEAK_TF, ["knn_kernel"]),
+    "kdpc_cost_volume_fwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF, ["cost_volume_fwd_kernel"]),
+    "kdpc_cost_volume_bwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF, ["cost_volume_bwd_kernel"]),
 }
 # the step's dominant entry point (rocprofv3 step profile, profiles/); the gather-bound
 # grouping_operation the north star names is measured by gather_roofline()

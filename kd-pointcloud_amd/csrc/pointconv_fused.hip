@@ -42,6 +42,15 @@ using namespace kdpc;
 #ifndef KDPC_DAT_MODE  // diagnostic variants of the data kernel (0 = the real kernel)
 #define KDPC_DAT_MODE 0
 #endif
+#ifndef KDPC_DEFER_DG  // data kernel: a chunk's dG stores issued after the next chunk's MFMAs
+#define KDPC_DEFER_DG 1
+#endif
+#ifndef KDPC_PIPE_PF  // pipelined data kernel: B blocks issued ahead of their MFMAs
+#define KDPC_PIPE_PF 8
+#endif
+#ifndef KDPC_DG_CHUNK_MAJOR  // dG rows stored chunk-major: [chunk][pair][8] (else [pair][C8])
+#define KDPC_DG_CHUNK_MAJOR 0
+#endif
 #ifndef KDPC_WGT_MODE
 #define KDPC_WGT_MODE 0
 #endif
@@ -93,6 +102,16 @@ __device__ __forceinline__ int nbr_of(const Geo& g, int row, int kk) {
 // Gathers go through buffer loads: 32-bit byte offsets (one VGPR per in-flight slot instead
 // of a 64-bit address) and hardware bounds checks (an offset past the buffer reads 0).
 constexpr unsigned kOOB = 0x80000000u;  // byte offset that is always out of range
+
+// float offset of pair pos's 8 dG values of chunk ch in the dG buffer.  Pair-major (the
+// default): each pair's 32 bytes of a chunk sit C8*4 bytes apart (partial-line stores: the
+// data kernel's dG stores cost 137 of its 575 us at flow0, round 2) and pc_csr_sum reads a
+// pair's whole row contiguously.  Chunk-major (KDPC_DG_CHUNK_MAJOR=1): a wave's 64 pairs
+// store one contiguous 2 KiB run per chunk -- measured: data kernel 576 -> 514 us but
+// pc_csr_sum 86 -> 173 us (32-byte gathers), a net loss, so pair-major stays.
+__device__ __forceinline__ long long dg_off(long long pos, int ch, long long rk, int c8) {
+  return KDPC_DG_CHUNK_MAJOR ? ((long long)ch * rk + pos) * kCC : pos * c8 + (long long)ch * kCC;
+}
 
 struct Srcs {
   __amdgpu_buffer_rsrc_t xyz, center, feats;
@@ -362,6 +381,44 @@ __global__ __launch_bounds__(256) void pc_slab_sum_kernel(int nslabs, long long 
 // 28-row tiles, one pair per thread (934 vs 854 us, round 1); 320 threads, one pair each,
 // a fifth wave with no MFMA tile (931 us at 3 waves/SIMD with spills, 761 us at 2, vs 622):
 // the second pair pass of wave 0 is cheaper than the lost occupancy.
+#if KDPC_WGT_MODE == 9
+// diagnostic build only (tools/pc_stamps.py --weight): per-wave sums of the weight kernel's
+// tile phases (s_memtime deltas accumulated in scalar registers, stored once at the end)
+constexpr int kWStampWG = 4096, kWStampN = 8;
+__device__ unsigned long long g_pcw_stamps[kWStampWG * 8 * kWStampN];
+#define KDPC_WSTAMP(i)                                                                    \
+  do {                                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    unsigned long long _t;                                                                \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");            \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    wsum[(i)] += _t - wprev;                                                              \
+    wprev = _t;                                                                           \
+  } while (0)
+#else
+#define KDPC_WSTAMP(i) \
+  do {                 \
+  } while (0)
+#endif
+#if KDPC_DAT_MODE == 9
+// diagnostic build only (tools/pc_stamps.py): per-wave s_memtime stamps of the data kernel's
+// chunk phases, kept in LDS and copied to a buffer of their own (no output reads them)
+constexpr int kStampWG = 4096, kStampN = 80;
+__device__ unsigned long long g_pc_stamps[kStampWG * 4 * kStampN];
+#define KDPC_STAMP(i)                                                                     \
+  do {                                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    unsigned long long _t;                                                                \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");            \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    if (lane == 0) tsl[wv][(i)] = _t;                                                     \
+  } while (0)
+#else
+#define KDPC_STAMP(i) \
+  do {                \
+  } while (0)
+#endif
+
 template <int KM>
 constexpr int bwd_tile_rows() { return 32; }
 template <int KM>
@@ -375,7 +432,14 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
                         int chunks_per_split) {
   constexpr int TR = bwd_tile_rows<KM>();
   constexpr int NT = bwd_threads<KM>();
-  constexpr int PP = (TR * KM + NT - 1) / NT;  // pairs per thread
+  // (row, neighbour) pairs: PP whole pairs per thread, then the XP left over (K = 9: 288 =
+  // 256 + 32) as (pair, chunk channel) items, one per thread -- so every wave carries the
+  // same VALU work (round 2 stamps: with a second whole pair on wave 0 its pair phase took
+  // 1.8x the other waves', which waited for it at the barrier)
+  constexpr int PP = (TR * KM) / NT;
+  constexpr int XP = TR * KM - PP * NT;
+  constexpr bool XI = XP > 0;
+  static_assert(PP >= 1 && (!XI || XP * kCC == NT), "left-over pairs must fill one item/thread");
   __shared__ __attribute__((aligned(16))) float dyl[(O / 4) * kBlk];
   __shared__ __attribute__((aligned(16))) float dal[32 * kDaS];
   __shared__ float dcl[TR * KM * 3];
@@ -387,6 +451,10 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
   const long long c16 = (long long)g.c * kW;
   const long long rk_total = (long long)g.r * g.k;
   const Srcs src = srcs_of(g);
+#if KDPC_DAT_MODE == 9
+  __shared__ unsigned long long tsl[4][kStampN];
+#endif
+  KDPC_STAMP(0);
 
   for (int e = t; e < 32 * O; e += NT) {
     const int r = e / O, o = e % O;
@@ -416,6 +484,36 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
 #pragma unroll
     for (int w = 0; w < kW; ++w) dw[q][w] = 0.f;
   }
+  // left-over item: pair xp, channel xc of every chunk (8 consecutive lanes share the pair)
+  const int xp = PP * NT + t / kCC, xc = t % kCC;
+  const int xr = XI ? xp / g.k : 0;
+  const int xrc = min(xr, TR - 1);  // dA row read (any row when the item is dead)
+  const bool xok = XI && xp < TR * g.k && row0 + xr < g.r;
+  const int xn = xok ? nbr_of(g, row0 + xr, xp - xr * g.k) : -1;
+  const long long xpos = (long long)(row0 + xr) * g.k + (xp - xr * g.k);
+  float xw[kW], xd[kW], xg = 0.f, xgn = 0.f;
+  if constexpr (XI) {
+#pragma unroll
+    for (int v = 0; v < kW / 4; ++v) {
+      const float4 x = xok ? reinterpret_cast<const float4*>(wt + xpos * kW)[v]
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+      xw[4 * v + 0] = x.x;
+      xw[4 * v + 1] = x.y;
+      xw[4 * v + 2] = x.z;
+      xw[4 * v + 3] = x.w;
+    }
+#pragma unroll
+    for (int w = 0; w < kW; ++w) xd[w] = 0.f;
+  }
+  // the item's G value of a chunk: branch-free loads, out-of-range offsets read 0
+  auto gather_x = [&](int ch) {
+    const int cg = ch * kCC + xc;
+    const bool live = xn >= 0;
+    const unsigned fo = (live && cg >= 3 && cg < g.c) ? ((unsigned)xn * (unsigned)g.d + (unsigned)(cg - 3)) * 4u : kOOB;
+    const unsigned xo = (live && cg < 3) ? ((unsigned)xn * 3u + (unsigned)cg) * 4u : kOOB;
+    const unsigned co = (live && cg < 3) ? ((unsigned)(row0 + xr) * 3u + (unsigned)cg) * 4u : kOOB;
+    return bload(src.feats, fo) + (bload(src.xyz, xo) - bload(src.center, co));
+  };
   __syncthreads();
 
   const bool mw = wv < 4;            // the MFMA waves (wave 4 of a 320-thread group: none)
@@ -475,9 +573,30 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
 #pragma unroll
     for (int p2 = 0; p2 < PF; ++p2) bq[p2] = wr0[p2 * 64];
     gather(ch0, gv);
+    if constexpr (XI) xg = gather_x(ch0);
   }
+  // dG of chunk ch is stored after chunk ch+1's MFMA loop has issued its B loads: loads and
+  // stores retire in issue order (vmcnt), so a B block issued behind a chunk's dG stores waits
+  // for them; held here meanwhile
+  float svh[PP][kCC], xsh = 0.f;
+  auto store_dg = [&](int ch) {
+    if (KDPC_DAT_MODE == 5) return;
+    const int c0 = ch * kCC;
+#pragma unroll
+    for (int q = 0; q < PP; ++q) {
+      if (pn[q] < 0) continue;
+      const long long pos = (long long)(row0 + pr[q]) * g.k + pk[q];
+      float4* dgo = reinterpret_cast<float4*>(dgr + dg_off(pos, ch, rk_total, g.c8));
+      dgo[0] = make_float4(svh[q][0], svh[q][1], svh[q][2], svh[q][3]);
+      dgo[1] = make_float4(svh[q][4], svh[q][5], svh[q][6], svh[q][7]);
+    }
+    if (XI && xn >= 0) dgr[dg_off(xpos, ch, rk_total, g.c8) + xc] = xsh;
+  };
+  KDPC_STAMP(1);
   for (int ch = ch0; ch < ch1; ++ch) {
     const int c0 = ch * kCC;
+    const int si = 2 + 4 * min(ch - ch0, 18);
+    KDPC_STAMP(si);
     const float4* wrow = brow(ch);
     f32x16 acc = zero16();
     if (mw) {  // wave-uniform
@@ -489,18 +608,22 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
         if (og + PF < NOG) bq[og % PF] = wrow[(og + PF) * 64];
       }
     }
+    if (KDPC_DEFER_DG && ch > ch0) store_dg(ch - 1);
     if (ch + 1 < ch1) {
       const float4* wr1 = brow(ch + 1);
 #pragma unroll
       for (int p2 = 0; p2 < PF; ++p2) bq[p2] = wr1[p2 * 64];
       gather(ch + 1, gn);
+      if constexpr (XI) xgn = gather_x(ch + 1);
     }
+    KDPC_STAMP(si + 1);
     if (mw) {
 #pragma unroll
       for (int e = 0; e < 16; ++e)
         dal[((e & 3) + 8 * (e >> 2) + 4 * half) * kDaS + n0 + l32] = acc[e];
     }
     __syncthreads();
+    KDPC_STAMP(si + 2);
 #pragma unroll
     for (int q = 0; q < PP && KDPC_DAT_MODE != 2; ++q) {
       if (pn[q] < 0) continue;
@@ -509,7 +632,6 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
       // the pair's 8 dG values are 32 contiguous (32-byte aligned) bytes: two 16-byte stores.
       // Channel cl + 1's dA row is read from LDS while channel cl computes (the scheduling
       // barrier keeps the compiler from hoisting further reads, which spilled).
-      float4* dgo = reinterpret_cast<float4*>(dgr + pos * g.c8 + c0);
       const float4* drow = reinterpret_cast<const float4*>(dal + r * kDaS);
       float4 cur[kW / 4], nxt[kW / 4];
 #pragma unroll
@@ -541,17 +663,40 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
         for (int v = 0; v < kW / 4; ++v) cur[v] = nxt[v];
         __builtin_amdgcn_sched_barrier(0);
       }
-      if (KDPC_DAT_MODE != 5) {
-        dgo[0] = make_float4(sv[0], sv[1], sv[2], sv[3]);
-        dgo[1] = make_float4(sv[4], sv[5], sv[6], sv[7]);
-      }
+#pragma unroll
+      for (int c = 0; c < kCC; ++c) svh[q][c] = sv[c];
+      (void)pos;
     }
+    if constexpr (XI) {  // the left-over item: same fma order as a whole pair's channel
+      const float4* drow = reinterpret_cast<const float4*>(dal + xrc * kDaS) + xc * (kW / 4);
+      float da[kW];
+#pragma unroll
+      for (int v = 0; v < kW / 4; ++v) {
+        const float4 x = drow[v];
+        da[4 * v + 0] = x.x;
+        da[4 * v + 1] = x.y;
+        da[4 * v + 2] = x.z;
+        da[4 * v + 3] = x.w;
+      }
+      float sacc = 0.f;
+#pragma unroll
+      for (int w = 0; w < kW; ++w) sacc = __builtin_fmaf(da[w], xw[w], sacc);
+#pragma unroll
+      for (int w = 0; w < kW; ++w) xd[w] = __builtin_fmaf(da[w], xg, xd[w]);
+      xsh = sacc;
+      if (xn >= 0 && c0 == 0 && xc < 3) dcl[xp * 3 + xc] = sacc;
+    }
+    if (!KDPC_DEFER_DG) store_dg(ch);
+    KDPC_STAMP(si + 3);
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < PP; ++q)
 #pragma unroll
       for (int c = 0; c < kCC; ++c) gv[q][c] = gn[q][c];
+    xg = xgn;
   }
+  if (KDPC_DEFER_DG && ch0 < ch1) store_dg(ch1 - 1);
+  KDPC_STAMP(78);
   if (ch0 == 0 && t < TR * 3) {
     const int r = t / 3, i = t - (t / 3) * 3;
     const int row = row0 + r;
@@ -571,6 +716,31 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
     for (int v = 0; v < kW / 4; ++v)
       dst[v] = make_float4(dw[q][4 * v], dw[q][4 * v + 1], dw[q][4 * v + 2], dw[q][4 * v + 3]);
   }
+  if constexpr (XI) {
+    // the item's dwt partials (channels xc, xc + 8, ...) summed over the pair's 8 lanes in a
+    // fixed butterfly (every lane ends with the same value); lane xc stores w = 2xc, 2xc + 1
+#pragma unroll
+    for (int w = 0; w < kW; ++w) {
+      float v = xd[w];
+      v += __shfl_xor(v, 4);
+      v += __shfl_xor(v, 2);
+      v += __shfl_xor(v, 1);
+      xd[w] = v;
+    }
+    float2 out = make_float2(xd[0], xd[1]);
+#pragma unroll
+    for (int c = 1; c < kCC; ++c)
+      if (xc == c) out = make_float2(xd[2 * c], xd[2 * c + 1]);
+    if (xn >= 0) reinterpret_cast<float2*>(dwt_dst + xpos * kW)[xc] = out;
+  }
+#if KDPC_DAT_MODE == 9
+  if (lane == 0) tsl[wv][79] = ((unsigned long long)__builtin_amdgcn_s_getreg(63508) << 32) |
+                               (unsigned)__builtin_amdgcn_s_getreg(63492);  // XCC_ID, HW_ID
+  const unsigned wg = blockIdx.y * gridDim.x + blockIdx.x;
+  if (wg < (unsigned)kStampWG) {
+    for (int i = lane; i < kStampN; i += 64) g_pc_stamps[((size_t)wg * 4 + wv) * kStampN + i] = tsl[wv][i];
+  }
+#endif
 }
 
 // Software-pipelined variant of the data kernel.  The kernel above runs each chunk as an
@@ -590,14 +760,21 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
                              int chunks_per_split) {
   constexpr int TR = 32;
   constexpr int NT = 256;
-  constexpr int PP = (TR * KM + NT - 1) / NT;  // pairs per thread
+  // whole pairs per thread + the left-over pairs as one (pair, channel) item per thread, as
+  // in pc_bwd_data_kernel (every wave the same VALU work)
+  constexpr int PP = (TR * KM) / NT;
+  constexpr int XP = TR * KM - PP * NT;
+  constexpr bool XI = XP > 0;
+  static_assert(PP >= 1 && (!XI || XP * kCC == NT), "left-over pairs must fill one item/thread");
   constexpr int NOG = O / 8;
-  constexpr int PF = NOG < 4 ? NOG : 4;
-  constexpr int NIT = PP * kCC;                // VALU items per chunk per thread
+  // B blocks in flight: the first PF of the next chunk are issued before its gathers, the
+  // rest inside the step, PF steps ahead of their MFMAs (behind the gathers in vmcnt order)
+  constexpr int PF = NOG < KDPC_PIPE_PF ? NOG : KDPC_PIPE_PF;
+  constexpr int NIT = PP * kCC + (XI ? 1 : 0);  // VALU items per chunk per thread
   constexpr int STEPS = NOG > NIT ? NOG : NIT;
   __shared__ __attribute__((aligned(16))) float dyl[(O / 4) * kBlk];
   __shared__ __attribute__((aligned(16))) float dal[2][32 * kDaS];
-  __shared__ float dcl[NT * PP * 3];  // every pair slot (invalid ones write zeros)
+  __shared__ float dcl[TR * KM * 3];  // every pair slot (invalid ones write zeros)
   const int row0 = blockIdx.x * TR;
   const int split = blockIdx.y;
   const int ch0 = split * chunks_per_split;
@@ -634,6 +811,34 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
 #pragma unroll
     for (int w = 0; w < kW; ++w) dw[q][w] = 0.f;
   }
+  const int xp = PP * NT + t / kCC, xc = t % kCC;
+  const int xr = XI ? xp / g.k : 0;
+  const int xrc = min(xr, TR - 1);
+  const bool xok = XI && xp < TR * g.k && row0 + xr < g.r;
+  const int xn = xok ? nbr_of(g, row0 + xr, xp - xr * g.k) : -1;
+  const long long xpos = (long long)(row0 + xr) * g.k + (xp - xr * g.k);
+  float xw[kW], xd[kW], xg = 0.f, xgn = 0.f, xs = 0.f;
+  if constexpr (XI) {
+#pragma unroll
+    for (int v = 0; v < kW / 4; ++v) {
+      const float4 x = xok ? reinterpret_cast<const float4*>(wt + xpos * kW)[v]
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+      xw[4 * v + 0] = x.x;
+      xw[4 * v + 1] = x.y;
+      xw[4 * v + 2] = x.z;
+      xw[4 * v + 3] = x.w;
+    }
+#pragma unroll
+    for (int w = 0; w < kW; ++w) xd[w] = 0.f;
+  }
+  auto gather_x = [&](int ch) {
+    const int cg = ch * kCC + xc;
+    const bool live = xn >= 0;
+    const unsigned fo = (live && cg >= 3 && cg < g.c) ? ((unsigned)xn * (unsigned)g.d + (unsigned)(cg - 3)) * 4u : kOOB;
+    const unsigned xo = (live && cg < 3) ? ((unsigned)xn * 3u + (unsigned)cg) * 4u : kOOB;
+    const unsigned co = (live && cg < 3) ? ((unsigned)(row0 + xr) * 3u + (unsigned)cg) * 4u : kOOB;
+    return bload(src.feats, fo) + (bload(src.xyz, xo) - bload(src.center, co));
+  };
 
   auto brow = [&](int ch) { return wsw + (long long)((ch * 4 + wv) * NOG) * 64 + lane; };
   auto gather = [&](int ch, float (&dst)[PP][kCC]) {
@@ -678,6 +883,7 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
 #pragma unroll
     for (int p2 = 0; p2 < PF; ++p2) bq[p2] = wr0[p2 * 64];
     gather(ch0, gv);
+    if constexpr (XI) xg = gather_x(ch0);
   }
   __syncthreads();  // dyl
   if (ch0 < ch1) {  // prologue: chunk ch0's dA
@@ -700,8 +906,35 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
   // one chunk step: chunk ch+1's MFMAs (when MF) interleaved with chunk ch's VALU items.
   // Branch-free body (dead pair slots compute zeros from zero weights / gathers on a clamped
   // dA row) so the MFMAs and the VALU work share one basic block for the scheduler.
+  // dG of chunk ch-1 is held in registers and stored inside chunk ch's step, right after its
+  // last B load is issued: a B wait then never waits behind dG stores (vmcnt retires in order)
+  float svh[PP][kCC], xsh = 0.f;
+  // branch-free buffer stores (a store under a uniform branch would split the step's block):
+  // nothing to store -> an out-of-range offset, which the hardware drops
+  const __amdgpu_buffer_rsrc_t dg_rs = __builtin_amdgcn_make_buffer_rsrc(
+      dgr, (short)0, (int)((long long)g.r * g.k * g.c8 * 4), 0x00020000);
+  auto store_dg = [&](int ch) {
+    const bool on = ch >= 0;
+    const int chs = on ? ch : 0;
+#pragma unroll
+    for (int q = 0; q < PP; ++q) {
+      const unsigned pos = (unsigned)((row0 + pr[q]) * g.k + pk[q]);
+      const unsigned off = (on && pn[q] >= 0) ? (unsigned)dg_off(pos, chs, rk_total, g.c8) * 4u : kOOB;
+      __builtin_amdgcn_raw_buffer_store_b128(
+          __builtin_bit_cast(f32x4, make_float4(svh[q][0], svh[q][1], svh[q][2], svh[q][3])),
+          dg_rs, (int)off, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(
+          __builtin_bit_cast(f32x4, make_float4(svh[q][4], svh[q][5], svh[q][6], svh[q][7])),
+          dg_rs, (int)(off == kOOB ? kOOB : off + 16u), 0, 0);
+    }
+    if constexpr (XI) {
+      const unsigned off = (on && xn >= 0) ? (unsigned)(dg_off(xpos, chs, rk_total, g.c8) + xc) * 4u : kOOB;
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, xsh), dg_rs, (int)off, 0, 0);
+    }
+  };
+  constexpr int SI = NOG - PF > 0 ? NOG - PF - 1 : 0;  // step issuing the last B load
   auto step = [&](auto mf, const float* dab, const float4* wr1, f32x16& acc,
-                  float (&sv)[PP][kCC]) {
+                  float (&sv)[PP][kCC], int prev) {
 #pragma unroll
     for (int i = 0; i < STEPS; ++i) {
       if constexpr (decltype(mf)::value) {
@@ -712,7 +945,24 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
           if (i + PF < NOG) bq[i % PF] = wr1[(i + PF) * 64];
         }
       }
-      if (i < NIT) {
+      if (XI && i == NIT - 1) {  // the left-over item
+        const float4* drow = reinterpret_cast<const float4*>(dab + xrc * kDaS) + xc * (kW / 4);
+        float da[kW];
+#pragma unroll
+        for (int v = 0; v < kW / 4; ++v) {
+          const float4 x = drow[v];
+          da[4 * v + 0] = x.x;
+          da[4 * v + 1] = x.y;
+          da[4 * v + 2] = x.z;
+          da[4 * v + 3] = x.w;
+        }
+        float sacc = 0.f;
+#pragma unroll
+        for (int w = 0; w < kW; ++w) sacc = __builtin_fmaf(da[w], xw[w], sacc);
+        xs = sacc;
+#pragma unroll
+        for (int w = 0; w < kW; ++w) xd[w] = __builtin_fmaf(da[w], xg, xd[w]);
+      } else if (i < NIT) {
         const int q = i / kCC, cl = i % kCC;
         const float4* drow = reinterpret_cast<const float4*>(dab + prc[q] * kDaS) + cl * (kW / 4);
         float da[kW];
@@ -732,6 +982,7 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
 #pragma unroll
         for (int w = 0; w < kW; ++w) dw[q][w] = __builtin_fmaf(da[w], gc, dw[q][w]);
       }
+      if (i == SI) store_dg(prev);  // prev < 0: nothing stored (branch-free)
       // keep each step's loads with its own math (hoisting every step's dA reads spilled)
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -740,25 +991,29 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
     const int buf = (ch - ch0) & 1;
     const bool more = ch + 1 < ch1;  // uniform
     const int c0 = ch * kCC;
-    if (more) gather(ch + 1, gn);
+    if (more) {
+      gather(ch + 1, gn);
+      if constexpr (XI) xgn = gather_x(ch + 1);
+    }
     f32x16 acc = zero16();
     float sv[PP][kCC];
+    const int prev = ch > ch0 ? ch - 1 : -1;
     if (more)
-      step(std::true_type{}, dal[buf], brow(ch + 1), acc, sv);
+      step(std::true_type{}, dal[buf], brow(ch + 1), acc, sv, prev);
     else
-      step(std::false_type{}, dal[buf], brow(ch + 1), acc, sv);
+      step(std::false_type{}, dal[buf], brow(ch + 1), acc, sv, prev);
 #pragma unroll
     for (int q = 0; q < PP; ++q) {
       if (c0 == 0) {
 #pragma unroll
         for (int cl = 0; cl < 3; ++cl) dcl[(t + NT * q) * 3 + cl] = sv[q][cl];
       }
-      if (pn[q] >= 0) {
-        const long long pos = (long long)(row0 + pr[q]) * g.k + pk[q];
-        float4* dgo = reinterpret_cast<float4*>(dgr + pos * g.c8 + c0);
-        dgo[0] = make_float4(sv[q][0], sv[q][1], sv[q][2], sv[q][3]);
-        dgo[1] = make_float4(sv[q][4], sv[q][5], sv[q][6], sv[q][7]);
-      }
+#pragma unroll
+      for (int c = 0; c < kCC; ++c) svh[q][c] = sv[q][c];
+    }
+    if constexpr (XI) {
+      xsh = xs;
+      if (xn >= 0 && c0 == 0 && xc < 3) dcl[xp * 3 + xc] = xs;
     }
     if (more) {
       store_da(acc, buf ^ 1);
@@ -773,7 +1028,9 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
     for (int q = 0; q < PP; ++q)
 #pragma unroll
       for (int c = 0; c < kCC; ++c) gv[q][c] = gn[q][c];
+    xg = xgn;
   }
+  if (ch0 < ch1) store_dg(ch1 - 1);
   if (ch0 == 0 && t < TR * 3) {
     const int r = t / 3, i = t - (t / 3) * 3;
     const int row = row0 + r;
@@ -792,6 +1049,21 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
 #pragma unroll
     for (int v = 0; v < kW / 4; ++v)
       dst[v] = make_float4(dw[q][4 * v], dw[q][4 * v + 1], dw[q][4 * v + 2], dw[q][4 * v + 3]);
+  }
+  if constexpr (XI) {  // as in pc_bwd_data_kernel
+#pragma unroll
+    for (int w = 0; w < kW; ++w) {
+      float v = xd[w];
+      v += __shfl_xor(v, 4);
+      v += __shfl_xor(v, 2);
+      v += __shfl_xor(v, 1);
+      xd[w] = v;
+    }
+    float2 out = make_float2(xd[0], xd[1]);
+#pragma unroll
+    for (int c = 1; c < kCC; ++c)
+      if (xc == c) out = make_float2(xd[2 * c], xd[2 * c + 1]);
+    if (xn >= 0) reinterpret_cast<float2*>(dwt_dst + xpos * kW)[xc] = out;
   }
 }
 
@@ -824,7 +1096,7 @@ __global__ __launch_bounds__(256) void pc_swizzle_bwd_kernel(int o, int c16, int
 
 // d_xyz / d_feats of every point = sum of its dG rows through the CSR (ascending
 // position); one thread per (point, 4 channels)
-__global__ __launch_bounds__(256) void pc_csr_sum_kernel(long long npts, int c, int c8, int d,
+__global__ __launch_bounds__(256) void pc_csr_sum_kernel(long long npts, long long rk, int c, int c8, int d,
                                                          const float* __restrict__ dgr,
                                                          const int* __restrict__ offsets,
                                                          const int* __restrict__ perm,
@@ -854,12 +1126,12 @@ __global__ __launch_bounds__(256) void pc_csr_sum_kernel(long long npts, int c, 
       for (int u = 0; u < 8; ++u) pj[u] = perm[j + u];
 #pragma unroll
       for (int u = 0; u < 8; ++u)
-        x[u] = *reinterpret_cast<const float4*>(dgr + (long long)pj[u] * c8 + 4 * v);
+        x[u] = *reinterpret_cast<const float4*>(dgr + dg_off(pj[u], v >> 1, rk, c8) + 4 * (v & 1));
 #pragma unroll
       for (int u = 0; u < 8; ++u) add(x[u]);
     }
     for (; j < j1; ++j)
-      add(*reinterpret_cast<const float4*>(dgr + (long long)perm[j] * c8 + 4 * v));
+      add(*reinterpret_cast<const float4*>(dgr + dg_off(perm[j], v >> 1, rk, c8) + 4 * (v & 1)));
     const float sv[4] = {s.x, s.y, s.z, s.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -1071,6 +1343,10 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
 #pragma unroll
   for (int i = 0; i < MPW; ++i) acc[i] = zero16();
   if (ntiles <= 0) return;
+#if KDPC_WGT_MODE == 9
+  unsigned long long wsum[7] = {0, 0, 0, 0, 0, 0, 0}, wprev;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(wprev)::"memory");
+#endif
   // prologue: tile 0 staged and built, tile 1 staged
   fetch_idx(0);
   fetch(0);
@@ -1081,11 +1357,13 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
   __syncthreads();
   stage(1);
   __syncthreads();
+  KDPC_WSTAMP(0);
   for (int tile = 0; tile < ntiles; ++tile) {
     const int cur = tile & 1;
     // tile+2's loads are issued first and land under this tile's MFMAs; tile's MFMAs || tile+1's
     // build (independent: at[cur] / dyt[cur] vs gl, wc -> at[!cur])
     if (KDPC_WGT_MODE != 3 && KDPC_WGT_MODE != 5) fetch(tile + 2);
+    KDPC_WSTAMP(1);
     const float* dt = dyt[cur];
     const float* ab = at[cur];
 #pragma unroll
@@ -1098,11 +1376,23 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
         acc[i] = mfma4(av, bv, acc[i]);
       }
     }
+    KDPC_WSTAMP(2);
     if (KDPC_WGT_MODE != 2 && KDPC_WGT_MODE != 5) build(cur ^ 1);
+    KDPC_WSTAMP(3);
     __syncthreads();  // at[cur] / dyt[cur] / gl consumed; at[cur ^ 1] complete
+    KDPC_WSTAMP(4);
     if (KDPC_WGT_MODE != 4 && KDPC_WGT_MODE != 5) stage(cur);  // tile + 2
+    KDPC_WSTAMP(5);
     __syncthreads();
+    KDPC_WSTAMP(6);
   }
+#if KDPC_WGT_MODE == 9
+  if (lane == 0 && L < kWStampWG) {
+    unsigned long long* o = g_pcw_stamps + ((size_t)L * 8 + wv) * kWStampN;
+    for (int i = 0; i < 7; ++i) o[i] = wsum[i];
+    o[7] = (unsigned long long)ntiles;
+  }
+#endif
   const long long col = (long long)c0 * kW + nt * 32 + l32;
   if (col >= c16) return;
   float* dst = dwl + (long long)split * O * c16;  // slab index when the rows are split
@@ -1208,17 +1498,20 @@ hipError_t fwd_launch(const Geo& g, const Plan& p, const float* wt, const float*
   return slab_sum(p.ks, (long long)p.r * O, slab, bias, O, y, st);
 }
 
-// KDPC_PC_BWD_PIPE=1 selects the software-pipelined data kernel.  Measured round 2 (flow0,
-// B=8, N=8192): bit-identical outputs, 1199 vs 1191 us for the whole backward -- interleaving
-// the phases did not pay (the chunk loop waits on memory: a B-fragment wait also waits for
-// older gathers and dG stores, vmcnt retiring in order), so the unpipelined kernel stays the
-// default.
+// Data kernel choice.  The pipelined kernel (chunk ch+1's MFMAs interleaved with chunk ch's
+// pair work) is the default for K <= 9: with every wave carrying the same pair work (one whole
+// pair + one left-over item) it is faster there (flow0, B=8, N=8192: 534 vs 584 us per
+// launch, round 2); for K = 16 (two whole pairs per thread) the two are within 2 % and the
+// unpipelined kernel stays.  KDPC_PC_BWD_PIPE=0 / =1 forces either (A/B runs; bit-identical
+// outputs).  Round-1 note: the pipelined kernel without the balanced pair mapping made every
+// wave run two pairs and did not pay (1199 vs 1191 us).
+template <int KM>
 inline bool bwd_pipe_enabled() {
-  static const bool on = [] {
+  static const int force = [] {
     const char* v = getenv("KDPC_PC_BWD_PIPE");
-    return v && v[0] == '1';
+    return v && (v[0] == '0' || v[0] == '1') ? v[0] - '0' : -1;
   }();
-  return on;
+  return force >= 0 ? force == 1 : KM <= 9;
 }
 
 template <int O, int KM>
@@ -1237,7 +1530,8 @@ hipError_t bwd_launch(const Geo& g, const Plan& p, int b, const float* wt, const
                      O, c16, g.nch, wl, wsw);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  if (bwd_pipe_enabled())
+  // the pipelined kernel stores dG through a buffer resource (31-bit byte offsets)
+  if (bwd_pipe_enabled<KM>() && (long long)p.r * g.k * p.c8 * 4 < (1ll << 31))
     hipLaunchKernelGGL((pc_bwd_data_pipe_kernel<O, KM>), dim3(divup(p.r, 32), p.bks), dim3(256),
                        0, st, g, wt, wsw, dy, dgr, p.bks > 1 ? dwt_slab : dwt, dcenter, p.bcps);
   else
@@ -1252,7 +1546,7 @@ hipError_t bwd_launch(const Geo& g, const Plan& p, int b, const float* wt, const
   const long long work = npts * (p.c8 / 4);
   hipLaunchKernelGGL(pc_csr_sum_kernel,
                      dim3((unsigned)std::min<long long>(divupll(work, 256), 1 << 20)), dim3(256),
-                     0, st, npts, g.c, p.c8, g.d, dgr, offsets, perm, dxyz, dfeats);
+                     0, st, npts, rk, g.c, p.c8, g.d, dgr, offsets, perm, dxyz, dfeats);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (g.k == KM)
     hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM, true>), dim3(p.wgs), dim3(512), 0, st, g, wt,
@@ -1292,6 +1586,19 @@ Geo geo_of(int b, int n, int s, int k, int d, const Plan& p, const float* xyz, c
                   : (o == 128 ? FN<128, 16>(__VA_ARGS__) : FN<256, 16>(__VA_ARGS__))))
 
 }  // namespace
+
+#if KDPC_WGT_MODE == 9
+KDPC_API int kdpc_debug_pcw_stamps(void* dst, size_t bytes) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_pcw_stamps),
+                                  std::min(bytes, sizeof(g_pcw_stamps)), 0, hipMemcpyDeviceToHost);
+}
+#endif
+#if KDPC_DAT_MODE == 9
+KDPC_API int kdpc_debug_pc_stamps(void* dst, size_t bytes) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_pc_stamps),
+                                  std::min(bytes, sizeof(g_pc_stamps)), 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 KDPC_API int kdpc_pointconv_supported(int k, int d, int o) {
   Plan p;

@@ -263,6 +263,11 @@ class GraphedStep:
                 self._unpack()
                 self._tail(fork)
         torch.cuda.synchronize()
+        # keep the static loss buffer, not the captured autograd graph: while that graph
+        # lives, an eager step on the same parameters reuses its AccumulateGrad nodes (bound
+        # to the capture stream) and torch warns of a stream mismatch (bench's eager
+        # measurement steps after the timed region)
+        self.loss = self.loss.detach()
         self._pending = None
 
     def _tail(self, fork):

@@ -404,8 +404,15 @@ def cost_volume_fwd(x1, x2, idx, p1, p2, wpos, bpos, w1, b1):
 
 def cost_volume_bwd(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout):
     """-> dp1 (B,N1,Din), dp2_rows (B,N1,K,Din), dx1 (B,N1,3), ddir_rows (B,N1,K,3), dparams."""
-    return _op("kdpc_cost_volume_bwd", "cost_volume_bwd", _gpu(x1, "x1"), x2, idx, p1, p2,
-               wpos, bpos, w1, out, amax, gout)
+    B, N1, _ = _gpu(x1, "x1").shape
+    K = idx.shape[2]
+    din, dout = p1.shape[2], w1.shape[0]
+    # reads x1, idx, p1, the K gathered p2 rows, out, gout, amax; writes dp1, dp2_rows,
+    # dx1, ddir_rows.  flops: dh0 = M W1 and dW1 = h0^T M over the K x Din x Dout tile
+    return _op("kdpc_cost_volume_bwd", "cost_volume_bwd", x1, x2, idx, p1, p2,
+               wpos, bpos, w1, out, amax, gout,
+               work=(4 * B * N1 * (3 + K + din + K * din + 2 * dout + din + K * din + 3 + 3 * K)
+                     + B * N1 * dout, 4.0 * B * N1 * K * din * dout))
 
 
 # ------------------------------------------------------------------ wide cost volume

@@ -102,7 +102,7 @@ def test_pointconv_fused_equals_unfused(down, d, n, bsz, out, bn):
 @pytest.mark.parametrize("b,n,s,k,d,o", [(2, 700, 700, 9, 61, 256), (1, 256, 64, 16, 512, 256),
                                          (3, 300, 300, 9, 5, 64), (2, 2048, 512, 16, 128, 128),
                                          (1, 100, 37, 1, 0, 64),
-                                         (1, 256, 256, 9, 512, 128)])
+                                         (1, 256, 256, 9, 512, 128), (2, 500, 333, 5, 40, 128)])
 def test_pointconv_layer_vs_fp64(b, n, s, k, d, o):
     """The fused layer's C entry points against an fp64 torch evaluation of the reference
     formulation (group -> cat -> matmul -> Linear) on the same inputs: forward and every

@@ -75,3 +75,23 @@ def test_fps_prefetch_equals_inline():
     assert l1 == l2, (l1, l2)
     for (n, a), b in zip(m1.named_parameters(), m2.parameters()):
         assert torch.equal(a, b), n
+
+
+def test_eager_step_after_capture_has_no_stream_mismatch():
+    """bench.py runs eager steps on the graphed model after the timed region (per-kernel
+    roofline): the captured autograd graph must not outlive the capture, or those steps reuse
+    its AccumulateGrad nodes (bound to the capture stream) -- the round-2 bench warning."""
+    from distill import FlowTrainStep, graphed_flow_step, make_optimizer
+    from models_bid_pointconv import PointConvBidirection
+    torch.manual_seed(0)
+    model = PointConvBidirection().to(DEV)
+    opt = make_optimizer(model, capturable=True)
+    b = _batch(2, 2048, 7)
+    graphed = graphed_flow_step(model, opt, b, warmup=1)
+    graphed(*b)
+    with warnings.catch_warnings(record=True) as caught:
+        warnings.simplefilter("always")
+        FlowTrainStep(model, opt)(*b)
+        torch.cuda.synchronize()
+    bad = [str(w.message) for w in caught if "AccumulateGrad" in str(w.message)]
+    assert not bad, bad
