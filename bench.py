@@ -40,8 +40,9 @@ FP32_VALU_PEAK_TF = 157.3
 # durations per entry launch to cross-check the live average.
 ROOFLINE = {
     "kdpc_pointconv_bwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF,
-                           ["pc_bwd_data_kernel", "pc_csr_sum_kernel", "pc_bwd_weight_kernel",
-                            "pc_slab_sum_kernel"]),
+                           # first name: one launch per entry call (tools count launches by it)
+                           ["pc_csr_sum_kernel", "pc_bwd_data_kernel", "pc_bwd_data_pipe_kernel",
+                            "pc_bwd_weight_kernel", "pc_slab_sum_kernel", "pc_swizzle_bwd_kernel"]),
     "kdpc_pointconv_fwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF,
                            ["pc_fwd_kernel", "pc_slab_sum_kernel"]),
     "kdpc_group_rows": ("hbm", "GB/s", HBM_PEAK_GBS, ["group_rows_kernel"]),
@@ -50,6 +51,7 @@ ROOFLINE = {
     "kdpc_knn_point": ("valu", "TFLOP/s", FP32_VALU_PEAK_TF, ["knn_kernel"]),
     "kdpc_cost_volume_fwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF, ["cost_volume_fwd_kernel"]),
     "kdpc_cost_volume_bwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF, ["cost_volume_bwd_kernel"]),
+    "kdpc_idw_blend_fwd": ("hbm", "GB/s", HBM_PEAK_GBS, ["idw_fwd_kernel"]),
 }
 # the step's dominant entry point (rocprofv3 step profile, profiles/); the gather-bound
 # grouping_operation the north star names is measured by gather_roofline()

@@ -353,6 +353,30 @@ int kdpc_batchnorm_lrelu_bwd(int r, int c, const float *dy_act, const float *y_a
                              float *dbias, void *workspace, size_t workspace_bytes,
                              void *stream);
 
+/* ---- 3-NN inverse-distance blend (UpsampleFlow / PointWarping, pointconv_util.py:2114-2172,
+ *      replaces its torch norm/clamp/reciprocal/sum/div/mul/sum[/sub] chain) ------------- */
+
+/* out[b,n,:] = sum_k w[b,n,k] vals[b, idx[b,n,k], :] (warp = 0) or qry[b,n,:] - that sum
+ * (warp = 1, PointWarping, c must be 3), w_k = (1/d_k) / sum_j (1/d_j),
+ * d_k = max(||ref[b,idx[b,n,k]] - qry[b,n]||, 1e-10); ref (B,S,3), qry (B,N,3), vals (B,S,C),
+ * idx (B,N,3) int32, out (B,N,C); w (B,N,3) is written for the backward. */
+int kdpc_idw_blend_fwd(int b, int n, int s, int c, const float *ref, const float *qry,
+                       const float *vals, const int *idx, float *out, float *w, int warp,
+                       void *stream);
+
+/* dvals (B,S,C): the values' gradient, summed per reference point through the CSR of idx
+ * (offsets B*S+1, perm B*3N from kdpc_csr_build over idx viewed as (B,3N)). */
+int kdpc_idw_blend_bwd_vals(int b, int n, int s, int c, const float *dout, const float *w,
+                            const int *offsets, const int *perm, float *dvals, int warp,
+                            void *stream);
+
+/* The coordinates' gradient: drow (B,N,3,3) per (query, neighbour) rows of d/d ref[idx]
+ * (sum them per reference point with kdpc_group_rows_grad_csr over the same CSR), dqry
+ * (B,N,3) (may be NULL). */
+int kdpc_idw_blend_bwd_coords(int b, int n, int s, int c, const float *ref, const float *qry,
+                              const float *vals, const int *idx, const float *dout,
+                              float *drow, float *dqry, int warp, void *stream);
+
 /* ---- deterministic column sums (bias gradients, partial-slab reductions) -------------- */
 
 /* Scratch bytes for kdpc_colsum over an (nrows, len) matrix (0 for nrows <= 64). */

@@ -82,6 +82,9 @@ _SIGNATURES = {
     "kdpc_wn_wsum_fwd": [_c_int] * 5 + [_vp] * 11,
     "kdpc_wn_wsum_bwd_workspace_bytes": [_c_int] * 3,
     "kdpc_wn_wsum_bwd": [_c_int] * 5 + [_vp] * 14 + [_c_size, _vp],
+    "kdpc_idw_blend_fwd": [_c_int] * 4 + [_vp] * 6 + [_c_int, _vp],
+    "kdpc_idw_blend_bwd_vals": [_c_int] * 4 + [_vp] * 5 + [_c_int, _vp],
+    "kdpc_idw_blend_bwd_coords": [_c_int] * 4 + [_vp] * 7 + [_c_int, _vp],
 }
 _RESTYPES = {"kdpc_build_id": ctypes.c_char_p, "kdpc_grad_workspace_bytes": _c_size,
              "kdpc_csr_workspace_bytes": _c_size, "kdpc_cost_volume_bwd_workspace_bytes": _c_size,
@@ -498,6 +501,27 @@ def pointconv_bwd(xyz, center, feats, idx, wt, wl, dy, csr, need_xyz=True):
                csr.offsets, csr.perm, bool(need_xyz),
                work=(4 * R * (2 * K * C + 32 * K + 2 * O) + 8 * O * 16 * C,
                      4.0 * R * K * C * 16 + 4.0 * R * 16 * C * O))
+
+
+# ------------------------------------------------ 3-NN inverse-distance blend
+def idw_blend_fwd(ref, qry, vals, idx, warp=False):
+    """UpsampleFlow / PointWarping blend: -> (out (B,N,C), w (B,N,3)); see include/kdpc.h."""
+    B, S, _ = _gpu(ref, "ref").shape
+    N, C = qry.shape[1], vals.shape[2]
+    return _op("kdpc_idw_blend_fwd", "idw_blend_fwd", ref, qry, vals, idx, bool(warp),
+               work=(4 * B * N * (3 + 3 + 3 * 3 + 3 * C + C + 3), 0))
+
+
+def idw_blend_bwd_vals(dout, w, csr, S, warp=False):
+    """-> dvals (B,S,C) through the CSR of the blend's idx (B,N,3)."""
+    return _op("kdpc_idw_blend_bwd_vals", "idw_blend_bwd_vals", _gpu(dout, "dout").contiguous(),
+               w, csr.offsets, csr.perm, S, bool(warp))
+
+
+def idw_blend_bwd_coords(ref, qry, vals, idx, dout, warp=False):
+    """-> (drow (B,3N,3) per-neighbour rows of d/d ref, dqry (B,N,3))."""
+    return _op("kdpc_idw_blend_bwd_coords", "idw_blend_bwd_coords", _gpu(ref, "ref"), qry,
+               vals, idx, dout.contiguous(), bool(warp))
 
 
 # ------------------------------------------------------------------- fused WeightNet

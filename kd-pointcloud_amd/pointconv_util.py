@@ -872,6 +872,50 @@ class _WnWeightedSum(torch.autograd.Function):
         return (ddir if ctx.needs_input_grad[0] else None, None, dv, *dparams)
 
 
+_FUSED_IDW = True  # test seam: False forces the reference torch expression below
+
+
+class _IdwBlend(torch.autograd.Function):
+    """3-NN inverse-distance blend in one HIP pass (csrc/idw_blend.hip): out = sum_k w_k
+    vals[idx_k] (or qry - that sum for PointWarping), w from the distances of the reference
+    points ref[idx_k] to qry.  Backward: the values' gradient through the CSR of idx, the
+    coordinates' only when asked for (PointWarping's reference points carry the flow)."""
+
+    @staticmethod
+    def forward(ctx, ref, qry, vals, idx, warp):
+        ref, qry, vals = ref.contiguous(), qry.contiguous(), vals.contiguous()
+        out, w = _nat.idw_blend_fwd(ref, qry, vals, idx, warp)
+        ctx.save_for_backward(ref, qry, vals, idx, w)
+        ctx.warp = warp
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        ref, qry, vals, idx, w = ctx.saved_tensors
+        B, S = ref.shape[0], ref.shape[1]
+        csr = _nat.csr_of(idx, S)
+        dref = dqry = dvals = None
+        if ctx.needs_input_grad[2]:
+            dvals = _nat.idw_blend_bwd_vals(dout, w, csr, S, ctx.warp)
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            drow, dq = _nat.idw_blend_bwd_coords(ref, qry, vals, idx, dout, ctx.warp)
+            if ctx.needs_input_grad[0]:
+                dref = _nat.group_rows_grad(drow, csr, B, S, 3)
+            dqry = dq if ctx.needs_input_grad[1] else None
+        return dref, dqry, dvals, None, None
+
+
+def _idw_blend(ref, qry, vals, idx, warp=False):
+    """ref (B,S,3), qry (B,N,3), vals (B,S,C), idx (B,N,3) i32 -> (B,N,C): the reference's
+    index_points_group + _inverse_distance_blend [+ qry - ...] (ref :2129-2140, :2165-2170)."""
+    if _FUSED_IDW:
+        return _IdwBlend.apply(ref, qry, vals, idx, warp)
+    B, N, C = qry.shape
+    blend = _inverse_distance_blend(index_points_group(ref, idx) - qry.view(B, N, 1, C),
+                                    index_points_group(vals, idx))
+    return qry - blend if warp else blend
+
+
 def _inverse_distance_blend(grouped_xyz_norm, grouped_values):
     """weight = (1/d)/sum(1/d), d = ||.||.clamp(1e-10); sum_k weight * value  (ref :2130-2139)."""
     dist = torch.norm(grouped_xyz_norm, dim=3).clamp(min=1e-10)
@@ -892,13 +936,10 @@ class PointWarping(nn.Module):
         """Point-major: x1 (B,N1,3), x2 (B,N2,3), flow1 (B,N1,3) -> warped x2 (B,N2,3)."""
         if flow1 is None:
             return x2
-        B, N2, C = x2.shape
         xyz1_to_2 = (x1 + flow1).contiguous()
         x2 = x2.contiguous()
         knn_idx = knn_point(3, xyz1_to_2, x2)
-        grouped_xyz_norm = index_points_group(xyz1_to_2, knn_idx) - x2.view(B, N2, 1, C)
-        flow2 = _inverse_distance_blend(grouped_xyz_norm, index_points_group(flow1, knn_idx))
-        return x2 - flow2
+        return _idw_blend(xyz1_to_2, x2, flow1, knn_idx, warp=True)
 
 
 class UpsampleFlow(nn.Module):
@@ -916,11 +957,9 @@ class UpsampleFlow(nn.Module):
 
     def forward_cl(self, x, sx, sf, knn_idx=None):
         """Point-major: x (B,N,3), sx (B,S,3), sf (B,S,C) -> (B,N,C)."""
-        B, N, C = x.shape
         if knn_idx is None:
             knn_idx = knn_point(3, sx.contiguous(), x.contiguous())
-        grouped_xyz_norm = index_points_group(sx, knn_idx) - x.view(B, N, 1, C)
-        return _inverse_distance_blend(grouped_xyz_norm, index_points_group(sf, knn_idx))
+        return _idw_blend(sx, x, sf, knn_idx)
 
 
 class SceneFlowEstimatorResidual(nn.Module):

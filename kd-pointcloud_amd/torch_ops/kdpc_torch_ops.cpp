@@ -634,6 +634,53 @@ Tensor colsum(Tensor x) {
 
 }  // namespace
 
+// ------------------------------------------- 3-NN inverse-distance blend (idw_blend.hip)
+TT idw_blend_fwd(Tensor ref, Tensor qry, Tensor vals, Tensor idx, bool warp) {
+  dev(ref, kF, "ref"), dev(qry, kF, "qry"), dev(vals, kF, "vals"), dev(idx, kI, "idx");
+  same_device(ref, qry, "qry"), same_device(ref, vals, "vals"), same_device(ref, idx, "idx");
+  TORCH_CHECK(ref.dim() == 3 && ref.size(2) == 3 && qry.dim() == 3 && qry.size(2) == 3 &&
+                  vals.dim() == 3 && idx.dim() == 3 && idx.size(2) == 3 &&
+                  vals.size(1) == ref.size(1) && idx.size(1) == qry.size(1) &&
+                  ref.size(0) == qry.size(0) && vals.size(0) == ref.size(0) &&
+                  idx.size(0) == ref.size(0),
+              "kdpc: idw_blend expects ref (B,S,3), qry (B,N,3), vals (B,S,C), idx (B,N,3)");
+  GUARD(ref);
+  const int64_t b = ref.size(0), s = ref.size(1), n = qry.size(1), c = vals.size(2);
+  Tensor out = empty_f({b, n, c}, ref);
+  Tensor w = empty_f({b, n, 3}, ref);
+  check(kdpc_idw_blend_fwd(b, n, s, c, F(ref), F(qry), F(vals), I(idx), F(out), F(w), warp,
+                           stream_of(ref)), "idw_blend_fwd");
+  return {out, w};
+}
+
+Tensor idw_blend_bwd_vals(Tensor dout, Tensor w, Tensor offsets, Tensor perm, int64_t s,
+                          bool warp) {
+  dev(dout, kF, "dout"), dev(w, kF, "w"), dev(offsets, kI, "offsets"), dev(perm, kI, "perm");
+  TORCH_CHECK(dout.dim() == 3 && w.dim() == 3 && w.size(2) == 3 && w.size(1) == dout.size(1),
+              "kdpc: idw_blend_bwd_vals expects dout (B,N,C), w (B,N,3)");
+  GUARD(dout);
+  const int64_t b = dout.size(0), n = dout.size(1), c = dout.size(2);
+  Tensor dvals = empty_f({b, s, c}, dout);
+  check(kdpc_idw_blend_bwd_vals(b, n, s, c, F(dout), F(w), I(offsets), I(perm), F(dvals), warp,
+                                stream_of(dout)), "idw_blend_bwd_vals");
+  return dvals;
+}
+
+TT idw_blend_bwd_coords(Tensor ref, Tensor qry, Tensor vals, Tensor idx, Tensor dout,
+                        bool warp) {
+  dev(ref, kF, "ref"), dev(qry, kF, "qry"), dev(vals, kF, "vals"), dev(idx, kI, "idx");
+  dev(dout, kF, "dout");
+  GUARD(ref);
+  const int64_t b = ref.size(0), s = ref.size(1), n = qry.size(1), c = vals.size(2);
+  TORCH_CHECK(dout.dim() == 3 && dout.size(1) == n && dout.size(2) == c,
+              "kdpc: idw_blend_bwd_coords expects dout (B,N,C)");
+  Tensor drow = empty_f({b, n * 3, 3}, ref);
+  Tensor dq = empty_f({b, n, 3}, ref);
+  check(kdpc_idw_blend_bwd_coords(b, n, s, c, F(ref), F(qry), F(vals), I(idx), F(dout),
+                                  F(drow), F(dq), warp, stream_of(ref)), "idw_blend_bwd_coords");
+  return {drow, dq};
+}
+
 TORCH_LIBRARY(kdpc, m) {
   // reference pointnet2_cuda surface (pointnet2_api.cpp:10-24), in-place, returns 1
   m.def("ball_query_wrapper(int b, int n, int m, float radius, int nsample, Tensor new_xyz, "
@@ -709,6 +756,12 @@ TORCH_LIBRARY(kdpc, m) {
   m.def("batchnorm_lrelu_bwd(Tensor dy, Tensor y, Tensor x, Tensor weight, Tensor mean, "
         "Tensor invstd, float slope) -> (Tensor, Tensor, Tensor)");
   m.def("colsum(Tensor x) -> Tensor");
+  m.def("idw_blend_fwd(Tensor ref, Tensor qry, Tensor vals, Tensor idx, bool warp) "
+        "-> (Tensor, Tensor)");
+  m.def("idw_blend_bwd_vals(Tensor dout, Tensor w, Tensor offsets, Tensor perm, int s, "
+        "bool warp) -> Tensor");
+  m.def("idw_blend_bwd_coords(Tensor ref, Tensor qry, Tensor vals, Tensor idx, Tensor dout, "
+        "bool warp) -> (Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(kdpc, CUDA, m) {
@@ -754,4 +807,7 @@ TORCH_LIBRARY_IMPL(kdpc, CUDA, m) {
   m.impl("batchnorm_lrelu_apply", batchnorm_lrelu_apply);
   m.impl("batchnorm_lrelu_bwd", batchnorm_lrelu_bwd);
   m.impl("colsum", colsum);
+  m.impl("idw_blend_fwd", idw_blend_fwd);
+  m.impl("idw_blend_bwd_vals", idw_blend_bwd_vals);
+  m.impl("idw_blend_bwd_coords", idw_blend_bwd_coords);
 }

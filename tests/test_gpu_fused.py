@@ -244,3 +244,52 @@ def test_pointconv_flow_fused_equals_unfused(k, d, mlp, n1, n2, bsz):
         assert (a is None) == (b is None), i
         if a is not None:  # (the WeightNets' unused BatchNorm modules have none)
             _scale_close(a, b, rtol=2e-5, name=f"grad {i}")
+
+
+@pytest.mark.parametrize("b,s,n,c,warp", [(2, 300, 1000, 3, True), (3, 128, 700, 64, False),
+                                         (1, 50, 333, 5, False), (2, 2048, 8192, 3, True)])
+def test_idw_blend_vs_fp64(b, s, n, c, warp):
+    """UpsampleFlow / PointWarping's fused inverse-distance blend (csrc/idw_blend.hip) against
+    a float64 autograd evaluation of the reference expression (pointconv_util.py:2129-2140):
+    forward and the gradients of the reference points, the queries and the values, on the
+    build's own 3-NN index; one query sits exactly on a reference point (clamped distance,
+    masked gradient), as warped points can."""
+    import kdpc_native as nat
+    import pointconv_util as P
+    g = torch.Generator(device="cpu").manual_seed(b * 100 + s + n + c)
+    ref = torch.randn(b, s, 3, generator=g).to(DEV)
+    qry = torch.randn(b, n, 3, generator=g).to(DEV)
+    qry[0, 0] = ref[0, 7]
+    vals = torch.randn(b, s, c, generator=g).to(DEV)
+    if warp:
+        vals = vals * 0.1
+    idx = nat.knn_point(3, ref.contiguous(), qry.contiguous())
+    dout = torch.randn(b, n, c, generator=g).to(DEV)
+    R, Q, V = (t.clone().requires_grad_(True) for t in (ref, qry, vals))
+    out = P._IdwBlend.apply(R, Q, V, idx, warp)
+    out.backward(dout)
+    R64, Q64, V64 = (t.double().requires_grad_(True) for t in (ref, qry, vals))
+    il = idx.long()
+    bi = torch.arange(b, device=DEV).view(b, 1, 1)
+    gxyz = R64[bi, il] - Q64.unsqueeze(2)
+    dist = torch.norm(gxyz, dim=3).clamp(min=1e-10)
+    weight = (1.0 / dist) / torch.sum(1.0 / dist, dim=2, keepdim=True)
+    blend = torch.sum(weight.unsqueeze(-1) * V64[bi, il], dim=2)
+    out64 = Q64 - blend if warp else blend
+    out64.backward(dout.double())
+    _scale_close(out, out64, name="out")
+    _scale_close(V.grad, V64.grad, name="dvals")
+    _scale_close(R.grad, R64.grad, rtol=2e-5, name="dref")
+    _scale_close(Q.grad, Q64.grad, rtol=2e-5, name="dqry")
+    assert float(R.grad[0, 7].abs().max()) == float(R64.grad[0, 7].abs().max()) == 0.0 or \
+        torch.allclose(R.grad[0, 7].double(), R64.grad[0, 7], atol=1e-5 * float(R64.grad.abs().max()))
+    # the unfused fp32 torch path of the layers agrees too
+    P._FUSED_IDW = False
+    try:
+        R2, Q2, V2 = (t.clone().requires_grad_(True) for t in (ref, qry, vals))
+        out2 = P._idw_blend(R2, Q2, V2, idx, warp)
+        out2.backward(dout)
+    finally:
+        P._FUSED_IDW = True
+    _scale_close(out, out2, name="out vs unfused")
+    _scale_close(V.grad, V2.grad, name="dvals vs unfused")

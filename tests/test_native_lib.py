@@ -134,6 +134,8 @@ TORCH_OPS = {
     "batchnorm_lrelu_fwd": "kdpc_batchnorm_lrelu_fwd",
     "batchnorm_lrelu_apply": "kdpc_batchnorm_lrelu_apply",
     "batchnorm_lrelu_bwd": "kdpc_batchnorm_lrelu_bwd", "colsum": "kdpc_colsum",
+    "idw_blend_fwd": "kdpc_idw_blend_fwd", "idw_blend_bwd_vals": "kdpc_idw_blend_bwd_vals",
+    "idw_blend_bwd_coords": "kdpc_idw_blend_bwd_coords",
 }
 
 
