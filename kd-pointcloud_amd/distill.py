@@ -19,6 +19,7 @@ multi-process path be tested on CPU with gloo.
 import torch
 import torch.distributed as dist
 
+import kdpc_native
 import loss_functions
 
 
@@ -247,6 +248,7 @@ class GraphedStep:
                     self.fps_next = list(prefetch_fn(*self.static_next))
             self.loss = self.loss_fn(*self.static, **self._fps_kw(self.fps_cur))
             self.loss.backward()
+            kdpc_native.csr_join()  # side-stream CSR builds (csr_prefetch) rejoin the capture
             self.grads = [p.grad for p in self.params if p.grad is not None]
             self.flat = torch.cat([g.reshape(-1) for g in self.grads]) if self.world > 1 else None
             if fork is not None:
