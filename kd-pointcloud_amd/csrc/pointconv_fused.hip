@@ -51,6 +51,9 @@ using namespace kdpc;
 #ifndef KDPC_DG_CHUNK_MAJOR  // dG rows stored chunk-major: [chunk][pair][8] (else [pair][C8])
 #define KDPC_DG_CHUNK_MAJOR 0
 #endif
+#ifndef KDPC_AGPR  // 1: MFMA accumulators in the AccVGPR file (see agpr_form())
+#define KDPC_AGPR 0
+#endif
 #ifndef KDPC_WGT_MODE
 #define KDPC_WGT_MODE 0
 #endif
@@ -84,6 +87,20 @@ __device__ __forceinline__ f32x16 mfma4(float4 a, float4 b, f32x16 c) {
   c = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, c, 0, 0, 0);
   c = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, c, 0, 0, 0);
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, c, 0, 0, 0);
+}
+
+// An inline-asm operand in an AccVGPR tells the compiler the kernel may use AGPRs; it then
+// selects the AGPR form of the MFMAs (SrcC / vDst in the AccVGPR file) instead of the
+// all-VGPR form it picks for kernels without AGPR uses.  With the accumulators out of the
+// architectural VGPR file the MFMAs' 16-register C reads / D writes stop competing with the
+// VALU work of the same SIMD for its register ports (round-2 stamps: the co-resident wave's
+// VALU ran ~3x slower while MFMAs were in flight).  Measured (forward and weight kernels,
+// 128 VGPR + 65-93 AGPR instead of 190-199 VGPR): flow0 fwd 437 -> 449 us, bwd 1101 -> 1132 us
+// -- no gain, so the default stays the VGPR form (KDPC_AGPR=1 for A/B builds).
+__device__ __forceinline__ void agpr_form() {
+#if KDPC_AGPR
+  asm volatile("; kdpc: AGPR-form MFMAs" ::"a"(0));
+#endif
 }
 
 __device__ __forceinline__ f32x16 zero16() {
@@ -187,6 +204,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 void pc_fwd_kernel(Geo g, const float* __restrict__ wt, const float* __restrict__ wl,
                    const float* __restrict__ bias, float* __restrict__ y,
                    float* __restrict__ slab, int chunks_per_split) {
+  agpr_form();
   constexpr int MT = KM <= 9 ? 2 : 1;
   constexpr int TM = 32 * MT;
   constexpr int NT = O / 32;
@@ -1172,6 +1190,7 @@ template <int O, int KM, bool EX>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
 void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __restrict__ dy,
                           float* __restrict__ dwl, int rows_per_split, int nsplit, int xcd_map) {
+  agpr_form();
   constexpr int TR = wgt_tile_rows<O, KM>();
   constexpr int TS = TR + 4;               // row stride of the transposed tiles
   constexpr int RP = TR / 32;              // build passes (rows rb, rb + 32, ...)
