@@ -54,6 +54,12 @@ using namespace kdpc;
 #ifndef KDPC_AGPR  // 1: MFMA accumulators in the AccVGPR file (see agpr_form())
 #define KDPC_AGPR 0
 #endif
+#ifndef KDPC_WGT_NT  // weight-gradient kernel threads (512: 2 waves per SIMD; 256: 1)
+#define KDPC_WGT_NT 512
+#endif
+#ifndef KDPC_WGT_SCHED  // weight kernel: explicit MFMA / VALU / LDS interleave (experiment)
+#define KDPC_WGT_SCHED 0
+#endif
 #ifndef KDPC_WGT_MODE
 #define KDPC_WGT_MODE 0
 #endif
@@ -1187,18 +1193,22 @@ template <int O, int KM>
 constexpr int wgt_tile_rows() { return O == 256 || (O == 128 && KM > 9) ? 32 : 64; }
 
 template <int O, int KM, bool EX>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+__global__ __launch_bounds__(KDPC_WGT_NT) __attribute__((amdgpu_waves_per_eu(KDPC_WGT_NT / 256)))
 void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __restrict__ dy,
                           float* __restrict__ dwl, int rows_per_split, int nsplit, int xcd_map) {
   agpr_form();
   constexpr int TR = wgt_tile_rows<O, KM>();
   constexpr int TS = TR + 4;               // row stride of the transposed tiles
-  constexpr int RP = TR / 32;              // build passes (rows rb, rb + 32, ...)
+  constexpr int NT = KDPC_WGT_NT;          // threads: 512 = 2 waves / SIMD, 256 = 1
+  constexpr int RS = NT / 16;              // rows per build pass (16 threads per row)
+  constexpr int RP = TR / RS;              // build passes (rows rb, rb + RS, ...)
   constexpr int MT = O / 32;
-  constexpr int MPW = MT / 2 > 0 ? MT / 2 : 1;  // 8 waves: 4 column tiles x 2 row-tile groups
-  constexpr int GS = (TR * KM + 255) / 256;     // gather slots (float4) per thread
-  constexpr int DV = TR * O / (512 * 4);        // dy float4 slots per thread
-  static_assert(DV >= 1 && TR * O % 2048 == 0, "dy tile must split into float4 slots");
+  constexpr int RG = NT / 256;             // row-tile groups (waves = 4 column tiles x RG)
+  constexpr int MPW = MT / RG > 0 ? MT / RG : 1;
+  constexpr int GS = (TR * KM + NT / 2 - 1) / (NT / 2);  // gather slots (float4) per thread
+  constexpr int DV = TR * O / (NT * 4);    // dy float4 slots per thread
+  static_assert(RP >= 1 && TR % RS == 0, "tile rows must split into build passes");
+  static_assert(DV >= 1 && TR * O % (NT * 4) == 0, "dy tile must split into float4 slots");
   static_assert(MT >= 2, "O >= 64");
   __shared__ __attribute__((aligned(16))) float gl[TR * KM * kCC];
   __shared__ __attribute__((aligned(16))) float dyt[2][O * TS];
@@ -1262,7 +1272,7 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
     const int rr = row0 - b0 * g.s;
 #pragma unroll
     for (int i = 0; i < GS; ++i) {
-      const int rk = (t >> 1) + 256 * i;
+      const int rk = (t >> 1) + (NT / 2) * i;
       const int r = rk / kk;
       const int rw = row0 + r;
       const bool ok = rk < tk && rw < rend;
@@ -1279,7 +1289,7 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
     const int row0 = rbeg + tile * TR;
 #pragma unroll
     for (int p2 = 0; p2 < RP; ++p2) {
-      const int row = row0 + rb + 32 * p2;
+      const int row = row0 + rb + RS * p2;
       const unsigned base = row < rend ? ((unsigned)row * (unsigned)kk * kW + w) * 4u : kOOB;
 #pragma unroll
       for (int k = 0; k < KM; ++k) {
@@ -1295,7 +1305,7 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
     // feature 0, lane half 1 features 1..4; otherwise 4 consecutive features.
 #pragma unroll
     for (int i = 0; i < GS; ++i) {
-      const int rk = (t >> 1) + 256 * i;
+      const int rk = (t >> 1) + (NT / 2) * i;
       const int rw = row0 + rk / kk;
       const int nb = nbi[i];
       const bool live = (unsigned)nb < (unsigned)g.bn;
@@ -1324,7 +1334,7 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
     // transposed LDS writes below hit consecutive banks), columns 4 (q / TR) .. +3
 #pragma unroll
     for (int i = 0; i < DV; ++i) {
-      const int q = t + 512 * i;
+      const int q = t + NT * i;
       const int rw = row0 + q % TR;
       const unsigned off = rw < rend ? ((unsigned)rw * O + 4u * (unsigned)(q / TR)) * 4u : kOOB;
       dr[i] = KDPC_WGT_MODE == 7 ? make_float4(1.f, 2.f, 3.f, (float)q) : __builtin_bit_cast(
@@ -1335,13 +1345,13 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
   auto stage = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < GS; ++i) {
-      const int rk = (t >> 1) + 256 * i;
+      const int rk = (t >> 1) + (NT / 2) * i;
       if (rk < tk) *reinterpret_cast<float4*>(gl + rk * kCC + 4 * h4) = gr[i];
     }
     float* dt = dyt[buf];
 #pragma unroll
     for (int i = 0; i < DV; ++i) {
-      const int q = t + 512 * i;
+      const int q = t + NT * i;
       const int r = q % TR, o = 4 * (q / TR);
       dt[(o + 0) * TS + r] = dr[i].x;
       dt[(o + 1) * TS + r] = dr[i].y;
@@ -1359,9 +1369,9 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
 #pragma unroll
     for (int p2 = 0; p2 < RP; ++p2) {
       float a[kCC];
-      build_row<KM>(gl, rb + 32 * p2, kk, wc[p2], a);
+      build_row<KM>(gl, rb + RS * p2, kk, wc[p2], a);
 #pragma unroll
-      for (int c = 0; c < kCC; ++c) ab[(c * kW + w) * TS + rb + 32 * p2] = a[c];
+      for (int c = 0; c < kCC; ++c) ab[(c * kW + w) * TS + rb + RS * p2] = a[c];
     }
   };
 
@@ -1404,6 +1414,18 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
     }
     KDPC_WSTAMP(2);
     if (KDPC_WGT_MODE != 2 && KDPC_WGT_MODE != 5) build(cur ^ 1);
+#if KDPC_WGT_SCHED
+    // one wave per SIMD: interleave the tile's MFMAs with the build's VALU / LDS work and the
+    // fetch's loads (the scheduler otherwise clusters the MFMAs and the wave idles through
+    // them); per MFMA: two VALU, one LDS read, and a load slot
+#pragma unroll
+    for (int i = 0; i < MPW * (TR / 8) * 4; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    }
+#endif
     KDPC_WSTAMP(3);
     __syncthreads();  // at[cur] / dyt[cur] / gl consumed; at[cur ^ 1] complete
     KDPC_WSTAMP(4);
@@ -1575,10 +1597,10 @@ hipError_t bwd_launch(const Geo& g, const Plan& p, int b, const float* wt, const
                      0, st, npts, rk, g.c, p.c8, g.d, dgr, offsets, perm, dxyz, dfeats);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (g.k == KM)
-    hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM, true>), dim3(p.wgs), dim3(512), 0, st, g, wt,
+    hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM, true>), dim3(p.wgs), dim3(KDPC_WGT_NT), 0, st, g, wt,
                        dy, p.rs > 1 ? dwl_slab : dwl, p.rps, p.rs, p.xcd);
   else
-    hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM, false>), dim3(p.wgs), dim3(512), 0, st, g, wt,
+    hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM, false>), dim3(p.wgs), dim3(KDPC_WGT_NT), 0, st, g, wt,
                        dy, p.rs > 1 ? dwl_slab : dwl, p.rps, p.rs, p.xcd);
   if ((e = hipGetLastError()) != hipSuccess || p.rs == 1) return e;
   return slab_sum(p.rs, (long long)O * g.c * kW, dwl_slab, nullptr, 1, dwl, st);
