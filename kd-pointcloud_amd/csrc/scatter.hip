@@ -121,6 +121,111 @@ __global__ __launch_bounds__(256) void csr_segsort_kernel(long long m, int n, in
   }
 }
 
+// CSR build for key spaces that fit in LDS (n <= kLdsKeys per batch): one 1024-thread
+// workgroup per batch element counts its index row into an LDS histogram (LDS atomics:
+// no device-scope atomics, which ran at ~27 G/s for the 4.2 M-entry cost-volume index),
+// scans it in LDS, and later fills the segments from LDS cursors.  Two launches replace the
+// memset / count / scan (2) / fill chain; the segment rank sort stays (LDS cursors hand out
+// slots in arbitrary order inside a key, exactly like the global-atomic fill).
+constexpr int kLdsKeys = 15872;  // histogram ints per workgroup (<= 62 KiB of LDS)
+constexpr int kLdsThreads = 1024;
+
+// inclusive block scan of one int per thread (1024 threads = 16 waves); -> block total
+__device__ __forceinline__ int block_incl_scan(int v, int* wsum, int* total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(v, o, 64);
+    if (lane >= o) v += u;
+  }
+  if (lane == 63) wsum[wv] = v;
+  __syncthreads();
+  if (wv == 0) {
+    int w = lane < kLdsThreads / 64 ? wsum[lane] : 0;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const int u = __shfl_up(w, o, 64);
+      if (lane >= o) w += u;
+    }
+    if (lane < kLdsThreads / 64) wsum[lane] = w;
+  }
+  __syncthreads();
+  const int add = wv > 0 ? wsum[wv - 1] : 0;
+  *total = wsum[kLdsThreads / 64 - 1];
+  return v + add;
+}
+
+// per batch b: histogram of idx[b,:] over [0,n), its exclusive scan -> offsets[b*n + k]
+// (batch-local; csr_lds_fill adds the batch's base), and the batch's valid count -> tot[b]
+__global__ __launch_bounds__(kLdsThreads) void csr_lds_count_kernel(int n, int p,
+                                                                    const int* __restrict__ idx,
+                                                                    int* __restrict__ offsets,
+                                                                    int* __restrict__ tot) {
+  extern __shared__ int h[];  // n histogram ints + 16 wave sums
+  int* wsum = h + n;
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int* row = idx + (long long)b * p;
+  for (int k = t; k < n; k += kLdsThreads) h[k] = 0;
+  __syncthreads();
+  int i = t;
+  for (; i + 3 * kLdsThreads < p; i += 4 * kLdsThreads) {  // four loads in flight
+    int v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = row[i + u * kLdsThreads];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if ((unsigned)v[u] < (unsigned)n) atomicAdd(&h[v[u]], 1);
+  }
+  for (; i < p; i += kLdsThreads) {
+    const int v = row[i];
+    if ((unsigned)v < (unsigned)n) atomicAdd(&h[v], 1);
+  }
+  __syncthreads();
+  // thread t owns keys [t*E, t*E + E): its block sum, the block scan, then the running sum
+  const int E = (n + kLdsThreads - 1) / kLdsThreads;
+  const int k0 = t * E, k1 = min(n, k0 + E);
+  int s = 0;
+  for (int k = k0; k < k1; ++k) s += h[k];
+  int total;
+  int run = block_incl_scan(s, wsum, &total) - s;
+  int* off = offsets + (long long)b * n;
+  for (int k = k0; k < k1; ++k) {
+    const int c = h[k];
+    off[k] = run;
+    run += c;
+  }
+  if (t == 0) tot[b] = total;
+}
+
+// per batch b: base = valid positions of batches < b; final offsets; fill from LDS cursors
+__global__ __launch_bounds__(kLdsThreads) void csr_lds_fill_kernel(int n, int p, int nb,
+                                                                   const int* __restrict__ idx,
+                                                                   int* __restrict__ offsets,
+                                                                   const int* __restrict__ tot,
+                                                                   int* __restrict__ perm) {
+  extern __shared__ int cur[];  // n cursors + 16 wave sums
+  int* wsum = cur + n;
+  const int b = blockIdx.x, t = threadIdx.x;
+  int part = 0;
+  for (int j = t; j < b; j += kLdsThreads) part += tot[j];
+  int base;
+  block_incl_scan(part, wsum, &base);
+  int* off = offsets + (long long)b * n;
+  for (int k = t; k < n; k += kLdsThreads) {
+    const int o = off[k] + base;
+    off[k] = o;
+    cur[k] = o;
+  }
+  if (b == nb - 1 && t == 0) offsets[(long long)nb * n] = base + tot[b];
+  __syncthreads();
+  const int* row = idx + (long long)b * p;
+  const int e0 = b * p;
+  for (int i = t; i < p; i += kLdsThreads) {
+    const int v = row[i];
+    if ((unsigned)v < (unsigned)n) perm[atomicAdd(&cur[v], 1)] = e0 + i;
+  }
+}
+
 inline int grid_for(long long total, int block) {
   long long g = divupll(total, block);
   if (g > 65536) g = 65536;
@@ -159,6 +264,19 @@ hipError_t csr_build(int b, int n, int p, const int* idx, void* ws, size_t ws_by
   int* cnt = reinterpret_cast<int*>(base + L.cnt);
   int* fill = reinterpret_cast<int*>(base + L.fill);
   const long long m = (long long)b * n;
+  const int sgrid = (int)std::min<long long>(divupll(m, 4), 8192);  // 4 waves per workgroup
+  if (n <= kLdsKeys) {  // LDS histogram path (cnt holds the per-batch totals)
+    const size_t lds = (size_t)(n + 16) * sizeof(int);
+    hipLaunchKernelGGL(csr_lds_count_kernel, dim3(b), dim3(kLdsThreads), lds, st, n, p, idx,
+                       offsets, cnt);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(csr_lds_fill_kernel, dim3(b), dim3(kLdsThreads), lds, st, n, p, b, idx,
+                       offsets, cnt, perm);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(csr_segsort_kernel, dim3(sgrid), dim3(256), 0, st, m, n, p, idx, offsets,
+                       perm);
+    return hipGetLastError();
+  }
   if ((e = hipMemsetAsync(cnt, 0, L.fill + sizeof(int) * m, st)) != hipSuccess) return e;
   const dim3 pgrid((unsigned)std::min(divup(p, 256), std::max(1, 4096 / b)), (unsigned)b);
   hipLaunchKernelGGL(csr_count_kernel, pgrid, dim3(256), 0, st, n, p, idx, cnt);
@@ -166,7 +284,6 @@ hipError_t csr_build(int b, int n, int p, const int* idx, void* ws, size_t ws_by
   e = hipcub::DeviceScan::ExclusiveSum(base + L.scan, scan_bytes, cnt, offsets, (int)(m + 1), st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(csr_fill_kernel, pgrid, dim3(256), 0, st, n, p, idx, offsets, fill, perm);
-  const int sgrid = (int)std::min<long long>(divupll(m, 4), 8192);  // 4 waves per workgroup
   hipLaunchKernelGGL(csr_segsort_kernel, dim3(sgrid), dim3(256), 0, st, m, n, p, idx, offsets,
                      perm);
   return hipGetLastError();

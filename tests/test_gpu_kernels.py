@@ -352,21 +352,30 @@ def test_colsum_fixed_order(nat, rows, cols):
     assert ((a.double() - want).abs() <= bound + 1e-6).all()
 
 
-@pytest.mark.parametrize("b,n,p,hub", [(1, 1, 5, 0), (2, 100, 37, 0), (16, 8192, 32768, 0),
-                                       (16, 8192, 262144, 0), (4, 512, 4096, 1000),
-                                       (2, 64, 20000, 20000)])
-def test_csr_build_is_stable_counting_sort(nat, b, n, p, hub):
-    """kdpc_csr_build (count / scan / atomic fill / segment rank sort) equals a stable sort
-    of the keys b*N + idx: offsets = segment starts, perm = positions in ascending order per
-    key -- including hub keys with long segments (the ballot-scan path) and the degenerate
-    case of every position on one key."""
+@pytest.mark.parametrize("b,n,p,hub,bad", [(1, 1, 5, 0, 0), (2, 100, 37, 0, 0),
+                                           (16, 8192, 32768, 0, 0), (16, 8192, 262144, 0, 0),
+                                           (4, 512, 4096, 1000, 0), (2, 64, 20000, 20000, 0),
+                                           (3, 700, 5000, 0, 300), (2, 20000, 30000, 0, 0),
+                                           (2, 20000, 30000, 50, 400), (1, 15872, 9000, 0, 0)])
+def test_csr_build_is_stable_counting_sort(nat, b, n, p, hub, bad):
+    """kdpc_csr_build equals a stable sort of the keys b*N + idx: offsets = segment starts,
+    perm = positions in ascending order per key -- on both build paths (LDS histogram for
+    N <= 15872 keys per batch, global count / scan / fill above), including hub keys with long
+    segments (the ballot-scan path), every position on one key, and out-of-range indices
+    (left out of every segment)."""
     g = np.random.default_rng(b * 7 + n + p)
     idx = g.integers(0, n, size=(b, p)).astype(np.int32)
     if hub:
         idx[:, g.choice(p, size=min(hub, p), replace=False)] = 0
+    if bad:
+        sel = g.choice(p, size=bad, replace=False)
+        idx[:, sel] = np.where(g.random(bad) < 0.5, -1, n + 3).astype(np.int32)
     csr = nat.Csr(torch.from_numpy(idx).to(DEV), n)
+    valid = ((idx >= 0) & (idx < n)).reshape(-1)
     keys = (np.arange(b)[:, None] * n + idx).reshape(-1)
-    want_perm = np.argsort(keys, kind="stable")
+    pos = np.nonzero(valid)[0]
+    want_perm = pos[np.argsort(keys[pos], kind="stable")]
     want_off = np.searchsorted(keys[want_perm], np.arange(b * n + 1))
     np.testing.assert_array_equal(csr.offsets.cpu().numpy(), want_off)
-    np.testing.assert_array_equal(csr.perm.cpu().numpy(), want_perm)
+    # perm holds B*P slots; past the valid positions its tail is unspecified
+    np.testing.assert_array_equal(csr.perm.cpu().numpy()[:len(want_perm)], want_perm)
