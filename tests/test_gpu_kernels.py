@@ -379,3 +379,42 @@ def test_csr_build_is_stable_counting_sort(nat, b, n, p, hub, bad):
     np.testing.assert_array_equal(csr.offsets.cpu().numpy(), want_off)
     # perm holds B*P slots; past the valid positions its tail is unspecified
     np.testing.assert_array_equal(csr.perm.cpu().numpy()[:len(want_perm)], want_perm)
+
+
+def _colsum_order_ref(x):
+    """float32 restatement of csrc/colsum.hip's summation order (plan, slabs, quarters)."""
+    def quarters(rows):  # rows (r, len) float32 -> the 4-row-group sum in the kernel's order
+        q = -(-rows.shape[0] // 4)
+        parts = []
+        for gi in range(4):
+            acc = np.zeros(rows.shape[1], np.float32)
+            for r in rows[gi * q:gi * q + q]:
+                acc = (acc + r).astype(np.float32)
+            parts.append(acc)
+        s = parts[0]
+        for pk in parts[1:]:
+            s = (s + pk).astype(np.float32)
+        return s
+    nrows, ln = x.shape
+    if nrows <= 256:
+        return quarters(x)
+    cb = -(-ln // 64)
+    g = max(2, -(-1024 // cb))
+    g = max(1, min(min(g, -(-nrows // 64)), 1024))
+    rpw = -(-nrows // g)
+    slabs = -(-nrows // rpw)
+    part = np.stack([quarters(x[y * rpw:(y + 1) * rpw]) for y in range(slabs)])
+    return quarters(part)
+
+
+@pytest.mark.parametrize("rows,cols", [(300, 5), (4096, 256), (20000, 7), (65536, 128)])
+def test_colsum_matches_its_stated_order(nat, rows, cols):
+    """The column sum is exactly its documented fixed order (plan -> slabs -> row-group
+    quarters, csrc/colsum.hip): bit-identical to a float32 restatement, on repeated calls."""
+    g = torch.Generator(device="cpu").manual_seed(rows * 3 + cols)
+    x = torch.randn(rows, cols, generator=g)
+    want = _colsum_order_ref(x.numpy())
+    xd = x.to(DEV)
+    outs = [nat.colsum(xd) for _ in range(5)]
+    for o in outs:
+        np.testing.assert_array_equal(o.cpu().numpy(), want)
