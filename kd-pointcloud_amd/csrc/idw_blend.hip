@@ -80,6 +80,20 @@ __global__ __launch_bounds__(256) void idw_fwd_kernel(int b, int n, int s, int c
 #pragma unroll
       for (int k = 0; k < 3; ++k) wout[row * 3 + k] = o.w[k];
     }
+    if ((c & 3) == 0) {  // 16-byte value rows (warp implies c = 3: never here)
+      float4 x[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        x[k] = *reinterpret_cast<const float4*>(vals + (long long)o.nb[k] * c + 4 * v);
+      auto blend = [&](float a0, float a1, float a2) {
+        return __fadd_rn(__fadd_rn(__fmul_rn(o.w[0], a0), __fmul_rn(o.w[1], a1)),
+                         __fmul_rn(o.w[2], a2));
+      };
+      *reinterpret_cast<float4*>(out + row * c + 4 * v) =
+          make_float4(blend(x[0].x, x[1].x, x[2].x), blend(x[0].y, x[1].y, x[2].y),
+                      blend(x[0].z, x[1].z, x[2].z), blend(x[0].w, x[1].w, x[2].w));
+      continue;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int ch = 4 * v + i;
@@ -93,26 +107,43 @@ __global__ __launch_bounds__(256) void idw_fwd_kernel(int b, int n, int s, int c
 }
 
 // dvals[b,j,ch] = sum over the CSR entries p = (n*3 + k) of reference point j of
-// w[p] * dblend[n, ch] (dblend = -dout for PointWarping), ascending p
+// w[p] * dblend[n, ch] (dblend = -dout for PointWarping), ascending p.  One thread per
+// (reference point, V channels): the segment's perm / w entries are read once per V channels
+// (V = 4 with 16-byte dout rows when C % 4 == 0), in the same per-channel order.
+template <int V>
 __global__ __launch_bounds__(256) void idw_bwd_vals_kernel(int b, int s, int c,
                                                            const float* __restrict__ dout,
                                                            const float* __restrict__ w,
                                                            const int* __restrict__ offsets,
                                                            const int* __restrict__ perm,
                                                            float* __restrict__ dvals, int warp) {
-  const long long total = (long long)b * s * c;
+  const int cv = c / V;
+  const long long total = (long long)b * s * cv;
+  const float sg = warp ? -1.f : 1.f;
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (long long)gridDim.x * blockDim.x) {
-    const long long key = e / c;
-    const int ch = (int)(e - key * c);
+    const long long key = e / cv;
+    const int v = (int)(e - key * cv);
     const int j0 = offsets[key], j1 = offsets[key + 1];
-    float acc = 0.f;
+    float acc[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) acc[i] = 0.f;
     for (int j = j0; j < j1; ++j) {
       const int p = perm[j];
-      const float g = dout[(long long)(p / 3) * c + ch];
-      acc = __fadd_rn(acc, __fmul_rn(w[p], warp ? -g : g));
+      const float wp = w[p];
+      const float* g = dout + (long long)(p / 3) * c + V * v;
+      float gv[V];
+      if constexpr (V == 4) {
+        const float4 x = *reinterpret_cast<const float4*>(g);
+        gv[0] = x.x, gv[1] = x.y, gv[2] = x.z, gv[3] = x.w;
+      } else {
+        gv[0] = g[0];
+      }
+#pragma unroll
+      for (int i = 0; i < V; ++i) acc[i] = __fadd_rn(acc[i], __fmul_rn(wp, sg * gv[i]));
     }
-    dvals[e] = acc;
+#pragma unroll
+    for (int i = 0; i < V; ++i) dvals[key * c + V * v + i] = acc[i];
   }
 }
 
@@ -193,8 +224,12 @@ KDPC_API int kdpc_idw_blend_bwd_vals(int b, int n, int s, int c, const float* do
   KDPC_CHECK_ARG(b >= 0 && n >= 0 && s > 0 && c > 0 && (!warp || c == 3));
   if ((long long)b * s == 0) return (int)hipSuccess;
   KDPC_CHECK_ARG(offsets && perm && dvals && ((long long)b * n == 0 || (dout && w)));
-  hipLaunchKernelGGL(idw_bwd_vals_kernel, dim3(grid_of((long long)b * s * c)), dim3(256), 0,
-                     (hipStream_t)stream, b, s, c, dout, w, offsets, perm, dvals, warp);
+  if (c % 4 == 0)
+    hipLaunchKernelGGL(idw_bwd_vals_kernel<4>, dim3(grid_of((long long)b * s * c / 4)), dim3(256),
+                       0, (hipStream_t)stream, b, s, c, dout, w, offsets, perm, dvals, warp);
+  else
+    hipLaunchKernelGGL(idw_bwd_vals_kernel<1>, dim3(grid_of((long long)b * s * c)), dim3(256), 0,
+                       (hipStream_t)stream, b, s, c, dout, w, offsets, perm, dvals, warp);
   return (int)hipGetLastError();
 }
 
