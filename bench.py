@@ -229,10 +229,19 @@ def main():
             for t in list(student.parameters()) + list(student.buffers()):
                 dist.broadcast(t.data, 0)
         opt = make_optimizer(student, capturable=True)
-        if args.mode == "kd":
-            step = graphed_kd_step(teacher, student, opt, batches[0])
-        else:
-            step = graphed_flow_step(student, opt, batches[0])
+        try:
+            if args.mode == "kd":
+                step = graphed_kd_step(teacher, student, opt, batches[0])
+            else:
+                step = graphed_flow_step(student, opt, batches[0])
+        except RuntimeError as exc:  # capture refused on this runtime: measure the eager step
+            if world == 1:
+                raise
+            print(f"rank {rank}: HIP-graph capture failed ({exc}); eager DDP step instead",
+                  file=sys.stderr, flush=True)
+            graph = False
+            torch.cuda.synchronize()
+    if graph:
         eager = (KDTrainStep(teacher, student, opt) if args.mode == "kd"
                  else FlowTrainStep(student, opt))
     else:

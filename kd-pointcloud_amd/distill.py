@@ -238,6 +238,10 @@ class GraphedStep:
         self.opt.zero_grad(set_to_none=True)
         self.graph_a = torch.cuda.CUDAGraph()
         kw = {"stream": side} if self.capture_on_side_stream else {}
+        if self.world > 1:
+            # a process group's background threads (RCCL watchdog: event queries) may touch the
+            # runtime while this thread captures; "global" mode would fail those calls
+            kw["capture_error_mode"] = "thread_local"
         fork = torch.cuda.Stream() if prefetch_fn is not None else None
         with torch.cuda.graph(self.graph_a, **kw):
             cap = torch.cuda.current_stream()
