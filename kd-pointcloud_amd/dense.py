@@ -67,9 +67,15 @@ def fixed_sum(x, dim=None):
 
 
 def splitk_tn(a, b):
-    """a (R,O), b (R,I) -> a^T b (O,I) with the R reduction split over chunks."""
+    """a (R,O), b (R,I) -> a^T b (O,I) with the R reduction split over chunks.  Skinny
+    layers (O or I <= 4: the xyz input convs, the 3-channel flow heads) go to the HIP slab
+    kernel (csrc/dense_small.hip): the BLAS library ran them on 16-wide tiles at ~50 us each."""
     R, O = a.shape
     I = b.shape[1]
+    if a.is_cuda and a.dtype == torch.float32 and min(O, I) <= 4 and R >= 2048:
+        import kdpc_native
+        if kdpc_native.dense_tn_small_supported(R, O, I):
+            return kdpc_native.dense_tn_small(a, b)
     c = _chunks(R, O * I)
     if c == 1:
         return a.t().mm(b)

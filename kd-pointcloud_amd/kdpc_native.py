@@ -85,6 +85,8 @@ _SIGNATURES = {
     "kdpc_idw_blend_fwd": [_c_int] * 4 + [_vp] * 6 + [_c_int, _vp],
     "kdpc_idw_blend_bwd_vals": [_c_int] * 4 + [_vp] * 5 + [_c_int, _vp],
     "kdpc_idw_blend_bwd_coords": [_c_int] * 4 + [_vp] * 7 + [_c_int, _vp],
+    "kdpc_dense_tn_small_workspace_bytes": [_c_int] * 3,
+    "kdpc_dense_tn_small": [_c_int] * 3 + [_vp] * 4 + [_c_size, _vp],
 }
 _RESTYPES = {"kdpc_build_id": ctypes.c_char_p, "kdpc_grad_workspace_bytes": _c_size,
              "kdpc_csr_workspace_bytes": _c_size, "kdpc_cost_volume_bwd_workspace_bytes": _c_size,
@@ -94,7 +96,8 @@ _RESTYPES = {"kdpc_build_id": ctypes.c_char_p, "kdpc_grad_workspace_bytes": _c_s
              "kdpc_wn_wsum_bwd_workspace_bytes": _c_size,
              "kdpc_knn_feature_workspace_bytes": _c_size,
              "kdpc_batchnorm_workspace_bytes": _c_size,
-             "kdpc_colsum_workspace_bytes": _c_size, "kdpc_knn_workspace_bytes": _c_size}
+             "kdpc_colsum_workspace_bytes": _c_size, "kdpc_knn_workspace_bytes": _c_size,
+             "kdpc_dense_tn_small_workspace_bytes": _c_size}
 
 EXPORTED = tuple(_SIGNATURES)
 
@@ -641,6 +644,19 @@ def batchnorm_lrelu_bwd(dy, y, x2, weight, mean, invstd, slope):
     R, C = _gpu(x2, "x").shape
     return _op("kdpc_batchnorm_lrelu_bwd", "batchnorm_lrelu_bwd", dy, y, x2, weight, mean,
                invstd, float(slope), work=(20 * R * C, 0))
+
+
+@functools.lru_cache(maxsize=None)
+def dense_tn_small_supported(r, o, i):
+    return load_library().kdpc_dense_tn_small_workspace_bytes(r, o, i) > 0
+
+
+def dense_tn_small(a, b):
+    """a (R,O), b (R,I) -> a^T b (O,I) for tiny O*I (see include/kdpc.h)."""
+    R, O = _gpu(a, "a").shape
+    I = b.shape[1]
+    return _op("kdpc_dense_tn_small", "dense_tn_small", a.contiguous(), b.contiguous(),
+               work=(4 * R * (O + I) + 4 * O * I, 2.0 * R * O * I))
 
 
 def colsum(x2):

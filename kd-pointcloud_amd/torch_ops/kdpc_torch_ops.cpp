@@ -681,6 +681,22 @@ TT idw_blend_bwd_coords(Tensor ref, Tensor qry, Tensor vals, Tensor idx, Tensor 
   return {drow, dq};
 }
 
+// -------------------------------------- skinny weight gradients (dense_small.hip)
+Tensor dense_tn_small(Tensor a, Tensor b) {
+  dev(a, kF, "a"), dev(b, kF, "b"), same_device(a, b, "b");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.size(0) == b.size(0),
+              "kdpc: dense_tn_small expects a (R,O), b (R,I)");
+  GUARD(a);
+  const int64_t r = a.size(0), o = a.size(1), i = b.size(1);
+  const size_t nb = kdpc_dense_tn_small_workspace_bytes(r, o, i);
+  TORCH_CHECK(nb > 0, "kdpc: dense_tn_small: unsupported shape r=", r, " o=", o, " i=", i);
+  Tensor ws = workspace(nb, a);
+  Tensor out = empty_f({o, i}, a);
+  check(kdpc_dense_tn_small(r, o, i, F(a), F(b), F(out), ws.data_ptr(), nb, stream_of(a)),
+        "dense_tn_small");
+  return out;
+}
+
 TORCH_LIBRARY(kdpc, m) {
   // reference pointnet2_cuda surface (pointnet2_api.cpp:10-24), in-place, returns 1
   m.def("ball_query_wrapper(int b, int n, int m, float radius, int nsample, Tensor new_xyz, "
@@ -762,6 +778,7 @@ TORCH_LIBRARY(kdpc, m) {
         "bool warp) -> Tensor");
   m.def("idw_blend_bwd_coords(Tensor ref, Tensor qry, Tensor vals, Tensor idx, Tensor dout, "
         "bool warp) -> (Tensor, Tensor)");
+  m.def("dense_tn_small(Tensor a, Tensor b) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(kdpc, CUDA, m) {
@@ -810,4 +827,5 @@ TORCH_LIBRARY_IMPL(kdpc, CUDA, m) {
   m.impl("idw_blend_fwd", idw_blend_fwd);
   m.impl("idw_blend_bwd_vals", idw_blend_bwd_vals);
   m.impl("idw_blend_bwd_coords", idw_blend_bwd_coords);
+  m.impl("dense_tn_small", dense_tn_small);
 }

@@ -418,3 +418,20 @@ def test_colsum_matches_its_stated_order(nat, rows, cols):
     outs = [nat.colsum(xd) for _ in range(5)]
     for o in outs:
         np.testing.assert_array_equal(o.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("r,o,i", [(131072, 32, 3), (65536, 3, 64), (262144, 3, 128),
+                                   (5000, 4, 4), (2048, 1, 511), (4097, 3, 256)])
+def test_dense_tn_small_vs_float64(nat, r, o, i):
+    """Skinny weight gradient A^T B (csrc/dense_small.hip) vs float64 within the fp32
+    accumulation bound, bitwise repeatable, and what dense.splitk_tn returns for that shape."""
+    import dense
+    g = torch.Generator(device="cpu").manual_seed(r + o * 7 + i)
+    a = torch.randn(r, o, generator=g).to(DEV)
+    b = torch.randn(r, i, generator=g).to(DEV)
+    got = nat.dense_tn_small(a, b)
+    assert torch.equal(got, nat.dense_tn_small(a, b))
+    assert torch.equal(got, dense.splitk_tn(a, b))
+    want = a.double().t() @ b.double()
+    bound = 1e-6 * (a.double().abs().t() @ b.double().abs()) * max(1.0, float(np.log2(r)))
+    assert ((got.double() - want).abs() <= bound + 1e-6).all()
