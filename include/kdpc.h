@@ -379,12 +379,17 @@ int kdpc_idw_blend_bwd_coords(int b, int n, int s, int c, const float *ref, cons
 
 /* ---- skinny 1x1-layer weight gradients (dense_small.hip) ---------------------------- */
 
-/* out (O x I) = A^T B for row-major A (R x O), B (R x I), O*I <= 1024, O + I <= 512: slab
+/* out (O x I) = A^T B for row-major A (R x O), B (R x I), min(O,I) <= 4, O + I <= 512: slab
  * partials + fixed-order column sum (replaces the BLAS split-K GEMM of dense.splitk_tn for
  * the 3-channel layers).  workspace: kdpc_dense_tn_small_workspace_bytes (0 = unsupported). */
 size_t kdpc_dense_tn_small_workspace_bytes(int r, int o, int i);
 int kdpc_dense_tn_small(int r, int o, int i, const float *a, const float *b, float *out,
                         void *workspace, size_t workspace_bytes, void *stream);
+
+/* y (R x N) = x (R x K) m (K x N) [+ bias (N), may be NULL] for min(K, N) <= 4, K*N <= 4096:
+ * the skinny forward / input-gradient GEMMs of the same layers. */
+int kdpc_dense_small(int r, int k, int n, const float *x, const float *m, const float *bias,
+                     float *y, void *stream);
 
 /* ---- deterministic column sums (bias gradients, partial-slab reductions) -------------- */
 

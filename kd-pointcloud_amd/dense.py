@@ -87,6 +87,13 @@ def splitk_tn(a, b):
     return out
 
 
+def _skinny(x2, weight):
+    """A GEMM against a weight with a side <= 4 (xyz input layers, 3-channel flow heads) on a
+    large row count: BLAS runs those on 16-wide tiles; csrc/dense_small.hip is memory-bound."""
+    return (x2.is_cuda and x2.dtype == torch.float32 and min(weight.shape) <= 4 and
+            weight.numel() <= 4096 and x2.shape[0] >= 2048)
+
+
 class _Linear(Function):
     """y (..., out) = x (..., in) W^T + b.  The N-d output is allocated by the Function itself
     (the GEMM writes through a 2-D view of it), so it is not a view: callers apply in-place
@@ -99,7 +106,10 @@ class _Linear(Function):
         x2 = x.reshape(-1, x.shape[-1])
         y = torch.empty((*x.shape[:-1], weight.shape[0]), dtype=x.dtype, device=x.device)
         y2 = y.view(-1, weight.shape[0])
-        if bias is not None:
+        if _skinny(x2, weight):  # 3-channel layers: the HIP kernel writes through y2
+            import kdpc_native
+            kdpc_native.dense_small_out(x2, weight.t(), bias, y2)
+        elif bias is not None:
             torch.addmm(bias, x2, weight.t(), out=y2)
         else:
             torch.mm(x2, weight.t(), out=y2)
@@ -114,7 +124,11 @@ class _Linear(Function):
         g2 = g.reshape(-1, g.shape[-1])
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
-            gx = g2.mm(weight).view(ctx.xshape)
+            if _skinny(g2, weight):
+                import kdpc_native
+                gx = kdpc_native.dense_small(g2.contiguous(), weight).view(ctx.xshape)
+            else:
+                gx = g2.mm(weight).view(ctx.xshape)
         if ctx.needs_input_grad[1]:
             gw = splitk_tn(g2.contiguous(), x2)
         if ctx.has_bias and ctx.needs_input_grad[2]:

@@ -87,6 +87,7 @@ _SIGNATURES = {
     "kdpc_idw_blend_bwd_coords": [_c_int] * 4 + [_vp] * 7 + [_c_int, _vp],
     "kdpc_dense_tn_small_workspace_bytes": [_c_int] * 3,
     "kdpc_dense_tn_small": [_c_int] * 3 + [_vp] * 4 + [_c_size, _vp],
+    "kdpc_dense_small": [_c_int] * 3 + [_vp] * 5,
 }
 _RESTYPES = {"kdpc_build_id": ctypes.c_char_p, "kdpc_grad_workspace_bytes": _c_size,
              "kdpc_csr_workspace_bytes": _c_size, "kdpc_cost_volume_bwd_workspace_bytes": _c_size,
@@ -657,6 +658,22 @@ def dense_tn_small(a, b):
     I = b.shape[1]
     return _op("kdpc_dense_tn_small", "dense_tn_small", a.contiguous(), b.contiguous(),
                work=(4 * R * (O + I) + 4 * O * I, 2.0 * R * O * I))
+
+
+def dense_small(x2, m, bias=None):
+    """x2 (R,K) @ m (K,N) [+ bias] for min(K, N) <= 4 (see include/kdpc.h)."""
+    R, K = _gpu(x2, "x").shape
+    N = m.shape[1]
+    return _op("kdpc_dense_small", "dense_small", x2.contiguous(), m.contiguous(), bias,
+               work=(4 * (R * K + R * N + K * N), 2.0 * R * K * N))
+
+
+def dense_small_out(x2, m, bias, y2):
+    """dense_small into y2 (R,N), a contiguous view of a caller-owned output."""
+    R, K = _gpu(x2, "x").shape
+    N = m.shape[1]
+    _op("kdpc_dense_small", "dense_small_out", x2.contiguous(), m.contiguous(), bias, y2,
+        work=(4 * (R * K + R * N + K * N), 2.0 * R * K * N))
 
 
 def colsum(x2):

@@ -697,6 +697,44 @@ Tensor dense_tn_small(Tensor a, Tensor b) {
   return out;
 }
 
+Tensor dense_small(Tensor x, Tensor m, c10::optional<Tensor> bias) {
+  dev(x, kF, "x"), dev(m, kF, "m"), same_device(x, m, "m");
+  TORCH_CHECK(x.dim() == 2 && m.dim() == 2 && x.size(1) == m.size(0),
+              "kdpc: dense_small expects x (R,K), m (K,N)");
+  const int64_t r = x.size(0), k = x.size(1), n = m.size(1);
+  TORCH_CHECK(std::min(k, n) <= 4 && k * n <= 4096, "kdpc: dense_small: unsupported k=", k,
+              " n=", n);
+  const float* bp = nullptr;
+  if (bias.has_value()) {
+    dev(*bias, kF, "bias");
+    TORCH_CHECK(bias->numel() == n, "kdpc: dense_small: bias must have N entries");
+    bp = F(*bias);
+  }
+  GUARD(x);
+  Tensor y = empty_f({r, n}, x);
+  check(kdpc_dense_small(r, k, n, F(x), F(m), bp, F(y), stream_of(x)), "dense_small");
+  return y;
+}
+
+// the same into a caller tensor (a contiguous (R, N) view of an N-d output the caller owns)
+void dense_small_out(Tensor x, Tensor m, c10::optional<Tensor> bias, Tensor y) {
+  dev(x, kF, "x"), dev(m, kF, "m"), dev(y, kF, "y"), same_device(x, y, "y");
+  TORCH_CHECK(x.dim() == 2 && m.dim() == 2 && x.size(1) == m.size(0) && y.dim() == 2 &&
+                  y.size(0) == x.size(0) && y.size(1) == m.size(1) && y.is_contiguous(),
+              "kdpc: dense_small_out expects x (R,K), m (K,N), y (R,N) contiguous");
+  const int64_t r = x.size(0), k = x.size(1), n = m.size(1);
+  TORCH_CHECK(std::min(k, n) <= 4 && k * n <= 4096, "kdpc: dense_small: unsupported k=", k,
+              " n=", n);
+  const float* bp = nullptr;
+  if (bias.has_value()) {
+    dev(*bias, kF, "bias");
+    TORCH_CHECK(bias->numel() == n, "kdpc: dense_small: bias must have N entries");
+    bp = F(*bias);
+  }
+  GUARD(x);
+  check(kdpc_dense_small(r, k, n, F(x), F(m), bp, F(y), stream_of(x)), "dense_small");
+}
+
 TORCH_LIBRARY(kdpc, m) {
   // reference pointnet2_cuda surface (pointnet2_api.cpp:10-24), in-place, returns 1
   m.def("ball_query_wrapper(int b, int n, int m, float radius, int nsample, Tensor new_xyz, "
@@ -779,6 +817,8 @@ TORCH_LIBRARY(kdpc, m) {
   m.def("idw_blend_bwd_coords(Tensor ref, Tensor qry, Tensor vals, Tensor idx, Tensor dout, "
         "bool warp) -> (Tensor, Tensor)");
   m.def("dense_tn_small(Tensor a, Tensor b) -> Tensor");
+  m.def("dense_small(Tensor x, Tensor m, Tensor? bias) -> Tensor");
+  m.def("dense_small_out(Tensor x, Tensor m, Tensor? bias, Tensor(a!) y) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(kdpc, CUDA, m) {
@@ -828,4 +868,6 @@ TORCH_LIBRARY_IMPL(kdpc, CUDA, m) {
   m.impl("idw_blend_bwd_vals", idw_blend_bwd_vals);
   m.impl("idw_blend_bwd_coords", idw_blend_bwd_coords);
   m.impl("dense_tn_small", dense_tn_small);
+  m.impl("dense_small", dense_small);
+  m.impl("dense_small_out", dense_small_out);
 }

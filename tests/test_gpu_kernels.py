@@ -435,3 +435,22 @@ def test_dense_tn_small_vs_float64(nat, r, o, i):
     want = a.double().t() @ b.double()
     bound = 1e-6 * (a.double().abs().t() @ b.double().abs()) * max(1.0, float(np.log2(r)))
     assert ((got.double() - want).abs() <= bound + 1e-6).all()
+
+
+@pytest.mark.parametrize("r,k,n,bias", [(262144, 128, 3, True), (131072, 3, 32, True),
+                                        (65536, 256, 3, False), (4099, 5, 4, True),
+                                        (3000, 3, 130, False), (2048, 1023, 4, True)])
+def test_dense_small_vs_float64(nat, r, k, n, bias):
+    """Skinny GEMM x @ m [+ bias] with min(K, N) <= 4 (csrc/dense_small.hip) vs float64, and
+    the Linear layer routed through it equals the same kernel's result."""
+    import dense
+    g = torch.Generator(device="cpu").manual_seed(r + k * 5 + n)
+    x = torch.randn(r, k, generator=g).to(DEV)
+    m = torch.randn(k, n, generator=g).to(DEV)
+    b = torch.randn(n, generator=g).to(DEV) if bias else None
+    got = nat.dense_small(x, m, b)
+    want = x.double() @ m.double() + (b.double() if bias else 0)
+    bound = 1e-6 * (x.double().abs() @ m.double().abs()) * max(1.0, float(np.log2(k))) + 1e-6
+    assert ((got.double() - want).abs() <= bound).all()
+    y = dense.linear(x, m.t().contiguous(), b)
+    assert torch.equal(y, got)

@@ -136,7 +136,8 @@ TORCH_OPS = {
     "batchnorm_lrelu_bwd": "kdpc_batchnorm_lrelu_bwd", "colsum": "kdpc_colsum",
     "idw_blend_fwd": "kdpc_idw_blend_fwd", "idw_blend_bwd_vals": "kdpc_idw_blend_bwd_vals",
     "idw_blend_bwd_coords": "kdpc_idw_blend_bwd_coords",
-    "dense_tn_small": "kdpc_dense_tn_small",
+    "dense_tn_small": "kdpc_dense_tn_small", "dense_small": "kdpc_dense_small",
+    "dense_small_out": "kdpc_dense_small",
 }
 
 
