@@ -693,7 +693,14 @@ SeedWs seed_ws(int b, int n, int s, void* base) {
 #ifndef KNN_QW
 #define KNN_QW 4
 #endif
-inline bool use_seed(int b, int n, int s) { return n >= 2048 && (long long)b * s >= 8192; }
+// smallest reference set the culled scan is used for (round 2, whole-step A/B: 1024 beats
+// 2048 by 0.5 %, 512 loses -- below that the sort / box setup launches outweigh the culling)
+#ifndef KDPC_KNN_CULL_MIN_N
+#define KDPC_KNN_CULL_MIN_N 1024
+#endif
+inline bool use_seed(int b, int n, int s) {
+  return n >= KDPC_KNN_CULL_MIN_N && (long long)b * s >= 8192;
+}
 
 void launch_knn(int b, int n, int s, int k, const float* xyz, const float* new_xyz, int* idx,
                 float* dist, hipStream_t st) {

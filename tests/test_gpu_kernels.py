@@ -125,7 +125,8 @@ def _knn_both(nat, k, ref, qry):
     return [t.cpu().numpy() for t in a + b]
 
 
-@pytest.mark.parametrize("b,n,s,k", [(2, 4096, 4100, 32), (3, 2048, 3000, 9)])
+@pytest.mark.parametrize("b,n,s,k", [(2, 4096, 4100, 32), (3, 2048, 3000, 9),
+                                     (16, 1024, 2048, 3), (8, 1500, 1100, 16)])
 def test_knn_seeded_scan_matches_oracle(nat, b, n, s, k):
     """The seeded-threshold scan (cell-sorted refs, per-query window radix select) against
     the oracle, at sizes that select it (kdpc_knn_workspace_bytes > 0), padded tails."""
