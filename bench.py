@@ -3,19 +3,26 @@
 
 One step = one training iteration of PointConvBidirection on B synthetic
 FlyingThings3D-shaped pairs per GPU (BASELINE.json configs[2]: B=8, N=8192): forward,
-multiScaleLoss, backward, Adam step (`--mode kd` adds the frozen teacher forward and the
-biDirection_loss_ht KD objective of configs[3]).  With N GPUs: one process per GPU, DDP over
-RCCL, per-GPU batch fixed (weak scaling), no data-path collective beyond DDP's gradient
-all-reduce.
+multiScaleLoss, backward, Adam step.  With N GPUs: one process per GPU, per-GPU batch fixed
+(weak scaling); the only collective is the gradient all-reduce (bucketed, overlapped with
+the backward: distill.GraphedStep).
 
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
-Rank 0 prints ONE JSON line.  `roofline` is measured live over the timed region: every
-launch of the chosen kernel is bracketed by HIP events on its stream, and its algorithmic
-bytes (or flops) per launch are summed by the op wrapper.  `cpu_baseline` is the oracle's
-pure-PyTorch CPU restatement of the reference path (square_distance+topk kNN,
-torch.gather indexing, FPS replaced by a random subsample) on a bounded sample, rank 0 only.
+Rank 0 prints ONE JSON line.  Besides the headline (configs[2]) it carries sub-records:
+  kd_step         configs[3]'s per-GPU slice: the KD step (teacher fwd + student fwd/bwd +
+                  biDirection_loss_ht + Adam) at B=4 per GPU, its own timed region, roofline
+                  and CPU baseline (every N: at N=8 it is configs[3]'s B=32 over 8 GPUs);
+  configs1        configs[1] microbench (N=1): FPS, ball_query, grouping_operation, gather;
+  roofline_knn    configs[4] (N=1): culled kNN K=32 at N=65536, B=4;
+  step_roofline   the whole step against the model's algorithmic flops / bytes.
+`roofline` objects are measured live: HIP events on the launch stream around the timed
+launches, algorithmic bytes (or flops) per launch from SURVEY §8d.  `traffic` is the PMC
+HBM bytes per launch from profiles/pmc_traffic.json for the SAME (workload, entry) only,
+else null.  `cpu_baseline` is the oracle's pure-PyTorch CPU restatement of the reference
+path (square_distance+topk kNN, torch.gather indexing, FPS replaced by a random subsample)
+on a bounded sample, rank 0 at N=1 only.
 """
 import argparse
 import json
@@ -27,13 +34,12 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "kd-pointcloud_amd"))
 
-import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK_TF = 157.3  # dense f32 MFMA peak (MI355X_MICROARCH.md, F32 row)
-FP32_VALU_PEAK_TF = 157.3
+FP32_VALU_PEAK_TF = 157.3  # f32 vector peak (same table)
 
 # C entry point -> (bound, unit, peak, HIP kernels it launches).  An entry point is the unit
 # the live timer brackets; tools/roofline_check.py sums the listed kernels' rocprofv3
@@ -41,58 +47,120 @@ FP32_VALU_PEAK_TF = 157.3
 ROOFLINE = {
     "kdpc_pointconv_bwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF,
                            # first name: one launch per entry call (tools count launches by it)
-                           ["pc_csr_sum_kernel", "pc_bwd_data_kernel", "pc_bwd_data_pipe_kernel",
-                            "pc_bwd_weight_kernel", "pc_slab_sum_kernel", "pc_swizzle_bwd_kernel"]),
+                           ["pc_swizzle_bwd_kernel", "pc_bwd_data_kernel",
+                            "pc_bwd_data_pipe_kernel", "pc_csr_sum_kernel",
+                            "pc_bwd_weight_kernel", "pc_slab_sum_kernel"]),
     "kdpc_pointconv_fwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF,
                            ["pc_fwd_kernel", "pc_slab_sum_kernel"]),
     "kdpc_group_rows": ("hbm", "GB/s", HBM_PEAK_GBS, ["group_rows_kernel"]),
     "kdpc_group_points": ("hbm", "GB/s", HBM_PEAK_GBS, ["group_points_lds_kernel",
                                                          "group_points_kernel"]),
-    "kdpc_knn_point": ("valu", "TFLOP/s", FP32_VALU_PEAK_TF, ["knn_kernel"]),
+    # kNN: plain scan (knn_kernel) or the culled scan (ref_sort / query_sort / chunk boxes /
+    # knn_cull); work = brute-force-equivalent distance evaluations (8 flops each), bytes =
+    # B*(12Nq + 12Nr + 4*Nq*K)
+    "kdpc_knn_point": ("hbm", "GB/s", HBM_PEAK_GBS,
+                       ["ref_sort_kernel", "query_sort_kernel", "chunk_box_kernel",
+                        "knn_cull_kernel", "knn_kernel"]),
+    "kdpc_gather_points": ("hbm", "GB/s", HBM_PEAK_GBS, ["gather_points_kernel"]),
     "kdpc_cost_volume_fwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF, ["cost_volume_fwd_kernel"]),
     "kdpc_cost_volume_bwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF, ["cost_volume_bwd_kernel"]),
     "kdpc_idw_blend_fwd": ("hbm", "GB/s", HBM_PEAK_GBS, ["idw_fwd_kernel"]),
 }
-# the step's dominant entry point (rocprofv3 step profile, profiles/); the gather-bound
-# grouping_operation the north star names is measured by gather_roofline()
+# the step's dominant entry point (rocprofv3 step profile, profiles/)
 PRIMARY_KERNEL = "kdpc_pointconv_bwd"
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+# per-pair algorithmic work of the whole model step: fwd+bwd dense flops and
+# grouping traffic
+STEP_FLOPS_PER_PAIR = 78.8e9
+STEP_BYTES_PER_PAIR = 894e6
 
 
-def parse():
+def workload_key(mode, batch, npoints):
+    """The PMC workload key of a step section (profiles/pmc_traffic.json `workloads`)."""
+    return f"{mode}_b{batch}_n{npoints}"
+
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=8, help="pairs per GPU")
+    ap.add_argument("--batch", type=int, default=8, help="pairs per GPU (train step)")
+    ap.add_argument("--kd-batch", type=int, default=4,
+                    help="pairs per GPU of the KD step (configs[3]: 32 over 8 GPUs)")
     ap.add_argument("--npoints", type=int, default=8192)
-    ap.add_argument("--mode", choices=["train", "kd"], default="train")
+    ap.add_argument("--mode", choices=["train", "kd"], default="train",
+                    help="the headline step (kd: the KD step at --batch is the headline)")
+    ap.add_argument("--sections", default="train,kd,configs1,knn",
+                    help="comma list of train, kd, configs1, knn (PMC passes run one each)")
     ap.add_argument("--roofline-kernel", default=PRIMARY_KERNEL)
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true",
                     help="issue the step eagerly from Python (DDP for N>1) instead of replaying "
-                         "it from HIP graphs (distill.GraphedStep, the default since round 2: "
-                         "the eager step needs ~21 ms of host time per step, as much as the "
-                         "GPU, and the graph replay carries the next batch's FPS chain on a "
-                         "forked stream like the eager FpsPrefetch)")
+                         "it from HIP graphs (distill.GraphedStep, the default: the eager step "
+                         "needs about as much host time as the GPU needs)")
     ap.add_argument("--graph", action="store_true", help="(default; kept for old command lines)")
     ap.add_argument("--measure-steps", type=int, default=2,
                     help="eager steps after the timed region for the per-kernel roofline")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-def cpu_baseline(args):
-    """Oracle CPU path on a bounded sample: B=1 pair, N=npoints, fwd+bwd+Adam (--mode kd:
+def _events(stream):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    return e0, e1
+
+
+# ------------------------------------------------------------------ PMC / roofline helpers
+def pmc_traffic(workload, entry):
+    """HBM bytes per launch of `entry` measured by the committed rocprofv3 --pmc passes on the
+    SAME workload (tools/pmc_traffic.py; FETCH_SIZE and WRITE_SIZE in separate passes,
+    FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM), or None when that (workload, entry)
+    was not measured."""
+    try:
+        with open(PMC_FILE) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    e = d.get("workloads", {}).get(workload, {}).get("entries", {}).get(entry)
+    return None if e is None else e.get("hbm_bytes_per_launch")
+
+
+def roofline_obj(entry, workload, ms, launches, nbytes, flops, bound=None, **extra):
+    """A roofline object from summed live launch times and summed algorithmic work."""
+    if ms <= 0 or launches <= 0:
+        return None
+    b0, unit, peak, kernels = ROOFLINE.get(entry, ("hbm", "GB/s", HBM_PEAK_GBS, []))
+    bound = bound or b0
+    if bound == "hbm":
+        unit, peak = "GB/s", HBM_PEAK_GBS
+        achieved = nbytes / (ms * 1e-3) / 1e9
+    else:
+        achieved = flops / (ms * 1e-3) / 1e12
+    out = {"bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
+           "frac": round(achieved / peak, 4), "traffic": pmc_traffic(workload, entry),
+           "kernel": entry, "hip_kernels": kernels, "workload": workload,
+           "launches": launches, "avg_launch_us": round(ms / launches * 1e3, 2),
+           "algorithmic_bytes_per_launch": round(nbytes / launches),
+           "algorithmic_flops_per_launch": round(flops / launches),
+           "traffic_source": os.path.relpath(PMC_FILE, ROOT)}
+    out.update(extra)
+    return out
+
+
+# ------------------------------------------------------------------------- CPU baseline
+def cpu_baseline(args, mode):
+    """Oracle CPU path on a bounded sample: B=1 pair, N=npoints, fwd+bwd+Adam (mode kd:
     frozen teacher fwd + student fwd+bwd + biDirection_loss_ht + Adam)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import torch_model as M
     import synthetic
+    import torch_model as M
     torch.manual_seed(0)
     M.FPS_MODE["mode"] = "random"
     M.FPS_MODE["generator"] = torch.Generator().manual_seed(0)
     model = M.PointConvBidirection().train()
-    teacher = M.PointConvBidirection().eval() if args.mode == "kd" else None
+    teacher = M.PointConvBidirection().eval() if mode == "kd" else None
     opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-4)
     p1, p2, fl = (torch.from_numpy(a) for a in synthetic.ft3d_batch(1, args.npoints, seed=99))
 
@@ -116,93 +184,20 @@ def cpu_baseline(args):
         step()
         times.append(time.perf_counter() - t0)
     med = statistics.median(times)
+    what = ("KD step (teacher fwd + student fwd+bwd + biDirection_loss_ht + Adam)"
+            if teacher is not None else "fwd+multiScaleLoss+bwd+Adam")
     return {"value": round(1.0 / med, 4), "unit": "pairs/s", "cores": torch.get_num_threads(),
             "kind": "port",
-            "sample": f"1 pair x N={args.npoints}, "
-                      f"{'KD step (teacher fwd + ' if teacher is not None else ''}"
-                      f"fwd+bwd+Adam{')' if teacher is not None else ''}, median of {args.cpu_steps} "
-                      f"steps after 1 warm-up ({med:.2f} s/step); oracle/torch_model.py "
+            "sample": f"1 pair x N={args.npoints}, {what}, median of {args.cpu_steps} steps after "
+                      f"1 warm-up ({med:.2f} s/step); oracle/torch_model.py "
                       f"(square_distance+topk kNN, torch.gather, FPS->randperm); "
                       f"host os.cpu_count()={os.cpu_count()}"}
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc passes
-    (tools/pmc_traffic.py; FETCH_SIZE and WRITE_SIZE in separate passes, FETCH_SIZE doubled
-    per MI355X_MICROARCH.md §HBM), or None when that kernel was not measured."""
-    try:
-        with open(PMC_FILE) as f:
-            d = json.load(f)
-    except (OSError, ValueError):
-        return None
-    e = d.get("entries", {}).get(kernel)
-    return None if e is None else e.get("hbm_bytes_per_launch")
-
-
-def gather_roofline(dev, iters=20):
-    """The north star's gather target at BASELINE configs[1]: grouping_operation (reference
-    (B,C,N) layout) at B=8, C=64, N=8192, S=2048, K=16 on FPS centres + ball_query(r=0.5)
-    indices, timed with HIP events over `iters` back-to-back launches on the launch stream
-    (single ~15 us launches cannot be bracketed individually: the event packets cost as
-    much as the kernel).  Algorithmic bytes B*(4CN + 4SK + 4CSK)."""
-    import kdpc_native as K
-    import synthetic
-    B, C, N, S, Kn = 8, 64, 8192, 2048, 16
-    xyz = torch.from_numpy(synthetic.ft3d_batch(B, N, seed=7)[0]).to(dev)
-    centres = K.group_rows(xyz, K.furthest_point_sampling(xyz, S))
-    idx = K.ball_query(0.5, Kn, xyz, centres)
-    feats = torch.randn(B, C, N, device=dev)
-    for _ in range(3):
-        K.group_points(feats, idx)
-    stream = torch.cuda.current_stream(dev)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for _ in range(iters):
-        K.group_points(feats, idx)
-    e1.record(stream)
-    e1.synchronize()
-    us = e0.elapsed_time(e1) * 1e3 / iters
-    nbytes = B * (4 * C * N + 4 * S * Kn + 4 * C * S * Kn)
-    achieved = nbytes / (us * 1e-6) / 1e9
-    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic("kdpc_group_points"),
-            "kernel": "kdpc_group_points", "hip_kernels": ROOFLINE["kdpc_group_points"][3],
-            "workload": "grouping_operation B=8 C=64 N=8192 S=2048 K=16 (configs[1]), "
-                        f"{iters} back-to-back launches",
-            "avg_launch_us": round(us, 2), "algorithmic_bytes_per_launch": nbytes}
-
-
-def roofline(kernel, summ):
-    """Live roofline of one C entry point from the HIP-event launch timer."""
-    if not summ or summ["ms"] <= 0:
-        return None
-    bound, unit, peak, kernels = ROOFLINE.get(kernel, ("hbm", "GB/s", HBM_PEAK_GBS, []))
-    per_launch_ms = summ["ms"] / summ["launches"]
-    if unit == "GB/s":
-        achieved = summ["bytes"] / (summ["ms"] * 1e-3) / 1e9
-    else:
-        achieved = summ["flops"] / (summ["ms"] * 1e-3) / 1e12
-    return {"bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
-            "frac": round(achieved / peak, 4), "traffic": pmc_traffic(kernel),
-            "kernel": kernel, "hip_kernels": kernels, "launches": summ["launches"],
-            "avg_launch_us": round(per_launch_ms * 1e3, 2),
-            "algorithmic_bytes_per_launch": round(summ["bytes"] / summ["launches"]),
-            "algorithmic_flops_per_launch": round(summ["flops"] / summ["launches"]),
-            "traffic_source": os.path.relpath(PMC_FILE, ROOT) if os.path.exists(PMC_FILE) else None}
-
-
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-    if os.environ.get("KDPC_BLAS"):
-        torch.backends.cuda.preferred_blas_library(os.environ["KDPC_BLAS"])
-
+# --------------------------------------------------------------------------- step section
+def step_section(args, mode, batch, dev, world, rank):
+    """Build the (graphed) train or KD step at `batch` pairs per GPU, time args.steps of it,
+    then the live per-kernel roofline of args.roofline_kernel over eager replays."""
     import kdpc_native
     import synthetic
     from distill import (FlowTrainStep, KDTrainStep, graphed_flow_step, graphed_kd_step,
@@ -213,45 +208,39 @@ def main():
     nb = 4
     batches = []
     for i in range(nb):
-        p1, p2, fl = synthetic.ft3d_batch(args.batch, args.npoints, seed=1000 + rank,
-                                          first_pair=i * args.batch)
+        p1, p2, fl = synthetic.ft3d_batch(batch, args.npoints, seed=1000 + rank,
+                                          first_pair=i * batch)
         batches.append(tuple(torch.from_numpy(a).to(dev) for a in (p1, p2, fl)))
 
     torch.manual_seed(0)
     student = PointConvBidirection().to(dev)
     teacher = None
-    if args.mode == "kd":
+    if mode == "kd":
         torch.manual_seed(1)
         teacher = PointConvBidirection().to(dev)
     graph = not args.eager
+    step_kind = "hip-graph"
     if graph:
         if world > 1:  # replicas start identical (DDP does this broadcast at construction)
             for t in list(student.parameters()) + list(student.buffers()):
                 dist.broadcast(t.data, 0)
         opt = make_optimizer(student, capturable=True)
-        try:
-            if args.mode == "kd":
-                step = graphed_kd_step(teacher, student, opt, batches[0])
-            else:
-                step = graphed_flow_step(student, opt, batches[0])
-        except RuntimeError as exc:  # capture refused on this runtime: measure the eager step
-            if world == 1:
-                raise
-            print(f"rank {rank}: HIP-graph capture failed ({exc}); eager DDP step instead",
-                  file=sys.stderr, flush=True)
-            graph = False
-            torch.cuda.synchronize()
-    if graph:
-        eager = (KDTrainStep(teacher, student, opt) if args.mode == "kd"
+        if mode == "kd":
+            step = graphed_kd_step(teacher, student, opt, batches[0])
+        else:
+            step = graphed_flow_step(student, opt, batches[0])
+        step_kind += step.schedule_name()
+        eager = (KDTrainStep(teacher, student, opt) if mode == "kd"
                  else FlowTrainStep(student, opt))
     else:
         model = wrap_ddp(student, dev)
         opt = make_optimizer(model)
-        step = KDTrainStep(teacher, model, opt) if args.mode == "kd" else FlowTrainStep(model, opt)
+        step = KDTrainStep(teacher, model, opt) if mode == "kd" else FlowTrainStep(model, opt)
         eager = step
+        step_kind = "eager" + (" ddp" if world > 1 else "")
 
-    # the eager steps issue the next batch's FPS chain on a side stream (distill.FpsPrefetch)
-    # (the graphed step does the same inside graph A, on a forked stream)
+    # the eager steps issue the next batch's FPS chain on a side stream (distill.FpsPrefetch);
+    # the graphed step does the same inside its graph, on a forked stream
     nxt = lambda i: {"next_batch": batches[(i + 1) % nb]}  # noqa: E731
     for i in range(args.warmup):
         step(*batches[i % nb], **nxt(i))
@@ -270,8 +259,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
-    # host enqueue time of one eager step: the Python/torch.ops time to issue it, measured
-    # from an idle device (the step is GPU-bound while this stays below ms_per_step)
+    # host enqueue time of one eager step (Python / torch.ops issue time from an idle device)
     host = []
     for i in range(2):
         torch.cuda.synchronize()
@@ -279,43 +267,185 @@ def main():
         eager(*batches[i % nb])
         host.append(time.perf_counter() - h0)
         torch.cuda.synchronize()
-    host_ms = round(min(host) * 1e3, 3)
 
-    # per-kernel roofline: HIP events around every launch of the named C entry points, over
-    # eager replays of the same step after the timed region (a graph replay has no
-    # per-launch host hook); kernel durations do not depend on how the launch was issued
+    # per-kernel roofline: HIP events around every launch of the entry point, over eager
+    # replays of the same step after the timed region (a graph replay has no per-launch host
+    # hook); kernel durations do not depend on how the launch was issued
     timer = kdpc_native.LaunchTimer([args.roofline_kernel])
     kdpc_native.set_launch_timer(timer)
     for i in range(args.measure_steps):
         eager(*batches[i % nb])
     torch.cuda.synchronize()
     kdpc_native.set_launch_timer(None)
-    summary = timer.summary()
-    roof = roofline(args.roofline_kernel, summary.get(args.roofline_kernel))
-    roof_gather = gather_roofline(dev)
+    s = timer.summary().get(args.roofline_kernel)
+    wl = workload_key(mode, batch, args.npoints)
+    roof = None if not s else roofline_obj(args.roofline_kernel, wl, s["ms"], s["launches"],
+                                           s["bytes"], s["flops"])
+    pairs = world * batch * args.steps
+    ms = dt / args.steps * 1e3
+    res = {"value": round(pairs / dt, 3), "unit": "pairs/s", "ms_per_step": round(ms, 3),
+           "steps": args.steps, "warmup": args.warmup, "batch_per_gpu": batch,
+           "global_batch": world * batch, "step": step_kind,
+           "host_enqueue_ms": round(min(host) * 1e3, 3), "roofline": roof,
+           "step_roofline": {
+               "bound": "mfma", "unit": "TFLOP/s", "peak": FP32_MFMA_PEAK_TF,
+               "achieved": round(batch * STEP_FLOPS_PER_PAIR / (ms * 1e-3) / 1e12, 2),
+               "frac": round(batch * STEP_FLOPS_PER_PAIR / (ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TF, 4),
+               "hbm_frac": round(batch * STEP_BYTES_PER_PAIR / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+               "work_per_pair": "78.8 GFLOP dense fwd+bwd, 894 MB grouping traffic (SURVEY §8d)"
+                                + (" + the teacher fwd (26.25 GFLOP, not counted)"
+                                   if mode == "kd" else "")}}
+    del step, eager, opt, student, teacher, batches
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return res
 
-    pairs = world * args.batch * args.steps
-    line = {
-        "metric": "scene-flow pairs/sec fwd+bwd @ N=8192; EPE3D vs ref; 1/2/4/8 MI355X",
-        "value": round(pairs / dt, 3), "unit": "pairs/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-        "data": "synthetic FlyingThings3D-shaped pairs (kd-pointcloud_amd/synthetic.py), "
-                "random-init weights",
-        "config": {"workload": "PointConvBidirection fwd+bwd+Adam (BASELINE configs[2])"
-                   if args.mode == "train" else
-                   "KD step: teacher fwd + student fwd+bwd + biDirection_loss_ht (configs[3])",
-                   "model": "models_bid_pointconv.PointConvBidirection",
-                   "batch_per_gpu": args.batch, "global_batch": world * args.batch,
-                   "npoints": args.npoints, "parallelism": f"dp{world}",
-                   "step": "hip-graph" if graph else "eager"},
-        "host_enqueue_ms": host_ms,
-        "roofline": roof,
-        "roofline_gather": roof_gather,
+
+# ----------------------------------------------------------------------- microbenchmarks
+def _time_launches(fn, iters, stream):
+    for _ in range(3):
+        fn()
+    e0, e1 = _events(stream)
+    for _ in range(iters):
+        fn()
+    e1.record(stream)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / iters  # ms per launch
+
+
+def configs1_section(dev):
+    """BASELINE configs[1]: FPS + ball_query + grouping_operation (+ gather_operation) at
+    B=8, N=8192, S=2048, K=16, C=64; indices bit-exact (tests/test_gpu_kernels.py).  Each op
+    timed with HIP events on its launch stream over back-to-back launches (a single ~15 us
+    launch cannot be bracketed alone: the event packets cost as much as the kernel)."""
+    import kdpc_native as K
+    import synthetic
+    B, C, N, S, Kn = 8, 64, 8192, 2048, 16
+    stream = torch.cuda.current_stream(dev)
+    xyz = torch.from_numpy(synthetic.ft3d_batch(B, N, seed=7)[0]).to(dev)
+    fps_ms = _time_launches(lambda: K.furthest_point_sampling(xyz, S), 5, stream)
+    fidx = K.furthest_point_sampling(xyz, S)
+    centres = K.group_rows(xyz, fidx)
+    bq_ms = _time_launches(lambda: K.ball_query(0.5, Kn, xyz, centres), 20, stream)
+    idx = K.ball_query(0.5, Kn, xyz, centres)
+    feats = torch.randn(B, C, N, device=dev)
+    wl = "configs1_b8_n8192_s2048_k16_c64"
+    g_ms = _time_launches(lambda: K.group_points(feats, idx), 20, stream)
+    g_bytes = B * (4 * C * N + 4 * S * Kn + 4 * C * S * Kn)
+    # gather_operation: the model gathers xyz (C=3, index_points_gather); C=64 as well
+    xyz_cn = xyz.permute(0, 2, 1).contiguous()
+    ga3_ms = _time_launches(lambda: K.gather_points(xyz_cn, fidx), 50, stream)
+    ga64_ms = _time_launches(lambda: K.gather_points(feats, fidx), 50, stream)
+    ga_bytes = lambda c: B * (4 * c * N + 4 * S + 4 * c * S)  # noqa: E731 (SURVEY §8d)
+    return {
+        "workload": "B=8 N=8192: FPS 8192->2048, ball_query r=0.5 K=16, grouping C=64 S=2048 "
+                    "K=16, gather C=3 (the model's xyz) and C=64 (BASELINE configs[1])",
+        "fps": {"us_per_call": round(fps_ms * 1e3, 2),
+                "us_per_dependent_step": round(fps_ms * 1e3 / (S - 1), 4),
+                "distance_updates_per_s": round(B * N * S / (fps_ms * 1e-3), 1),
+                "bound": "latency (S-1 dependent block-wide argmax steps per cloud)"},
+        "ball_query": {"us_per_call": round(bq_ms * 1e3, 2), "queries": B * S,
+                       "bound": "latency (per-query serial scan with early exit)"},
+        "grouping_operation": roofline_obj("kdpc_group_points", wl, g_ms, 1, g_bytes, 0),
+        "gather_operation_c3": roofline_obj("kdpc_gather_points", wl, ga3_ms, 1, ga_bytes(3), 0,
+                                            bound="hbm", note="1.0 MB per launch: "
+                                                              "launch-latency-bound"),
+        "gather_operation_c64": roofline_obj("kdpc_gather_points", wl, ga64_ms, 1, ga_bytes(64),
+                                             0, bound="hbm"),
     }
+
+
+def knn_section(dev):
+    """BASELINE configs[4]: kNN K=32 at N=65536 per frame, B=4 (queries pc1, refs pc2), the
+    culled scan (ref/query Morton sorts + chunk boxes + knn_cull), plus the grouping of C=32
+    features by its indices."""
+    import kdpc_native as K
+    import synthetic
+    B, N, Kn, C = 4, 65536, 32, 32
+    stream = torch.cuda.current_stream(dev)
+    p1, p2, _ = (torch.from_numpy(a).to(dev) for a in synthetic.ft3d_batch(B, N, seed=11))
+    ms = _time_launches(lambda: K.knn_point(Kn, p2, p1), 5, stream)
+    idx = K.knn_point(Kn, p2, p1)
+    nbytes = B * (12 * N + 12 * N + 4 * N * Kn)
+    evals = float(B) * N * N
+    wl = "knn_b4_n65536_k32"
+    roof = roofline_obj("kdpc_knn_point", wl, ms, 1, nbytes, 8.0 * evals, bound="hbm",
+                        brute_force_equiv_evals_per_launch=evals,
+                        valu_equiv={"achieved_tflops": round(8.0 * evals / (ms * 1e-3) / 1e12, 2),
+                                    "peak": FP32_VALU_PEAK_TF,
+                                    "frac": round(8.0 * evals / (ms * 1e-3) / 1e12
+                                                  / FP32_VALU_PEAK_TF, 4),
+                                    "note": "brute-force-equivalent: the culled scan visits a "
+                                            "sub-linear fraction of the refs"})
+    feats = torch.randn(B, C, N, device=dev)
+    g_ms = _time_launches(lambda: K.group_points(feats, idx), 10, stream)
+    g_bytes = B * (4 * C * N + 4 * N * Kn + 4 * C * N * Kn)
+    roof["grouping_c32"] = roofline_obj("kdpc_group_points", wl, g_ms, 1, g_bytes, 0)
+    return roof
+
+
+# -------------------------------------------------------------------------------- main
+def main(argv=None):
+    args = parse(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if os.environ.get("KDPC_BLAS"):
+        torch.backends.cuda.preferred_blas_library(os.environ["KDPC_BLAS"])
+    sections = set(args.sections.split(","))
+    head_mode = args.mode
+    head_batch = args.batch
+    line = {}
+    head = None
+    if head_mode in sections:
+        head = step_section(args, head_mode, head_batch, dev, world, rank)
+    sub_kd = None
+    if head_mode == "train" and "kd" in sections:
+        sub_kd = step_section(args, "kd", args.kd_batch, dev, world, rank)
+    cfg1 = configs1_section(dev) if world == 1 and "configs1" in sections else None
+    knn = knn_section(dev) if world == 1 and "knn" in sections else None
+
+    if head is not None:
+        line = {
+            "metric": "scene-flow pairs/sec fwd+bwd @ N=8192; EPE3D vs ref; 1/2/4/8 MI355X",
+            "value": head["value"], "unit": "pairs/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": head["ms_per_step"], "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic FlyingThings3D-shaped pairs (kd-pointcloud_amd/synthetic.py), "
+                    "random-init weights",
+            "config": {"workload": "PointConvBidirection fwd+bwd+Adam (BASELINE configs[2])"
+                       if head_mode == "train" else
+                       "KD step: teacher fwd + student fwd+bwd + biDirection_loss_ht "
+                       "(configs[3])",
+                       "model": "models_bid_pointconv.PointConvBidirection",
+                       "batch_per_gpu": head_batch, "global_batch": world * head_batch,
+                       "npoints": args.npoints, "parallelism": f"dp{world}",
+                       "step": head["step"]},
+            "host_enqueue_ms": head["host_enqueue_ms"],
+            "roofline": head["roofline"],
+            "step_roofline": head["step_roofline"],
+        }
+    if sub_kd is not None:
+        sub_kd["workload"] = ("KD step: teacher fwd (eval, no_grad) + student fwd+bwd + "
+                              "biDirection_loss_ht(gamma=0.3, beta=0.8, layer=3) + Adam "
+                              f"(BASELINE configs[3]: B={args.kd_batch}/GPU, global "
+                              f"{world * args.kd_batch})")
+        line["kd_step"] = sub_kd
+    if cfg1 is not None:
+        line["configs1"] = cfg1
+        line["roofline_gather"] = cfg1["grouping_operation"]  # the north star's gather target
+    if knn is not None:
+        line["roofline_knn"] = knn
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args)
+        if head is not None:
+            line["cpu_baseline"] = cpu_baseline(args, head_mode)
+        if sub_kd is not None:
+            sub_kd["cpu_baseline"] = cpu_baseline(args, "kd")
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -129,7 +129,25 @@ def build_torch_ops(verbose=True):
     return TORCH_OPS_LIB
 
 
+def _lib_current(sid):
+    """The shipped library was linked from exactly these sources (its kdpc_build_id string is
+    embedded in the binary): nothing to compile.  The GPU box receives lib/ with the tree (the
+    driver runs the GPU tests there without building) but not build/, so without this check a
+    build() there would recompile every object only to find the link up to date."""
+    try:
+        with open(LIB, "rb") as f:
+            return sid.encode() in f.read()
+    except OSError:
+        return False
+
+
 def build(verbose=True):
+    sid = source_id()
+    if _lib_current(sid):
+        if verbose:
+            print(f"{LIB} is current (sources {sid[:12]})")
+        build_torch_ops(verbose)
+        return LIB
     os.makedirs(OBJ, exist_ok=True)
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
@@ -138,7 +156,6 @@ def build(verbose=True):
         with open(p, "rb") as f:
             hd.update(f.read())
     tool = _hipcc_version()
-    sid = source_id()
     with concurrent.futures.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
         objs = list(ex.map(lambda s: _compile(s, hd.hexdigest(), tool), srcs))
     # the build id: a one-function host object naming the sources' hash

@@ -36,34 +36,6 @@
 
 using namespace kdpc;
 
-// diagnostic builds only (tools/build_variants.sh): 0 = the real kernel; weight-gradient
-// kernel with 2 no build, 3 no loads in the loop, 4 no staging, 5 MFMAs only,
-// 6 / 7 / 8 no WeightNet-weight / dy / gathered-feature loads
-#ifndef KDPC_DAT_MODE  // diagnostic variants of the data kernel (0 = the real kernel)
-#define KDPC_DAT_MODE 0
-#endif
-#ifndef KDPC_DEFER_DG  // data kernel: a chunk's dG stores issued after the next chunk's MFMAs
-#define KDPC_DEFER_DG 1
-#endif
-#ifndef KDPC_PIPE_PF  // pipelined data kernel: B blocks issued ahead of their MFMAs
-#define KDPC_PIPE_PF 8
-#endif
-#ifndef KDPC_DG_CHUNK_MAJOR  // dG rows stored chunk-major: [chunk][pair][8] (else [pair][C8])
-#define KDPC_DG_CHUNK_MAJOR 0
-#endif
-#ifndef KDPC_AGPR  // 1: MFMA accumulators in the AccVGPR file (see agpr_form())
-#define KDPC_AGPR 0
-#endif
-#ifndef KDPC_WGT_NT  // weight-gradient kernel threads (512: 2 waves per SIMD; 256: 1)
-#define KDPC_WGT_NT 512
-#endif
-#ifndef KDPC_WGT_SCHED  // weight kernel: explicit MFMA / VALU / LDS interleave (experiment)
-#define KDPC_WGT_SCHED 0
-#endif
-#ifndef KDPC_WGT_MODE
-#define KDPC_WGT_MODE 0
-#endif
-
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -95,20 +67,6 @@ __device__ __forceinline__ f32x16 mfma4(float4 a, float4 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, c, 0, 0, 0);
 }
 
-// An inline-asm operand in an AccVGPR tells the compiler the kernel may use AGPRs; it then
-// selects the AGPR form of the MFMAs (SrcC / vDst in the AccVGPR file) instead of the
-// all-VGPR form it picks for kernels without AGPR uses.  With the accumulators out of the
-// architectural VGPR file the MFMAs' 16-register C reads / D writes stop competing with the
-// VALU work of the same SIMD for its register ports (round-2 stamps: the co-resident wave's
-// VALU ran ~3x slower while MFMAs were in flight).  Measured (forward and weight kernels,
-// 128 VGPR + 65-93 AGPR instead of 190-199 VGPR): flow0 fwd 437 -> 449 us, bwd 1101 -> 1132 us
-// -- no gain, so the default stays the VGPR form (KDPC_AGPR=1 for A/B builds).
-__device__ __forceinline__ void agpr_form() {
-#if KDPC_AGPR
-  asm volatile("; kdpc: AGPR-form MFMAs" ::"a"(0));
-#endif
-}
-
 __device__ __forceinline__ f32x16 zero16() {
   f32x16 z;
 #pragma unroll
@@ -126,14 +84,12 @@ __device__ __forceinline__ int nbr_of(const Geo& g, int row, int kk) {
 // of a 64-bit address) and hardware bounds checks (an offset past the buffer reads 0).
 constexpr unsigned kOOB = 0x80000000u;  // byte offset that is always out of range
 
-// float offset of pair pos's 8 dG values of chunk ch in the dG buffer.  Pair-major (the
-// default): each pair's 32 bytes of a chunk sit C8*4 bytes apart (partial-line stores: the
-// data kernel's dG stores cost 137 of its 575 us at flow0, round 2) and pc_csr_sum reads a
-// pair's whole row contiguously.  Chunk-major (KDPC_DG_CHUNK_MAJOR=1): a wave's 64 pairs
-// store one contiguous 2 KiB run per chunk -- measured: data kernel 576 -> 514 us but
-// pc_csr_sum 86 -> 173 us (32-byte gathers), a net loss, so pair-major stays.
-__device__ __forceinline__ long long dg_off(long long pos, int ch, long long rk, int c8) {
-  return KDPC_DG_CHUNK_MAJOR ? ((long long)ch * rk + pos) * kCC : pos * c8 + (long long)ch * kCC;
+// float offset of pair pos's 8 dG values of chunk ch in the dG buffer: pair-major, each
+// pair's 32 bytes of a chunk sit C8*4 bytes apart and pc_csr_sum reads a pair's whole row
+// contiguously (chunk-major rows -- full-line stores -- measured round 2: data kernel
+// 576 -> 514 us but pc_csr_sum 86 -> 173 us from its 32-byte gathers, a net loss).
+__device__ __forceinline__ long long dg_off(long long pos, int ch, long long /*rk*/, int c8) {
+  return pos * c8 + (long long)ch * kCC;
 }
 
 struct Srcs {
@@ -210,7 +166,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 void pc_fwd_kernel(Geo g, const float* __restrict__ wt, const float* __restrict__ wl,
                    const float* __restrict__ bias, float* __restrict__ y,
                    float* __restrict__ slab, int chunks_per_split) {
-  agpr_form();
   constexpr int MT = KM <= 9 ? 2 : 1;
   constexpr int TM = 32 * MT;
   constexpr int NT = O / 32;
@@ -412,44 +367,6 @@ __global__ __launch_bounds__(256) void pc_slab_sum_kernel(int nslabs, long long 
 // 28-row tiles, one pair per thread (934 vs 854 us, round 1); 320 threads, one pair each,
 // a fifth wave with no MFMA tile (931 us at 3 waves/SIMD with spills, 761 us at 2, vs 622):
 // the second pair pass of wave 0 is cheaper than the lost occupancy.
-#if KDPC_WGT_MODE == 9
-// diagnostic build only (tools/pc_stamps.py --weight): per-wave sums of the weight kernel's
-// tile phases (s_memtime deltas accumulated in scalar registers, stored once at the end)
-constexpr int kWStampWG = 4096, kWStampN = 8;
-__device__ unsigned long long g_pcw_stamps[kWStampWG * 8 * kWStampN];
-#define KDPC_WSTAMP(i)                                                                    \
-  do {                                                                                    \
-    __builtin_amdgcn_sched_barrier(0);                                                    \
-    unsigned long long _t;                                                                \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");            \
-    __builtin_amdgcn_sched_barrier(0);                                                    \
-    wsum[(i)] += _t - wprev;                                                              \
-    wprev = _t;                                                                           \
-  } while (0)
-#else
-#define KDPC_WSTAMP(i) \
-  do {                 \
-  } while (0)
-#endif
-#if KDPC_DAT_MODE == 9
-// diagnostic build only (tools/pc_stamps.py): per-wave s_memtime stamps of the data kernel's
-// chunk phases, kept in LDS and copied to a buffer of their own (no output reads them)
-constexpr int kStampWG = 4096, kStampN = 80;
-__device__ unsigned long long g_pc_stamps[kStampWG * 4 * kStampN];
-#define KDPC_STAMP(i)                                                                     \
-  do {                                                                                    \
-    __builtin_amdgcn_sched_barrier(0);                                                    \
-    unsigned long long _t;                                                                \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");            \
-    __builtin_amdgcn_sched_barrier(0);                                                    \
-    if (lane == 0) tsl[wv][(i)] = _t;                                                     \
-  } while (0)
-#else
-#define KDPC_STAMP(i) \
-  do {                \
-  } while (0)
-#endif
-
 template <int KM>
 constexpr int bwd_tile_rows() { return 32; }
 template <int KM>
@@ -482,10 +399,6 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
   const long long c16 = (long long)g.c * kW;
   const long long rk_total = (long long)g.r * g.k;
   const Srcs src = srcs_of(g);
-#if KDPC_DAT_MODE == 9
-  __shared__ unsigned long long tsl[4][kStampN];
-#endif
-  KDPC_STAMP(0);
 
   for (int e = t; e < 32 * O; e += NT) {
     const int r = e / O, o = e % O;
@@ -561,7 +474,7 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
   constexpr int NOG = O / 8;
   constexpr int PF = NOG < 4 ? NOG : 4;  // (16 ahead measured slower: 949 vs 854 us)
   auto brow = [&](int ch) {
-    return KDPC_DAT_MODE == 3 ? wsw + lane : wsw + (long long)((ch * 4 + n0 / 32) * NOG) * 64 + lane;
+    return wsw + (long long)((ch * 4 + n0 / 32) * NOG) * 64 + lane;
   };
   float4 bq[PF];
   float gv[PP][kCC], gn[PP][kCC];
@@ -578,12 +491,12 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
     for (int q = 0; q < PP; ++q) {
       const int nb = pn[q];
       const bool live = nb >= 0;
-      const unsigned fo = (live && KDPC_DAT_MODE != 4) ? (unsigned)nb * (unsigned)g.d * 4u : kOOB;
+      const unsigned fo = live ? (unsigned)nb * (unsigned)g.d * 4u : kOOB;
       const f32x4 lo = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                                      src.feats, (int)(fo + lo_ch), 0, 0));
       const f32x4 hi = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                                      src.feats, (int)(fo + hi_ch), 0, 0));
-      const unsigned xo = (c0 && live && KDPC_DAT_MODE != 4) ? (unsigned)nb * 12u : kOOB;
+      const unsigned xo = (c0 && live) ? (unsigned)nb * 12u : kOOB;
       const unsigned co = (c0 && live) ? (unsigned)(row0 + pr[q]) * 12u : kOOB;
       const f32x4 x = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                                     src.xyz, (int)xo, 0, 0));
@@ -611,7 +524,6 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
   // for them; held here meanwhile
   float svh[PP][kCC], xsh = 0.f;
   auto store_dg = [&](int ch) {
-    if (KDPC_DAT_MODE == 5) return;
     const int c0 = ch * kCC;
 #pragma unroll
     for (int q = 0; q < PP; ++q) {
@@ -623,23 +535,19 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
     }
     if (XI && xn >= 0) dgr[dg_off(xpos, ch, rk_total, g.c8) + xc] = xsh;
   };
-  KDPC_STAMP(1);
   for (int ch = ch0; ch < ch1; ++ch) {
     const int c0 = ch * kCC;
-    const int si = 2 + 4 * min(ch - ch0, 18);
-    KDPC_STAMP(si);
     const float4* wrow = brow(ch);
     f32x16 acc = zero16();
     if (mw) {  // wave-uniform
 #pragma unroll
       for (int og = 0; og < NOG; ++og) {
         const float4 av = *reinterpret_cast<const float4*>(dyl + (2 * og + half) * kBlk + l32 * 4);
-        if (KDPC_DAT_MODE != 1) acc = mfma4(av, bq[og % PF], acc);
-        else acc[og & 15] += av.x * bq[og % PF].y;
+        acc = mfma4(av, bq[og % PF], acc);
         if (og + PF < NOG) bq[og % PF] = wrow[(og + PF) * 64];
       }
     }
-    if (KDPC_DEFER_DG && ch > ch0) store_dg(ch - 1);
+    if (ch > ch0) store_dg(ch - 1);
     if (ch + 1 < ch1) {
       const float4* wr1 = brow(ch + 1);
 #pragma unroll
@@ -647,16 +555,14 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
       gather(ch + 1, gn);
       if constexpr (XI) xgn = gather_x(ch + 1);
     }
-    KDPC_STAMP(si + 1);
     if (mw) {
 #pragma unroll
       for (int e = 0; e < 16; ++e)
         dal[((e & 3) + 8 * (e >> 2) + 4 * half) * kDaS + n0 + l32] = acc[e];
     }
     __syncthreads();
-    KDPC_STAMP(si + 2);
 #pragma unroll
-    for (int q = 0; q < PP && KDPC_DAT_MODE != 2; ++q) {
+    for (int q = 0; q < PP; ++q) {
       if (pn[q] < 0) continue;
       const int r = pr[q];
       const long long pos = (long long)(row0 + r) * g.k + pk[q];
@@ -717,8 +623,6 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
       xsh = sacc;
       if (xn >= 0 && c0 == 0 && xc < 3) dcl[xp * 3 + xc] = sacc;
     }
-    if (!KDPC_DEFER_DG) store_dg(ch);
-    KDPC_STAMP(si + 3);
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < PP; ++q)
@@ -726,8 +630,7 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
       for (int c = 0; c < kCC; ++c) gv[q][c] = gn[q][c];
     xg = xgn;
   }
-  if (KDPC_DEFER_DG && ch0 < ch1) store_dg(ch1 - 1);
-  KDPC_STAMP(78);
+  if (ch0 < ch1) store_dg(ch1 - 1);
   if (ch0 == 0 && t < TR * 3) {
     const int r = t / 3, i = t - (t / 3) * 3;
     const int row = row0 + r;
@@ -764,14 +667,6 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
       if (xc == c) out = make_float2(xd[2 * c], xd[2 * c + 1]);
     if (xn >= 0) reinterpret_cast<float2*>(dwt_dst + xpos * kW)[xc] = out;
   }
-#if KDPC_DAT_MODE == 9
-  if (lane == 0) tsl[wv][79] = ((unsigned long long)__builtin_amdgcn_s_getreg(63508) << 32) |
-                               (unsigned)__builtin_amdgcn_s_getreg(63492);  // XCC_ID, HW_ID
-  const unsigned wg = blockIdx.y * gridDim.x + blockIdx.x;
-  if (wg < (unsigned)kStampWG) {
-    for (int i = lane; i < kStampN; i += 64) g_pc_stamps[((size_t)wg * 4 + wv) * kStampN + i] = tsl[wv][i];
-  }
-#endif
 }
 
 // Software-pipelined variant of the data kernel.  The kernel above runs each chunk as an
@@ -800,7 +695,7 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
   constexpr int NOG = O / 8;
   // B blocks in flight: the first PF of the next chunk are issued before its gathers, the
   // rest inside the step, PF steps ahead of their MFMAs (behind the gathers in vmcnt order)
-  constexpr int PF = NOG < KDPC_PIPE_PF ? NOG : KDPC_PIPE_PF;
+  constexpr int PF = NOG < 8 ? NOG : 8;
   constexpr int NIT = PP * kCC + (XI ? 1 : 0);  // VALU items per chunk per thread
   constexpr int STEPS = NOG > NIT ? NOG : NIT;
   __shared__ __attribute__((aligned(16))) float dyl[(O / 4) * kBlk];
@@ -1193,13 +1088,12 @@ template <int O, int KM>
 constexpr int wgt_tile_rows() { return O == 256 || (O == 128 && KM > 9) ? 32 : 64; }
 
 template <int O, int KM, bool EX>
-__global__ __launch_bounds__(KDPC_WGT_NT) __attribute__((amdgpu_waves_per_eu(KDPC_WGT_NT / 256)))
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
 void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __restrict__ dy,
                           float* __restrict__ dwl, int rows_per_split, int nsplit, int xcd_map) {
-  agpr_form();
   constexpr int TR = wgt_tile_rows<O, KM>();
   constexpr int TS = TR + 4;               // row stride of the transposed tiles
-  constexpr int NT = KDPC_WGT_NT;          // threads: 512 = 2 waves / SIMD, 256 = 1
+  constexpr int NT = 512;                  // threads: 2 waves per SIMD
   constexpr int RS = NT / 16;              // rows per build pass (16 threads per row)
   constexpr int RP = TR / RS;              // build passes (rows rb, rb + RS, ...)
   constexpr int MT = O / 32;
@@ -1294,7 +1188,7 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
 #pragma unroll
       for (int k = 0; k < KM; ++k) {
         const unsigned off = k < kk ? base + (unsigned)(k * kW * 4) : kOOB;
-        wr[p2][k] = KDPC_WGT_MODE == 6 ? 0.5f : __builtin_bit_cast(
+        wr[p2][k] = __builtin_bit_cast(
             float, __builtin_amdgcn_raw_buffer_load_b32(wt_rs, (int)off, 0, 0));
       }
     }
@@ -1314,7 +1208,7 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
       const unsigned voff = live ? (unsigned)nb * (unsigned)g.d * 4u + (unsigned)vch * 4u : kOOB;
       const unsigned xoff = (xyz && live) ? (unsigned)nb * 12u : kOOB;
       const unsigned coff = (xyz && live) ? (unsigned)rw * 12u : kOOB;
-      const f32x4 v = KDPC_WGT_MODE == 8 ? f32x4{(float)voff, 1.f, 2.f, 3.f} :
+      const f32x4 v =
           __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(src.feats, (int)voff, 0, 0));
       const f32x4 x = __builtin_bit_cast(
           f32x4, __builtin_amdgcn_raw_buffer_load_b128(src.xyz, (int)xoff, 0, 0));
@@ -1337,7 +1231,7 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
       const int q = t + NT * i;
       const int rw = row0 + q % TR;
       const unsigned off = rw < rend ? ((unsigned)rw * O + 4u * (unsigned)(q / TR)) * 4u : kOOB;
-      dr[i] = KDPC_WGT_MODE == 7 ? make_float4(1.f, 2.f, 3.f, (float)q) : __builtin_bit_cast(
+      dr[i] = __builtin_bit_cast(
           float4, __builtin_amdgcn_raw_buffer_load_b128(dy_rs, (int)off, 0, 0));
     }
   };
@@ -1379,10 +1273,6 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
 #pragma unroll
   for (int i = 0; i < MPW; ++i) acc[i] = zero16();
   if (ntiles <= 0) return;
-#if KDPC_WGT_MODE == 9
-  unsigned long long wsum[7] = {0, 0, 0, 0, 0, 0, 0}, wprev;
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(wprev)::"memory");
-#endif
   // prologue: tile 0 staged and built, tile 1 staged
   fetch_idx(0);
   fetch(0);
@@ -1393,17 +1283,15 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
   __syncthreads();
   stage(1);
   __syncthreads();
-  KDPC_WSTAMP(0);
   for (int tile = 0; tile < ntiles; ++tile) {
     const int cur = tile & 1;
     // tile+2's loads are issued first and land under this tile's MFMAs; tile's MFMAs || tile+1's
     // build (independent: at[cur] / dyt[cur] vs gl, wc -> at[!cur])
-    if (KDPC_WGT_MODE != 3 && KDPC_WGT_MODE != 5) fetch(tile + 2);
-    KDPC_WSTAMP(1);
+    fetch(tile + 2);
     const float* dt = dyt[cur];
     const float* ab = at[cur];
 #pragma unroll
-    for (int gb = 0; gb < TR / 8 && KDPC_WGT_MODE != 1; ++gb) {
+    for (int gb = 0; gb < TR / 8; ++gb) {
       const float4 bv = *reinterpret_cast<const float4*>(ab + (nt * 32 + l32) * TS + 8 * gb + 4 * half);
 #pragma unroll
       for (int i = 0; i < MPW; ++i) {
@@ -1412,35 +1300,11 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
         acc[i] = mfma4(av, bv, acc[i]);
       }
     }
-    KDPC_WSTAMP(2);
-    if (KDPC_WGT_MODE != 2 && KDPC_WGT_MODE != 5) build(cur ^ 1);
-#if KDPC_WGT_SCHED
-    // one wave per SIMD: interleave the tile's MFMAs with the build's VALU / LDS work and the
-    // fetch's loads (the scheduler otherwise clusters the MFMAs and the wave idles through
-    // them); per MFMA: two VALU, one LDS read, and a load slot
-#pragma unroll
-    for (int i = 0; i < MPW * (TR / 8) * 4; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-    }
-#endif
-    KDPC_WSTAMP(3);
+    build(cur ^ 1);
     __syncthreads();  // at[cur] / dyt[cur] / gl consumed; at[cur ^ 1] complete
-    KDPC_WSTAMP(4);
-    if (KDPC_WGT_MODE != 4 && KDPC_WGT_MODE != 5) stage(cur);  // tile + 2
-    KDPC_WSTAMP(5);
+    stage(cur);  // tile + 2
     __syncthreads();
-    KDPC_WSTAMP(6);
   }
-#if KDPC_WGT_MODE == 9
-  if (lane == 0 && L < kWStampWG) {
-    unsigned long long* o = g_pcw_stamps + ((size_t)L * 8 + wv) * kWStampN;
-    for (int i = 0; i < 7; ++i) o[i] = wsum[i];
-    o[7] = (unsigned long long)ntiles;
-  }
-#endif
   const long long col = (long long)c0 * kW + nt * 32 + l32;
   if (col >= c16) return;
   float* dst = dwl + (long long)split * O * c16;  // slab index when the rows are split
@@ -1597,10 +1461,10 @@ hipError_t bwd_launch(const Geo& g, const Plan& p, int b, const float* wt, const
                      0, st, npts, rk, g.c, p.c8, g.d, dgr, offsets, perm, dxyz, dfeats);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (g.k == KM)
-    hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM, true>), dim3(p.wgs), dim3(KDPC_WGT_NT), 0, st, g, wt,
+    hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM, true>), dim3(p.wgs), dim3(512), 0, st, g, wt,
                        dy, p.rs > 1 ? dwl_slab : dwl, p.rps, p.rs, p.xcd);
   else
-    hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM, false>), dim3(p.wgs), dim3(KDPC_WGT_NT), 0, st, g, wt,
+    hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM, false>), dim3(p.wgs), dim3(512), 0, st, g, wt,
                        dy, p.rs > 1 ? dwl_slab : dwl, p.rps, p.rs, p.xcd);
   if ((e = hipGetLastError()) != hipSuccess || p.rs == 1) return e;
   return slab_sum(p.rs, (long long)O * g.c * kW, dwl_slab, nullptr, 1, dwl, st);
@@ -1635,18 +1499,6 @@ Geo geo_of(int b, int n, int s, int k, int d, const Plan& p, const float* xyz, c
 
 }  // namespace
 
-#if KDPC_WGT_MODE == 9
-KDPC_API int kdpc_debug_pcw_stamps(void* dst, size_t bytes) {
-  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_pcw_stamps),
-                                  std::min(bytes, sizeof(g_pcw_stamps)), 0, hipMemcpyDeviceToHost);
-}
-#endif
-#if KDPC_DAT_MODE == 9
-KDPC_API int kdpc_debug_pc_stamps(void* dst, size_t bytes) {
-  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_pc_stamps),
-                                  std::min(bytes, sizeof(g_pc_stamps)), 0, hipMemcpyDeviceToHost);
-}
-#endif
 
 KDPC_API int kdpc_pointconv_supported(int k, int d, int o) {
   Plan p;

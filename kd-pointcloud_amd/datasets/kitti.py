@@ -2,9 +2,13 @@
 Reference: datasets/kitti.py:11-104.
 
 The scene filter is the reference's KITTI_mapping.txt (a scene is kept when its line is
-non-empty).  The file is KITTI metadata, not shipped here: it is looked up as
-`mapping_path`, else `<data_root>/KITTI_mapping.txt`, else next to this module; without it
-every scene is kept (and a warning says so)."""
+non-empty; 142 of 200).  It is looked up as `mapping_path`, else
+`<data_root>/KITTI_mapping.txt`, else the copy shipped next to this module (one line per
+scene, "x" where the reference's line is non-empty -- all the filter reads -- generated from
+the reference-produced fixture tests/golden/data_path_ref.npz `mapping_nonempty`).  Without
+any of them the dataset raises, as the reference does (its open() fails): metrics on all 200
+scenes are not comparable with the reference's.  `allow_unfiltered=True` is the explicit
+opt-out (every scene kept)."""
 import os.path as osp
 import warnings
 
@@ -19,12 +23,13 @@ class KITTI(SceneFlowDataset):
     SUBDIR = "kitti_processed"
 
     def __init__(self, train, transform, num_points, data_root, remove_ground=True,
-                 mapping_path=None):
+                 mapping_path=None, allow_unfiltered=False):
         self.root = osp.join(data_root, self.SUBDIR)
         self.train = train
         self.transform = transform
         self.num_points = num_points
         self.remove_ground = remove_ground
+        self.allow_unfiltered = allow_unfiltered
         self.mapping_path = mapping_path or next(
             (p for p in (osp.join(data_root, "KITTI_mapping.txt"),
                          osp.join(osp.dirname(osp.abspath(__file__)), "KITTI_mapping.txt"))
@@ -41,7 +46,12 @@ class KITTI(SceneFlowDataset):
         if len(paths) != 200:
             warnings.warn("KITTI: expected 200 scenes, found {}".format(len(paths)))
         if self.mapping_path is None:
-            warnings.warn("KITTI: no KITTI_mapping.txt found; keeping every scene")
+            if not self.allow_unfiltered:
+                raise FileNotFoundError(
+                    "KITTI: KITTI_mapping.txt not found (mapping_path, <data_root>/ or next to "
+                    "datasets/kitti.py); it selects the 142 evaluation scenes.  Pass "
+                    "allow_unfiltered=True to evaluate every scene instead.")
+            warnings.warn("KITTI: no KITTI_mapping.txt; keeping every scene (allow_unfiltered)")
             return paths
         with open(self.mapping_path) as fd:
             lines = [line.strip() for line in fd.readlines()]

@@ -19,7 +19,6 @@ multi-process path be tested on CPU with gloo.
 import torch
 import torch.distributed as dist
 
-import kdpc_native
 import loss_functions
 
 
@@ -44,6 +43,9 @@ def make_optimizer(model, lr=1e-3, weight_decay=1e-4, capturable=False):
     update (L2 weight decay, not AdamW) in one launch instead of ~10 foreach passes."""
     params = list(model.parameters())
     fused = len(params) > 0 and all(p.is_cuda for p in params)
+    if capturable and fused:
+        # a device tensor: a graph replay reads it, so LR changes reach the captured update
+        lr = torch.tensor(float(lr), device=params[0].device)
     return torch.optim.Adam(params, lr=lr, betas=(0.9, 0.999), eps=1e-08,
                             weight_decay=weight_decay, capturable=capturable,
                             fused=True if fused else None)
@@ -179,31 +181,47 @@ def epe3d(model, pos1, pos2, flow):
 
 class GraphedStep:
     """One training step replayed from HIP graphs (MI355X: the eager step issues ~2000
-    launches per iteration from Python, ~21 ms of host time, about as much as the GPU needs).
+    launches per iteration from Python, as much host time as the GPU needs).
 
-        graph A: [FPS of the NEXT batch on a forked stream] + forward + loss + backward
-                 (+ packing the gradients into one flat buffer)
-        eager:   one all_reduce of the flat gradient buffer (world > 1; RCCL over xGMI)
-        graph B: unpack the averaged gradients + optimizer step (Adam, capturable=True)
-    With one process there is no all-reduce and the optimizer step is captured at the end of
-    graph A (a single graph per step).
+    world 1:  graph A = [FPS of the NEXT batch on a forked stream] + forward + loss +
+              backward + gradient pack + flat Adam step: one graph launch per step.
+    world > 1 (one process per GPU, RCCL over xGMI):
+              graph A = [FPS fork] + forward + loss + backward; the gradients are packed,
+                        in the order the backward finalises them, into buckets of about
+                        `bucket_bytes`, and each bucket's pack ends in an EXTERNAL event
+                        record node (torch.cuda.Event(external=True));
+              host    : right after launching graph A, per bucket: the communication stream
+                        waits for that bucket's event, then an async all_reduce of it.  The
+                        GPU starts each bucket's all-reduce as soon as the backward has
+                        produced it, beside the rest of the backward (DDP's overlap, without
+                        DDP's per-step host work);
+              graph B = the main stream waits for every all-reduce, then grad / world +
+                        flat Adam step (+ hand the prefetched FPS to the next replay).
+    The averaged-gradient semantics are DDP's (and the reference DataParallel's): every
+    replica applies the same Adam update to the mean gradient.
 
-    The collective stays outside the graphs on purpose: it is one 31.8 MB all-reduce per
-    step, and keeping it eager avoids depending on collective capture.  `loss_fn(*inputs)`
-    must run the whole forward (model call(s) and loss) and return the loss; the inputs are
-    copied into static buffers before each replay.  Warm-up iterations run eagerly on a side
-    stream (they allocate lazily-initialised state: optimizer moments, cached attributes).
+    Optimizer: the trained parameters (and Adam's moments) become views of flat buffers laid
+    out in gradient-ready order, updated by ONE fused Adam over all 8 M values.  The caller's
+    optimizer keeps working on the same storage: its per-parameter `step` counters are
+    copied from the flat counter inside the graph (and the flat counter from them before
+    each update, so eager steps in between are honoured), and the learning rate is one
+    device tensor shared by both optimizers -- an LR scheduler (or a plain
+    `param_groups[0]['lr'] = x`, re-read before every replay) reaches the graph.
+
+    `loss_fn(*inputs)` must run the whole forward (model call(s) and loss) and return the
+    loss; the inputs are copied into static buffers before each replay.  Warm-up iterations
+    run eagerly on a side stream (they allocate lazily-initialised state: optimizer moments,
+    cached attributes).
 
     prefetch_fn (optional, e.g. PointConvBidirection.precompute_fps): a function of the first
     `n_prefetch` inputs whose result loss_fn takes as `fps=`.  Graph A then runs it for the
-    next batch on a forked stream, beside this batch's forward/backward (FpsPrefetch inside
-    the graph: FPS is ~2.4 ms of latency-bound work on 16 CUs), into buffers the next replay
-    reads.  A call whose batch is not the previous call's `next_batch` recomputes it eagerly
-    first, so results never depend on what was prefetched."""
+    next batch on a forked stream, beside this batch's forward/backward, into buffers the next
+    replay reads.  A call whose batch is not the previous call's `next_batch` recomputes it
+    eagerly first, so results never depend on what was prefetched."""
 
     drop_warmup_graph = True  # diagnostics seam (tools/graph_diag.py)
-    flat_adam = True  # seam: False keeps the caller's per-tensor optimizer step
     capture_on_side_stream = False
+    bucket_bytes = 8 << 20  # all-reduce bucket size (world > 1)
 
     def __init__(self, loss_fn, params, optimizer, example_inputs, warmup=3, prefetch_fn=None,
                  n_prefetch=2):
@@ -216,14 +234,20 @@ class GraphedStep:
         self.n_prefetch = n_prefetch
         self.static_next = [t.detach().clone() for t in example_inputs[:n_prefetch]]
         self._pending = None  # (tensors, versions) the buffered prefetch was computed for
+        self._check_optimizer()
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
+        order = []
         with torch.cuda.stream(side):
             loss = None
-            for _ in range(warmup):
+            for i in range(warmup):
                 self.opt.zero_grad(set_to_none=True)
                 loss = self.loss_fn(*self.static, **self._fps_kw(self._eager_prefetch()))
+                hooks = ([p.register_post_accumulate_grad_hook(order.append)
+                          for p in self.params] if i == warmup - 1 else [])
                 loss.backward()
+                for h in hooks:
+                    h.remove()
                 self._allreduce_eager()
                 self.opt.step()
             # drop the last warm-up graph: while it lives, the parameters' AccumulateGrad
@@ -235,8 +259,7 @@ class GraphedStep:
                 self.fps_cur = [t.clone() for t in self.fps_cur]
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
-        self.flat_opt = self._flat_adam() if self.world == 1 and self.flat_adam else None
-        # graph A: forward + backward; .grad tensors are allocated inside (static addresses)
+        self._flat_adam(order)
         self.opt.zero_grad(set_to_none=True)
         self.graph_a = torch.cuda.CUDAGraph()
         kw = {"stream": side} if self.capture_on_side_stream else {}
@@ -245,31 +268,31 @@ class GraphedStep:
             # runtime while this thread captures; "global" mode would fail those calls
             kw["capture_error_mode"] = "thread_local"
         fork = torch.cuda.Stream() if prefetch_fn is not None else None
+        hooks = self._bucket_hooks() if self.world > 1 else []
         with torch.cuda.graph(self.graph_a, **kw):
             cap = torch.cuda.current_stream()
             if fork is not None:
-                # graph B of the previous replay copied its fps_next into fps_cur
+                # the previous replay's tail copied its fps_next into fps_cur
                 fork.wait_stream(cap)
                 with torch.cuda.stream(fork):
                     self.fps_next = list(prefetch_fn(*self.static_next))
             self.loss = self.loss_fn(*self.static, **self._fps_kw(self.fps_cur))
             self.loss.backward()
-            kdpc_native.csr_join()  # side-stream CSR builds (csr_prefetch) rejoin the capture
-            self.grads = [p.grad for p in self.params if p.grad is not None]
-            self.flat = torch.cat([g.reshape(-1) for g in self.grads]) if self.world > 1 else None
             if fork is not None:
                 cap.wait_stream(fork)
             if self.world == 1:  # nothing runs between the halves: one graph, one launch
                 self._tail(fork)
-        # graph B: unpack + optimizer step (+ hand the prefetched FPS to the next replay);
-        # a second graph launch costs ~0.5 ms of idle GPU between the replays (rocprofv3,
-        # round 2), so it exists only when the all-reduce has to run between the two
+        for h in hooks:
+            h.remove()
+        if self.world > 1 and any(not b["done"] for b in self.buckets):
+            raise RuntimeError("GraphedStep: a gradient bucket was never completed in capture")
         self.graph_b = None
         if self.world > 1:
             self.graph_b = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph_b, pool=self.graph_a.pool(), **kw):
-                self._unpack()
-                self._tail(fork)
+                self.G.div_(float(self.world))
+                self._tail(fork, pack=False)
+            self.comm = torch.cuda.Stream()
         torch.cuda.synchronize()
         # keep the static loss buffer, not the captured autograd graph: while that graph
         # lives, an eager step on the same parameters reuses its AccumulateGrad nodes (bound
@@ -278,28 +301,45 @@ class GraphedStep:
         self.loss = self.loss.detach()
         self._pending = None
 
-    def _flat_adam(self):
-        """One flat Adam over the trained parameters instead of the per-tensor fused Adam: the
-        parameters (and the optimizer's moments) become views of flat buffers, the step copies
-        the ~440 gradient tensors into one buffer and updates all 8 M values in one pass (the
-        per-tensor fused Adam: 7 launches, ~0.3 ms for 31.8 MB).  Same elementwise update, so
-        the same bits.  Only for a single-group fused capturable Adam; None otherwise."""
+    def schedule_name(self):
+        if self.world == 1:
+            return " (1 graph: fwd+bwd+flat Adam)"
+        return (f" (graph A fwd+bwd -> {len(self.buckets)} gradient buckets all-reduced on a "
+                f"side stream as the backward completes them -> graph B flat Adam)")
+
+    def _check_optimizer(self):
         opt = self.opt
-        if type(opt) is not torch.optim.Adam or len(opt.param_groups) != 1:
-            return None
+        ok = type(opt) is torch.optim.Adam and len(opt.param_groups) == 1
+        grp = opt.param_groups[0] if ok else {}
+        if not (ok and grp.get("fused") and grp.get("capturable") and not grp.get("amsgrad")):
+            raise ValueError("GraphedStep needs a single-group torch.optim.Adam with fused=True, "
+                             "capturable=True (distill.make_optimizer(..., capturable=True))")
+        ids = {id(p) for p in self.params}
+        if {id(p) for p in grp["params"] if p.requires_grad} != ids:
+            raise ValueError("GraphedStep: the optimizer must hold exactly the trained parameters")
+
+    def _flat_adam(self, order):
+        """Parameters, moments and gradients as views of flat buffers in `order` (the order the
+        backward finalises the gradients); one fused Adam over them, sharing the caller's lr
+        tensor.  Same elementwise update as the caller's fused Adam, so the same bits."""
+        opt = self.opt
         grp = opt.param_groups[0]
-        if not grp.get("fused") or not grp.get("capturable") or grp.get("amsgrad"):
-            return None
-        used = [p for p in grp["params"] if "exp_avg" in opt.state.get(p, {})]
-        if not used:
-            return None
+        used = [p for p in order if "exp_avg" in opt.state.get(p, {})]
+        seen = {id(p) for p in used}
+        missing = [p for p in self.params if id(p) not in seen and p.grad is not None]
+        if missing:
+            raise RuntimeError("GraphedStep: a parameter with a gradient has no Adam state")
         steps = [opt.state[p]["step"] for p in used]
         if not all(torch.equal(steps[0], st) for st in steps[1:]):
-            return None
+            raise RuntimeError("GraphedStep: the parameters' Adam step counters differ")
+        dev = used[0].device
+        if not torch.is_tensor(grp["lr"]):
+            grp["lr"] = torch.tensor(float(grp["lr"]), device=dev)
+        self._lr = grp["lr"]
         n = sum(p.numel() for p in used)
-        P = torch.empty(n, device=used[0].device, dtype=used[0].dtype)
+        P = torch.empty(n, device=dev, dtype=used[0].dtype)
         M, V, G = torch.empty_like(P), torch.empty_like(P), torch.zeros_like(P)
-        self._gviews, self._used, off = [], used, 0
+        self._gviews, self._used, self._offs, off = [], used, [], 0
         with torch.no_grad():
             for p in used:
                 k, st = p.numel(), opt.state[p]
@@ -310,21 +350,64 @@ class GraphedStep:
                 st["exp_avg"] = M[off:off + k].view_as(p)  # the eager optimizer shares them
                 st["exp_avg_sq"] = V[off:off + k].view_as(p)
                 self._gviews.append(G[off:off + k].view_as(p))
+                self._offs.append(off)
                 off += k
+        self.G = G
+        self._steps = steps
         flat = torch.nn.Parameter(P)
         flat.grad = G
-        fo = torch.optim.Adam([flat], lr=grp["lr"], betas=grp["betas"], eps=grp["eps"],
+        fo = torch.optim.Adam([flat], lr=self._lr, betas=grp["betas"], eps=grp["eps"],
                               weight_decay=grp["weight_decay"], maximize=grp["maximize"],
                               fused=True, capturable=True)
         fo.state[flat] = {"step": steps[0].clone(), "exp_avg": M, "exp_avg_sq": V}
-        return fo
+        self.flat_opt = fo
+        self._flat_step = fo.state[flat]["step"]
+        # gradient buckets (world > 1): consecutive runs of `used` of about bucket_bytes
+        self.buckets = []
+        if self.world > 1:
+            cur, nb = [], 0
+            for i, p in enumerate(used):
+                cur.append(i)
+                nb += p.numel() * p.element_size()
+                if nb >= self.bucket_bytes or i == len(used) - 1:
+                    lo = self._offs[cur[0]]
+                    hi = self._offs[cur[-1]] + used[cur[-1]].numel()
+                    self.buckets.append({"idx": cur, "lo": lo, "hi": hi, "left": len(cur),
+                                         "done": False,
+                                         "event": torch.cuda.Event(external=True)})
+                    cur, nb = [], 0
 
-    def _tail(self, fork):
-        if self.flat_opt is not None:
+    def _bucket_hooks(self):
+        """Capture-time hooks: when the backward has finalised every gradient of a bucket,
+        pack them into the bucket's slice of G and record the bucket's external event."""
+        where = {}
+        for bi, b in enumerate(self.buckets):
+            b["left"], b["done"] = len(b["idx"]), False
+            for i in b["idx"]:
+                where[id(self._used[i])] = bi
+
+        def hook(p):
+            bi = where.get(id(p))
+            if bi is None:
+                return
+            b = self.buckets[bi]
+            b["left"] -= 1
+            if b["left"] == 0:
+                idx = b["idx"]
+                torch._foreach_copy_([self._gviews[i] for i in idx],
+                                     [self._used[i].grad for i in idx])
+                b["event"].record()
+                b["done"] = True
+        return [p.register_post_accumulate_grad_hook(hook) for p in self._used]
+
+    def _tail(self, fork, pack=True):
+        """Flat Adam step (+ the prefetched FPS handed over), inside a graph."""
+        if pack:
             torch._foreach_copy_(self._gviews, [p.grad for p in self._used])
-            self.flat_opt.step()
-        else:
-            self.opt.step()
+        # an eager optimizer step in between advanced the per-parameter counters
+        self._flat_step.copy_(self._steps[0])
+        self.flat_opt.step()
+        torch._foreach_copy_(self._steps, [self._flat_step] * len(self._steps))
         if fork is not None:
             for c, n in zip(self.fps_cur, self.fps_next):
                 c.copy_(n)
@@ -341,14 +424,6 @@ class GraphedStep:
     def _key(ts):
         return tuple(ts), tuple(t._version for t in ts)
 
-    def _unpack(self):
-        off = 0
-        for g in self.grads:
-            n = g.numel()
-            g.copy_(self.flat[off:off + n].view_as(g))
-            off += n
-        torch._foreach_div_(self.grads, float(self.world))
-
     def _allreduce_eager(self):
         """Warm-up path: the same averaging as the graphed step, eagerly."""
         if self.world == 1:
@@ -362,7 +437,16 @@ class GraphedStep:
             off += g.numel()
         torch._foreach_div_(grads, float(self.world))
 
+    def _sync_lr(self):
+        """A plain `param_groups[0]['lr'] = x` replaced the shared tensor: fold it back."""
+        grp = self.opt.param_groups[0]
+        lr = grp["lr"]
+        if lr is not self._lr:
+            self._lr.fill_(float(lr))
+            grp["lr"] = self._lr
+
     def __call__(self, *inputs, next_batch=None):
+        self._sync_lr()
         for s, t in zip(self.static, inputs):
             s.copy_(t, non_blocking=True)
         if self.prefetch_fn is not None:
@@ -382,7 +466,17 @@ class GraphedStep:
                              else None)
         self.graph_a.replay()
         if self.graph_b is not None:
-            dist.all_reduce(self.flat)
+            main = torch.cuda.current_stream()
+            # each all-reduce waits for its bucket's event in THIS replay of graph A (which
+            # runs after the previous replay's graph B on the main stream)
+            works = []
+            with torch.cuda.stream(self.comm):
+                for b in self.buckets:
+                    self.comm.wait_event(b["event"])
+                    works.append(dist.all_reduce(self.G[b["lo"]:b["hi"]], async_op=True))
+            for w in works:
+                w.wait()  # NCCL: the current (main) stream waits for the collective
+            main.wait_stream(self.comm)
             self.graph_b.replay()
         return self.loss.detach()
 

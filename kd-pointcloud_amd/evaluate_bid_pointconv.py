@@ -91,12 +91,18 @@ def main(config_path):
     from models_bid_lighttoken_res import PointConvBidirection
     dev = torch.device("cuda", 0)
     model = PointConvBidirection()
-    ckpt = os.path.join(getattr(args, "ckpt_dir", ""), getattr(args, "pretrain", "") or "")
-    if os.path.isfile(ckpt):
+    pretrain = getattr(args, "pretrain", "") or ""
+    ckpt = os.path.join(getattr(args, "ckpt_dir", "") or "", pretrain)
+    if pretrain:
+        if not os.path.isfile(ckpt):  # the reference's torch.load raises here too
+            raise FileNotFoundError(f"checkpoint {ckpt!r} (ckpt_dir + pretrain) does not exist")
         model.load_state_dict(torch.load(ckpt, map_location="cpu", weights_only=True))
         print("load model %s" % ckpt)
+    elif getattr(args, "allow_random_init", False):
+        print("no pretrain given (allow_random_init): evaluating random-init weights")
     else:
-        print("no checkpoint at %r: evaluating random-init weights" % ckpt)
+        raise ValueError("no checkpoint: set `pretrain` (with `ckpt_dir`), or "
+                         "`allow_random_init: true` to evaluate random-init weights")
     model.to(dev)
     loader = datasets.DeviceLoader(make_val_dataset(args), args.batch_size, dev,
                                    num_workers=getattr(args, "workers", 0))

@@ -332,77 +332,12 @@ def group_rows(points, idx):
 
 
 class Csr:
-    """Inverted index of an int32 index tensor (B,P) over a key space of n values.  `ready`:
-    the event of a side-stream build (csr_prefetch) that consumers must wait for, else None."""
-    __slots__ = ("offsets", "perm", "n", "p", "ready")
+    """Inverted index of an int32 index tensor (B,P) over a key space of n values."""
+    __slots__ = ("offsets", "perm", "n", "p")
 
     def __init__(self, idx2d, n):
         self.offsets, self.perm = _op("kdpc_csr_build", "csr_build", _gpu(idx2d, "idx"), n)
         self.n, self.p = n, idx2d.shape[1]
-        self.ready = None
-
-
-# The CSR of an index is consumed only by backward gather-sums, but its inputs exist as soon
-# as the forward's kNN has run: csr_prefetch() issues the build then, on a side stream, so
-# its ~5 small latency-bound launches (count / scan / fill / segment sort) overlap the rest of
-# the forward instead of sitting in the backward's critical path.  Inside a captured graph
-# this is a fork joined by the consumer's event wait (csr_join() joins any left over).
-# Measured round 2 (bench, graph step): 19.81 -> 21.44 ms/step with the side stream -- the
-# builds' atomics-heavy kernels run beside the forward's MFMA kernels and slow them more than
-# the builds cost in line -- so it is off by default; the lazy build on the consumer's
-# stream is the product path.
-CSR_AHEAD = False  # seam: True issues each CSR build at forward time on a side stream
-_csr_streams = {}
-
-
-def _csr_stream(device):
-    key = device.index if device.index is not None else torch.cuda.current_device()
-    st = _csr_streams.get(key)
-    if st is None:
-        st = _csr_streams[key] = torch.cuda.Stream(device=device)
-    return st
-
-
-def csr_prefetch(idx, n):
-    """Start building idx's CSR over n keys on the side stream (no-op if cached/disabled)."""
-    if not CSR_AHEAD or not idx.is_cuda:
-        return
-    parent = getattr(idx, "_kdpc_parent", None)
-    if parent is not None:
-        return csr_prefetch(parent[0], n)
-    cache = getattr(idx, "_kdpc_csr", None)
-    if cache is not None and cache.n == n:
-        return
-    cur = torch.cuda.current_stream(idx.device)
-    side = _csr_stream(idx.device)
-    side.wait_stream(cur)
-    with torch.cuda.stream(side):
-        csr = Csr(idx.reshape(idx.shape[0], -1), n)
-        csr.ready = torch.cuda.Event()
-        csr.ready.record(side)
-    idx.record_stream(side)  # the side stream reads idx: keep its block until the build ran
-    try:
-        idx._kdpc_csr = csr
-    except AttributeError:
-        pass
-
-
-def csr_join():
-    """Order the current stream after every side-stream CSR build issued so far."""
-    for st in _csr_streams.values():
-        if st.device == torch.cuda.current_stream().device:
-            torch.cuda.current_stream().wait_stream(st)
-
-
-def _claim(csr):
-    """Order the current stream after the CSR's side-stream build; its buffers then belong
-    to this stream too (the allocator waits for both before reusing them)."""
-    if csr.ready is not None:
-        cur = torch.cuda.current_stream(csr.offsets.device)
-        cur.wait_event(csr.ready)
-        csr.offsets.record_stream(cur)
-        csr.perm.record_stream(cur)
-    return csr
 
 
 def batch_prefix(idx, b):
@@ -421,14 +356,14 @@ def csr_of(idx, n):
     """CSR for idx (B,...) flattened to (B,P), cached on the index tensor object."""
     cache = getattr(idx, "_kdpc_csr", None)
     if cache is not None and cache.n == n:
-        return _claim(cache)
+        return cache
     parent = getattr(idx, "_kdpc_parent", None)
     if parent is not None:
         pidx, b = parent
         pc = csr_of(pidx, n)
         csr = Csr.__new__(Csr)
         csr.offsets, csr.perm = pc.offsets[:b * n + 1], pc.perm[:b * pc.p]
-        csr.n, csr.p, csr.ready = n, pc.p, None
+        csr.n, csr.p = n, pc.p
     else:
         csr = Csr(idx.reshape(idx.shape[0], -1), n)
     try:

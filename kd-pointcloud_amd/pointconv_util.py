@@ -200,8 +200,6 @@ class _GroupRows(torch.autograd.Function):
         B, N, C = points.shape
         ctx.save_for_backward(idx)
         ctx.shape = (B, N, C)
-        if ctx.needs_input_grad[0]:
-            _nat.csr_prefetch(idx, N)
         return _nat.group_rows(points, idx.view(B, -1))
 
     @staticmethod
@@ -345,8 +343,6 @@ class _PointConvContract(torch.autograd.Function):
     @staticmethod
     def forward(ctx, xyz, center, feats, idx, wt):
         ctx.save_for_backward(xyz, center, feats, idx, wt)
-        if ctx.needs_input_grad[0] or ctx.needs_input_grad[2]:
-            _nat.csr_prefetch(idx, xyz.shape[1])
         return _nat.pointconv_contract_fwd(xyz, center, feats, idx, wt)
 
     @staticmethod
@@ -368,8 +364,6 @@ class _PointConvLayer(torch.autograd.Function):
     @staticmethod
     def forward(ctx, xyz, center, feats, idx, wt, wl, bias):
         ctx.save_for_backward(xyz, center, feats, idx, wt, wl)
-        if any(ctx.needs_input_grad):
-            _nat.csr_prefetch(idx, xyz.shape[1])
         return _nat.pointconv_fwd(xyz, center, feats, idx, wt, wl, bias)
 
     @staticmethod
@@ -496,8 +490,6 @@ class _CostVolume(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x1, x2, idx, p1, p2, wpos, bpos, w1, b1, amax_override=None):
-        if ctx.needs_input_grad[1] or ctx.needs_input_grad[4]:
-            _nat.csr_prefetch(idx, x2.shape[1])
         out, amax = _nat.cost_volume_fwd(x1, x2, idx, p1, p2, wpos, bpos, w1, b1)
         if amax_override is not None:
             amax = amax_override(amax)
@@ -531,8 +523,6 @@ class _CostVolumeWide(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x1, x2, idx, p1, p2, wpos, bpos, w1, b1, amax_override=None):
         B, N1, K = idx.shape
-        if ctx.needs_input_grad[1] or ctx.needs_input_grad[4]:
-            _nat.csr_prefetch(idx, x2.shape[1])
         h0 = _nat.cost_volume_wide_h0(x1, x2, idx, p1, p2, wpos, bpos)
         z1 = torch.addmm(b1, h0.view(-1, h0.shape[-1]), w1.t())
         out, amax = _nat.cost_volume_wide_max(z1, B, N1, K, w1.shape[0])
@@ -864,8 +854,6 @@ class _WnWeightedSum(torch.autograd.Function):
     @staticmethod
     def forward(ctx, direction, idx, v, *params):
         ctx.save_for_backward(direction, idx, v, *params)
-        if idx is not None and ctx.needs_input_grad[2]:
-            _nat.csr_prefetch(idx, v.shape[1])
         return _nat.wn_wsum_fwd(direction, idx, v, params)
 
     @staticmethod
@@ -896,8 +884,6 @@ class _IdwBlend(torch.autograd.Function):
     @staticmethod
     def forward(ctx, ref, qry, vals, idx, warp):
         ref, qry, vals = ref.contiguous(), qry.contiguous(), vals.contiguous()
-        if ctx.needs_input_grad[0] or ctx.needs_input_grad[2]:
-            _nat.csr_prefetch(idx, ref.shape[1])
         out, w = _nat.idw_blend_fwd(ref, qry, vals, idx, warp)
         ctx.save_for_backward(ref, qry, vals, idx, w)
         ctx.warp = warp

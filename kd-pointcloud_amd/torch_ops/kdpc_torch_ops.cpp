@@ -656,10 +656,16 @@ TT idw_blend_fwd(Tensor ref, Tensor qry, Tensor vals, Tensor idx, bool warp) {
 Tensor idw_blend_bwd_vals(Tensor dout, Tensor w, Tensor offsets, Tensor perm, int64_t s,
                           bool warp) {
   dev(dout, kF, "dout"), dev(w, kF, "w"), dev(offsets, kI, "offsets"), dev(perm, kI, "perm");
-  TORCH_CHECK(dout.dim() == 3 && w.dim() == 3 && w.size(2) == 3 && w.size(1) == dout.size(1),
+  same_device(dout, w, "w"), same_device(dout, offsets, "offsets");
+  same_device(dout, perm, "perm");
+  TORCH_CHECK(dout.dim() == 3 && w.dim() == 3 && w.size(2) == 3 && w.size(1) == dout.size(1) &&
+                  w.size(0) == dout.size(0),
               "kdpc: idw_blend_bwd_vals expects dout (B,N,C), w (B,N,3)");
-  GUARD(dout);
   const int64_t b = dout.size(0), n = dout.size(1), c = dout.size(2);
+  TORCH_CHECK(s >= 0 && offsets.numel() == b * s + 1 && perm.numel() == b * n * 3,
+              "kdpc: idw_blend_bwd_vals expects the CSR of idx (B,N,3) over S keys: offsets "
+              "(B*S+1), perm (B*N*3); got ", offsets.numel(), " and ", perm.numel());
+  GUARD(dout);
   Tensor dvals = empty_f({b, s, c}, dout);
   check(kdpc_idw_blend_bwd_vals(b, n, s, c, F(dout), F(w), I(offsets), I(perm), F(dvals), warp,
                                 stream_of(dout)), "idw_blend_bwd_vals");
@@ -670,9 +676,18 @@ TT idw_blend_bwd_coords(Tensor ref, Tensor qry, Tensor vals, Tensor idx, Tensor 
                         bool warp) {
   dev(ref, kF, "ref"), dev(qry, kF, "qry"), dev(vals, kF, "vals"), dev(idx, kI, "idx");
   dev(dout, kF, "dout");
+  same_device(ref, qry, "qry"), same_device(ref, vals, "vals"), same_device(ref, idx, "idx");
+  same_device(ref, dout, "dout");
+  TORCH_CHECK(ref.dim() == 3 && ref.size(2) == 3 && qry.dim() == 3 && qry.size(2) == 3 &&
+                  vals.dim() == 3 && idx.dim() == 3 && idx.size(2) == 3 &&
+                  vals.size(1) == ref.size(1) && idx.size(1) == qry.size(1) &&
+                  ref.size(0) == qry.size(0) && vals.size(0) == ref.size(0) &&
+                  idx.size(0) == ref.size(0),
+              "kdpc: idw_blend_bwd_coords expects ref (B,S,3), qry (B,N,3), vals (B,S,C), "
+              "idx (B,N,3)");
   GUARD(ref);
   const int64_t b = ref.size(0), s = ref.size(1), n = qry.size(1), c = vals.size(2);
-  TORCH_CHECK(dout.dim() == 3 && dout.size(1) == n && dout.size(2) == c,
+  TORCH_CHECK(dout.dim() == 3 && dout.size(0) == b && dout.size(1) == n && dout.size(2) == c,
               "kdpc: idw_blend_bwd_coords expects dout (B,N,C)");
   Tensor drow = empty_f({b, n * 3, 3}, ref);
   Tensor dq = empty_f({b, n, 3}, ref);

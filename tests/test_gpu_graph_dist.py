@@ -1,8 +1,10 @@
-"""GraphedStep with world size 2 (the N>1 path of `bench.py --graph`: graph A -> one flat
-all-reduce of the gradients -> graph B) on ONE GPU: two processes share cuda:0 and talk over
-gloo (which accepts device tensors).  Each rank trains on its own batch; after the steps both
-ranks hold identical parameters, equal to a single-process eager step on the averaged
-gradient of the two batches."""
+"""GraphedStep with world size 2 (the N>1 path of bench.py: graph A = fwd+bwd whose gradient
+buckets end in external events -> one async all-reduce per bucket on a side stream, each
+waiting only for its bucket -> graph B = mean + flat Adam) on ONE GPU: two processes share
+cuda:0 and talk over gloo (which accepts device tensors).  Each rank trains on its own
+batch; after the steps both ranks hold identical parameters, equal to a single-process eager
+step on the averaged gradient of the two batches -- for the flow step (configs[2]) and the KD
+step (configs[3], distilTrain.py:156-185)."""
 import os
 import socket
 
@@ -26,20 +28,24 @@ def _batches(rank):
             for s in range(3)]
 
 
-def _worker(rank, port, out_dir):
+def _worker(rank, port, out_dir, mode):
     import sys
     sys.path.insert(0, os.path.join(ROOT, "kd-pointcloud_amd"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=2)
     torch.cuda.set_device(0)
-    from distill import graphed_flow_step, make_optimizer
+    from distill import graphed_flow_step, graphed_kd_step, make_optimizer
     from models_bid_pointconv import PointConvBidirection
     torch.manual_seed(0)
     model = PointConvBidirection().cuda()
     opt = make_optimizer(model, capturable=True)
     mine = _batches(rank)
-    step = graphed_flow_step(model, opt, mine[0], warmup=1)
+    if mode == "kd":
+        step = graphed_kd_step(_teacher(), model, opt, mine[0], warmup=1)
+    else:
+        step = graphed_flow_step(model, opt, mine[0], warmup=1)
+    assert len(step.buckets) > 1  # the gradients really go out in several buckets
     for i in (1, 2):
         step(*mine[i], next_batch=mine[i + 1] if i + 1 < len(mine) else None)
     torch.cuda.synchronize()
@@ -49,12 +55,31 @@ def _worker(rank, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_graphed_step_world2_matches_averaged_eager(tmp_path):
+def _teacher():
+    from models_bid_pointconv import PointConvBidirection
+    torch.manual_seed(5)
+    return PointConvBidirection().cuda().eval()
+
+
+def _loss(model, teacher, bt):
+    import loss_functions
+    if teacher is None:
+        flows, fps1 = model(bt[0], bt[1], bt[0], bt[1])[:2]
+        return loss_functions.multiScaleLoss(flows, bt[2], fps1)
+    with torch.no_grad():
+        t = teacher(bt[0], bt[1], bt[0], bt[1])
+    o = model(bt[0], bt[1], bt[0], bt[1])
+    return loss_functions.biDirection_loss_ht(o[0], o[5], o[6], o[1], o[2], bt[2], t[0], t[5],
+                                              t[6], t[1], t[2], 0.3, 0.8, layer=3)
+
+
+@pytest.mark.parametrize("mode", ["train", "kd"])
+def test_graphed_step_world2_matches_averaged_eager(tmp_path, mode):
     import sys
     sys.path.insert(0, os.path.join(ROOT, "kd-pointcloud_amd"))
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, str(tmp_path))) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, port, str(tmp_path), mode)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
@@ -65,11 +90,11 @@ def test_graphed_step_world2_matches_averaged_eager(tmp_path):
     for k in p0:
         assert torch.equal(p0[k], p1[k]), k
     # the same three steps eagerly in one process, gradients of the two ranks' batches averaged
-    import loss_functions
     from distill import make_optimizer
     from models_bid_pointconv import PointConvBidirection
     torch.manual_seed(0)
     model = PointConvBidirection().cuda().train()
+    teacher = _teacher() if mode == "kd" else None
     opt = make_optimizer(model, capturable=True)
     b0, b1 = _batches(0), _batches(1)
     for i in range(3):
@@ -78,8 +103,7 @@ def test_graphed_step_world2_matches_averaged_eager(tmp_path):
         for bt in (b0[i], b1[i]):
             for p in model.parameters():
                 p.grad = None
-            flows, fps1 = model(bt[0], bt[1], bt[0], bt[1])[:2]
-            loss_functions.multiScaleLoss(flows, bt[2], fps1).backward()
+            _loss(model, teacher, bt).backward()
             grads.append([None if p.grad is None else p.grad.clone() for p in model.parameters()])
         for p, g0, g1 in zip(model.parameters(), *grads):
             p.grad = None if g0 is None else (g0 + g1) / 2

@@ -1,0 +1,132 @@
+"""BASELINE configs[3] -- the KD step of distilTrain.py:156-185 (teacher fwd in eval/no_grad,
+student fwd+bwd, biDirection_loss_ht, Adam) -- at its per-GPU slice of B=32 over 8 GPUs:
+B=4 pairs of N=8192 points, through the product step (distill.graphed_kd_step, the step the
+bench times).  Plus the graphed step's optimizer contract (eager steps and LR changes in
+between) and HIP-graph replay of the step's reductions."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _batch(b, n, seed):
+    import synthetic
+    return tuple(torch.from_numpy(a).to(DEV) for a in synthetic.ft3d_batch(b, n, seed=seed))
+
+
+def test_graphed_kd_step_b4_n8192():
+    """FPS chain per cloud equals the oracle's; loss and gradients finite; the graphed KD
+    step is bit-identical to the eager KDTrainStep (losses and parameters) over replays with
+    and without an in-graph FPS prefetch."""
+    import pointnet2_oracle as O
+    from distill import KDTrainStep, graphed_kd_step, make_optimizer
+    from models_bid_lighttoken_res import PointConvBidirection as Student
+    from models_bid_pointconv import PointConvBidirection as Teacher
+    torch.manual_seed(1)
+    teacher = Teacher().to(DEV)
+    torch.manual_seed(2)
+    base = Student().to(DEV)
+    batches = [_batch(4, 8192, s) for s in (31, 32, 33)]
+    # FPS chain (levels 1-4, both clouds) vs the C oracle, cloud by cloud
+    fps = base.precompute_fps(batches[0][0], batches[0][1])
+    x = torch.cat([batches[0][0], batches[0][1]], 0).cpu().numpy()
+    for lv, idx in enumerate(fps):
+        want, _ = O.furthest_point_sample(x, idx.shape[1])
+        np.testing.assert_array_equal(idx.cpu().numpy(), want, err_msg=f"FPS level {lv + 1}")
+        x = np.take_along_axis(x, want[..., None].astype(np.int64), 1)
+    eager_model, graph_model = copy.deepcopy(base), copy.deepcopy(base)
+    opt_e = make_optimizer(eager_model, capturable=True)
+    opt_g = make_optimizer(graph_model, capturable=True)
+    eager = KDTrainStep(teacher, eager_model, opt_e)
+    graphed = graphed_kd_step(teacher, graph_model, opt_g, batches[0], warmup=1)
+    eager(*batches[0])  # the graphed step's constructor ran one eager warm-up step
+    seq = [(batches[1], batches[2]), (batches[2], None), (batches[1], None)]
+    for b, nxt in seq:
+        le = eager(*b, next_batch=nxt)
+        lg = graphed(*b, next_batch=nxt)
+        torch.cuda.synchronize()
+        assert torch.isfinite(lg).all(), float(lg)
+        assert float(le) == float(lg), (float(le), float(lg))
+        assert torch.isfinite(graphed.G).all()  # the packed student gradients of this replay
+    for (n, pe), pg in zip(eager_model.named_parameters(), graph_model.parameters()):
+        assert torch.equal(pe, pg), n
+    assert all(p.grad is None for p in teacher.parameters())  # frozen teacher
+
+
+def test_graphed_step_honours_eager_steps_and_lr_changes():
+    """the graphed step's flat Adam shares state with the caller's optimizer.  An
+    eager step on that optimizer between replays, and an LR change by plain assignment (the
+    reference's per-epoch LR clip, distilTrain.py:146-149) or by a torch scheduler, must
+    reach the graph: parameters and Adam step counters equal an all-eager run."""
+    from distill import FlowTrainStep, graphed_flow_step, make_optimizer
+    from models_bid_pointconv import PointConvBidirection
+    torch.manual_seed(0)
+    base = PointConvBidirection().to(DEV)
+    b = [_batch(1, 2048, s) for s in (41, 42, 43)]
+    mg, me = copy.deepcopy(base), copy.deepcopy(base)
+    og, oe = make_optimizer(mg, capturable=True), make_optimizer(me, capturable=True)
+    graphed = graphed_flow_step(mg, og, b[0], warmup=1)
+    eager_e = FlowTrainStep(me, oe)
+    eager_e(*b[0])
+    graphed(*b[1])
+    eager_e(*b[1])
+    FlowTrainStep(mg, og)(*b[2])  # an eager step on the graphed model's optimizer
+    eager_e(*b[2])
+    for o in (og, oe):
+        o.param_groups[0]["lr"] = 5e-4  # plain assignment
+    graphed(*b[1])
+    eager_e(*b[1])
+    for o in (og, oe):
+        torch.optim.lr_scheduler.StepLR(o, step_size=1, gamma=0.5).step()  # 2.5e-4
+    graphed(*b[2])
+    eager_e(*b[2])
+    torch.cuda.synchronize()
+    worst = 0.0
+    for (n, pg), pe in zip(mg.named_parameters(), me.parameters()):
+        scale = float(pe.detach().abs().max()) + 1e-12
+        worst = max(worst, float((pg - pe).abs().max()) / scale)
+        sg, se = og.state.get(pg, {}).get("step"), oe.state.get(pe, {}).get("step")
+        assert (sg is None) == (se is None), n
+        if sg is not None:
+            assert float(sg) == float(se) == 5.0, (n, float(sg), float(se))
+    # the LR tensor (graph) and the float LR (eager) round 5e-4 / 2.5e-4 differently; a stale
+    # LR or a stale bias correction would be off by ~1e-4 of the parameter scale
+    assert worst < 2e-6, worst
+
+
+def test_reductions_replay_from_graph():
+    """The step's reductions replayed from a captured HIP graph equal their eager values on
+    new data: torch's multi-block sum / mean / norm (loss and BN-statistics shapes) and the
+    fixed-order dense.fixed_sum.  (Pins the claim in dense._FixedSum's docstring.)"""
+    import dense
+    x = torch.randn(8, 8192, 64, device=DEV)
+    fns = {
+        "sum_all": lambda t: t.sum(),
+        "mean_all": lambda t: t.mean(),
+        "norm_rows_mean": lambda t: torch.norm(t[..., :3], dim=2).sum(1).mean(),
+        "sum_dim0_rows": lambda t: t.view(-1, 64).sum(0),
+        "var_dim0_rows": lambda t: t.view(-1, 64).var(0, unbiased=False),
+        "fixed_sum_all": lambda t: dense.fixed_sum(t),
+        "fixed_sum_dim": lambda t: dense.fixed_sum(t.view(-1, 64), 0),
+    }
+    for f in fns.values():  # warm-up (lazy init) outside the capture
+        f(x)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        outs = {k: f(x) for k, f in fns.items()}
+    bad = {}
+    for seed in range(3):
+        torch.manual_seed(100 + seed)
+        x.copy_(torch.randn_like(x) * (seed + 1))
+        g.replay()
+        torch.cuda.synchronize()
+        for k, f in fns.items():
+            want = f(x)
+            if not torch.equal(outs[k], want):
+                bad[(seed, k)] = float((outs[k] - want).abs().max())
+    assert not bad, bad

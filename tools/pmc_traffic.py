@@ -1,14 +1,18 @@
 """HBM traffic per entry-point launch from rocprofv3 --pmc passes of bench.py.
 
-    python tools/pmc_traffic.py --fetch <dir of FETCH_SIZE pass> --write <dir of WRITE_SIZE pass>
-                                [--out profiles/pmc_traffic.json]
+    python tools/pmc_traffic.py --workload train_b8_n8192 --fetch <dir of FETCH_SIZE pass>
+                                --write <dir of WRITE_SIZE pass> [--out profiles/pmc_traffic.json]
+                                [--command "<the bench command both passes profiled>"]
 
 Each pass is its own `rocprofv3 --pmc <counter> --output-format csv` run of the same bench
 command (gfx950 cannot hold FETCH_SIZE and WRITE_SIZE in one pass).  Per
 MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are in KiB, and on gfx950 FETCH_SIZE reports
 1/2 of the bytes of a wide coalesced read, so hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024.
 The per-launch figure of a C entry point sums its HIP kernels (bench.ROOFLINE) and divides by
-the number of launches of the entry's first kernel.
+the number of launches of the entry's first kernel.  Each pass must profile ONE workload (a
+single-section bench command, e.g. `bench.py --sections kd`); the result is merged into the
+output file under workloads[<workload>], the key bench.py looks traffic up by, so a figure is
+never attached to a roofline of another workload.
 """
 import argparse
 import collections
@@ -51,6 +55,8 @@ def match(name, short):
 def main():
     import bench
     ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", required=True,
+                    help="bench workload key (bench.workload_key / the section's `workload`)")
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -75,12 +81,17 @@ def main():
             "hbm_bytes_per_launch": round((2 * fkb + wkb) * 1024 / launches),
             "kernels": kernels,
         }
-    res = {"command": args.command,
-           "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 per launch (MI355X_MICROARCH.md §HBM)",
-           "entries": entries}
+    try:
+        with open(args.out) as f:
+            res = json.load(f)
+    except (OSError, ValueError):
+        res = {}
+    res["formula"] = "(2*FETCH_SIZE + WRITE_SIZE) * 1024 per launch (MI355X_MICROARCH.md §HBM)"
+    res.setdefault("workloads", {})[args.workload] = {"command": args.command,
+                                                      "entries": entries}
     with open(args.out, "w") as f:
         json.dump(res, f, indent=1)
-    print(json.dumps(res, indent=1))
+    print(json.dumps(res["workloads"][args.workload], indent=1))
 
 
 if __name__ == "__main__":

@@ -2,9 +2,11 @@
 
     python tools/roofline_check.py <rocprof dir with *kernel_trace.csv> <bench json line file>
 
-For each roofline entry point in the bench line: rocprof per-launch duration = the summed
-durations of its HIP kernels / launches of its first kernel, next to the live HIP-event
-average (avg_launch_us).
+For each roofline object in the bench line (the headline `roofline`, `kd_step.roofline`,
+`configs1.*`, `roofline_knn`, ...): rocprof per-launch duration = the summed durations of its
+entry's HIP kernels / launches of its first kernel, next to the live HIP-event average
+(avg_launch_us).  Profile a single-section bench command (`--sections train`, `kd`,
+`configs1` or `knn`): the rocprof sums cover every launch in the process.
 """
 import csv
 import glob
@@ -27,10 +29,15 @@ def main():
     trace = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)[0]
     rows = list(csv.DictReader(open(trace)))
     out = {}
-    for key in ("roofline", "roofline_gather"):
-        r = line.get(key) if line else None
-        if not r:
-            continue
+
+    def objs(d, path):
+        for k, v in d.items():
+            if isinstance(v, dict):
+                if "avg_launch_us" in v and v.get("kernel") in bench.ROOFLINE:
+                    yield path + k, v
+                yield from objs(v, path + k + ".")
+
+    for key, r in objs(line or {}, ""):
         kernels = bench.ROOFLINE[r["kernel"]][3]
         head = kernels[0]
         n = sum(1 for x in rows if head in x["Kernel_Name"])
