@@ -225,10 +225,20 @@ def step_section(args, mode, batch, dev, world, rank):
             for t in list(student.parameters()) + list(student.buffers()):
                 dist.broadcast(t.data, 0)
         opt = make_optimizer(student, capturable=True)
-        if mode == "kd":
-            step = graphed_kd_step(teacher, student, opt, batches[0])
-        else:
-            step = graphed_flow_step(student, opt, batches[0])
+
+        def build(overlap=None):
+            if mode == "kd":
+                return graphed_kd_step(teacher, student, opt, batches[0], overlap=overlap)
+            return graphed_flow_step(student, opt, batches[0], overlap=overlap)
+        try:
+            step = build()
+        except RuntimeError as exc:  # RCCL capture refused: the serial multi-rank schedule
+            if world == 1:
+                raise
+            print(f"rank {rank}: captured all-reduce failed ({exc}); serial schedule instead",
+                  file=sys.stderr, flush=True)
+            torch.cuda.synchronize()
+            step = build(overlap=False)
         step_kind += step.schedule_name()
         eager = (KDTrainStep(teacher, student, opt) if mode == "kd"
                  else FlowTrainStep(student, opt))

@@ -36,11 +36,13 @@ def _chunks(rows, out_elems):
 
 
 class _FixedSum(Function):
-    """x.sum(dim) with the HIP fixed-order column sum (csrc/colsum.hip): bitwise
-    reproducible, and safe inside a captured HIP graph.  torch's multi-block ("global")
-    reductions -- a few large outputs over many elements, e.g. a loss summed over all points
-    -- returned wrong values when replayed from a captured graph on this ROCm torch build
-    (tools/graph_diag.py, round 2), so the step's large loss reductions use this."""
+    """x.sum(dim) with the HIP fixed-order column sum (csrc/colsum.hip): the summation order
+    is fixed by the kernel, not by torch's launch heuristics, so a loss is bitwise
+    reproducible across batch sizes and runs.  (Round 2 suspected torch's multi-block
+    reductions of going wrong under HIP-graph replay; the minimal replay test
+    tests/test_gpu_kd.py::test_reductions_replay_from_graph -- torch sum / mean / norm / var
+    of the step's shapes, replayed on new data -- finds them equal to eager, so that
+    suspicion is withdrawn; the fixed order is kept for reproducibility.)"""
 
     @staticmethod
     def forward(ctx, x, dim):

@@ -183,20 +183,17 @@ class GraphedStep:
     """One training step replayed from HIP graphs (MI355X: the eager step issues ~2000
     launches per iteration from Python, as much host time as the GPU needs).
 
-    world 1:  graph A = [FPS of the NEXT batch on a forked stream] + forward + loss +
-              backward + gradient pack + flat Adam step: one graph launch per step.
-    world > 1 (one process per GPU, RCCL over xGMI):
-              graph A = [FPS fork] + forward + loss + backward; the gradients are packed,
-                        in the order the backward finalises them, into buckets of about
-                        `bucket_bytes`, and each bucket's pack ends in an EXTERNAL event
-                        record node (torch.cuda.Event(external=True));
-              host    : right after launching graph A, per bucket: the communication stream
-                        waits for that bucket's event, then an async all_reduce of it.  The
-                        GPU starts each bucket's all-reduce as soon as the backward has
-                        produced it, beside the rest of the backward (DDP's overlap, without
-                        DDP's per-step host work);
-              graph B = the main stream waits for every all-reduce, then grad / world +
-                        flat Adam step (+ hand the prefetched FPS to the next replay).
+    world 1:  ONE graph = [FPS of the NEXT batch on a forked stream] + forward + loss +
+              backward + gradient pack + flat Adam step.
+    world > 1, RCCL (`nccl` backend; one process per GPU over xGMI) -- "overlap" schedule:
+              still ONE graph.  The gradients are packed, in the order the backward
+              finalises them, into buckets of about `bucket_bytes`; as soon as the backward
+              has produced a bucket it is all-reduced on a side stream forked from the
+              capture (RCCL kernels captured into the graph), beside the rest of the
+              backward; the main stream joins the side stream before the mean + flat Adam.
+              DDP's overlap, without DDP's per-step host work.
+    world > 1, other backends (gloo cannot be captured) -- "serial" schedule: graph A (fwd +
+              bwd + pack), one eager all-reduce of the flat gradient, graph B (mean + Adam).
     The averaged-gradient semantics are DDP's (and the reference DataParallel's): every
     replica applies the same Adam update to the mean gradient.
 
@@ -206,30 +203,41 @@ class GraphedStep:
     copied from the flat counter inside the graph (and the flat counter from them before
     each update, so eager steps in between are honoured), and the learning rate is one
     device tensor shared by both optimizers -- an LR scheduler (or a plain
-    `param_groups[0]['lr'] = x`, re-read before every replay) reaches the graph.
+    `param_groups[0]['lr'] = x`, re-read before every replay) reaches the graph.  After the
+    capture the parameters' `.grad` are None again (the graph keeps its own buffers), so an
+    eager step in between starts from empty gradients as it would without the graph.
 
     `loss_fn(*inputs)` must run the whole forward (model call(s) and loss) and return the
     loss; the inputs are copied into static buffers before each replay.  Warm-up iterations
     run eagerly on a side stream (they allocate lazily-initialised state: optimizer moments,
-    cached attributes).
+    cached attributes, the communicator).
 
     prefetch_fn (optional, e.g. PointConvBidirection.precompute_fps): a function of the first
-    `n_prefetch` inputs whose result loss_fn takes as `fps=`.  Graph A then runs it for the
+    `n_prefetch` inputs whose result loss_fn takes as `fps=`.  The graph then runs it for the
     next batch on a forked stream, beside this batch's forward/backward, into buffers the next
     replay reads.  A call whose batch is not the previous call's `next_batch` recomputes it
-    eagerly first, so results never depend on what was prefetched."""
+    eagerly first, so results never depend on what was prefetched.
+
+    overlap: None = "overlap" schedule when world > 1 and the backend is nccl (RCCL);
+    True forces it (also at world 1, where the all-reduces are one-rank collectives: the
+    capture mechanics test); False forces "serial"."""
 
     drop_warmup_graph = True  # diagnostics seam (tools/graph_diag.py)
     capture_on_side_stream = False
     bucket_bytes = 8 << 20  # all-reduce bucket size (world > 1)
 
     def __init__(self, loss_fn, params, optimizer, example_inputs, warmup=3, prefetch_fn=None,
-                 n_prefetch=2):
+                 n_prefetch=2, overlap=None):
         self.loss_fn = loss_fn
         self.opt = optimizer
         self.params = [p for p in params if p.requires_grad]
         self.static = [t.detach().clone() for t in example_inputs]
         self.world = dist.get_world_size() if is_dist() else 1
+        if overlap is None:
+            overlap = self.world > 1 and dist.get_backend() == "nccl"
+        if overlap and not is_dist():
+            raise ValueError("GraphedStep(overlap=True) needs an initialised process group")
+        self.schedule = "overlap" if overlap else ("serial" if self.world > 1 else "single")
         self.prefetch_fn = prefetch_fn
         self.n_prefetch = n_prefetch
         self.static_next = [t.detach().clone() for t in example_inputs[:n_prefetch]]
@@ -263,14 +271,16 @@ class GraphedStep:
         self.opt.zero_grad(set_to_none=True)
         self.graph_a = torch.cuda.CUDAGraph()
         kw = {"stream": side} if self.capture_on_side_stream else {}
-        if self.world > 1:
+        if self.world > 1 or self.schedule == "overlap":
             # a process group's background threads (RCCL watchdog: event queries) may touch the
             # runtime while this thread captures; "global" mode would fail those calls
             kw["capture_error_mode"] = "thread_local"
         fork = torch.cuda.Stream() if prefetch_fn is not None else None
-        hooks = self._bucket_hooks() if self.world > 1 else []
+        self.comm = torch.cuda.Stream() if self.schedule == "overlap" else None
+        hooks = self._bucket_hooks() if self.schedule == "overlap" else []
         with torch.cuda.graph(self.graph_a, **kw):
             cap = torch.cuda.current_stream()
+            self._cap = cap
             if fork is not None:
                 # the previous replay's tail copied its fps_next into fps_cur
                 fork.wait_stream(cap)
@@ -280,20 +290,31 @@ class GraphedStep:
             self.loss.backward()
             if fork is not None:
                 cap.wait_stream(fork)
-            if self.world == 1:  # nothing runs between the halves: one graph, one launch
+            if self.schedule == "overlap":
+                cap.wait_stream(self.comm)  # every bucket's all-reduce
+                if self.world > 1:
+                    self.G.div_(float(self.world))
+                self._tail(fork, pack=False)
+            elif self.schedule == "single":
                 self._tail(fork)
+            else:  # serial: pack only; the all-reduce runs between graph A and graph B
+                self._pack()
         for h in hooks:
             h.remove()
-        if self.world > 1 and any(not b["done"] for b in self.buckets):
+        if self.schedule == "overlap" and any(not b["done"] for b in self.buckets):
             raise RuntimeError("GraphedStep: a gradient bucket was never completed in capture")
         self.graph_b = None
-        if self.world > 1:
+        if self.schedule == "serial":
             self.graph_b = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph_b, pool=self.graph_a.pool(), **kw):
                 self.G.div_(float(self.world))
                 self._tail(fork, pack=False)
-            self.comm = torch.cuda.Stream()
         torch.cuda.synchronize()
+        # the graph owns its gradient buffers; the parameters' .grad go back to None so an
+        # eager step in between does not accumulate onto the last replay's gradients
+        self._grad_refs = [p.grad for p in self.params]
+        for p in self.params:
+            p.grad = None
         # keep the static loss buffer, not the captured autograd graph: while that graph
         # lives, an eager step on the same parameters reuses its AccumulateGrad nodes (bound
         # to the capture stream) and torch warns of a stream mismatch (bench's eager
@@ -302,10 +323,12 @@ class GraphedStep:
         self._pending = None
 
     def schedule_name(self):
-        if self.world == 1:
+        if self.schedule == "single":
             return " (1 graph: fwd+bwd+flat Adam)"
-        return (f" (graph A fwd+bwd -> {len(self.buckets)} gradient buckets all-reduced on a "
-                f"side stream as the backward completes them -> graph B flat Adam)")
+        if self.schedule == "overlap":
+            return (f" (1 graph: fwd+bwd with {len(self.buckets)} gradient buckets all-reduced "
+                    "on a captured side stream as the backward completes them, then flat Adam)")
+        return " (graph A fwd+bwd -> eager flat all-reduce -> graph B flat Adam)"
 
     def _check_optimizer(self):
         opt = self.opt
@@ -324,8 +347,11 @@ class GraphedStep:
         tensor.  Same elementwise update as the caller's fused Adam, so the same bits."""
         opt = self.opt
         grp = opt.param_groups[0]
-        used = [p for p in order if "exp_avg" in opt.state.get(p, {})]
-        seen = {id(p) for p in used}
+        used, seen = [], set()
+        for p in order:  # gradient-ready order, each parameter once
+            if id(p) not in seen and "exp_avg" in opt.state.get(p, {}):
+                used.append(p)
+                seen.add(id(p))
         missing = [p for p in self.params if id(p) not in seen and p.grad is not None]
         if missing:
             raise RuntimeError("GraphedStep: a parameter with a gradient has no Adam state")
@@ -364,7 +390,7 @@ class GraphedStep:
         self._flat_step = fo.state[flat]["step"]
         # gradient buckets (world > 1): consecutive runs of `used` of about bucket_bytes
         self.buckets = []
-        if self.world > 1:
+        if self.schedule == "overlap":
             cur, nb = [], 0
             for i, p in enumerate(used):
                 cur.append(i)
@@ -373,13 +399,13 @@ class GraphedStep:
                     lo = self._offs[cur[0]]
                     hi = self._offs[cur[-1]] + used[cur[-1]].numel()
                     self.buckets.append({"idx": cur, "lo": lo, "hi": hi, "left": len(cur),
-                                         "done": False,
-                                         "event": torch.cuda.Event(external=True)})
+                                         "done": False})
                     cur, nb = [], 0
 
     def _bucket_hooks(self):
         """Capture-time hooks: when the backward has finalised every gradient of a bucket,
-        pack them into the bucket's slice of G and record the bucket's external event."""
+        pack them into the bucket's slice of G (capture stream) and all-reduce that slice on
+        the communication stream, forked from the capture stream at this point."""
         where = {}
         for bi, b in enumerate(self.buckets):
             b["left"], b["done"] = len(b["idx"]), False
@@ -396,14 +422,19 @@ class GraphedStep:
                 idx = b["idx"]
                 torch._foreach_copy_([self._gviews[i] for i in idx],
                                      [self._used[i].grad for i in idx])
-                b["event"].record()
+                self.comm.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(self.comm):
+                    dist.all_reduce(self.G[b["lo"]:b["hi"]])
                 b["done"] = True
         return [p.register_post_accumulate_grad_hook(hook) for p in self._used]
+
+    def _pack(self):
+        torch._foreach_copy_(self._gviews, [p.grad for p in self._used])
 
     def _tail(self, fork, pack=True):
         """Flat Adam step (+ the prefetched FPS handed over), inside a graph."""
         if pack:
-            torch._foreach_copy_(self._gviews, [p.grad for p in self._used])
+            self._pack()
         # an eager optimizer step in between advanced the per-parameter counters
         self._flat_step.copy_(self._steps[0])
         self.flat_opt.step()
@@ -425,8 +456,9 @@ class GraphedStep:
         return tuple(ts), tuple(t._version for t in ts)
 
     def _allreduce_eager(self):
-        """Warm-up path: the same averaging as the graphed step, eagerly."""
-        if self.world == 1:
+        """Warm-up path: the same averaging as the graphed step, eagerly (also initialises
+        the communicator before any capture)."""
+        if self.world == 1 and self.schedule != "overlap":
             return
         grads = [p.grad for p in self.params if p.grad is not None]
         flat = torch.cat([g.reshape(-1) for g in grads])
@@ -466,22 +498,13 @@ class GraphedStep:
                              else None)
         self.graph_a.replay()
         if self.graph_b is not None:
-            main = torch.cuda.current_stream()
-            # each all-reduce waits for its bucket's event in THIS replay of graph A (which
-            # runs after the previous replay's graph B on the main stream)
-            works = []
-            with torch.cuda.stream(self.comm):
-                for b in self.buckets:
-                    self.comm.wait_event(b["event"])
-                    works.append(dist.all_reduce(self.G[b["lo"]:b["hi"]], async_op=True))
-            for w in works:
-                w.wait()  # NCCL: the current (main) stream waits for the collective
-            main.wait_stream(self.comm)
+            dist.all_reduce(self.G)
             self.graph_b.replay()
         return self.loss.detach()
 
 
-def graphed_flow_step(model, optimizer, example_inputs, loss_fn=None, warmup=3, prefetch=True):
+def graphed_flow_step(model, optimizer, example_inputs, loss_fn=None, warmup=3, prefetch=True,
+                      overlap=None):
     """FlowTrainStep as a GraphedStep (model: the bare module, not DDP-wrapped).  prefetch:
     the next batch's FPS chain runs inside graph A on a forked stream (see GraphedStep)."""
     loss_fn = loss_fn or loss_functions.multiScaleLoss
@@ -492,11 +515,11 @@ def graphed_flow_step(model, optimizer, example_inputs, loss_fn=None, warmup=3, 
         flows, fps1, _, _, _, _, _, _ = model(pos1, pos2, pos1, pos2, **kw)
         return loss_fn(flows, flow, fps1)
     return GraphedStep(run, model.parameters(), optimizer, example_inputs, warmup,
-                       prefetch_fn=model.precompute_fps if prefetch else None)
+                       prefetch_fn=model.precompute_fps if prefetch else None, overlap=overlap)
 
 
 def graphed_kd_step(teacher, student, optimizer, example_inputs, gamma=0.3, beta=0.8, layer=3,
-                    warmup=3, prefetch=True):
+                    warmup=3, prefetch=True, overlap=None):
     """KDTrainStep (distilTrain.py:164-182) as a GraphedStep; teacher and student share the
     (prefetched) FPS chain, as KDTrainStep does."""
     for p in teacher.parameters():
@@ -514,4 +537,4 @@ def graphed_kd_step(teacher, student, optimizer, example_inputs, gamma=0.3, beta
             flows, feat1s, feat2s, fps1, fps2, flow, t_flows, t_feat1s, t_feat2s, t_fps1, t_fps2,
             gamma, beta, layer=layer)
     return GraphedStep(run, student.parameters(), optimizer, example_inputs, warmup,
-                       prefetch_fn=student.precompute_fps if prefetch else None)
+                       prefetch_fn=student.precompute_fps if prefetch else None, overlap=overlap)

@@ -1,10 +1,13 @@
-"""GraphedStep with world size 2 (the N>1 path of bench.py: graph A = fwd+bwd whose gradient
-buckets end in external events -> one async all-reduce per bucket on a side stream, each
-waiting only for its bucket -> graph B = mean + flat Adam) on ONE GPU: two processes share
-cuda:0 and talk over gloo (which accepts device tensors).  Each rank trains on its own
-batch; after the steps both ranks hold identical parameters, equal to a single-process eager
-step on the averaged gradient of the two batches -- for the flow step (configs[2]) and the KD
-step (configs[3], distilTrain.py:156-185)."""
+"""The multi-rank GraphedStep on ONE GPU.
+
+* world size 2 over gloo (two processes share cuda:0; gloo accepts device tensors): the
+  "serial" schedule (graph A fwd+bwd -> eager flat all-reduce -> graph B mean + flat Adam).
+  Each rank trains on its own batch; after the steps both ranks hold identical parameters,
+  equal to a single-process eager step on the averaged gradient of the two batches -- for
+  the flow step (configs[2]) and the KD step (configs[3], distilTrain.py:156-185).
+* the RCCL "overlap" schedule (bucketed all-reduces captured into the graph on a side stream
+  as the backward completes each bucket) with a one-rank `nccl` process group (RCCL refuses
+  two ranks on one device): the capture mechanics, bit-identical to the eager step."""
 import os
 import socket
 
@@ -45,7 +48,7 @@ def _worker(rank, port, out_dir, mode):
         step = graphed_kd_step(_teacher(), model, opt, mine[0], warmup=1)
     else:
         step = graphed_flow_step(model, opt, mine[0], warmup=1)
-    assert len(step.buckets) > 1  # the gradients really go out in several buckets
+    assert step.schedule == "serial"  # gloo collectives cannot be captured
     for i in (1, 2):
         step(*mine[i], next_batch=mine[i + 1] if i + 1 < len(mine) else None)
     torch.cuda.synchronize()
@@ -115,3 +118,55 @@ def test_graphed_step_world2_matches_averaged_eager(tmp_path, mode):
         scale = float(v.detach().abs().max()) + 1e-12
         worst = max(worst, d / scale)
     assert worst <= 1e-5, worst
+
+
+def _nccl_worker(port, out_dir, mode):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "kd-pointcloud_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    from distill import graphed_flow_step, graphed_kd_step, make_optimizer
+    from models_bid_pointconv import PointConvBidirection
+    torch.manual_seed(0)
+    model = PointConvBidirection().cuda()
+    opt = make_optimizer(model, capturable=True)
+    mine = _batches(0)
+    if mode == "kd":
+        step = graphed_kd_step(_teacher(), model, opt, mine[0], warmup=1, overlap=True)
+    else:
+        step = graphed_flow_step(model, opt, mine[0], warmup=1, overlap=True)
+    assert step.schedule == "overlap" and len(step.buckets) > 1, (step.schedule, step.buckets)
+    losses = [float(step(*mine[i], next_batch=mine[i + 1] if i + 1 < len(mine) else None))
+              for i in (1, 2)]
+    torch.cuda.synchronize()
+    torch.save({"params": {k: v.detach().cpu() for k, v in model.named_parameters()},
+                "losses": losses, "buckets": len(step.buckets)},
+               os.path.join(out_dir, "nccl.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["train", "kd"])
+def test_overlap_schedule_nccl_one_rank_equals_eager(tmp_path, mode):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "kd-pointcloud_amd"))
+    ctx = mp.get_context("spawn")
+    p = ctx.Process(target=_nccl_worker, args=(_free_port(), str(tmp_path), mode))
+    p.start()
+    p.join(timeout=240)
+    assert p.exitcode == 0, p.exitcode
+    got = torch.load(tmp_path / "nccl.pt", weights_only=True)
+    from distill import FlowTrainStep, KDTrainStep, make_optimizer
+    from models_bid_pointconv import PointConvBidirection
+    torch.manual_seed(0)
+    model = PointConvBidirection().cuda()
+    opt = make_optimizer(model, capturable=True)
+    eager = (KDTrainStep(_teacher(), model, opt) if mode == "kd" else FlowTrainStep(model, opt))
+    b = _batches(0)
+    eager(*b[0])
+    losses = [float(eager(*b[i])) for i in (1, 2)]
+    torch.cuda.synchronize()
+    assert losses == got["losses"], (losses, got["losses"])
+    for k, v in model.named_parameters():
+        assert torch.equal(v.detach().cpu(), got["params"][k]), k

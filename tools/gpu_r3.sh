@@ -11,7 +11,7 @@ TAG=${1:-a}
 SEL=()
 if [ -n "${K:-}" ]; then SEL=(-k "$K"); fi
 timeout -k 10 ${TEST_LIMIT:-600} python -u -m pytest tests -m gpu -v --timeout 300 \
-    --timeout-method thread "${SEL[@]}" > gpurun_out/r3_pytest_$TAG.log 2>&1
+    --timeout-method thread ${PYARGS:-} "${SEL[@]}" > gpurun_out/r3_pytest_$TAG.log 2>&1
 rc=$?
 tail -5 gpurun_out/r3_pytest_$TAG.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP pytest rc=$rc"; exit $rc; fi
