@@ -176,7 +176,8 @@ int kdpc_three_interpolate_grad_csr(int b, int c, int n, int m, const float *gra
 /* out[b,n,:] = max_k LeakyReLU(W1 LeakyReLU((P2[idx]+P1[n]) + Wpos(x2[idx]-x1[n]) + bpos) + b1)
  * x1 (B,N1,3), x2 (B,N2,3), idx (B,N1,K) int32, p1 (B,N1,Din), p2 (B,N2,Din), wpos (Din,3),
  * bpos (Din), w1 (Dout,Din), b1 (Dout) -> out (B,N1,Dout) channel-last, amax (B,N1,Dout) u8.
- * Din, Dout in {32,64}; 1 <= K <= 32. */
+ * Din, Dout in {32,64}, or Din = Dout in {128,256} (fused wide kernels: the Din x Dout MLP on
+ * the f32 matrix cores inside the same kernel); 1 <= K <= 32. */
 int kdpc_cost_volume_fwd(int b, int n1, int n2, int k, int din, int dout, const float *x1,
                          const float *x2, const int *idx, const float *p1, const float *p2,
                          const float *wpos, const float *bpos, const float *w1, const float *b1,
@@ -194,8 +195,9 @@ int kdpc_cost_volume_bwd(int b, int n1, int n2, int k, int din, int dout, const 
                          float *dp2_rows, float *dx1, float *ddir_rows, void *workspace,
                          size_t workspace_bytes, float *dparams, void *stream);
 
-/* ---- wide cost volume (same layers, Din in {64,128,256,512}): the Din -> Dout MLP GEMM
- *      stays a BLAS GEMM, everything around it is fused (csrc/cost_volume_wide.hip) ------ */
+/* ---- unfused wide cost volume (same layers, the widths kdpc_cost_volume_fwd does not take,
+ *      Din in {64,128,256,512}): the Din -> Dout MLP is the caller's BLAS GEMM between these
+ *      fused pieces (csrc/cost_volume_wide.hip) --------------------------------------- */
 
 int kdpc_cost_volume_wide_supported(int din, int dout, int k);
 

@@ -23,8 +23,9 @@
 //   dx1[n] = -sum_k d(dir_k)
 //   dW1, db1, dWpos, dbpos             (per-workgroup partial slabs in registers -> summed in a
 //                                       fixed order by a second kernel)
-// Supported: D_IN, D_OUT in {32, 64}, K <= 32 (the K=32 levels 0-1 of the models; the
-// small levels 2-3 with D >= 128 keep the unfused path).
+// Supported here: D_IN, D_OUT in {32, 64}, K <= 32 (the K=32 levels 0-1 of the models);
+// D_IN = D_OUT in {128, 256} (levels 2-3) dispatch to the fused wide kernels of
+// cost_volume_wide.hip (one workgroup per query stream, a 32-column block per wave).
 #include <algorithm>
 
 #include "kdpc_common.h"
@@ -482,8 +483,12 @@ hipError_t bwd_launch(int b, int n1, int n2, int k, const float* x1, const float
   return colsum(nslab, len, slab, dparams, slab + (size_t)nslab * len, st);
 }
 
-bool supported(int din, int dout, int k) {
+bool narrow(int din, int dout, int k) {
   return (din == 32 || din == 64) && (dout == 32 || dout == 64) && k >= 1 && k <= 32;
+}
+
+bool supported(int din, int dout, int k) {
+  return narrow(din, dout, k) || cost_volume_wide_fused_supported(din, dout, k);
 }
 
 }  // namespace
@@ -500,6 +505,9 @@ KDPC_API int kdpc_cost_volume_fwd(int b, int n1, int n2, int k, int din, int dou
   if ((long long)b * n1 == 0) return (int)hipSuccess;
   KDPC_CHECK_ARG(x1 && x2 && idx && p1 && p2 && wpos && bpos && w1 && b1 && out && amax);
   hipStream_t st = (hipStream_t)stream;
+  if (!narrow(din, dout, k))
+    return (int)cost_volume_wide_fused_fwd(b, n1, n2, k, din, x1, x2, idx, p1, p2, wpos, bpos, w1,
+                                           b1, out, amax, st);
 #define KDPC_CV_FWD(DI, DO)                                                                  \
   if (din == DI && dout == DO)                                                               \
     return (int)fwd_launch<DI, DO>(b, n1, n2, k, x1, x2, idx, p1, p2, wpos, bpos, w1, b1, out, \
@@ -515,6 +523,8 @@ KDPC_API int kdpc_cost_volume_fwd(int b, int n1, int n2, int k, int din, int dou
 // Scratch for the backward's per-workgroup parameter-gradient slabs.
 KDPC_API size_t kdpc_cost_volume_bwd_workspace_bytes(int b, int n1, int din, int dout) {
   if (b <= 0 || n1 <= 0 || !supported(din, dout, 1)) return 0;
+  if (!narrow(din, dout, 1))
+    return cost_volume_wide_fused_bwd_workspace_floats(b, n1, din) * sizeof(float);
   const long long nslabs = (long long)divup(n1, kWaves * bwd_qpw(b, n1)) * b;
   const int len = slab_len(din, dout);
   return (size_t)(nslabs * len + colsum_scratch_floats((int)nslabs, len)) * sizeof(float);
@@ -538,6 +548,10 @@ KDPC_API int kdpc_cost_volume_bwd(int b, int n1, int n2, int k, int din, int dou
   KDPC_CHECK_ARG(workspace_bytes >= kdpc_cost_volume_bwd_workspace_bytes(b, n1, din, dout));
   hipStream_t st = (hipStream_t)stream;
   float* slab = (float*)workspace;
+  if (!narrow(din, dout, k))
+    return (int)cost_volume_wide_fused_bwd(b, n1, n2, k, din, x1, x2, idx, p1, p2, wpos, bpos, w1,
+                                           out, amax, dout_grad, dp1, dp2_rows, dx1, ddir_rows,
+                                           slab, dparams, st);
 #define KDPC_CV_BWD(DI, DO)                                                                    \
   if (din == DI && dout == DO)                                                                 \
     return (int)bwd_launch<DI, DO>(b, n1, n2, k, x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, \

@@ -164,6 +164,629 @@ __global__ __launch_bounds__(256) void cvw_h0_bwd_kernel(int nq, int n1, int n2,
   }
 }
 
+// ===================================================================================
+// Fused wide cost volume, Din = Dout = D in {128, 256}, K <= 32: the whole
+//   gather -> position transform -> add -> LeakyReLU -> W1 (MFMA) -> LeakyReLU -> max over K
+// in one kernel, and the backward in one kernel, so neither h0 (rows x D) nor z1 ever
+// reaches HBM (the unfused path above writes and re-reads both, around two BLAS GEMMs).
+//
+// Workgroup = D/32 waves; wave w owns the 32-column block [32w, 32w+32) of the D x D MLP.
+// Queries are walked in a software pipeline: query q's 32 neighbour rows of h0 sit in one
+// of two LDS tiles while the next query's gathers (issued at the top of the iteration) land
+// and are turned into the other tile.  The 32 rows of the v_mfma_f32_32x32x2_f32 tile ARE
+// the query's neighbours: the max over K is a column reduction of the accumulator.
+// -----------------------------------------------------------------------------------
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr unsigned kOOB = 0x80000000u;  // out-of-range buffer offset: loads read 0, stores drop
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float bld(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ float4 bld4(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ f32x16 mfma4(float4 a, float4 b, f32x16 c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, c, 0, 0, 0);
+}
+
+template <int D>
+struct WideGeo {
+  static constexpr int NW = D / 32;      // waves per workgroup
+  static constexpr int NT = NW * 64;     // threads = 2D
+  static constexpr int LD = D + 4;       // LDS row stride (floats)
+  static constexpr int C4 = D / 4;       // float4 column groups
+  static constexpr int RG = NT / C4;     // row groups of the build / column passes (8)
+  static constexpr int RPT = 32 / RG;    // rows per thread (4)
+  static_assert(RG * RPT == 32, "build mapping");
+};
+
+// The gathered inputs of one query for this thread's build slots (rows rg + RG*i,
+// channels 4 c4 .. +3), loaded one query ahead.
+template <int D>
+struct WideLoads {
+  float4 p2[WideGeo<D>::RPT];
+  float x2[WideGeo<D>::RPT][3];
+  float4 p1;
+  float x1[3];
+};
+
+// Buffers over whole tensors (batch offsets folded into the byte offsets).
+struct WideSrc {
+  __amdgpu_buffer_rsrc_t x1, x2, idx, p1, p2;
+  int n1, n2, k, nq;
+};
+
+template <int D>
+__device__ __forceinline__ void wide_load_idx(const WideSrc& s, int q, int (&j)[WideGeo<D>::RPT],
+                                              int rg) {
+  using G = WideGeo<D>;
+  const bool live = q < s.nq;
+#pragma unroll
+  for (int i = 0; i < G::RPT; ++i) {
+    const int r = rg + G::RG * i;
+    const unsigned off = (live && r < s.k) ? ((unsigned)q * (unsigned)s.k + r) * 4u : kOOB;
+    j[i] = (int)__builtin_amdgcn_raw_buffer_load_b32(s.idx, (int)off, 0, 0);
+  }
+}
+
+template <int D>
+__device__ __forceinline__ void wide_load(const WideSrc& s, int q, const int (&j)[WideGeo<D>::RPT],
+                                          int rg, int c4, WideLoads<D>& L) {
+  using G = WideGeo<D>;
+  const bool live = q < s.nq;
+  const int b = live ? q / s.n1 : 0;
+#pragma unroll
+  for (int i = 0; i < G::RPT; ++i) {
+    const int r = rg + G::RG * i;
+    const bool ok = live && r < s.k;
+    const unsigned pt = (unsigned)b * (unsigned)s.n2 + (unsigned)j[i];
+    const unsigned po = ok ? (pt * D + 4u * c4) * 4u : kOOB;
+    L.p2[i] = bld4(s.p2, po);
+    const unsigned xo = ok ? pt * 12u : kOOB;
+    L.x2[i][0] = bld(s.x2, xo);
+    L.x2[i][1] = bld(s.x2, xo == kOOB ? kOOB : xo + 4u);
+    L.x2[i][2] = bld(s.x2, xo == kOOB ? kOOB : xo + 8u);
+  }
+  L.p1 = bld4(s.p1, live ? ((unsigned)q * D + 4u * c4) * 4u : kOOB);
+  const unsigned qo = live ? (unsigned)q * 12u : kOOB;
+  L.x1[0] = bld(s.x1, qo);
+  L.x1[1] = bld(s.x1, qo == kOOB ? kOOB : qo + 4u);
+  L.x1[2] = bld(s.x1, qo == kOOB ? kOOB : qo + 8u);
+}
+
+// h0 rows of the staged query into the LDS tile H (rows >= K are zero), same arithmetic as
+// cvw_h0_kernel / cost_volume.hip build_h0; directions into dirs[32] when asked.
+template <int D>
+__device__ __forceinline__ void wide_build(const WideLoads<D>& L, int k, int rg, int c4,
+                                           const float4* wposT, float* H, float4* dirs) {
+  using G = WideGeo<D>;
+  float wp[4][3], bp[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float4 v = wposT[4 * c4 + e];
+    wp[e][0] = v.x;
+    wp[e][1] = v.y;
+    wp[e][2] = v.z;
+    bp[e] = v.w;
+  }
+#pragma unroll
+  for (int i = 0; i < G::RPT; ++i) {
+    const int r = rg + G::RG * i;
+    const float dx = L.x2[i][0] - L.x1[0], dy = L.x2[i][1] - L.x1[1], dz = L.x2[i][2] - L.x1[2];
+    const float g[4] = {L.p2[i].x, L.p2[i].y, L.p2[i].z, L.p2[i].w};
+    const float p[4] = {L.p1.x, L.p1.y, L.p1.z, L.p1.w};
+    float h[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float pos = __fadd_rn(
+          __builtin_fmaf(wp[e][2], dz, __builtin_fmaf(wp[e][1], dy, __fmul_rn(wp[e][0], dx))), bp[e]);
+      h[e] = r < k ? lrelu(__fadd_rn(__fadd_rn(g[e], p[e]), pos)) : 0.f;
+    }
+    *reinterpret_cast<float4*>(H + r * G::LD + 4 * c4) = make_float4(h[0], h[1], h[2], h[3]);
+    if (dirs != nullptr && c4 == 0) dirs[r] = make_float4(dx, dy, dz, 0.f);
+  }
+}
+
+// (Wpos row, bpos) per channel into an LDS table: wposT[c] = (wx, wy, wz, b)
+template <int D>
+__device__ __forceinline__ void wide_consts(const float* __restrict__ wpos,
+                                            const float* __restrict__ bpos, float4* wposT) {
+  for (int c = threadIdx.x; c < D; c += blockDim.x)
+    wposT[c] = make_float4(wpos[c * 3 + 0], wpos[c * 3 + 1], wpos[c * 3 + 2], bpos[c]);
+}
+
+template <int D>
+__device__ __forceinline__ WideSrc wide_src(int b, int n1, int n2, int k, const float* x1,
+                                            const float* x2, const int* idx, const float* p1,
+                                            const float* p2) {
+  WideSrc s;
+  const long long nq = (long long)b * n1;
+  s.x1 = rsrc_of(x1, nq * 12);
+  s.x2 = rsrc_of(x2, (long long)b * n2 * 12);
+  s.idx = rsrc_of(idx, nq * k * 4);
+  s.p1 = rsrc_of(p1, nq * D * 4);
+  s.p2 = rsrc_of(p2, (long long)b * n2 * D * 4);
+  s.n1 = n1;
+  s.n2 = n2;
+  s.k = k;
+  s.nq = (int)nq;
+  return s;
+}
+
+// Forward.  grid.x workgroups, `qpw` consecutive queries each.
+template <int D>
+__global__ __launch_bounds__(2 * D) void cvw_fused_fwd_kernel(
+    int b, int n1, int n2, int k, int qpw, const float* __restrict__ x1,
+    const float* __restrict__ x2, const int* __restrict__ idx, const float* __restrict__ p1,
+    const float* __restrict__ p2, const float* __restrict__ wpos, const float* __restrict__ bpos,
+    const float* __restrict__ w1, const float* __restrict__ b1, float* __restrict__ out,
+    unsigned char* __restrict__ amax) {
+  using G = WideGeo<D>;
+  __shared__ __attribute__((aligned(16))) float Hs[2][32 * G::LD];
+  __shared__ __attribute__((aligned(16))) float4 wposT[D];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, half = lane >> 5, l32 = lane & 31;
+  const int c4 = t % G::C4, rg = t / G::C4;
+  const WideSrc s = wide_src<D>(b, n1, n2, k, x1, x2, idx, p1, p2);
+  const int q0 = blockIdx.x * qpw;
+  const int q1 = min(s.nq, q0 + qpw);
+  if (q0 >= q1) return;  // workgroup-uniform
+  wide_consts<D>(wpos, bpos, wposT);
+  // B fragments: lane supplies W1[32w + l32][8blk + 4half + 0..3] for MFMA block blk
+  float4 bw[D / 8];
+#pragma unroll
+  for (int blk = 0; blk < D / 8; ++blk)
+    bw[blk] = *reinterpret_cast<const float4*>(w1 + (long long)(32 * w + l32) * D + 8 * blk + 4 * half);
+  const float bias = b1[32 * w + l32];
+
+  int jn[G::RPT], jn2[G::RPT];
+  WideLoads<D> L;
+  wide_load_idx<D>(s, q0, jn, rg);
+  wide_load<D>(s, q0, jn, rg, c4, L);
+  wide_load_idx<D>(s, q0 + 1, jn2, rg);
+  __syncthreads();  // wposT
+  wide_build<D>(L, k, rg, c4, wposT, Hs[0], nullptr);
+  __syncthreads();
+  for (int q = q0; q < q1; ++q) {
+    const int p = (q - q0) & 1;
+    // next query's gathers (indices were loaded one iteration earlier), then q+2's indices
+#pragma unroll
+    for (int i = 0; i < G::RPT; ++i) jn[i] = jn2[i];
+    wide_load<D>(s, q + 1 < q1 ? q + 1 : s.nq, jn, rg, c4, L);
+    wide_load_idx<D>(s, q + 2 < q1 ? q + 2 : s.nq, jn2, rg);
+    const float* H = Hs[p];
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int blk = 0; blk < D / 8; ++blk) {
+      const float4 av = *reinterpret_cast<const float4*>(H + l32 * G::LD + 8 * blk + 4 * half);
+      acc = mfma4(av, bw[blk], acc);
+    }
+    // max over the query's rows (< k) in LeakyReLU space, first maximal row
+    float m = -INFINITY;
+    int mr = 0;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int row = (e & 3) + 8 * (e >> 2) + 4 * half;
+      const float v = lrelu(__fadd_rn(acc[e], bias));
+      if (row < k && v > m) {
+        m = v;
+        mr = row;
+      }
+    }
+    const float pm = __shfl_xor(m, 32, kWave);
+    const int pr = __shfl_xor(mr, 32, kWave);
+    if (pm > m || (pm == m && pr < mr)) {
+      m = pm;
+      mr = pr;
+    }
+    if (half == 0) {
+      out[(long long)q * D + 32 * w + l32] = m;
+      amax[(long long)q * D + 32 * w + l32] = (unsigned char)mr;
+    }
+    if (q + 1 < q1) wide_build<D>(L, k, rg, c4, wposT, Hs[p ^ 1], nullptr);
+    __syncthreads();
+  }
+}
+
+// Backward.  Per query: h0 rebuilt (LDS tile), g'[o] = dout * LReLU'(out) and the argmax
+// rows am[o]; dh0 = M W1 on the matrix cores (M[r][o] = g'[o] [am[o] == r]: one nonzero per
+// column, and the MFMA's fma chain over ascending o equals scattering g'[o] W1[o,:] into
+// row am[o] in ascending o); dW1[o,:] += g'[o] h0[am[o],:] on the VALU (1/32 of a dense
+// update); dz0 = dh0 * LReLU'(h0) in place; then per-row / per-channel passes write dP1,
+// the dP2 / d(dir) rows (summed per reference point by the caller through the CSR) and dx1,
+// and accumulate db1 / dWpos / dbpos.  Parameter gradients leave as one slab per workgroup
+// (summed in a fixed order by colsum: no float atomics).
+// B operand of dh0 (lane: W1[8blk + 4half + 0..3][32w + l32]): in registers for D = 128, read
+// per query from a transposed copy w1t (D x D, L2-resident) for D = 256 (the registers hold
+// the dW1 accumulators instead).
+template <int D>
+struct WideBwd {
+  static constexpr int OSPLIT = D <= 128 ? 1 : 2;  // dW1 o-halves (grid.y of the PART 2 kernel)
+  static constexpr bool BREG = D <= 128;
+  // the next query's gathers issued at the top of the iteration (held in registers across
+  // the MFMA phase) for D = 128; at D = 256 the dW1 accumulators need those registers
+  static constexpr bool PREFETCH = D <= 128;
+  static constexpr int OG = WideGeo<D>::NT / WideGeo<D>::C4;  // dW1 o-groups (8)
+  static constexpr int OPT = D / OG / OSPLIT;                   // o rows per thread
+  static constexpr int SLAB = D * D + D + 4 * D;                // dW1 | db1 | dWpos^T | dbpos
+};
+
+// PART: 0 = everything (D = 128), 1 = all but dW1 / db1, 2 = dW1 / db1 only (the D = 256
+// pair: the dW1 accumulators and the rest do not fit one wave's 256 registers together)
+template <int D, int PART>
+__global__ __launch_bounds__(2 * D) void cvw_fused_bwd_kernel(
+    int b, int n1, int n2, int k, int qpw, const float* __restrict__ x1,
+    const float* __restrict__ x2, const int* __restrict__ idx, const float* __restrict__ p1,
+    const float* __restrict__ p2, const float* __restrict__ wpos, const float* __restrict__ bpos,
+    const float* __restrict__ w1, const float* __restrict__ w1t, const float* __restrict__ out,
+    const unsigned char* __restrict__ amax, const float* __restrict__ dout,
+    float* __restrict__ dp1, float* __restrict__ dp2_rows, float* __restrict__ dx1,
+    float* __restrict__ ddir_rows, float* __restrict__ slab) {
+  using G = WideGeo<D>;
+  using W = WideBwd<D>;
+  constexpr int NG2 = G::NT / 32;  // channel groups of the direction pass
+  constexpr int CPG = D / NG2;     // channels per group
+  constexpr bool MAIN = PART != 2, DW1 = PART != 1;
+  __shared__ __attribute__((aligned(16))) float Hs[2][32 * G::LD];
+  __shared__ __attribute__((aligned(16))) float4 dirs[2][32];
+  __shared__ __attribute__((aligned(16))) float2 gam[2][D];   // (g', argmax row) per output
+  __shared__ __attribute__((aligned(16))) float4 red[G::RG][G::C4];  // dP1 partials
+  __shared__ __attribute__((aligned(16))) float4 red2[NG2][32];      // d(dir) partials
+  __shared__ __attribute__((aligned(16))) float4 wposT[D];           // Wpos rows (x, y, z, 0)
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, half = lane >> 5, l32 = lane & 31;
+  const int c4 = t % G::C4, rg = t / G::C4;
+  const WideSrc s = wide_src<D>(b, n1, n2, k, x1, x2, idx, p1, p2);
+  const int q0 = blockIdx.x * qpw;
+  const int q1 = min(s.nq, q0 + qpw);
+  float* sb = slab + (long long)blockIdx.x * W::SLAB;
+  const int obase = DW1 ? (int)blockIdx.y * (D / W::OSPLIT) : 0;  // this launch's dW1 rows
+  if (q0 >= q1) {  // every slab row is written (this PART's entries)
+    for (int e = t; e < W::SLAB; e += G::NT) {
+      const bool dw = e < D * D ? (e / D - obase >= 0 && e / D - obase < D / W::OSPLIT)
+                                : (e < D * D + D && blockIdx.y == 0);
+      if (dw ? DW1 : (MAIN && e >= D * D + D)) sb[e] = 0.f;
+    }
+    return;
+  }
+  const __amdgpu_buffer_rsrc_t outr = rsrc_of(out, (long long)s.nq * D * 4);
+  const __amdgpu_buffer_rsrc_t dor = rsrc_of(dout, (long long)s.nq * D * 4);
+  const __amdgpu_buffer_rsrc_t amr = rsrc_of(amax, (long long)s.nq * D);
+  wide_consts<D>(wpos, bpos, wposT);
+  float4 bt[W::BREG && MAIN ? D / 8 : 1];
+  if constexpr (W::BREG && MAIN) {
+#pragma unroll
+    for (int blk = 0; blk < D / 8; ++blk) {
+      const int o = 8 * blk + 4 * half;
+      const int c = 32 * w + l32;
+      bt[blk] = make_float4(w1[(long long)(o + 0) * D + c], w1[(long long)(o + 1) * D + c],
+                            w1[(long long)(o + 2) * D + c], w1[(long long)(o + 3) * D + c]);
+    }
+  }
+  const float* w1row = w1t + (long long)(32 * w + l32) * D + 4 * half;  // streamed B (D = 256)
+  // accumulators: dW1 rows o = og*OPT + i at channels 4 c4 .. +3 (og = rg), db1 (t < D),
+  // dWpos / dbpos at (rg rows, channels 4 c4 .. +3)
+  float4 gw[DW1 ? W::OPT : 1];
+#pragma unroll
+  for (int i = 0; i < (DW1 ? W::OPT : 1); ++i) gw[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  float gb1 = 0.f;
+  float4 gwp[3], gbp = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) gwp[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+
+  // per-output loads of a query: g' and argmax for outputs o = t (t < D)
+  float ov = 0.f, dv = 0.f;
+  unsigned av = 0;
+  auto load_out = [&](int q) {
+    const bool ok = q < s.nq && t < D;
+    const unsigned oo = (unsigned)q * D + t;
+    ov = bld(outr, ok ? oo * 4u : kOOB);
+    dv = bld(dor, ok ? oo * 4u : kOOB);
+    av = __builtin_amdgcn_raw_buffer_load_b8(amr, (int)(ok ? oo : kOOB), 0, 0);
+  };
+  auto stage_out = [&](int p) {
+    if (t < D) gam[p][t] = make_float2(ov > 0.f ? dv : dv * kSlope, __int_as_float((int)av));
+  };
+
+  int jn[G::RPT], jn2[G::RPT];
+  WideLoads<D> L;
+  wide_load_idx<D>(s, q0, jn, rg);
+  wide_load<D>(s, q0, jn, rg, c4, L);
+  load_out(q0);
+  wide_load_idx<D>(s, q0 + 1, jn2, rg);
+  __syncthreads();  // wposT
+  wide_build<D>(L, k, rg, c4, wposT, Hs[0], dirs[0]);
+  stage_out(0);
+  __syncthreads();
+  for (int q = q0; q < q1; ++q) {
+    const int p = (q - q0) & 1;
+    const bool more = q + 1 < q1;
+    auto next_loads = [&]() {
+#pragma unroll
+      for (int i = 0; i < G::RPT; ++i) jn[i] = jn2[i];
+      wide_load<D>(s, more ? q + 1 : s.nq, jn, rg, c4, L);
+      load_out(more ? q + 1 : s.nq);
+      wide_load_idx<D>(s, q + 2 < q1 ? q + 2 : s.nq, jn2, rg);
+    };
+    if constexpr (W::PREFETCH) next_loads();  // in flight under this query's MFMAs
+    float* H = Hs[p];
+    const float2* ga = gam[p];
+    // ---- dh0 = M W1 (rows = neighbours, columns 32w .. +31 of Din)
+    f32x16 dacc;
+    if constexpr (MAIN) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) dacc[e] = 0.f;
+    constexpr int PF = 4;  // streamed B blocks in flight (D = 256)
+    float4 bq[W::BREG ? 1 : PF];
+    if constexpr (!W::BREG) {
+#pragma unroll
+      for (int i = 0; i < PF; ++i) bq[i] = *reinterpret_cast<const float4*>(w1row + 8 * i);
+    }
+#pragma unroll
+    for (int blk = 0; blk < D / 8; ++blk) {
+      const float4 g01 = *reinterpret_cast<const float4*>(ga + 8 * blk + 4 * half);
+      const float4 g23 = *reinterpret_cast<const float4*>(ga + 8 * blk + 4 * half + 2);
+      float4 a;
+      a.x = __float_as_int(g01.y) == l32 ? g01.x : 0.f;
+      a.y = __float_as_int(g01.w) == l32 ? g01.z : 0.f;
+      a.z = __float_as_int(g23.y) == l32 ? g23.x : 0.f;
+      a.w = __float_as_int(g23.w) == l32 ? g23.z : 0.f;
+      if constexpr (W::BREG) {
+        dacc = mfma4(a, bt[blk], dacc);
+      } else {
+        dacc = mfma4(a, bq[blk % PF], dacc);
+        if (blk + PF < D / 8) bq[blk % PF] = *reinterpret_cast<const float4*>(w1row + 8 * (blk + PF));
+      }
+      // one block's LDS reads ahead at most (hoisting them all held 8 registers per block)
+      if (blk % 2 == 1) __builtin_amdgcn_sched_barrier(0);
+    }
+    }  // MAIN
+    // ---- dW1[o, 4c4..] += g'[o] h0[am[o], 4c4..] for this thread's o rows; db1
+    if constexpr (DW1) {
+#pragma unroll
+    for (int i = 0; i < W::OPT; ++i) {
+      const float2 g = ga[obase + rg * W::OPT + i];
+      const float4 hv = *reinterpret_cast<const float4*>(H + __float_as_int(g.y) * G::LD + 4 * c4);
+      gw[i].x = __builtin_fmaf(g.x, hv.x, gw[i].x);
+      gw[i].y = __builtin_fmaf(g.x, hv.y, gw[i].y);
+      gw[i].z = __builtin_fmaf(g.x, hv.z, gw[i].z);
+      gw[i].w = __builtin_fmaf(g.x, hv.w, gw[i].w);
+      if (i % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // bound the hoisted LDS reads
+    }
+    if (t < D && blockIdx.y == 0) gb1 = __fadd_rn(gb1, ga[t].x);
+    }  // DW1
+    __syncthreads();  // every read of h0 done
+    if constexpr (MAIN) {
+    // ---- dz0 = dh0 * LeakyReLU'(h0), in place (accumulator layout)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int a = ((e & 3) + 8 * (e >> 2) + 4 * half) * G::LD + 32 * w + l32;
+      const float hv = H[a];
+      H[a] = dacc[e] * (hv > 0.f ? 1.f : kSlope);
+    }
+    __syncthreads();
+    // ---- column pass: dP2 rows out, dP1 partials, dWpos / dbpos
+    {
+      float4 sp = make_float4(0.f, 0.f, 0.f, 0.f);
+      float* d2 = dp2_rows + (long long)q * k * D + 4 * c4;
+#pragma unroll
+      for (int i = 0; i < G::RPT; ++i) {
+        const int r = rg + G::RG * i;
+        const float4 v = *reinterpret_cast<const float4*>(H + r * G::LD + 4 * c4);
+        const float4 dr = dirs[p][r];
+        if (r < k) *reinterpret_cast<float4*>(d2 + (long long)r * D) = v;
+        sp.x = __fadd_rn(sp.x, v.x);
+        sp.y = __fadd_rn(sp.y, v.y);
+        sp.z = __fadd_rn(sp.z, v.z);
+        sp.w = __fadd_rn(sp.w, v.w);
+        const float dd[3] = {dr.x, dr.y, dr.z};
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          gwp[j].x = __builtin_fmaf(v.x, dd[j], gwp[j].x);
+          gwp[j].y = __builtin_fmaf(v.y, dd[j], gwp[j].y);
+          gwp[j].z = __builtin_fmaf(v.z, dd[j], gwp[j].z);
+          gwp[j].w = __builtin_fmaf(v.w, dd[j], gwp[j].w);
+        }
+      }
+      red[rg][c4] = sp;
+    }
+    // ---- direction pass: d(dir_r) = Wpos^T dz0[r], partial over channel group g2
+    {
+      const int r = t & 31, g2 = t >> 5;
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+#pragma unroll 4
+      for (int i = 0; i < CPG / 4; ++i) {
+        const int c = g2 * CPG + 4 * i;
+        const float4 v = *reinterpret_cast<const float4*>(H + r * G::LD + c);
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float4 wq = wposT[c + e];
+          a0 = __builtin_fmaf(wq.x, vv[e], a0);
+          a1 = __builtin_fmaf(wq.y, vv[e], a1);
+          a2 = __builtin_fmaf(wq.z, vv[e], a2);
+        }
+      }
+      red2[g2][r] = make_float4(a0, a1, a2, 0.f);
+    }
+    // ---- the next query's tile (other buffer) from the loads issued at the top
+    }  // MAIN
+    if constexpr (!W::PREFETCH) next_loads();
+    if (more) {
+      wide_build<D>(L, k, rg, c4, wposT, Hs[p ^ 1], dirs[p ^ 1]);
+      stage_out(p ^ 1);
+    }
+    __syncthreads();
+    // ---- per-query sums in a fixed order: dP1 (threads of row group 0), d(dir) rows + dx1
+    if (MAIN && rg == 0) {
+      float4 v = red[0][c4];
+#pragma unroll
+      for (int g = 1; g < G::RG; ++g) {
+        const float4 x = red[g][c4];
+        v.x = __fadd_rn(v.x, x.x);
+        v.y = __fadd_rn(v.y, x.y);
+        v.z = __fadd_rn(v.z, x.z);
+        v.w = __fadd_rn(v.w, x.w);
+      }
+      *reinterpret_cast<float4*>(dp1 + (long long)q * D + 4 * c4) = v;
+      gbp.x = __fadd_rn(gbp.x, v.x);
+      gbp.y = __fadd_rn(gbp.y, v.y);
+      gbp.z = __fadd_rn(gbp.z, v.z);
+      gbp.w = __fadd_rn(gbp.w, v.w);
+    }
+    if (MAIN && w == G::NW - 1 && half == 0) {  // one half-wave: lane l32 = neighbour row
+      float4 v = red2[0][l32];
+#pragma unroll
+      for (int g = 1; g < NG2; ++g) {
+        const float4 x = red2[g][l32];
+        v.x = __fadd_rn(v.x, x.x);
+        v.y = __fadd_rn(v.y, x.y);
+        v.z = __fadd_rn(v.z, x.z);
+      }
+      const bool row = l32 < k;
+      if (row) {
+        float* dd = ddir_rows + ((long long)q * k + l32) * 3;
+        dd[0] = v.x;
+        dd[1] = v.y;
+        dd[2] = v.z;
+      }
+      float s0 = row ? v.x : 0.f, s1 = row ? v.y : 0.f, s2 = row ? v.z : 0.f;
+#pragma unroll
+      for (int m = 16; m >= 1; m >>= 1) {
+        s0 = __fadd_rn(s0, __shfl_xor(s0, m, kWave));
+        s1 = __fadd_rn(s1, __shfl_xor(s1, m, kWave));
+        s2 = __fadd_rn(s2, __shfl_xor(s2, m, kWave));
+      }
+      if (l32 == 0) {
+        float* o = dx1 + (long long)q * 3;
+        o[0] = -s0;
+        o[1] = -s1;
+        o[2] = -s2;
+      }
+    }
+  }
+  // ---- workgroup slab: dW1 (o, c) | db1 | dWpos^T (x, y, z rows) | dbpos; the dWpos partials
+  // of the row groups are folded in row-group order through LDS
+  if constexpr (DW1) {
+#pragma unroll
+    for (int i = 0; i < W::OPT; ++i)
+      *reinterpret_cast<float4*>(sb + (long long)(obase + rg * W::OPT + i) * D + 4 * c4) = gw[i];
+    if (t < D && blockIdx.y == 0) sb[D * D + t] = gb1;
+  }
+  if constexpr (!MAIN) return;
+  __syncthreads();
+  float4* fold = reinterpret_cast<float4*>(&Hs[0][0]);  // [RG][3][C4]
+#pragma unroll
+  for (int j = 0; j < 3; ++j) fold[(rg * 3 + j) * G::C4 + c4] = gwp[j];
+  __syncthreads();
+  if (rg == 0) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      float4 v = fold[j * G::C4 + c4];
+      for (int g = 1; g < G::RG; ++g) {
+        const float4 x = fold[(g * 3 + j) * G::C4 + c4];
+        v.x = __fadd_rn(v.x, x.x);
+        v.y = __fadd_rn(v.y, x.y);
+        v.z = __fadd_rn(v.z, x.z);
+        v.w = __fadd_rn(v.w, x.w);
+      }
+      *reinterpret_cast<float4*>(sb + D * D + D + j * D + 4 * c4) = v;
+    }
+    *reinterpret_cast<float4*>(sb + D * D + 4 * D + 4 * c4) = gbp;
+  }
+}
+
+// w1 (D, D) -> w1t = w1^T (the streamed B operand of the D = 256 backward)
+__global__ __launch_bounds__(256) void cvw_transpose_kernel(int d, const float* __restrict__ w1,
+                                                            float* __restrict__ w1t) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e < d * d) w1t[e] = w1[(e % d) * d + e / d];
+}
+
+inline int fused_qpw(long long nq) {  // ~512 workgroups
+  return (int)std::max<long long>(2, divupll(nq, 512));
+}
+
+}  // namespace
+
+namespace kdpc {
+
+bool cost_volume_wide_fused_supported(int din, int dout, int k) {
+  return din == dout && (din == 128 || din == 256) && k >= 1 && k <= 32;
+}
+
+hipError_t cost_volume_wide_fused_fwd(int b, int n1, int n2, int k, int d, const float* x1,
+                                      const float* x2, const int* idx, const float* p1,
+                                      const float* p2, const float* wpos, const float* bpos,
+                                      const float* w1, const float* b1, float* out,
+                                      unsigned char* amax, hipStream_t st) {
+  const long long nq = (long long)b * n1;
+  const int qpw = fused_qpw(nq);
+  const dim3 grid((unsigned)divupll(nq, qpw));
+  if (d == 128)
+    hipLaunchKernelGGL(cvw_fused_fwd_kernel<128>, grid, dim3(256), 0, st, b, n1, n2, k, qpw, x1,
+                       x2, idx, p1, p2, wpos, bpos, w1, b1, out, amax);
+  else
+    hipLaunchKernelGGL(cvw_fused_fwd_kernel<256>, grid, dim3(512), 0, st, b, n1, n2, k, qpw, x1,
+                       x2, idx, p1, p2, wpos, bpos, w1, b1, out, amax);
+  return hipGetLastError();
+}
+
+size_t cost_volume_wide_fused_bwd_workspace_floats(int b, int n1, int d) {
+  const long long nq = (long long)b * n1;
+  const long long nwg = divupll(nq, fused_qpw(nq));
+  const long long len = (long long)d * d + 5 * d;
+  return (size_t)(nwg * len + colsum_scratch_floats((int)nwg, len) + (long long)d * d);
+}
+
+hipError_t cost_volume_wide_fused_bwd(int b, int n1, int n2, int k, int d, const float* x1,
+                                      const float* x2, const int* idx, const float* p1,
+                                      const float* p2, const float* wpos, const float* bpos,
+                                      const float* w1, const float* out,
+                                      const unsigned char* amax, const float* dout, float* dp1,
+                                      float* dp2_rows, float* dx1, float* ddir_rows, float* ws,
+                                      float* dparams, hipStream_t st) {
+  const long long nq = (long long)b * n1;
+  const int qpw = fused_qpw(nq);
+  const int nwg = (int)divupll(nq, qpw);
+  const long long len = (long long)d * d + 5 * d;
+  float* slab = ws;
+  float* scratch = ws + (long long)nwg * len;
+  float* w1t = scratch + colsum_scratch_floats(nwg, len);
+  if (d == 128) {
+    hipLaunchKernelGGL((cvw_fused_bwd_kernel<128, 0>), dim3(nwg), dim3(256), 0, st, b, n1, n2, k,
+                       qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, w1t, out, amax, dout, dp1,
+                       dp2_rows, dx1, ddir_rows, slab);
+  } else {
+    hipLaunchKernelGGL(cvw_transpose_kernel, dim3(divup(d * d, 256)), dim3(256), 0, st, d, w1,
+                       w1t);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((cvw_fused_bwd_kernel<256, 1>), dim3(nwg), dim3(512), 0, st, b, n1, n2, k,
+                       qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, w1t, out, amax, dout, dp1,
+                       dp2_rows, dx1, ddir_rows, slab);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL((cvw_fused_bwd_kernel<256, 2>), dim3(nwg, WideBwd<256>::OSPLIT), dim3(512),
+                       0, st, b, n1, n2, k,
+                       qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, w1t, out, amax, dout, dp1,
+                       dp2_rows, dx1, ddir_rows, slab);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return colsum(nwg, len, slab, dparams, scratch, st);
+}
+
+}  // namespace kdpc
+
+namespace {
 }  // namespace
 
 // ------------------------------------------------------------------------------ C ABI

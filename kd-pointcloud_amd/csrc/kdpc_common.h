@@ -77,6 +77,23 @@ size_t colsum_scratch_floats(int nrows, long long len);
 hipError_t colsum(int nrows, long long len, const float* slab, float* dst, float* scratch,
                   hipStream_t st);
 
+// Fused wide cost volume (csrc/cost_volume_wide.hip): Din = Dout = d in {128, 256}, K <= 32;
+// dispatched by kdpc_cost_volume_fwd / _bwd (csrc/cost_volume.hip).
+bool cost_volume_wide_fused_supported(int din, int dout, int k);
+hipError_t cost_volume_wide_fused_fwd(int b, int n1, int n2, int k, int d, const float* x1,
+                                      const float* x2, const int* idx, const float* p1,
+                                      const float* p2, const float* wpos, const float* bpos,
+                                      const float* w1, const float* b1, float* out,
+                                      unsigned char* amax, hipStream_t st);
+size_t cost_volume_wide_fused_bwd_workspace_floats(int b, int n1, int d);
+hipError_t cost_volume_wide_fused_bwd(int b, int n1, int n2, int k, int d, const float* x1,
+                                      const float* x2, const int* idx, const float* p1,
+                                      const float* p2, const float* wpos, const float* bpos,
+                                      const float* w1, const float* out,
+                                      const unsigned char* amax, const float* dout, float* dp1,
+                                      float* dp2_rows, float* dx1, float* ddir_rows, float* ws,
+                                      float* dparams, hipStream_t st);
+
 }  // namespace kdpc
 
 // Argument validation shared by every C entry point: a bad size is an error code,

@@ -396,7 +396,11 @@ def three_interpolate_grad(grad_out, idx, weight, m):
 
 # ------------------------------------------------------------------ fused cost volume
 def cost_volume_supported(din, dout, k):
-    return din in (32, 64) and dout in (32, 64) and 1 <= k <= 32
+    """Shapes of the fused cost-volume kernels: Din, Dout in {32, 64} (cost_volume.hip), or
+    Din = Dout in {128, 256} (the fused wide kernels of cost_volume_wide.hip); K <= 32."""
+    narrow = din in (32, 64) and dout in (32, 64)
+    wide = din == dout and din in (128, 256)
+    return (narrow or wide) and 1 <= k <= 32
 
 
 def cost_volume_fwd(x1, x2, idx, p1, p2, wpos, bpos, w1, b1):

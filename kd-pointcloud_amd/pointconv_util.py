@@ -565,7 +565,6 @@ def set_amax_override(fn):
     global _amax_override
     prev, _amax_override = _amax_override, fn
     return prev
-_WIDE_MIN_DIN = 128  # Din=64 through the wide path measured within noise (311.8 vs 309.9 pairs/s)
 
 
 def _fusable(nsample, pos, mlp, act, din):
@@ -579,12 +578,10 @@ def _fusable(nsample, pos, mlp, act, din):
         return False
     if pos.bias is None:
         return False
-    if din >= _WIDE_MIN_DIN and _nat.cost_volume_wide_supported(din, conv.out_channels, nsample):
-        return _CostVolumeWide
     if _nat.cost_volume_supported(din, conv.out_channels, nsample):
-        return _CostVolume
+        return _CostVolume  # one fused kernel forward, one backward
     if _nat.cost_volume_wide_supported(din, conv.out_channels, nsample):
-        return _CostVolumeWide
+        return _CostVolumeWide  # fused kernels around a BLAS GEMM (other widths)
     return False
 
 

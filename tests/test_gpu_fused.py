@@ -15,22 +15,22 @@ def _scale_close(a, b, rtol=1e-5, name="", floor=1e-6):
     assert err <= tol, (name, err, tol)
 
 
-@pytest.mark.parametrize("din,dout,n1,n2,bsz", [(32, 32, 1000, 900, 2), (64, 64, 513, 700, 3),
-                                                (32, 64, 300, 300, 1), (64, 32, 257, 600, 2),
-                                                (128, 128, 300, 280, 2), (256, 256, 200, 250, 2),
-                                                (128, 256, 130, 140, 1)])
-def test_cost_volume_fused_equals_unfused(din, dout, n1, n2, bsz):
+@pytest.mark.parametrize("din,dout,n1,n2,bsz,k", [
+    (32, 32, 1000, 900, 2, 32), (64, 64, 513, 700, 3, 32), (32, 64, 300, 300, 1, 32),
+    (64, 32, 257, 600, 2, 32), (128, 128, 300, 280, 2, 32), (256, 256, 200, 250, 2, 32),
+    (128, 128, 1025, 900, 3, 20), (256, 256, 3, 40, 1, 32), (128, 256, 130, 140, 1, 32)])
+def test_cost_volume_fused_equals_unfused(din, dout, n1, n2, bsz, k):
     import pointconv_util as P
     import synthetic
     torch.manual_seed(din + dout + n1)
-    layer = P.CrossLayerLight(32, din + 5, [din, dout], [dout, dout]).to(DEV)
+    layer = P.CrossLayerLight(k, din + 5, [din, dout], [dout, dout]).to(DEV)
     x1 = torch.from_numpy(synthetic.ft3d_batch(bsz, n1, seed=1)[0]).to(DEV).permute(0, 2, 1)
     x2 = torch.from_numpy(synthetic.ft3d_batch(bsz, n2, seed=2)[0]).to(DEV).permute(0, 2, 1)
     f1 = torch.randn(bsz, din, n1, device=DEV)
     f2 = torch.randn(bsz, din, n2, device=DEV)
     import kdpc_native
-    wide = not kdpc_native.cost_volume_supported(din, dout, 32)
-    assert P._fusable(32, layer.pos1, layer.mlp1, layer._act(layer.bn1), din) is (
+    wide = not kdpc_native.cost_volume_supported(din, dout, k)
+    assert P._fusable(k, layer.pos1, layer.mlp1, layer._act(layer.bn1), din) is (
         P._CostVolumeWide if wide else P._CostVolume)
     outs, grads = [], []
     for fused in (True, False):
