@@ -1317,6 +1317,198 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
     }
 }
 
+// Warp-specialised weight-gradient kernel.  In pc_bwd_weight_kernel every wave runs both
+// phases of a row tile (its MFMAs, then its share of the next tile's A build) between
+// workgroup barriers, so the two waves sharing a SIMD -- same workgroup, same barriers -- run
+// their MFMA phases together (the matrix core serialises them) and their build phases
+// together (the matrix core idles): round-2 stamps, 26 % MFMA issue per wave.  Here waves 0-3
+// only multiply and waves 4-7 only load and build, one per SIMD each: while a consumer wave
+// streams its MFMAs for tile t, the producer wave of the same SIMD gathers tile t+2 and builds
+// tile t+1's A block into the other LDS buffer; one barrier per tile.
+//   consumer wave c: the 32 A columns 32c..32c+31 of the chunk x all O/32 row tiles of dy^T
+//                    (O/32 accumulators), inner index = the tile's 32 rows;
+//   producer thread: (row r, 4 channels 4cq.., 4 weights 4wq..): A[r][c][w] = sum_k G wt over
+//                    its own gathered G / wt float4 (no LDS staging), dy rows -> dy^T in LDS.
+// Same rows, same inner order (rows 8gb+j / 8gb+4+j per MFMA block, tiles in order) and the
+// same fma chains as pc_bwd_weight_kernel: bit-identical dwl.
+template <int O, int KM, bool EX>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+void pc_bwd_weight_ws_kernel(Geo g, const float* __restrict__ wt, const float* __restrict__ dy,
+                             float* __restrict__ dwl, int rows_per_split, int nsplit, int xcd_map) {
+  constexpr int TR = 32;                   // rows per tile (MFMA inner dimension)
+  constexpr int TS = TR + 4;               // row stride of the transposed tiles
+  constexpr int MT = O / 32;               // dy^T row tiles = accumulators per consumer wave
+  constexpr int DV = TR * O / (256 * 4);   // dy float4 slots per producer thread
+  static_assert(DV >= 1 && TR * O % 1024 == 0, "dy tile must split into float4 slots");
+  __shared__ __attribute__((aligned(16))) float dyt[2][O * TS];
+  __shared__ __attribute__((aligned(16))) float at[2][kNC * TS];
+
+  const int L = blockIdx.x;
+  int ch, split;
+  if (xcd_map) {  // as pc_bwd_weight_kernel: a split's chunks on one or two XCDs
+    const int per_xcd = (int)gridDim.x >> 3;
+    const int pidx = (L & 7) * per_xcd + (L >> 3);
+    split = pidx / g.nch;
+    ch = pidx % g.nch;
+  } else {
+    ch = L % g.nch;
+    split = L / g.nch;
+  }
+  if (split >= nsplit) return;
+  const int c0 = ch * kCC;
+  const int kk = EX ? KM : g.k;
+  const int rbeg = split * rows_per_split;
+  const int rend = min(g.r, rbeg + rows_per_split);
+  const int ntiles = (rend - rbeg + TR - 1) / TR;
+  if (ntiles <= 0) return;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, half = lane >> 5, l32 = lane & 31;
+  const bool consumer = wv < 4;  // wave-uniform
+  const long long c16 = (long long)g.c * kW;
+
+  f32x16 acc[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) acc[i] = zero16();
+
+  // ---- producer state: thread pt -> (row r, channel quad cq, weight quad wq)
+  const int pt = t - 256;
+  const int pr = (pt >> 3) & 31, cq = (pt >> 2) & 1, wq = pt & 3;
+  const Srcs src = srcs_of(g);
+  const __amdgpu_buffer_rsrc_t idx_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<int*>(g.idx), (short)0, (int)((long long)g.r * g.k * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wt_rs = rsrc(wt, (long long)g.r * kk * kW);
+  const __amdgpu_buffer_rsrc_t dy_rs = rsrc(dy, (long long)g.r * O);
+  int nb_nx[KM];          // neighbour rows (b*N + idx, -1 for none) of the tile being loaded
+  f32x4 gq[KM], wq4[KM];  // gathered G (4 channels) and wt (4 weights) per neighbour
+  float4 dq[DV];          // dy slots
+  auto load_idx = [&](int tile, int (&nb)[KM]) {
+    const int row = rbeg + tile * TR + pr;
+    const bool ok = tile < ntiles && row < rend;
+    const int base = ok ? (row / g.s) * g.n : 0;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      const bool kv = ok && k < kk;
+      const unsigned off = kv ? ((unsigned)row * (unsigned)g.k + (unsigned)k) * 4u : kOOB;
+      const int j = (int)__builtin_amdgcn_raw_buffer_load_b32(idx_rs, (int)off, 0, 0);
+      nb[k] = kv ? base + j : -1;
+    }
+  };
+  // every load unconditional (out-of-range offsets read 0): no branch splits the load queue
+  auto load_tile = [&](int tile, const int (&nbs)[KM]) {
+    const int row = rbeg + tile * TR + pr;
+    const bool ok = tile < ntiles && row < rend;
+    const bool xyzq = c0 == 0 && cq == 0;   // chunk 0, channels 0..3 = xyz - center, feature 0
+    const int vch = c0 == 0 ? (cq ? 1 : 0) : c0 - 3 + 4 * cq;  // first feature of the load
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      const int nb = nbs[k];
+      const bool live = nb >= 0;
+      const unsigned voff = live ? (unsigned)nb * (unsigned)g.d * 4u + (unsigned)vch * 4u : kOOB;
+      const unsigned xoff = (xyzq && live) ? (unsigned)nb * 12u : kOOB;
+      const unsigned coff = (xyzq && live) ? (unsigned)row * 12u : kOOB;
+      const f32x4 v = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(src.feats, (int)voff, 0, 0));
+      const f32x4 x = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(src.xyz, (int)xoff, 0, 0));
+      const f32x4 cc = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(src.center, (int)coff, 0, 0));
+      const int cg = c0 + 4 * cq;
+      const float a0 = xyzq ? 0.f : (cg < g.c ? v[0] : 0.f);
+      const float a1 = xyzq ? 0.f : (cg + 1 < g.c ? v[1] : 0.f);
+      const float a2 = xyzq ? 0.f : (cg + 2 < g.c ? v[2] : 0.f);
+      const float a3 = xyzq ? (3 < g.c ? v[0] : 0.f) : (cg + 3 < g.c ? v[3] : 0.f);
+      gq[k] = f32x4{a0 + (x[0] - cc[0]), a1 + (x[1] - cc[1]), a2 + (x[2] - cc[2]), a3};
+      const unsigned woff = (ok && k < kk) ? (((unsigned)row * (unsigned)kk + k) * kW + 4u * wq) * 4u : kOOB;
+      wq4[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wt_rs, (int)woff, 0, 0));
+    }
+    // dy slot i: row (pt & 31), columns 4 ((pt >> 5) + 8 i) .. +3 (lanes = consecutive rows)
+#pragma unroll
+    for (int i = 0; i < DV; ++i) {
+      const int rw = rbeg + tile * TR + (pt & 31);
+      const int q = (pt >> 5) + 8 * i;
+      const unsigned off = (tile < ntiles && rw < rend) ? ((unsigned)rw * O + 4u * (unsigned)q) * 4u : kOOB;
+      dq[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(dy_rs, (int)off, 0, 0));
+    }
+  };
+  auto build = [&](int buf) {  // registers -> dy^T and A block of buffer buf
+    float* dt = dyt[buf];
+#pragma unroll
+    for (int i = 0; i < DV; ++i) {
+      const int r = pt & 31, o = 4 * ((pt >> 5) + 8 * i);
+      dt[(o + 0) * TS + r] = dq[i].x;
+      dt[(o + 1) * TS + r] = dq[i].y;
+      dt[(o + 2) * TS + r] = dq[i].z;
+      dt[(o + 3) * TS + r] = dq[i].w;
+    }
+    float a[4][4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int w = 0; w < 4; ++w) a[c][w] = 0.f;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      if (k < kk) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int w = 0; w < 4; ++w) a[c][w] = __builtin_fmaf(gq[k][c], wq4[k][w], a[c][w]);
+      }
+    }
+    float* ab = at[buf];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int w = 0; w < 4; ++w) ab[((4 * cq + c) * kW + 4 * wq + w) * TS + pr] = a[c][w];
+  };
+
+  // The two roles run separate loops with the same barrier sequence (one per tile), so
+  // their registers (accumulators vs. in-flight gathers) are never live at the same time.
+  if (!consumer) {
+    // prologue: tile 0 built, tile 1's loads in flight, tile 2's indices
+    load_idx(0, nb_nx);
+    load_tile(0, nb_nx);
+    build(0);
+    load_idx(1, nb_nx);
+    load_tile(1, nb_nx);
+    load_idx(2, nb_nx);
+    __syncthreads();
+    for (int tile = 0; tile < ntiles; ++tile) {
+      if (tile + 1 < ntiles) {
+        build((tile & 1) ^ 1);        // tile + 1 (its loads were issued one iteration ago)
+        load_tile(tile + 2, nb_nx);   // tile + 2 (indices loaded one iteration ago)
+        load_idx(tile + 3, nb_nx);
+      }
+      __syncthreads();
+    }
+    return;
+  }
+  __syncthreads();
+  for (int tile = 0; tile < ntiles; ++tile) {
+    const int cur = tile & 1;
+    const float* dt = dyt[cur];
+    const float* ab = at[cur];
+#pragma unroll
+    for (int gb = 0; gb < TR / 8; ++gb) {
+      const float4 bv = *reinterpret_cast<const float4*>(ab + (wv * 32 + l32) * TS + 8 * gb + 4 * half);
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const float4 av = *reinterpret_cast<const float4*>(dt + (i * 32 + l32) * TS + 8 * gb + 4 * half);
+        acc[i] = mfma4(av, bv, acc[i]);
+      }
+    }
+    __syncthreads();
+  }
+  const long long col = (long long)c0 * kW + wv * 32 + l32;
+  if (col >= c16) return;
+  float* dst = dwl + (long long)split * O * c16;  // slab index when the rows are split
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int o = i * 32 + (e & 3) + 8 * (e >> 2) + 4 * half;
+      dst[o * c16 + col] = acc[i][e];
+    }
+}
+
 // ------------------------------------------------------------------------------- host
 struct Plan {
   int r, c, nch, c8, tm, rt;  // tm: forward tile rows
@@ -1460,12 +1652,32 @@ hipError_t bwd_launch(const Geo& g, const Plan& p, int b, const float* wt, const
                      dim3((unsigned)std::min<long long>(divupll(work, 256), 1 << 20)), dim3(256),
                      0, st, npts, rk, g.c, p.c8, g.d, dgr, offsets, perm, dxyz, dfeats);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  if (g.k == KM)
+  // the specialised kernel for K <= 9 (the scene-flow estimators' layers); at K = 16 its
+  // producers' in-flight gathers (2 x 16 float4) do not fit beside the rest
+  static const bool ws_env = [] {  // KDPC_PC_WGT_WS=0: the unspecialised kernel (A/B runs)
+    const char* v = getenv("KDPC_PC_WGT_WS");
+    return !(v && v[0] == '0');
+  }();
+  float* wdst = p.rs > 1 ? dwl_slab : dwl;
+  bool done = false;
+  if constexpr (KM <= 9) {
+    if (ws_env) {
+      if (g.k == KM)
+        hipLaunchKernelGGL((pc_bwd_weight_ws_kernel<O, KM, true>), dim3(p.wgs), dim3(512), 0, st,
+                           g, wt, dy, wdst, p.rps, p.rs, p.xcd);
+      else
+        hipLaunchKernelGGL((pc_bwd_weight_ws_kernel<O, KM, false>), dim3(p.wgs), dim3(512), 0, st,
+                           g, wt, dy, wdst, p.rps, p.rs, p.xcd);
+      done = true;
+    }
+  }
+  if (done) {
+  } else if (g.k == KM)
     hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM, true>), dim3(p.wgs), dim3(512), 0, st, g, wt,
-                       dy, p.rs > 1 ? dwl_slab : dwl, p.rps, p.rs, p.xcd);
+                       dy, wdst, p.rps, p.rs, p.xcd);
   else
     hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM, false>), dim3(p.wgs), dim3(512), 0, st, g, wt,
-                       dy, p.rs > 1 ? dwl_slab : dwl, p.rps, p.rs, p.xcd);
+                       dy, wdst, p.rps, p.rs, p.xcd);
   if ((e = hipGetLastError()) != hipSuccess || p.rs == 1) return e;
   return slab_sum(p.rs, (long long)O * g.c * kW, dwl_slab, nullptr, 1, dwl, st);
 }
