@@ -1377,31 +1377,39 @@ void pc_bwd_weight_ws_kernel(Geo g, const float* __restrict__ wt, const float* _
       const_cast<int*>(g.idx), (short)0, (int)((long long)g.r * g.k * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t wt_rs = rsrc(wt, (long long)g.r * kk * kW);
   const __amdgpu_buffer_rsrc_t dy_rs = rsrc(dy, (long long)g.r * O);
-  int nb_nx[KM];          // neighbour rows (b*N + idx, -1 for none) of the tile being loaded
+  int nb_nx[KM];          // raw kNN indices of the tile whose gathers are issued next
+  int nb_base = 0;        // its row's b*N (kNoNbr when the row is past the split)
   f32x4 gq[KM], wq4[KM];  // gathered G (4 channels) and wt (4 weights) per neighbour
   float4 dq[DV];          // dy slots
-  auto load_idx = [&](int tile, int (&nb)[KM]) {
+  // The raw indices stay untouched until the next tile's gathers need them: adding the
+  // batch base right after the loads made the wave wait for them -- and, loads retiring in
+  // issue order, for the tile's gathers issued just before -- ahead of every barrier.
+  constexpr int kNoNbr = 1 << 30;
+  auto load_idx = [&](int tile, int (&nb)[KM], int& nbase) {
     const int row = rbeg + tile * TR + pr;
     const bool ok = tile < ntiles && row < rend;
-    const int base = ok ? (row / g.s) * g.n : 0;
+    // unconditional division, then selects: a division under the condition became a branch
+    const unsigned bq = (unsigned)row / (unsigned)g.s;
+    nbase = ok ? (int)bq * g.n : kNoNbr;
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
-      const bool kv = ok && k < kk;
-      const unsigned off = kv ? ((unsigned)row * (unsigned)g.k + (unsigned)k) * 4u : kOOB;
-      const int j = (int)__builtin_amdgcn_raw_buffer_load_b32(idx_rs, (int)off, 0, 0);
-      nb[k] = kv ? base + j : -1;
+      unsigned off = (ok && k < kk) ? ((unsigned)row * (unsigned)g.k + (unsigned)k) * 4u : kOOB;
+      // opaque to the optimiser: with the condition the same for every k it unswitched the
+      // selects into a branch per load (and a vmcnt(0) drain behind each)
+      asm volatile("" : "+v"(off));
+      nb[k] = (int)__builtin_amdgcn_raw_buffer_load_b32(idx_rs, (int)off, 0, 0);
     }
   };
   // every load unconditional (out-of-range offsets read 0): no branch splits the load queue
-  auto load_tile = [&](int tile, const int (&nbs)[KM]) {
+  auto load_tile = [&](int tile, const int (&nbs)[KM], int nbase) {
     const int row = rbeg + tile * TR + pr;
     const bool ok = tile < ntiles && row < rend;
     const bool xyzq = c0 == 0 && cq == 0;   // chunk 0, channels 0..3 = xyz - center, feature 0
     const int vch = c0 == 0 ? (cq ? 1 : 0) : c0 - 3 + 4 * cq;  // first feature of the load
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
-      const int nb = nbs[k];
-      const bool live = nb >= 0;
+      const int nb = (k < kk ? nbase : kNoNbr) + nbs[k];
+      const bool live = (unsigned)nb < (unsigned)g.bn;
       const unsigned voff = live ? (unsigned)nb * (unsigned)g.d * 4u + (unsigned)vch * 4u : kOOB;
       const unsigned xoff = (xyzq && live) ? (unsigned)nb * 12u : kOOB;
       const unsigned coff = (xyzq && live) ? (unsigned)row * 12u : kOOB;
@@ -1464,18 +1472,18 @@ void pc_bwd_weight_ws_kernel(Geo g, const float* __restrict__ wt, const float* _
   // their registers (accumulators vs. in-flight gathers) are never live at the same time.
   if (!consumer) {
     // prologue: tile 0 built, tile 1's loads in flight, tile 2's indices
-    load_idx(0, nb_nx);
-    load_tile(0, nb_nx);
+    load_idx(0, nb_nx, nb_base);
+    load_tile(0, nb_nx, nb_base);
     build(0);
-    load_idx(1, nb_nx);
-    load_tile(1, nb_nx);
-    load_idx(2, nb_nx);
+    load_idx(1, nb_nx, nb_base);
+    load_tile(1, nb_nx, nb_base);
+    load_idx(2, nb_nx, nb_base);
     __syncthreads();
     for (int tile = 0; tile < ntiles; ++tile) {
       if (tile + 1 < ntiles) {
         build((tile & 1) ^ 1);        // tile + 1 (its loads were issued one iteration ago)
-        load_tile(tile + 2, nb_nx);   // tile + 2 (indices loaded one iteration ago)
-        load_idx(tile + 3, nb_nx);
+        load_tile(tile + 2, nb_nx, nb_base);   // tile + 2 (indices loaded one iteration ago)
+        load_idx(tile + 3, nb_nx, nb_base);
       }
       __syncthreads();
     }
