@@ -1327,8 +1327,9 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
 // tile t+1's A block into the other LDS buffer; one barrier per tile.
 //   consumer wave c: the 32 A columns 32c..32c+31 of the chunk x all O/32 row tiles of dy^T
 //                    (O/32 accumulators), inner index = the tile's 32 rows;
-//   producer thread: (row r, 4 channels 4cq.., 4 weights 4wq..): A[r][c][w] = sum_k G wt over
-//                    its own gathered G / wt float4 (no LDS staging), dy rows -> dy^T in LDS.
+//   producer thread: (row r, 4 channels 4cq.., 4 weights 4wq..): A[r][c][w] = sum_k G wt, G
+//                    gathered once per wave into its own LDS region, wt in registers; dy rows
+//                    -> dy^T in LDS.
 // Same rows, same inner order (rows 8gb+j / 8gb+4+j per MFMA block, tiles in order) and the
 // same fma chains as pc_bwd_weight_kernel: bit-identical dwl.
 template <int O, int KM, bool EX>
@@ -1342,6 +1343,7 @@ void pc_bwd_weight_ws_kernel(Geo g, const float* __restrict__ wt, const float* _
   static_assert(DV >= 1 && TR * O % 1024 == 0, "dy tile must split into float4 slots");
   __shared__ __attribute__((aligned(16))) float dyt[2][O * TS];
   __shared__ __attribute__((aligned(16))) float at[2][kNC * TS];
+  __shared__ __attribute__((aligned(16))) float gls[4][8 * KM * kCC];  // producer waves' G
 
   const int L = blockIdx.x;
   int ch, split;
@@ -1369,47 +1371,60 @@ void pc_bwd_weight_ws_kernel(Geo g, const float* __restrict__ wt, const float* _
 #pragma unroll
   for (int i = 0; i < MT; ++i) acc[i] = zero16();
 
-  // ---- producer state: thread pt -> (row r, channel quad cq, weight quad wq)
+  // ---- producer state: thread pt -> (row r, channel quad cq, weight quad wq).  Producer
+  // wave pw owns rows 8pw .. 8pw+7 of the tile: it gathers their neighbours' chunk channels
+  // once (slot = (row, neighbour, channel half), 16 bytes, as pc_bwd_weight_kernel), stages
+  // them in a private LDS region and reads them back broadcast to the four weight-quad lanes
+  // of each row -- only this wave touches the region, so no workgroup barrier is needed
+  // between its write and its read (an lgkmcnt wait, and the wave's own LDS order).
   const int pt = t - 256;
+  const int pw = (pt >> 6) & 3, pl = pt & 63;
   const int pr = (pt >> 3) & 31, cq = (pt >> 2) & 1, wq = pt & 3;
+  constexpr int NPAIR = 8 * KM;                 // (row, neighbour) pairs per producer wave
+  constexpr int GSW = (2 * NPAIR + 63) / 64;    // gather slots (float4) per lane
+  float* glw = gls[pw];
   const Srcs src = srcs_of(g);
   const __amdgpu_buffer_rsrc_t idx_rs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<int*>(g.idx), (short)0, (int)((long long)g.r * g.k * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t wt_rs = rsrc(wt, (long long)g.r * kk * kW);
   const __amdgpu_buffer_rsrc_t dy_rs = rsrc(dy, (long long)g.r * O);
-  int nb_nx[KM];          // raw kNN indices of the tile whose gathers are issued next
-  int nb_base = 0;        // its row's b*N (kNoNbr when the row is past the split)
-  f32x4 gq[KM], wq4[KM];  // gathered G (4 channels) and wt (4 weights) per neighbour
-  float4 dq[DV];          // dy slots
-  // The raw indices stay untouched until the next tile's gathers need them: adding the
-  // batch base right after the loads made the wave wait for them -- and, loads retiring in
-  // issue order, for the tile's gathers issued just before -- ahead of every barrier.
+  // The raw indices stay untouched until the gathers that need them: adding the batch base
+  // right after the loads made the wave wait for them -- and, loads retiring in issue order,
+  // for the gathers issued just before -- ahead of every barrier.
   constexpr int kNoNbr = 1 << 30;
-  auto load_idx = [&](int tile, int (&nb)[KM], int& nbase) {
-    const int row = rbeg + tile * TR + pr;
-    const bool ok = tile < ntiles && row < rend;
-    // unconditional division, then selects: a division under the condition became a branch
-    const unsigned bq = (unsigned)row / (unsigned)g.s;
-    nbase = ok ? (int)bq * g.n : kNoNbr;
+  int sj[GSW];                 // raw kNN index of each gather slot (tile being loaded next)
+  int sbase[GSW];              // its row's b*N, kNoNbr for none
+  f32x4 gsl[GSW];              // gathered slots (tile in flight)
+  f32x4 wq4[KM];               // wt (4 weights) per neighbour
+  float4 dq[DV];               // dy slots
+  auto load_idx = [&](int tile) {
 #pragma unroll
-    for (int k = 0; k < KM; ++k) {
-      unsigned off = (ok && k < kk) ? ((unsigned)row * (unsigned)g.k + (unsigned)k) * 4u : kOOB;
-      // opaque to the optimiser: with the condition the same for every k it unswitched the
-      // selects into a branch per load (and a vmcnt(0) drain behind each)
+    for (int i = 0; i < GSW; ++i) {
+      const int sl = pl + 64 * i, pair = sl >> 1;
+      const int rr = pair / KM, k = pair - rr * KM;
+      const int row = rbeg + tile * TR + 8 * pw + rr;
+      const bool ok = sl < 2 * NPAIR && tile < ntiles && row < rend && k < kk;
+      // unconditional division, then selects (a division under the condition became a branch)
+      const unsigned bq = (unsigned)row / (unsigned)g.s;
+      sbase[i] = ok ? (int)bq * g.n : kNoNbr;
+      unsigned off = ok ? ((unsigned)row * (unsigned)g.k + (unsigned)k) * 4u : kOOB;
+      // opaque to the optimiser: it unswitched the selects into a branch per load (and a
+      // vmcnt(0) drain behind each)
       asm volatile("" : "+v"(off));
-      nb[k] = (int)__builtin_amdgcn_raw_buffer_load_b32(idx_rs, (int)off, 0, 0);
+      sj[i] = (int)__builtin_amdgcn_raw_buffer_load_b32(idx_rs, (int)off, 0, 0);
     }
   };
   // every load unconditional (out-of-range offsets read 0): no branch splits the load queue
-  auto load_tile = [&](int tile, const int (&nbs)[KM], int nbase) {
-    const int row = rbeg + tile * TR + pr;
-    const bool ok = tile < ntiles && row < rend;
-    const bool xyzq = c0 == 0 && cq == 0;   // chunk 0, channels 0..3 = xyz - center, feature 0
-    const int vch = c0 == 0 ? (cq ? 1 : 0) : c0 - 3 + 4 * cq;  // first feature of the load
+  auto load_tile = [&](int tile) {
 #pragma unroll
-    for (int k = 0; k < KM; ++k) {
-      const int nb = (k < kk ? nbase : kNoNbr) + nbs[k];
+    for (int i = 0; i < GSW; ++i) {
+      const int sl = pl + 64 * i, pair = sl >> 1, h4 = sl & 1;
+      const int rr = pair / KM;
+      const int row = rbeg + tile * TR + 8 * pw + rr;
+      const int nb = sbase[i] + sj[i];
       const bool live = (unsigned)nb < (unsigned)g.bn;
+      const bool xyzq = c0 == 0 && h4 == 0;  // chunk 0, channels 0..3 = xyz - center, feat 0
+      const int vch = c0 == 0 ? (h4 ? 1 : 0) : c0 - 3 + 4 * h4;  // first feature of the load
       const unsigned voff = live ? (unsigned)nb * (unsigned)g.d * 4u + (unsigned)vch * 4u : kOOB;
       const unsigned xoff = (xyzq && live) ? (unsigned)nb * 12u : kOOB;
       const unsigned coff = (xyzq && live) ? (unsigned)row * 12u : kOOB;
@@ -1419,12 +1434,17 @@ void pc_bwd_weight_ws_kernel(Geo g, const float* __restrict__ wt, const float* _
           f32x4, __builtin_amdgcn_raw_buffer_load_b128(src.xyz, (int)xoff, 0, 0));
       const f32x4 cc = __builtin_bit_cast(
           f32x4, __builtin_amdgcn_raw_buffer_load_b128(src.center, (int)coff, 0, 0));
-      const int cg = c0 + 4 * cq;
+      const int cg = c0 + 4 * h4;
       const float a0 = xyzq ? 0.f : (cg < g.c ? v[0] : 0.f);
       const float a1 = xyzq ? 0.f : (cg + 1 < g.c ? v[1] : 0.f);
       const float a2 = xyzq ? 0.f : (cg + 2 < g.c ? v[2] : 0.f);
       const float a3 = xyzq ? (3 < g.c ? v[0] : 0.f) : (cg + 3 < g.c ? v[3] : 0.f);
-      gq[k] = f32x4{a0 + (x[0] - cc[0]), a1 + (x[1] - cc[1]), a2 + (x[2] - cc[2]), a3};
+      gsl[i] = f32x4{a0 + (x[0] - cc[0]), a1 + (x[1] - cc[1]), a2 + (x[2] - cc[2]), a3};
+    }
+    const int row = rbeg + tile * TR + pr;
+    const bool ok = tile < ntiles && row < rend;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
       const unsigned woff = (ok && k < kk) ? (((unsigned)row * (unsigned)kk + k) * kW + 4u * wq) * 4u : kOOB;
       wq4[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wt_rs, (int)woff, 0, 0));
     }
@@ -1437,7 +1457,12 @@ void pc_bwd_weight_ws_kernel(Geo g, const float* __restrict__ wt, const float* _
       dq[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(dy_rs, (int)off, 0, 0));
     }
   };
-  auto build = [&](int buf) {  // registers -> dy^T and A block of buffer buf
+  auto build = [&](int buf) {  // registers -> this wave's G region, dy^T and A of buffer buf
+#pragma unroll
+    for (int i = 0; i < GSW; ++i) {
+      const int sl = pl + 64 * i;
+      if (sl < 2 * NPAIR) *reinterpret_cast<f32x4*>(glw + 4 * sl) = gsl[i];
+    }
     float* dt = dyt[buf];
 #pragma unroll
     for (int i = 0; i < DV; ++i) {
@@ -1447,18 +1472,22 @@ void pc_bwd_weight_ws_kernel(Geo g, const float* __restrict__ wt, const float* _
       dt[(o + 2) * TS + r] = dq[i].z;
       dt[(o + 3) * TS + r] = dq[i].w;
     }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's G stores have landed
+    __builtin_amdgcn_wave_barrier();
     float a[4][4];
 #pragma unroll
     for (int c = 0; c < 4; ++c)
 #pragma unroll
       for (int w = 0; w < 4; ++w) a[c][w] = 0.f;
+    const int rr = pr & 7;
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
       if (k < kk) {
+        const f32x4 gv = *reinterpret_cast<const f32x4*>(glw + ((rr * KM + k) * 2 + cq) * 4);
 #pragma unroll
         for (int c = 0; c < 4; ++c)
 #pragma unroll
-          for (int w = 0; w < 4; ++w) a[c][w] = __builtin_fmaf(gq[k][c], wq4[k][w], a[c][w]);
+          for (int w = 0; w < 4; ++w) a[c][w] = __builtin_fmaf(gv[c], wq4[k][w], a[c][w]);
       }
     }
     float* ab = at[buf];
@@ -1472,18 +1501,18 @@ void pc_bwd_weight_ws_kernel(Geo g, const float* __restrict__ wt, const float* _
   // their registers (accumulators vs. in-flight gathers) are never live at the same time.
   if (!consumer) {
     // prologue: tile 0 built, tile 1's loads in flight, tile 2's indices
-    load_idx(0, nb_nx, nb_base);
-    load_tile(0, nb_nx, nb_base);
+    load_idx(0);
+    load_tile(0);
     build(0);
-    load_idx(1, nb_nx, nb_base);
-    load_tile(1, nb_nx, nb_base);
-    load_idx(2, nb_nx, nb_base);
+    load_idx(1);
+    load_tile(1);
+    load_idx(2);
     __syncthreads();
     for (int tile = 0; tile < ntiles; ++tile) {
       if (tile + 1 < ntiles) {
         build((tile & 1) ^ 1);        // tile + 1 (its loads were issued one iteration ago)
-        load_tile(tile + 2, nb_nx, nb_base);   // tile + 2 (indices loaded one iteration ago)
-        load_idx(tile + 3, nb_nx, nb_base);
+        load_tile(tile + 2);   // tile + 2 (indices loaded one iteration ago)
+        load_idx(tile + 3);
       }
       __syncthreads();
     }

@@ -44,19 +44,17 @@ def main():
     torch.cuda.synchronize()
     kdpc_native.set_launch_timer(None)
     summ = timer.summary()
-    pmc = {}
-    if os.path.exists(bench.PMC_FILE):
-        pmc = json.load(open(bench.PMC_FILE))["entries"]
+    wl = bench.workload_key("train", args.batch, args.npoints)
     out = {"workload": f"PointConvBidirection train step B={args.batch} N={args.npoints}, "
                        f"{args.steps} eager steps", "entries": {}}
     for name, (bound, unit, peak, kernels) in bench.ROOFLINE.items():
         s = summ.get(name)
         if not s:
             continue
-        r = bench.roofline(name, s)
+        r = bench.roofline_obj(name, wl, s["ms"], s["launches"], s["bytes"], s["flops"])
         alg = r["algorithmic_bytes_per_launch"]
-        if name in pmc:
-            r["traffic_over_algorithmic"] = round(pmc[name]["hbm_bytes_per_launch"] / alg, 3)
+        if r["traffic"] is not None and alg:
+            r["traffic_over_algorithmic"] = round(r["traffic"] / alg, 3)
         r["launches_per_step"] = s["launches"] / args.steps
         r["ms_per_step"] = round(s["ms"] / args.steps, 3)
         out["entries"][name] = r

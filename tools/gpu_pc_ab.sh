@@ -11,13 +11,13 @@ if [ -n "${PRE:-}" ]; then
   timeout -k 10 300 bash -c "$PRE" > gpurun_out/pre_$TAG.log 2>&1 || { echo "STOP pre"; cat gpurun_out/pre_$TAG.log | tail -20; exit 1; }
   tail -40 gpurun_out/pre_$TAG.log
 fi
-KDPC_PC_WGT_WS=0 timeout -k 10 200 python -u tools/bench_pointconv.py --dump gpurun_out/pc_old.npz > gpurun_out/pc_old_$TAG.log 2>&1 || { echo "STOP old"; tail gpurun_out/pc_old_$TAG.log; exit 1; }
-KDPC_PC_WGT_WS=1 timeout -k 10 200 python -u tools/bench_pointconv.py --dump gpurun_out/pc_new.npz > gpurun_out/pc_new_$TAG.log 2>&1 || { echo "STOP new"; tail gpurun_out/pc_new_$TAG.log; exit 1; }
+KDPC_PC_WGT_WS=0 timeout -k 10 200 python -u tools/bench_pointconv.py --dump /tmp/pc_old.npz > gpurun_out/pc_old_$TAG.log 2>&1 || { echo "STOP old"; tail gpurun_out/pc_old_$TAG.log; exit 1; }
+KDPC_PC_WGT_WS=1 timeout -k 10 200 python -u tools/bench_pointconv.py --dump /tmp/pc_new.npz > gpurun_out/pc_new_$TAG.log 2>&1 || { echo "STOP new"; tail gpurun_out/pc_new_$TAG.log; exit 1; }
 echo "== old"; cat gpurun_out/pc_old_$TAG.log | grep -v amdgpu.ids
 echo "== new"; cat gpurun_out/pc_new_$TAG.log | grep -v amdgpu.ids
 python - <<'PY'
 import numpy as np
-a = np.load("gpurun_out/pc_old.npz"); b = np.load("gpurun_out/pc_new.npz")
+a = np.load("/tmp/pc_old.npz"); b = np.load("/tmp/pc_new.npz")
 for k in a.files:
     same = np.array_equal(a[k], b[k])
     d = float(np.abs(a[k].astype(np.float64) - b[k]).max()) if not same else 0.0
