@@ -156,6 +156,12 @@ size_t kdpc_csr_workspace_bytes(int b, int n, int p);
 int kdpc_csr_build(int b, int n, int p, const int *idx, void *workspace, size_t workspace_bytes,
                    int *offsets, int *perm, void *stream);
 
+/* Inverse permutation of that CSR: rank (B*P), perm[rank[i]] == i (the slot of position i),
+ * -1 where idx[i] is outside [0,N).  Lets a producer write per-position rows straight into
+ * CSR order (kdpc_cost_volume_bwd_csr). */
+int kdpc_csr_rank(int b, int n, int p, const int *idx, const int *offsets, const int *perm,
+                  int *rank, void *stream);
+
 /* grad_points[b,n,:] = sum of grad_out rows (B,P,C) that idx sent to n, ascending position. */
 int kdpc_group_rows_grad_csr(int b, int n, int c, const float *grad_out, const int *offsets,
                              const int *perm, float *grad_points, void *stream);
@@ -194,6 +200,20 @@ int kdpc_cost_volume_bwd(int b, int n1, int n2, int k, int din, int dout, const 
                          const unsigned char *amax, const float *dout_grad, float *dp1,
                          float *dp2_rows, float *dx1, float *ddir_rows, void *workspace,
                          size_t workspace_bytes, float *dparams, void *stream);
+
+/* Backward with the per-reference-point sums done inside: offsets (B*N2+1) / rank (B*N1*K)
+ * of the CSR of idx over the N2 points (kdpc_csr_build + kdpc_csr_rank).  The per-neighbour
+ * rows are written in CSR order into the workspace and summed contiguously:
+ * dp2 (B,N2,Din), dx2 (B,N2,3); dp1, dx1, dparams as kdpc_cost_volume_bwd.  Bit-identical to
+ * kdpc_cost_volume_bwd followed by kdpc_group_rows_grad_csr of its rows (same sum order). */
+size_t kdpc_cost_volume_bwd_csr_workspace_bytes(int b, int n1, int k, int din, int dout);
+int kdpc_cost_volume_bwd_csr(int b, int n1, int n2, int k, int din, int dout, const float *x1,
+                             const float *x2, const int *idx, const float *p1, const float *p2,
+                             const float *wpos, const float *bpos, const float *w1,
+                             const float *out, const unsigned char *amax,
+                             const float *dout_grad, const int *offsets, const int *rank,
+                             float *dp1, float *dp2, float *dx1, float *dx2, void *workspace,
+                             size_t workspace_bytes, float *dparams, void *stream);
 
 /* ---- unfused wide cost volume (same layers, the widths kdpc_cost_volume_fwd does not take,
  *      Din in {64,128,256,512}): the Din -> Dout MLP is the caller's BLAS GEMM between these

@@ -42,66 +42,17 @@ constexpr int kWaves = 4;        // per workgroup
 
 __device__ __forceinline__ float lrelu(float x) { return x > 0.f ? x : x * kSlope; }
 
-// Build h0 (and keep nothing else) for query n into lds_h[kRows][D_IN+1].
-// Lane roles: per pass, lanes cover (rows, channels): RPP = 64 / D_IN rows per pass.
-template <int D_IN>
-__device__ __forceinline__ void build_h0(int n, int k, const float* __restrict__ x1b,
-                                         const float* __restrict__ x2b,
-                                         const int* __restrict__ idxb,
-                                         const float* __restrict__ p1b,
-                                         const float* __restrict__ p2b,
-                                         const float* __restrict__ wpos,
-                                         const float* __restrict__ bpos, float* lds_h,
-                                         int& my_j, float& my_dx, float& my_dy, float& my_dz) {
-  constexpr int LD = D_IN + 1;
-  constexpr int RPP = 64 / D_IN;  // 2 for D_IN=32, 1 for 64
-  const int lane = lane_id();
-  // lane r (< k) owns neighbour row r: index and direction
-  const float qx = x1b[n * 3 + 0], qy = x1b[n * 3 + 1], qz = x1b[n * 3 + 2];
-  my_j = 0;
-  my_dx = my_dy = my_dz = 0.f;
-  if (lane < k) {
-    my_j = idxb[(long long)n * k + lane];
-    my_dx = x2b[my_j * 3 + 0] - qx;
-    my_dy = x2b[my_j * 3 + 1] - qy;
-    my_dz = x2b[my_j * 3 + 2] - qz;
-  }
-  const int c = lane % D_IN;
-  const int sub = lane / D_IN;  // row offset inside a pass
-  const float p1 = p1b[(long long)n * D_IN + c];
-  const float w0 = wpos[c * 3 + 0], w1 = wpos[c * 3 + 1], w2 = wpos[c * 3 + 2];
-  const float bp = bpos[c];
-  // row broadcasts by readlane (uniform lane index: SGPR, no LDS round trip); the loop is
-  // unrolled so all of the query's neighbour gathers are in flight together
-#pragma unroll
-  for (int r0 = 0; r0 < kRows; r0 += RPP) {
-    const int r = r0 + sub;
-    const int ja = __builtin_amdgcn_readlane(my_j, r0);
-    const float dxa = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_dx), r0));
-    const float dya = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_dy), r0));
-    const float dza = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_dz), r0));
-    int j = ja;
-    float dx = dxa, dy = dya, dz = dza;
-    if (RPP == 2) {
-      const int jb = __builtin_amdgcn_readlane(my_j, r0 + 1);
-      const float dxb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_dx), r0 + 1));
-      const float dyb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_dy), r0 + 1));
-      const float dzb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_dz), r0 + 1));
-      j = sub ? jb : ja;
-      dx = sub ? dxb : dxa;
-      dy = sub ? dyb : dya;
-      dz = sub ? dzb : dza;
-    }
-    float h = 0.f;
-    if (r < k) {
-      const float g2 = p2b[(long long)j * D_IN + c];
-      const float pos = __fadd_rn(__builtin_fmaf(w2, dz, __builtin_fmaf(w1, dy, __fmul_rn(w0, dx))), bp);
-      h = lrelu(__fadd_rn(__fadd_rn(g2, p1), pos));
-    }
-    lds_h[r * LD + c] = h;
-  }
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
 }
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+constexpr unsigned kOOB = 0x80000000u;  // out-of-range byte offset: loads read 0, stores drop
 
+// Forward: one wave per query, queries walked in a software pipeline (as the backward
+// below): query n+1's P2 rows / directions / P1 row and query n+2's neighbour indices are in
+// flight while query n's MLP runs on the matrix cores.  Rows r >= k build h0 = 0.
 template <int D_IN, int D_OUT>
 __global__ __launch_bounds__(256) void cost_volume_fwd_kernel(
     int n1, int n2, int k, int queries_per_wave, const float* __restrict__ x1,
@@ -111,19 +62,23 @@ __global__ __launch_bounds__(256) void cost_volume_fwd_kernel(
     unsigned char* __restrict__ amax) {
   constexpr int LD = D_IN + 1;
   constexpr int TILES = D_OUT / 32;
+  constexpr int RPP = 64 / D_IN;  // layout-L rows per pass
+  constexpr int RT = kRows / RPP;
   __shared__ float lds[kWaves][kRows * LD];
   const int b = blockIdx.y;
   const int wave = threadIdx.x >> 6;
   const int lane = lane_id();
+  const int c = lane % D_IN, sub = lane / D_IN;
   float* lds_h = lds[wave];
   const float* x1b = x1 + (long long)b * n1 * 3;
-  const float* x2b = x2 + (long long)b * n2 * 3;
-  const int* idxb = idx + (long long)b * n1 * k;
-  const float* p1b = p1 + (long long)b * n1 * D_IN;
-  const float* p2b = p2 + (long long)b * n2 * D_IN;
+  const __amdgpu_buffer_rsrc_t x2r = rsrc_of(x2 + (long long)b * n2 * 3, (long long)n2 * 12);
+  const __amdgpu_buffer_rsrc_t ixr = rsrc_of(idx + (long long)b * n1 * k, (long long)n1 * k * 4);
+  const __amdgpu_buffer_rsrc_t p1r = rsrc_of(p1 + (long long)b * n1 * D_IN, (long long)n1 * D_IN * 4);
+  const __amdgpu_buffer_rsrc_t p2r = rsrc_of(p2 + (long long)b * n2 * D_IN, (long long)n2 * D_IN * 4);
   float* outb = out + (long long)b * n1 * D_OUT;
   unsigned char* amb = amax + (long long)b * n1 * D_OUT;
   const int q0 = (blockIdx.x * kWaves + wave) * queries_per_wave;
+  const int q1 = min(n1, q0 + queries_per_wave);
   // B fragments of W1 (lane l: W1[t*32 + (l&31)][2s + (l>>5)]), reused for every query
   float bw[TILES][D_IN / 2];
 #pragma unroll
@@ -134,13 +89,67 @@ __global__ __launch_bounds__(256) void cost_volume_fwd_kernel(
   float bias[TILES];
 #pragma unroll
   for (int t = 0; t < TILES; ++t) bias[t] = b1[t * 32 + (lane & 31)];
+  const float w0 = wpos[c * 3 + 0], wy = wpos[c * 3 + 1], wz = wpos[c * 3 + 2], bp = bpos[c];
 
-  for (int qi = 0; qi < queries_per_wave; ++qi) {
-    const int n = q0 + qi;
-    if (n >= n1) break;  // wave-uniform
-    int j;
-    float dx, dy, dz;
-    build_h0<D_IN>(n, k, x1b, x2b, idxb, p1b, p2b, wpos, bpos, lds_h, j, dx, dy, dz);
+  // prefetched state (as the backward): lane r's neighbour index / x2 row, layout-L P2 values
+  int jn = 0;
+  float pv[RT];
+  float xv0, xv1, xv2, p1v;
+  auto load_idx = [&](int n) {
+    jn = (int)__builtin_amdgcn_raw_buffer_load_b32(ixr, (int)(((unsigned)n * (unsigned)k + lane) * 4u), 0, 0);
+  };
+  auto issue = [&](int n) {
+    const unsigned xo = (unsigned)jn * 12u;
+    xv0 = bload(x2r, xo);
+    xv1 = bload(x2r, xo + 4u);
+    xv2 = bload(x2r, xo + 8u);
+#pragma unroll
+    for (int i = 0; i < RT; ++i) {
+      int j;
+      if (RPP == 1) {
+        j = __builtin_amdgcn_readlane(jn, i);
+      } else {
+        const int ja = __builtin_amdgcn_readlane(jn, 2 * i), jb = __builtin_amdgcn_readlane(jn, 2 * i + 1);
+        j = sub ? jb : ja;
+      }
+      pv[i] = bload(p2r, ((unsigned)j * D_IN + c) * 4u);
+    }
+    p1v = bload(p1r, ((unsigned)n * D_IN + c) * 4u);
+  };
+  if (q0 < q1) {
+    load_idx(q0);
+    issue(q0);
+    load_idx(q0 + 1);
+  }
+  for (int n = q0; n < q1; ++n) {
+    // ---- h0 of query n into LDS (layout L) from the prefetched registers
+    const float qx = x1b[n * 3 + 0], qy = x1b[n * 3 + 1], qz = x1b[n * 3 + 2];
+    const float dxl = xv0 - qx, dyl = xv1 - qy, dzl = xv2 - qz;
+#pragma unroll
+    for (int i = 0; i < RT; ++i) {
+      const int r0 = RPP * i, r = r0 + sub;
+      float dx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dxl), r0));
+      float dy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dyl), r0));
+      float dz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dzl), r0));
+      if (RPP == 2) {
+        const float dxb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dxl), r0 + 1));
+        const float dyb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dyl), r0 + 1));
+        const float dzb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dzl), r0 + 1));
+        dx = sub ? dxb : dx;
+        dy = sub ? dyb : dy;
+        dz = sub ? dzb : dz;
+      }
+      const float pos = __fadd_rn(__builtin_fmaf(wz, dz, __builtin_fmaf(wy, dy, __fmul_rn(w0, dx))), bp);
+      const float h = lrelu(__fadd_rn(__fadd_rn(pv[i], p1v), pos));
+      lds_h[r * LD + c] = r < k ? h : 0.f;
+      if (i % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- the next query's loads, in flight during this query's MFMAs
+    if (n + 1 < q1) {
+      issue(n + 1);
+      if (n + 2 < q1) load_idx(n + 2);
+    }
+    __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_wave_barrier();
     f32x16 acc[TILES];
 #pragma unroll
@@ -192,13 +201,6 @@ __global__ __launch_bounds__(256) void cost_volume_fwd_kernel(
 // MFMA accumulator: lane (half, l32), tile t: column 32t + l32, rows (e&3) + 8(e>>2) + 4 half.
 // Row-per-lane (direction gradients): lane l32 = neighbour row, the two halves split the
 // channels.  D_IN = 32: the halves of L split the rows and the dW1 rows, nothing idles.
-__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
-}
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, long long bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
-}
-constexpr unsigned kOOB = 0x80000000u;  // out-of-range byte offset: loads read 0, stores drop
 
 template <int D_IN, int D_OUT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D_IN == 32 ? 2 : 1)))
@@ -209,8 +211,10 @@ void cost_volume_bwd_kernel(
     const float* __restrict__ w1, const float* __restrict__ out,
     const unsigned char* __restrict__ amax, const float* __restrict__ dout,
     float* __restrict__ dp1, float* __restrict__ dp2_rows, float* __restrict__ dx1,
-    float* __restrict__ ddir_rows, float* __restrict__ slab) {
+    float* __restrict__ ddir_rows, const int* __restrict__ rank, float* __restrict__ rows,
+    float* __restrict__ slab) {
   constexpr int LD = D_IN + 1;            // odd row stride: row-per-lane reads hit 32 banks
+  constexpr int RS = D_IN + 4;            // ranked row: dP2 (D_IN) | d(dir) (3) | 0
   constexpr int RPP = 64 / D_IN;          // layout-L rows per pass
   constexpr int RT = kRows / RPP;         // layout-L passes
   constexpr int TI = D_IN / 32;           // 32-column tiles of dh0
@@ -255,6 +259,11 @@ void cost_volume_bwd_kernel(
   const __amdgpu_buffer_rsrc_t outr = rsrc_of(out + ob0, (long long)n1 * D_OUT * 4);
   const __amdgpu_buffer_rsrc_t dor = rsrc_of(dout + ob0, (long long)n1 * D_OUT * 4);
   const __amdgpu_buffer_rsrc_t amr = rsrc_of(amax + ob0, (long long)n1 * D_OUT);
+  // ranked rows (rank != null): row (n, r) goes to slot rank[n, r] of the CSR of idx, so the
+  // per-point sums read each segment contiguously (cv_rows_sum_kernel)
+  const bool ranked = rank != nullptr;
+  const __amdgpu_buffer_rsrc_t rkr = rsrc_of(ranked ? rank + (long long)b * n1 * k : idx,
+                                             ranked ? (long long)n1 * k * 4 : 0);
 
   // parameter-gradient accumulators: gw1[i] = dW1[d0 + i][c]; gwp / gbp per (c, row parity)
   const int d0 = RPP == 2 ? sub * (D_OUT / 2) : 0;
@@ -305,6 +314,9 @@ void cost_volume_bwd_kernel(
   load_idx(q0 + 1);
 
   for (int n = q0; n < q1; ++n) {
+    // lane r: the slot of row r (used by the row passes, after this query's MFMAs)
+    const int rkv = (int)__builtin_amdgcn_raw_buffer_load_b32(
+        rkr, (int)(lane < k ? ((unsigned)n * (unsigned)k + lane) * 4u : kOOB), 0, 0);
     // ---- h0 of query n into T (layout L), directions into dirT, (g', argmax) into gdam
     const float qx = x1b[n * 3 + 0], qy = x1b[n * 3 + 1], qz = x1b[n * 3 + 2];
     if (lane < kRows) dirT[lane] = make_float4(xv0 - qx, xv1 - qy, xv2 - qz, 0.f);
@@ -362,10 +374,18 @@ void cost_volume_bwd_kernel(
     float dp1_acc = 0.f;
     float* dp2n = dp2_rows + (((long long)b * n1 + n) * k) * D_IN + c;
 #pragma unroll 4
-    for (int r = sub; r < k; r += RPP) {  // rows >= k are zero
+    for (int r0 = 0; r0 < k; r0 += RPP) {  // rows >= k are zero
+      const int r = r0 + sub;
+      if (RPP == 2 && r >= k) break;
       const float v = T[r * LD + c];
       const float4 dr = dirT[r];
-      dp2n[r * D_IN] = v;
+      if (ranked) {
+        const int sa = __builtin_amdgcn_readlane(rkv, r0);
+        const int slot = RPP == 2 ? (sub ? __builtin_amdgcn_readlane(rkv, r0 + 1) : sa) : sa;
+        if (slot >= 0) rows[(long long)slot * RS + c] = v;
+      } else {
+        dp2n[r * D_IN] = v;
+      }
       dp1_acc = __fadd_rn(dp1_acc, v);
       gwp0 = __builtin_fmaf(v, dr.x, gwp0);
       gwp1 = __builtin_fmaf(v, dr.y, gwp1);
@@ -390,7 +410,10 @@ void cost_volume_bwd_kernel(
     g1 = __fadd_rn(g1, __shfl_xor(g1, 32, kWave));
     g2 = __fadd_rn(g2, __shfl_xor(g2, 32, kWave));
     const bool row = lane < k;  // lanes >= 32 never (k <= 32)
-    if (row) {
+    if (row && ranked) {
+      if (rkv >= 0)
+        *reinterpret_cast<float4*>(rows + (long long)rkv * RS + D_IN) = make_float4(g0, g1, g2, 0.f);
+    } else if (row) {
       float* dd = ddir_rows + (((long long)b * n1 + n) * k + lane) * 3;
       dd[0] = g0;
       dd[1] = g1;
@@ -469,18 +492,83 @@ hipError_t bwd_launch(int b, int n1, int n2, int k, const float* x1, const float
                       const int* idx, const float* p1, const float* p2, const float* wpos,
                       const float* bpos, const float* w1, const float* out,
                       const unsigned char* amax, const float* dout, float* dp1, float* dp2_rows,
-                      float* dx1, float* ddir_rows, float* slab, float* dparams,
-                      hipStream_t st) {
+                      float* dx1, float* ddir_rows, const int* rank, float* rows, float* slab,
+                      float* dparams, hipStream_t st) {
   const int qpw = bwd_qpw(b, n1);
   dim3 grid(divup(n1, kWaves * qpw), b);
   hipLaunchKernelGGL((cost_volume_bwd_kernel<DI, DO>), grid, dim3(256), 0, st, n1, n2, k,
                      qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, dout, dp1,
-                     dp2_rows, dx1, ddir_rows, slab);
+                     dp2_rows, dx1, ddir_rows, rank, rows, slab);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int len = slab_len(DI, DO);
   const int nslab = (int)(grid.x * grid.y);
   return colsum(nslab, len, slab, dparams, slab + (size_t)nslab * len, st);
+}
+
+// Per-point sums of the ranked rows: key e = b*N2 + j owns the contiguous slots
+// [offsets[e], offsets[e+1]) (ascending position: the CSR order of every other gather-sum,
+// so dP2 / dx2 are bit-identical to summing the (n, k)-ordered rows through perm).
+// One thread per (key, 4-column chunk) of the D+4 wide rows; chunk D/4 is d(dir) -> dx2.
+constexpr int kSumU = 8;
+__device__ __forceinline__ float4 vadd(float4 a, float4 b) {
+  return make_float4(__fadd_rn(a.x, b.x), __fadd_rn(a.y, b.y), __fadd_rn(a.z, b.z),
+                     __fadd_rn(a.w, b.w));
+}
+template <int D>
+__global__ __launch_bounds__(256) void cv_rows_sum_kernel(long long nkeys,
+                                                          const float* __restrict__ rows,
+                                                          const int* __restrict__ offsets,
+                                                          float* __restrict__ dp2,
+                                                          float* __restrict__ dx2) {
+  constexpr int CH = D / 4 + 1;
+  const float4* src = reinterpret_cast<const float4*>(rows);
+  const long long total = nkeys * CH;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const long long key = e / CH;
+    const int ch = (int)(e - key * CH);
+    const int j0 = offsets[key], j1 = offsets[key + 1];
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int j = j0;
+    for (; j + kSumU <= j1; j += kSumU) {
+      float4 v[kSumU];
+#pragma unroll
+      for (int u = 0; u < kSumU; ++u) v[u] = src[(long long)(j + u) * CH + ch];
+#pragma unroll
+      for (int u = 0; u < kSumU; ++u) acc = vadd(acc, v[u]);
+    }
+    for (; j < j1; ++j) acc = vadd(acc, src[(long long)j * CH + ch]);
+    if (ch < D / 4) {
+      reinterpret_cast<float4*>(dp2)[key * (D / 4) + ch] = acc;
+    } else {
+      float* o = dx2 + key * 3;
+      o[0] = acc.x;
+      o[1] = acc.y;
+      o[2] = acc.z;
+    }
+  }
+}
+
+template <int D>
+hipError_t rows_sum_launch(long long nkeys, const float* rows, const int* offsets, float* dp2,
+                           float* dx2, hipStream_t st) {
+  const long long work = nkeys * (D / 4 + 1);
+  hipLaunchKernelGGL((cv_rows_sum_kernel<D>),
+                     dim3((unsigned)std::min<long long>(divupll(work, 256), 1 << 20)), dim3(256),
+                     0, st, nkeys, rows, offsets, dp2, dx2);
+  return hipGetLastError();
+}
+
+hipError_t rows_sum(int din, long long nkeys, const float* rows, const int* offsets, float* dp2,
+                    float* dx2, hipStream_t st) {
+  switch (din) {
+    case 32: return rows_sum_launch<32>(nkeys, rows, offsets, dp2, dx2, st);
+    case 64: return rows_sum_launch<64>(nkeys, rows, offsets, dp2, dx2, st);
+    case 128: return rows_sum_launch<128>(nkeys, rows, offsets, dp2, dx2, st);
+    case 256: return rows_sum_launch<256>(nkeys, rows, offsets, dp2, dx2, st);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 bool narrow(int din, int dout, int k) {
@@ -489,6 +577,29 @@ bool narrow(int din, int dout, int k) {
 
 bool supported(int din, int dout, int k) {
   return narrow(din, dout, k) || cost_volume_wide_fused_supported(din, dout, k);
+}
+
+hipError_t bwd_dispatch(int b, int n1, int n2, int k, int din, int dout, const float* x1,
+                        const float* x2, const int* idx, const float* p1, const float* p2,
+                        const float* wpos, const float* bpos, const float* w1, const float* out,
+                        const unsigned char* amax, const float* dout_grad, float* dp1,
+                        float* dp2_rows, float* dx1, float* ddir_rows, const int* rank,
+                        float* rows, float* slab, float* dparams, hipStream_t st) {
+  if (!narrow(din, dout, k))
+    return cost_volume_wide_fused_bwd(b, n1, n2, k, din, x1, x2, idx, p1, p2, wpos, bpos, w1, out,
+                                      amax, dout_grad, dp1, dp2_rows, dx1, ddir_rows, rank, rows,
+                                      slab, dparams, st);
+#define KDPC_CV_BWD(DI, DO)                                                                    \
+  if (din == DI && dout == DO)                                                                 \
+    return bwd_launch<DI, DO>(b, n1, n2, k, x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax,      \
+                              dout_grad, dp1, dp2_rows, dx1, ddir_rows, rank, rows, slab,        \
+                              dparams, st);
+  KDPC_CV_BWD(32, 32)
+  KDPC_CV_BWD(32, 64)
+  KDPC_CV_BWD(64, 32)
+  KDPC_CV_BWD(64, 64)
+#undef KDPC_CV_BWD
+  return hipErrorInvalidValue;
 }
 
 }  // namespace
@@ -548,18 +659,40 @@ KDPC_API int kdpc_cost_volume_bwd(int b, int n1, int n2, int k, int din, int dou
   KDPC_CHECK_ARG(workspace_bytes >= kdpc_cost_volume_bwd_workspace_bytes(b, n1, din, dout));
   hipStream_t st = (hipStream_t)stream;
   float* slab = (float*)workspace;
-  if (!narrow(din, dout, k))
-    return (int)cost_volume_wide_fused_bwd(b, n1, n2, k, din, x1, x2, idx, p1, p2, wpos, bpos, w1,
-                                           out, amax, dout_grad, dp1, dp2_rows, dx1, ddir_rows,
-                                           slab, dparams, st);
-#define KDPC_CV_BWD(DI, DO)                                                                    \
-  if (din == DI && dout == DO)                                                                 \
-    return (int)bwd_launch<DI, DO>(b, n1, n2, k, x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, \
-                                   dout_grad, dp1, dp2_rows, dx1, ddir_rows, slab, dparams, st);
-  KDPC_CV_BWD(32, 32)
-  KDPC_CV_BWD(32, 64)
-  KDPC_CV_BWD(64, 32)
-  KDPC_CV_BWD(64, 64)
-#undef KDPC_CV_BWD
-  return (int)hipErrorInvalidValue;
+  return (int)bwd_dispatch(b, n1, n2, k, din, dout, x1, x2, idx, p1, p2, wpos, bpos, w1, out,
+                           amax, dout_grad, dp1, dp2_rows, dx1, ddir_rows, nullptr, nullptr, slab,
+                           dparams, st);
+}
+
+// Backward with the per-point sums done here, through the CSR of idx over the N2 points
+// (offsets (B*N2+1) and rank (B*N1*K): the slot of each (n, k) position, kdpc_csr_rank).
+// The per-neighbour rows are written straight to their CSR slots (workspace) and summed
+// contiguously: dp2 (B,N2,Din), dx2 (B,N2,3).  Other outputs as kdpc_cost_volume_bwd.
+KDPC_API size_t kdpc_cost_volume_bwd_csr_workspace_bytes(int b, int n1, int k, int din, int dout) {
+  const size_t slab = kdpc_cost_volume_bwd_workspace_bytes(b, n1, din, dout);
+  if (slab == 0 || k <= 0) return 0;
+  return ((slab + 255) & ~(size_t)255) + (size_t)b * n1 * k * (din + 4) * sizeof(float);
+}
+
+KDPC_API int kdpc_cost_volume_bwd_csr(int b, int n1, int n2, int k, int din, int dout,
+                                      const float* x1, const float* x2, const int* idx,
+                                      const float* p1, const float* p2, const float* wpos,
+                                      const float* bpos, const float* w1, const float* out,
+                                      const unsigned char* amax, const float* dout_grad,
+                                      const int* offsets, const int* rank, float* dp1, float* dp2,
+                                      float* dx1, float* dx2, void* workspace,
+                                      size_t workspace_bytes, float* dparams, void* stream) {
+  KDPC_CHECK_ARG(b > 0 && n1 > 0 && n2 > 0 && supported(din, dout, k) && b <= 65535);
+  KDPC_CHECK_ARG(x1 && x2 && idx && p1 && p2 && wpos && bpos && w1 && out && amax && dout_grad &&
+                 offsets && rank && dp1 && dp2 && dx1 && dx2 && workspace && dparams);
+  KDPC_CHECK_ARG(workspace_bytes >= kdpc_cost_volume_bwd_csr_workspace_bytes(b, n1, k, din, dout));
+  hipStream_t st = (hipStream_t)stream;
+  const size_t slab_bytes = (kdpc_cost_volume_bwd_workspace_bytes(b, n1, din, dout) + 255) & ~(size_t)255;
+  float* slab = (float*)workspace;
+  float* rows = (float*)((char*)workspace + slab_bytes);
+  hipError_t e = bwd_dispatch(b, n1, n2, k, din, dout, x1, x2, idx, p1, p2, wpos, bpos, w1, out,
+                              amax, dout_grad, dp1, nullptr, dx1, nullptr, rank, rows, slab,
+                              dparams, st);
+  if (e != hipSuccess) return (int)e;
+  return (int)rows_sum(din, (long long)b * n2, rows, offsets, dp2, dx2, st);
 }

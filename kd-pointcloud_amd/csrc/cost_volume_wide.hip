@@ -430,8 +430,10 @@ __global__ __launch_bounds__(2 * D) void cvw_fused_bwd_kernel(
     const float* __restrict__ w1, const float* __restrict__ w1t, const float* __restrict__ out,
     const unsigned char* __restrict__ amax, const float* __restrict__ dout,
     float* __restrict__ dp1, float* __restrict__ dp2_rows, float* __restrict__ dx1,
-    float* __restrict__ ddir_rows, float* __restrict__ slab) {
+    float* __restrict__ ddir_rows, const int* __restrict__ rank, float* __restrict__ rows,
+    float* __restrict__ slab) {
   using G = WideGeo<D>;
+  constexpr int RS = D + 4;  // ranked row: dP2 (D) | d(dir) (3) | 0 (cost_volume.hip)
   using W = WideBwd<D>;
   constexpr int NG2 = G::NT / 32;  // channel groups of the direction pass
   constexpr int CPG = D / NG2;     // channels per group
@@ -460,6 +462,10 @@ __global__ __launch_bounds__(2 * D) void cvw_fused_bwd_kernel(
   const __amdgpu_buffer_rsrc_t outr = rsrc_of(out, (long long)s.nq * D * 4);
   const __amdgpu_buffer_rsrc_t dor = rsrc_of(dout, (long long)s.nq * D * 4);
   const __amdgpu_buffer_rsrc_t amr = rsrc_of(amax, (long long)s.nq * D);
+  // ranked rows: row (q, r) -> slot rank[q*k + r]; a query's slots are loaded as it starts
+  // and used by its column / direction passes after the MFMAs
+  const bool ranked = rank != nullptr;
+  const __amdgpu_buffer_rsrc_t rkr = rsrc_of(ranked ? rank : idx, ranked ? (long long)s.nq * k * 4 : 0);
   wide_consts<D>(wpos, bpos, wposT);
   float4 bt[W::BREG && MAIN ? D / 8 : 1];
   if constexpr (W::BREG && MAIN) {
@@ -492,6 +498,17 @@ __global__ __launch_bounds__(2 * D) void cvw_fused_bwd_kernel(
     dv = bld(dor, ok ? oo * 4u : kOOB);
     av = __builtin_amdgcn_raw_buffer_load_b8(amr, (int)(ok ? oo : kOOB), 0, 0);
   };
+  int rk[G::RPT], rkd = -1;  // slots: column-pass rows, row-per-lane (direction pass)
+  auto load_rank = [&](int q) {
+#pragma unroll
+    for (int i = 0; i < G::RPT; ++i) {
+      const int r = rg + G::RG * i;
+      rk[i] = (int)__builtin_amdgcn_raw_buffer_load_b32(
+          rkr, (int)(r < k ? ((unsigned)q * (unsigned)k + r) * 4u : kOOB), 0, 0);
+    }
+    rkd = (int)__builtin_amdgcn_raw_buffer_load_b32(
+        rkr, (int)(l32 < k ? ((unsigned)q * (unsigned)k + l32) * 4u : kOOB), 0, 0);
+  };
   auto stage_out = [&](int p) {
     if (t < D) gam[p][t] = make_float2(ov > 0.f ? dv : dv * kSlope, __int_as_float((int)av));
   };
@@ -509,6 +526,7 @@ __global__ __launch_bounds__(2 * D) void cvw_fused_bwd_kernel(
   for (int q = q0; q < q1; ++q) {
     const int p = (q - q0) & 1;
     const bool more = q + 1 < q1;
+    if (MAIN && ranked) load_rank(q);
     auto next_loads = [&]() {
 #pragma unroll
       for (int i = 0; i < G::RPT; ++i) jn[i] = jn2[i];
@@ -582,7 +600,11 @@ __global__ __launch_bounds__(2 * D) void cvw_fused_bwd_kernel(
         const int r = rg + G::RG * i;
         const float4 v = *reinterpret_cast<const float4*>(H + r * G::LD + 4 * c4);
         const float4 dr = dirs[p][r];
-        if (r < k) *reinterpret_cast<float4*>(d2 + (long long)r * D) = v;
+        if (ranked) {
+          if (r < k && rk[i] >= 0) *reinterpret_cast<float4*>(rows + (long long)rk[i] * RS + 4 * c4) = v;
+        } else if (r < k) {
+          *reinterpret_cast<float4*>(d2 + (long long)r * D) = v;
+        }
         sp.x = __fadd_rn(sp.x, v.x);
         sp.y = __fadd_rn(sp.y, v.y);
         sp.z = __fadd_rn(sp.z, v.z);
@@ -652,7 +674,10 @@ __global__ __launch_bounds__(2 * D) void cvw_fused_bwd_kernel(
         v.z = __fadd_rn(v.z, x.z);
       }
       const bool row = l32 < k;
-      if (row) {
+      if (row && ranked) {
+        if (rkd >= 0)
+          *reinterpret_cast<float4*>(rows + (long long)rkd * RS + D) = make_float4(v.x, v.y, v.z, 0.f);
+      } else if (row) {
         float* dd = ddir_rows + ((long long)q * k + l32) * 3;
         dd[0] = v.x;
         dd[1] = v.y;
@@ -752,7 +777,8 @@ hipError_t cost_volume_wide_fused_bwd(int b, int n1, int n2, int k, int d, const
                                       const float* p2, const float* wpos, const float* bpos,
                                       const float* w1, const float* out,
                                       const unsigned char* amax, const float* dout, float* dp1,
-                                      float* dp2_rows, float* dx1, float* ddir_rows, float* ws,
+                                      float* dp2_rows, float* dx1, float* ddir_rows,
+                                      const int* rank, float* rows, float* ws,
                                       float* dparams, hipStream_t st) {
   const long long nq = (long long)b * n1;
   const int qpw = fused_qpw(nq);
@@ -764,7 +790,7 @@ hipError_t cost_volume_wide_fused_bwd(int b, int n1, int n2, int k, int d, const
   if (d == 128) {
     hipLaunchKernelGGL((cvw_fused_bwd_kernel<128, 0>), dim3(nwg), dim3(256), 0, st, b, n1, n2, k,
                        qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, w1t, out, amax, dout, dp1,
-                       dp2_rows, dx1, ddir_rows, slab);
+                       dp2_rows, dx1, ddir_rows, rank, rows, slab);
   } else {
     hipLaunchKernelGGL(cvw_transpose_kernel, dim3(divup(d * d, 256)), dim3(256), 0, st, d, w1,
                        w1t);
@@ -772,12 +798,12 @@ hipError_t cost_volume_wide_fused_bwd(int b, int n1, int n2, int k, int d, const
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((cvw_fused_bwd_kernel<256, 1>), dim3(nwg), dim3(512), 0, st, b, n1, n2, k,
                        qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, w1t, out, amax, dout, dp1,
-                       dp2_rows, dx1, ddir_rows, slab);
+                       dp2_rows, dx1, ddir_rows, rank, rows, slab);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL((cvw_fused_bwd_kernel<256, 2>), dim3(nwg, WideBwd<256>::OSPLIT), dim3(512),
                        0, st, b, n1, n2, k,
                        qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, w1t, out, amax, dout, dp1,
-                       dp2_rows, dx1, ddir_rows, slab);
+                       dp2_rows, dx1, ddir_rows, rank, rows, slab);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;

@@ -32,131 +32,11 @@
 #include <algorithm>
 #include <type_traits>
 
-#include "kdpc_common.h"
+#include "pointconv_tile.h"
 
-using namespace kdpc;
+using namespace kdpc_pc;
 
 namespace {
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-constexpr int kW = 16;              // WeightNet width (weightnet=16 in every model layer)
-constexpr int kCC = 8;              // channels per chunk
-constexpr int kNC = kCC * kW;       // A columns per chunk (128)
-constexpr int kKMax = 16;           // neighbours per row supported
-constexpr int kBlk = 32 * 4 + 16;   // floats per 4-column block of a 32-row MFMA-A tile
-constexpr int kTS = 32 + 4;         // row stride of transposed (inner = row) 32-row tiles
-constexpr int kDaS = kNC + 4;       // row stride of the dA chunk
-constexpr int kTargetWG = 512;      // grid size the split heuristics aim for
-constexpr int kCUs = 256;           // MI355X compute units
-
-struct Geo {
-  int n, s, k, d, c, r, nch, c8;  // c = 3 + d, r = B*S rows, nch = ceil(c/8), c8 = 8*nch
-  int bn;                         // B*N points
-  const float* xyz;               // (B,N,3)
-  const float* center;            // (B,S,3)
-  const float* feats;             // (B,N,D)
-  const int* idx;                 // (B,S,K)
-};
-
-__device__ __forceinline__ f32x16 mfma4(float4 a, float4 b, f32x16 c) {
-  c = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, c, 0, 0, 0);
-  return __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, c, 0, 0, 0);
-}
-
-__device__ __forceinline__ f32x16 zero16() {
-  f32x16 z;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) z[i] = 0.f;
-  return z;
-}
-
-// global row of neighbour kk of row `row` (b*N + idx), -1 past the last row
-__device__ __forceinline__ int nbr_of(const Geo& g, int row, int kk) {
-  if (row >= g.r) return -1;
-  return (row / g.s) * g.n + g.idx[(long long)row * g.k + kk];
-}
-
-// Gathers go through buffer loads: 32-bit byte offsets (one VGPR per in-flight slot instead
-// of a 64-bit address) and hardware bounds checks (an offset past the buffer reads 0).
-constexpr unsigned kOOB = 0x80000000u;  // byte offset that is always out of range
-
-// float offset of pair pos's 8 dG values of chunk ch in the dG buffer: pair-major, each
-// pair's 32 bytes of a chunk sit C8*4 bytes apart and pc_csr_sum reads a pair's whole row
-// contiguously (chunk-major rows -- full-line stores -- measured round 2: data kernel
-// 576 -> 514 us but pc_csr_sum 86 -> 173 us from its 32-byte gathers, a net loss).
-__device__ __forceinline__ long long dg_off(long long pos, int ch, long long /*rk*/, int c8) {
-  return pos * c8 + (long long)ch * kCC;
-}
-
-struct Srcs {
-  __amdgpu_buffer_rsrc_t xyz, center, feats;
-};
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, long long nfloats) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, (int)(nfloats * 4),
-                                           0x00020000);
-}
-
-__device__ __forceinline__ Srcs srcs_of(const Geo& g) {
-  Srcs s;
-  s.xyz = rsrc(g.xyz, (long long)g.bn * 3);
-  s.center = rsrc(g.center, (long long)g.r * 3);
-  s.feats = rsrc(g.feats, (long long)g.bn * g.d);
-  return s;
-}
-
-__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, unsigned byte_off) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)byte_off, 0, 0));
-}
-
-// byte offset of neighbour nb's feature row (kOOB for none)
-__device__ __forceinline__ unsigned feat_off(const Geo& g, int nb) {
-  return nb < 0 ? kOOB : (unsigned)nb * (unsigned)g.d * 4u;
-}
-
-// G value of channel cg for neighbour row nb of row `row`
-__device__ __forceinline__ float g_fetch(const Geo& g, const Srcs& s, int nb, int row, int cg) {
-  if (nb < 0) return 0.f;
-  if (cg < 3)
-    return bload(s.xyz, ((unsigned)nb * 3u + cg) * 4u) - bload(s.center, ((unsigned)row * 3u + cg) * 4u);
-  if (cg < g.c) return bload(s.feats, (unsigned)nb * (unsigned)g.d * 4u + (unsigned)(cg - 3) * 4u);
-  return 0.f;
-}
-
-// acc[c] = sum_k G[r,k,c] wk[k] over the tile's LDS gather (ascending k, one fma each).
-// Channel pairs go through packed f32 fmas (v_pk_fma_f32: the same IEEE fma per element, half
-// the VALU issue): the build is the VALU work both the forward and the weight kernel issue
-// beside their MFMAs, and VALU issue is what the co-resident wave's MFMA phase slows down.
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-template <int KM>
-__device__ __forceinline__ void build_row(const float* gl, int r, int k_n, const float* wk,
-                                          float (&a)[kCC]) {
-  f32x2 acc[kCC / 2];
-#pragma unroll
-  for (int c = 0; c < kCC / 2; ++c) acc[c] = f32x2{0.f, 0.f};
-#pragma unroll
-  for (int k = 0; k < KM; ++k) {
-    if (k < k_n) {
-      const float4 lo = *reinterpret_cast<const float4*>(gl + (r * k_n + k) * kCC);
-      const float4 hi = *reinterpret_cast<const float4*>(gl + (r * k_n + k) * kCC + 4);
-      const f32x2 w = f32x2{wk[k], wk[k]};
-      acc[0] = __builtin_elementwise_fma(f32x2{lo.x, lo.y}, w, acc[0]);
-      acc[1] = __builtin_elementwise_fma(f32x2{lo.z, lo.w}, w, acc[1]);
-      acc[2] = __builtin_elementwise_fma(f32x2{hi.x, hi.y}, w, acc[2]);
-      acc[3] = __builtin_elementwise_fma(f32x2{hi.z, hi.w}, w, acc[3]);
-    }
-  }
-#pragma unroll
-  for (int c = 0; c < kCC / 2; ++c) {
-    a[2 * c] = acc[c].x;
-    a[2 * c + 1] = acc[c].y;
-  }
-}
 
 // ------------------------------------------------------------------------------ forward
 // grid (row tiles, channel splits); a split > 1 writes a partial tile to slab[split].
@@ -1363,8 +1243,9 @@ void pc_bwd_weight_ws_kernel(Geo g, const float* __restrict__ wt, const float* _
   const int rend = min(g.r, rbeg + rows_per_split);
   const int ntiles = (rend - rbeg + TR - 1) / TR;
   if (ntiles <= 0) return;
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, half = lane >> 5, l32 = lane & 31;
-  const bool consumer = wv < 4;  // wave-uniform
+  const int t = threadIdx.x, lane = t & 63, half = lane >> 5, l32 = lane & 31;
+  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);  // uniform role branch (see data ws)
+  const bool consumer = wv < 4;
   const long long c16 = (long long)g.c * kW;
 
   f32x16 acc[MT];
@@ -1671,8 +1552,23 @@ hipError_t bwd_launch(const Geo& g, const Plan& p, int b, const float* wt, const
                      O, c16, g.nch, wl, wsw);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  // the pipelined kernel stores dG through a buffer resource (31-bit byte offsets)
-  if (bwd_pipe_enabled<KM>() && (long long)p.r * g.k * p.c8 * 4 < (1ll << 31))
+  static const bool dat_ws = [] {  // KDPC_PC_DAT_WS=0: the single-role kernels (A/B runs)
+    const char* v = getenv("KDPC_PC_DAT_WS");
+    return !(v && v[0] == '0');
+  }();
+  bool launched = false;
+  // the pipelined kernels store dG through a buffer resource (31-bit byte offsets)
+  const bool dg31 = (long long)p.r * g.k * p.c8 * 4 < (1ll << 31);
+  if constexpr (KM <= 9) {
+    if (dat_ws && dg31) {
+      e = pc_bwd_data_ws(O, g, dim3(divup(p.r, 32), p.bks), wt, wsw, dy, dgr,
+                         p.bks > 1 ? dwt_slab : dwt, dcenter, p.bcps, st);
+      if (e != hipSuccess) return e;
+      launched = true;
+    }
+  }
+  if (launched) {
+  } else if (bwd_pipe_enabled<KM>() && dg31)
     hipLaunchKernelGGL((pc_bwd_data_pipe_kernel<O, KM>), dim3(divup(p.r, 32), p.bks), dim3(256),
                        0, st, g, wt, wsw, dy, dgr, p.bks > 1 ? dwt_slab : dwt, dcenter, p.bcps);
   else

@@ -226,6 +226,22 @@ __global__ __launch_bounds__(kLdsThreads) void csr_lds_fill_kernel(int n, int p,
   }
 }
 
+// rank[i] = the CSR slot of position i (perm[rank[i]] == i), -1 for an index outside
+// [0, n) (in no segment).  One thread per position: the slots in [0, offsets[b*n]) scatter
+// their position, the out-of-range positions mark themselves.
+__global__ __launch_bounds__(256) void csr_rank_kernel(long long total, int n,
+                                                       const int* __restrict__ idx,
+                                                       const int* __restrict__ perm,
+                                                       const int* __restrict__ end,
+                                                       int* __restrict__ rank) {
+  const long long valid = *end;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    if (i < valid) rank[perm[i]] = (int)i;
+    if ((unsigned)idx[i] >= (unsigned)n) rank[i] = -1;
+  }
+}
+
 inline int grid_for(long long total, int block) {
   long long g = divupll(total, block);
   if (g > 65536) g = 65536;
@@ -486,6 +502,19 @@ KDPC_API int kdpc_csr_build(int b, int n, int p, const int* idx, void* workspace
 }
 
 // (B,C,P) channel-major source -> (B,C,N): serves group_points_grad and gather_points_grad
+// Inverse of the CSR permutation: rank (B*P) with perm[rank[i]] == i, -1 where idx[i] is
+// outside [0, n).  offsets / perm from kdpc_csr_build of the same idx.
+KDPC_API int kdpc_csr_rank(int b, int n, int p, const int* idx, const int* offsets,
+                           const int* perm, int* rank, void* stream) {
+  KDPC_CHECK_ARG(b >= 0 && n > 0 && p >= 0);
+  const long long total = (long long)b * p;
+  if (total == 0) return (int)hipSuccess;
+  KDPC_CHECK_ARG(idx && offsets && perm && rank);
+  hipLaunchKernelGGL(csr_rank_kernel, dim3(grid_for(total, 256)), dim3(256), 0,
+                     (hipStream_t)stream, total, n, idx, perm, offsets + (long long)b * n, rank);
+  KDPC_RETURN_LAUNCH();
+}
+
 KDPC_API int kdpc_csr_sum_channels(int b, int c, int n, int p, const float* src,
                                    const int* offsets, const int* perm, float* dst,
                                    void* stream) {

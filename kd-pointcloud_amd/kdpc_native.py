@@ -51,6 +51,7 @@ _SIGNATURES = {
     "kdpc_csr_workspace_bytes": [_c_int, _c_int, _c_int],
     "kdpc_csr_build": [_c_int, _c_int, _c_int, _vp, _vp, _c_size, _vp, _vp, _vp],
     "kdpc_group_rows_grad_csr": [_c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
+    "kdpc_csr_rank": [_c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
     "kdpc_csr_sum_channels": [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
     "kdpc_three_interpolate_grad_csr": [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp,
                                         _vp, _vp],
@@ -59,6 +60,8 @@ _SIGNATURES = {
     "kdpc_pointconv_contract_bwd": [_c_int] * 5 + [_vp] * 10,
     "kdpc_cost_volume_bwd_workspace_bytes": [_c_int] * 4,
     "kdpc_cost_volume_bwd": [_c_int] * 6 + [_vp] * 16 + [_c_size, _vp, _vp],
+    "kdpc_cost_volume_bwd_csr_workspace_bytes": [_c_int] * 5,
+    "kdpc_cost_volume_bwd_csr": [_c_int] * 6 + [_vp] * 18 + [_c_size, _vp, _vp],
     "kdpc_pointconv_supported": [_c_int] * 3,
     "kdpc_pointconv_fwd_workspace_bytes": [_c_int] * 5,
     "kdpc_pointconv_fwd": [_c_int] * 6 + [_vp] * 9 + [_c_size, _vp],
@@ -91,6 +94,7 @@ _SIGNATURES = {
 }
 _RESTYPES = {"kdpc_build_id": ctypes.c_char_p, "kdpc_grad_workspace_bytes": _c_size,
              "kdpc_csr_workspace_bytes": _c_size, "kdpc_cost_volume_bwd_workspace_bytes": _c_size,
+             "kdpc_cost_volume_bwd_csr_workspace_bytes": _c_size,
              "kdpc_pointconv_fwd_workspace_bytes": _c_size,
              "kdpc_pointconv_bwd_workspace_bytes": _c_size,
              "kdpc_weightnet_bwd_workspace_bytes": _c_size,
@@ -333,11 +337,12 @@ def group_rows(points, idx):
 
 class Csr:
     """Inverted index of an int32 index tensor (B,P) over a key space of n values."""
-    __slots__ = ("offsets", "perm", "n", "p")
+    __slots__ = ("offsets", "perm", "n", "p", "rank")
 
     def __init__(self, idx2d, n):
         self.offsets, self.perm = _op("kdpc_csr_build", "csr_build", _gpu(idx2d, "idx"), n)
         self.n, self.p = n, idx2d.shape[1]
+        self.rank = None
 
 
 def batch_prefix(idx, b):
@@ -364,12 +369,30 @@ def csr_of(idx, n):
         csr = Csr.__new__(Csr)
         csr.offsets, csr.perm = pc.offsets[:b * n + 1], pc.perm[:b * pc.p]
         csr.n, csr.p = n, pc.p
+        csr.rank = None
     else:
         csr = Csr(idx.reshape(idx.shape[0], -1), n)
     try:
         idx._kdpc_csr = csr
     except AttributeError:
         pass
+    return csr
+
+
+def csr_rank_of(idx, n):
+    """The CSR of idx (csr_of) with its inverse permutation: rank (B*P) int32, the slot of
+    every position (perm[rank[i]] == i), built once and cached with the CSR.  A batch prefix
+    (batch_prefix) takes the parent's prefix: slots of the first b batches are < offsets[b*N]."""
+    csr = csr_of(idx, n)
+    if csr.rank is None:
+        parent = getattr(idx, "_kdpc_parent", None)
+        if parent is not None:
+            pidx, b = parent
+            csr.rank = csr_rank_of(pidx, n).rank[:b * csr.p]
+        else:
+            idx2d = idx.reshape(idx.shape[0], -1)
+            csr.rank = _op("kdpc_csr_rank", "csr_rank", _gpu(idx2d, "idx"), csr.offsets,
+                           csr.perm, n)
     return csr
 
 
@@ -424,6 +447,22 @@ def cost_volume_bwd(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout):
                wpos, bpos, w1, out, amax, gout,
                work=(4 * B * N1 * (3 + K + din + K * din + 2 * dout + din + K * din + 3 + 3 * K)
                      + B * N1 * dout, 4.0 * B * N1 * K * din * dout))
+
+
+def cost_volume_bwd_csr(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout):
+    """-> dp1 (B,N1,Din), dp2 (B,N2,Din), dx1 (B,N1,3), dx2 (B,N2,3), dparams: the backward
+    with the per-point sums through the (cached) CSR of idx done inside the entry point."""
+    B, N1, _ = _gpu(x1, "x1").shape
+    N2, K = x2.shape[1], idx.shape[2]
+    din, dout = p1.shape[2], w1.shape[0]
+    csr = csr_rank_of(idx, N2)
+    # reads x1, idx, rank, p1, the K gathered p2 rows, out, gout, amax, offsets; writes dp1,
+    # dx1 and the per-point dp2 / dx2 (the CSR-ordered rows in between are not counted)
+    return _op("kdpc_cost_volume_bwd_csr", "cost_volume_bwd_csr", x1, x2, idx, p1, p2,
+               wpos, bpos, w1, out, amax, gout, csr.offsets, csr.rank,
+               work=(4 * B * N1 * (3 + 2 * K + din + K * din + 2 * dout + din + 3)
+                     + B * N1 * dout + 4 * B * N2 * (din + 4) + 4,
+                     4.0 * B * N1 * K * din * dout))
 
 
 # ------------------------------------------------------------------ wide cost volume

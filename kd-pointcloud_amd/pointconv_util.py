@@ -502,11 +502,9 @@ class _CostVolume(torch.autograd.Function):
         B, N1, K = idx.shape
         N2 = x2.shape[1]
         din, dout = p1.shape[2], w1.shape[0]
-        dp1, dp2_rows, dx1, ddir_rows, dpar = _nat.cost_volume_bwd(
+        # per-neighbour rows straight into the CSR order of idx, summed per point inside
+        dp1, dp2, dx1, dx2, dpar = _nat.cost_volume_bwd_csr(
             x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout.contiguous())
-        csr = _nat.csr_of(idx, N2)
-        dp2 = _nat.group_rows_grad(dp2_rows.view(B, N1 * K, din), csr, B, N2, din)
-        dx2 = _nat.group_rows_grad(ddir_rows.view(B, N1 * K, 3), csr, B, N2, 3)
         o = dout * din
         dw1 = dpar[:o].view(dout, din)
         db1 = dpar[o:o + dout]

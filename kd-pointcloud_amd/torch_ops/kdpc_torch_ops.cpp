@@ -317,6 +317,19 @@ TT csr_build(Tensor idx, int64_t n) {
   return {offsets, perm};
 }
 
+Tensor csr_rank(Tensor idx, Tensor offsets, Tensor perm, int64_t n) {
+  dev(idx, kI, "idx"), dev(offsets, kI, "offsets"), dev(perm, kI, "perm");
+  TORCH_CHECK(idx.dim() == 2, "kdpc: csr_rank expects idx (B,P)");
+  GUARD(idx);
+  const int64_t b = idx.size(0), p = idx.size(1);
+  TORCH_CHECK(offsets.numel() >= b * n + 1 && perm.numel() >= b * p,
+              "kdpc: csr_rank: offsets / perm do not match idx");
+  Tensor rank = empty_i({b * p}, idx);
+  check(kdpc_csr_rank(b, n, p, I(idx), I(offsets), I(perm), I(rank), stream_of(idx)),
+        "csr_rank");
+  return rank;
+}
+
 Tensor group_rows_grad(Tensor grad_out, Tensor offsets, Tensor perm, int64_t n) {
   dev(grad_out, kF, "grad_out"), dev(offsets, kI, "offsets"), dev(perm, kI, "perm");
   TORCH_CHECK(grad_out.dim() == 3, "kdpc: group_rows_grad expects grad_out (B,P,C)");
@@ -389,6 +402,34 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> cost_volume_bwd(
                              F(dp1), F(dp2_rows), F(dx1), F(ddir_rows), ws.data_ptr(), nb,
                              F(dparams), stream_of(x1)), "cost_volume_bwd");
   return {dp1, dp2_rows, dx1, ddir_rows, dparams};
+}
+
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> cost_volume_bwd_csr(
+    Tensor x1, Tensor x2, Tensor idx, Tensor p1, Tensor p2, Tensor wpos, Tensor bpos, Tensor w1,
+    Tensor out, Tensor amax, Tensor gout, Tensor offsets, Tensor rank) {
+  for (auto* t : {&x1, &x2, &p1, &p2, &wpos, &bpos, &w1, &out, &gout})
+    dev(*t, kF, "cost volume input");
+  dev(idx, kI, "idx"), dev(amax, at::kByte, "amax"), dev(offsets, kI, "offsets");
+  dev(rank, kI, "rank");
+  GUARD(x1);
+  const int64_t b = x1.size(0), n1 = x1.size(1), n2 = x2.size(1), k = idx.size(2);
+  const int64_t din = p1.size(2), dout = w1.size(0);
+  TORCH_CHECK(offsets.numel() >= b * n2 + 1 && rank.numel() >= b * n1 * k,
+              "kdpc: cost_volume_bwd_csr: offsets / rank do not match idx");
+  Tensor dp1 = empty_f({b, n1, din}, x1);
+  Tensor dp2 = empty_f({b, n2, din}, x1);
+  Tensor dx1 = empty_f({b, n1, 3}, x1);
+  Tensor dx2 = empty_f({b, n2, 3}, x1);
+  Tensor dparams = empty_f({dout * din + dout + 4 * din}, x1);
+  const size_t nb = kdpc_cost_volume_bwd_csr_workspace_bytes(b, n1, k, din, dout);
+  TORCH_CHECK(nb > 0, "kdpc: cost_volume_bwd_csr: unsupported shape");
+  Tensor ws = workspace(nb, x1);
+  check(kdpc_cost_volume_bwd_csr(b, n1, n2, k, din, dout, F(x1), F(x2), I(idx), F(p1), F(p2),
+                                 F(wpos), F(bpos), F(w1), F(out), amax.data_ptr<uint8_t>(),
+                                 F(gout), I(offsets), I(rank), F(dp1), F(dp2), F(dx1), F(dx2),
+                                 ws.data_ptr(), nb, F(dparams), stream_of(x1)),
+        "cost_volume_bwd_csr");
+  return {dp1, dp2, dx1, dx2, dparams};
 }
 
 Tensor cost_volume_wide_h0(Tensor x1, Tensor x2, Tensor idx, Tensor p1, Tensor p2, Tensor wpos,
@@ -785,6 +826,7 @@ TORCH_LIBRARY(kdpc, m) {
   m.def("group_rows(Tensor points, Tensor idx) -> Tensor");
   m.def("csr_build(Tensor idx, int n) -> (Tensor, Tensor)");
   m.def("group_rows_grad(Tensor grad_out, Tensor offsets, Tensor perm, int n) -> Tensor");
+  m.def("csr_rank(Tensor idx, Tensor offsets, Tensor perm, int n) -> Tensor");
   m.def("csr_sum_channels(Tensor src, Tensor offsets, Tensor perm, int b, int c, int n) "
         "-> Tensor");
   m.def("three_interpolate_grad_csr(Tensor grad_out, Tensor weight, Tensor offsets, "
@@ -794,6 +836,9 @@ TORCH_LIBRARY(kdpc, m) {
   m.def("cost_volume_bwd(Tensor x1, Tensor x2, Tensor idx, Tensor p1, Tensor p2, Tensor wpos, "
         "Tensor bpos, Tensor w1, Tensor out, Tensor amax, Tensor gout) "
         "-> (Tensor, Tensor, Tensor, Tensor, Tensor)");
+  m.def("cost_volume_bwd_csr(Tensor x1, Tensor x2, Tensor idx, Tensor p1, Tensor p2, "
+        "Tensor wpos, Tensor bpos, Tensor w1, Tensor out, Tensor amax, Tensor gout, "
+        "Tensor offsets, Tensor rank) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("cost_volume_wide_h0(Tensor x1, Tensor x2, Tensor idx, Tensor p1, Tensor p2, "
         "Tensor wpos, Tensor bpos) -> Tensor");
   m.def("cost_volume_wide_max(Tensor z1, int b, int n1, int k, int dout) -> (Tensor, Tensor)");
@@ -857,10 +902,12 @@ TORCH_LIBRARY_IMPL(kdpc, CUDA, m) {
   m.impl("group_rows", group_rows);
   m.impl("csr_build", csr_build);
   m.impl("group_rows_grad", group_rows_grad);
+  m.impl("csr_rank", csr_rank);
   m.impl("csr_sum_channels", csr_sum_channels);
   m.impl("three_interpolate_grad_csr", three_interpolate_grad_csr);
   m.impl("cost_volume_fwd", cost_volume_fwd);
   m.impl("cost_volume_bwd", cost_volume_bwd);
+  m.impl("cost_volume_bwd_csr", cost_volume_bwd_csr);
   m.impl("cost_volume_wide_h0", cost_volume_wide_h0);
   m.impl("cost_volume_wide_max", cost_volume_wide_max);
   m.impl("cost_volume_wide_max_bwd", cost_volume_wide_max_bwd);

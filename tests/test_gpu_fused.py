@@ -58,6 +58,56 @@ def test_cost_volume_fused_equals_unfused(din, dout, n1, n2, bsz, k):
         _scale_close(a.reshape(b.shape), b, rtol=2e-5, name=n)
 
 
+@pytest.mark.parametrize("din,dout,n1,n2,bsz,k", [
+    (32, 32, 1000, 900, 2, 32), (64, 64, 513, 700, 3, 32), (32, 64, 300, 300, 1, 17),
+    (64, 32, 257, 600, 2, 9), (128, 128, 300, 280, 2, 32), (256, 256, 200, 250, 2, 20)])
+def test_cost_volume_bwd_csr_bitwise(din, dout, n1, n2, bsz, k):
+    """kdpc_cost_volume_bwd_csr (rows written in CSR order through kdpc_csr_rank, summed
+    contiguously) is bit-identical to kdpc_cost_volume_bwd + kdpc_group_rows_grad_csr of its
+    (n, k)-ordered rows: the same values summed in the same ascending-position order.  A
+    point no query picks (the last one of each cloud) gets exact zeros."""
+    import kdpc_native as K
+    g = torch.Generator(device="cpu").manual_seed(din * 7 + k)
+    x1 = torch.rand(bsz, n1, 3, generator=g).to(DEV)
+    x2 = torch.rand(bsz, n2, 3, generator=g).to(DEV)
+    idx = torch.randint(0, n2 - 1, (bsz, n1, k), generator=g, dtype=torch.int32).to(DEV)
+    p1 = torch.randn(bsz, n1, din, generator=g).to(DEV)
+    p2 = torch.randn(bsz, n2, din, generator=g).to(DEV)
+    wpos = (torch.randn(din, 3, generator=g) * 0.3).to(DEV)
+    bpos = (torch.randn(din, generator=g) * 0.1).to(DEV)
+    w1 = (torch.randn(dout, din, generator=g) / din ** 0.5).to(DEV)
+    b1 = (torch.randn(dout, generator=g) * 0.1).to(DEV)
+    out, amax = K.cost_volume_fwd(x1, x2, idx, p1, p2, wpos, bpos, w1, b1)
+    gout = torch.randn(bsz, n1, dout, generator=g).to(DEV)
+    dp1, dp2r, dx1, ddr, dpar = K.cost_volume_bwd(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax,
+                                                  gout)
+    csr = K.csr_of(idx, n2)
+    dp2 = K.group_rows_grad(dp2r.view(bsz, n1 * k, din), csr, bsz, n2, din)
+    dx2 = K.group_rows_grad(ddr.view(bsz, n1 * k, 3), csr, bsz, n2, 3)
+    r = K.cost_volume_bwd_csr(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout)
+    rank = K.csr_rank_of(idx, n2).rank
+    assert torch.equal(csr.perm[rank.long()], torch.arange(bsz * n1 * k, device=DEV,
+                                                          dtype=torch.int32))
+    for name, a, b in zip(["dp1", "dp2", "dx1", "dx2", "dparams"], r, [dp1, dp2, dx1, dx2, dpar]):
+        assert a.shape == b.shape and torch.equal(a, b), name
+    assert torch.count_nonzero(r[1][:, -1]) == 0 and torch.count_nonzero(r[3][:, -1]) == 0
+
+
+def test_csr_rank_marks_out_of_range():
+    """kdpc_csr_rank: perm[rank[i]] == i for in-range positions, -1 for the others."""
+    import kdpc_native as K
+    idx = torch.tensor([[3, 0, 7, 3, -1, 2], [1, 1, 9, 0, 2, 5]], dtype=torch.int32, device=DEV)
+    csr = K.csr_rank_of(idx, 4)
+    rank = csr.rank.cpu().numpy()
+    perm = csr.perm.cpu().numpy()
+    flat = idx.cpu().numpy().reshape(-1)
+    for i, v in enumerate(flat):
+        if 0 <= v < 4:
+            assert perm[rank[i]] == i
+        else:
+            assert rank[i] == -1
+
+
 # (PointConvD?, D, N, B, out, bn): the model's level-1/2/4 and estimator shapes, odd sizes
 # (rows not a multiple of 32, channels not a multiple of 8), and an out width the fused
 # layer does not take (96: contraction kernel + Linear GEMM).
