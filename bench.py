@@ -48,8 +48,9 @@ ROOFLINE = {
     "kdpc_pointconv_bwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF,
                            # first name: one launch per entry call (tools count launches by it)
                            ["pc_swizzle_bwd_kernel", "pc_bwd_data_kernel",
-                            "pc_bwd_data_pipe_kernel", "pc_csr_sum_kernel",
-                            "pc_bwd_weight_kernel", "pc_slab_sum_kernel"]),
+                            "pc_bwd_data_pipe_kernel", "pc_bwd_data_ws_kernel",
+                            "pc_csr_sum_kernel", "pc_bwd_weight_kernel",
+                            "pc_bwd_weight_ws_kernel", "pc_slab_sum_kernel"]),
     "kdpc_pointconv_fwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF,
                            ["pc_fwd_kernel", "pc_slab_sum_kernel"]),
     "kdpc_group_rows": ("hbm", "GB/s", HBM_PEAK_GBS, ["group_rows_kernel"]),
@@ -62,8 +63,13 @@ ROOFLINE = {
                        ["ref_sort_kernel", "query_sort_kernel", "chunk_box_kernel",
                         "knn_cull_kernel", "knn_kernel"]),
     "kdpc_gather_points": ("hbm", "GB/s", HBM_PEAK_GBS, ["gather_points_kernel"]),
-    "kdpc_cost_volume_fwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF, ["cost_volume_fwd_kernel"]),
+    "kdpc_cost_volume_fwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF,
+                             ["cost_volume_fwd_kernel", "cvw_fused_fwd_kernel"]),
     "kdpc_cost_volume_bwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF, ["cost_volume_bwd_kernel"]),
+    # the model's backward: rows in CSR order + contiguous per-point sums (+ the slab colsum)
+    "kdpc_cost_volume_bwd_csr": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF,
+                                 ["cv_rows_sum_kernel", "cost_volume_bwd_kernel",
+                                  "cvw_fused_bwd_kernel", "cvw_transpose_kernel"]),
     "kdpc_idw_blend_fwd": ("hbm", "GB/s", HBM_PEAK_GBS, ["idw_fwd_kernel"]),
 }
 # the step's dominant entry point (rocprofv3 step profile, profiles/)

@@ -281,12 +281,13 @@ int kdpc_pointconv_fwd(int b, int n, int s, int k, int d, int o, const float *xy
 
 /* Backward of kdpc_pointconv_fwd for dy (B,S,O): dxyz (B,N,3) (NULL to skip), dfeats (B,N,D),
  * dcenter (B,S,3), dwt (B,S,K,16), dwl (O,16C), all overwritten (bias grad = column sums of
- * dy, left to the caller).  offsets/perm: kdpc_csr_build of idx with key space N.
- * Deterministic: every sum runs in a fixed order. */
+ * dy, left to the caller).  offsets/rank: kdpc_csr_build + kdpc_csr_rank of idx with key
+ * space N (the per-neighbour dG rows are written straight into CSR order and summed as
+ * contiguous runs).  Deterministic: every sum runs in a fixed order. */
 size_t kdpc_pointconv_bwd_workspace_bytes(int b, int s, int k, int d, int o);
 int kdpc_pointconv_bwd(int b, int n, int s, int k, int d, int o, const float *xyz,
                        const float *center, const float *feats, const int *idx, const float *wt,
-                       const float *wl, const float *dy, const int *offsets, const int *perm,
+                       const float *wl, const float *dy, const int *offsets, const int *rank,
                        float *dxyz, float *dfeats, float *dcenter, float *dwt, float *dwl,
                        void *workspace, size_t workspace_bytes, void *stream);
 

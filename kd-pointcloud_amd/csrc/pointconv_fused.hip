@@ -287,7 +287,7 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
         (r < TR && row < g.r) ? dy[(long long)row * O + o] : 0.f;
   }
   float wp[PP][kW], dw[PP][kW];
-  int pr[PP], pk[PP], pn[PP];
+  int pr[PP], pk[PP], pn[PP], ps[PP];
 #pragma unroll
   for (int q = 0; q < PP; ++q) {
     const int p = t + NT * q;
@@ -295,6 +295,7 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
     pk[q] = p - pr[q] * g.k;
     const bool ok = p < TR * g.k && row0 + pr[q] < g.r;
     pn[q] = ok ? nbr_of(g, row0 + pr[q], pk[q]) : -1;
+    ps[q] = ok ? slot_of(g, row0 + pr[q], pk[q]) : -1;
     const long long pos = (long long)(row0 + pr[q]) * g.k + pk[q];
 #pragma unroll
     for (int v = 0; v < kW / 4; ++v) {
@@ -314,6 +315,7 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
   const int xrc = min(xr, TR - 1);  // dA row read (any row when the item is dead)
   const bool xok = XI && xp < TR * g.k && row0 + xr < g.r;
   const int xn = xok ? nbr_of(g, row0 + xr, xp - xr * g.k) : -1;
+  const int xsl = xok ? slot_of(g, row0 + xr, xp - xr * g.k) : -1;
   const long long xpos = (long long)(row0 + xr) * g.k + (xp - xr * g.k);
   float xw[kW], xd[kW], xg = 0.f, xgn = 0.f;
   if constexpr (XI) {
@@ -407,13 +409,12 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
     const int c0 = ch * kCC;
 #pragma unroll
     for (int q = 0; q < PP; ++q) {
-      if (pn[q] < 0) continue;
-      const long long pos = (long long)(row0 + pr[q]) * g.k + pk[q];
-      float4* dgo = reinterpret_cast<float4*>(dgr + dg_off(pos, ch, rk_total, g.c8));
+      if (ps[q] < 0) continue;
+      float4* dgo = reinterpret_cast<float4*>(dgr + dg_off(ps[q], ch, rk_total, g.c8));
       dgo[0] = make_float4(svh[q][0], svh[q][1], svh[q][2], svh[q][3]);
       dgo[1] = make_float4(svh[q][4], svh[q][5], svh[q][6], svh[q][7]);
     }
-    if (XI && xn >= 0) dgr[dg_off(xpos, ch, rk_total, g.c8) + xc] = xsh;
+    if (XI && xsl >= 0) dgr[dg_off(xsl, ch, rk_total, g.c8) + xc] = xsh;
   };
   for (int ch = ch0; ch < ch1; ++ch) {
     const int c0 = ch * kCC;
@@ -595,7 +596,7 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
     dyl[(o >> 2) * kBlk + r * 4 + (o & 3)] = row < g.r ? dy[(long long)row * O + o] : 0.f;
   }
   float wp[PP][kW], dw[PP][kW];
-  int pr[PP], pk[PP], pn[PP], prc[PP];
+  int pr[PP], pk[PP], pn[PP], ps[PP], prc[PP];
 #pragma unroll
   for (int q = 0; q < PP; ++q) {
     const int p = t + NT * q;
@@ -604,6 +605,7 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
     prc[q] = min(pr[q], TR - 1);  // dA row read by this slot (any row when the pair is dead)
     const bool ok = p < TR * g.k && row0 + pr[q] < g.r;
     pn[q] = ok ? nbr_of(g, row0 + pr[q], pk[q]) : -1;
+    ps[q] = ok ? slot_of(g, row0 + pr[q], pk[q]) : -1;
     const long long pos = (long long)(row0 + pr[q]) * g.k + pk[q];
 #pragma unroll
     for (int v = 0; v < kW / 4; ++v) {
@@ -622,6 +624,7 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
   const int xrc = min(xr, TR - 1);
   const bool xok = XI && xp < TR * g.k && row0 + xr < g.r;
   const int xn = xok ? nbr_of(g, row0 + xr, xp - xr * g.k) : -1;
+  const int xsl = xok ? slot_of(g, row0 + xr, xp - xr * g.k) : -1;
   const long long xpos = (long long)(row0 + xr) * g.k + (xp - xr * g.k);
   float xw[kW], xd[kW], xg = 0.f, xgn = 0.f, xs = 0.f;
   if constexpr (XI) {
@@ -724,8 +727,7 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
     const int chs = on ? ch : 0;
 #pragma unroll
     for (int q = 0; q < PP; ++q) {
-      const unsigned pos = (unsigned)((row0 + pr[q]) * g.k + pk[q]);
-      const unsigned off = (on && pn[q] >= 0) ? (unsigned)dg_off(pos, chs, rk_total, g.c8) * 4u : kOOB;
+      const unsigned off = (on && ps[q] >= 0) ? (unsigned)dg_off(ps[q], chs, rk_total, g.c8) * 4u : kOOB;
       __builtin_amdgcn_raw_buffer_store_b128(
           __builtin_bit_cast(f32x4, make_float4(svh[q][0], svh[q][1], svh[q][2], svh[q][3])),
           dg_rs, (int)off, 0, 0);
@@ -734,7 +736,7 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
           dg_rs, (int)(off == kOOB ? kOOB : off + 16u), 0, 0);
     }
     if constexpr (XI) {
-      const unsigned off = (on && xn >= 0) ? (unsigned)(dg_off(xpos, chs, rk_total, g.c8) + xc) * 4u : kOOB;
+      const unsigned off = (on && xsl >= 0) ? (unsigned)(dg_off(xsl, chs, rk_total, g.c8) + xc) * 4u : kOOB;
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, xsh), dg_rs, (int)off, 0, 0);
     }
   };
@@ -900,12 +902,12 @@ __global__ __launch_bounds__(256) void pc_swizzle_bwd_kernel(int o, int c16, int
   }
 }
 
-// d_xyz / d_feats of every point = sum of its dG rows through the CSR (ascending
-// position); one thread per (point, 4 channels)
+// d_xyz / d_feats of every point = sum of its dG rows, which the data kernels wrote in CSR
+// order (slot = rank of the pair): point key's rows are the contiguous slots
+// [offsets[key], offsets[key+1]), ascending position.  One thread per (point, 4 channels).
 __global__ __launch_bounds__(256) void pc_csr_sum_kernel(long long npts, long long rk, int c, int c8, int d,
                                                          const float* __restrict__ dgr,
                                                          const int* __restrict__ offsets,
-                                                         const int* __restrict__ perm,
                                                          float* __restrict__ dxyz,
                                                          float* __restrict__ dfeats) {
   const int nv = c8 / 4;
@@ -922,22 +924,18 @@ __global__ __launch_bounds__(256) void pc_csr_sum_kernel(long long npts, long lo
       s.z = __fadd_rn(s.z, x.z);
       s.w = __fadd_rn(s.w, x.w);
     };
-    // unrolled 8 wide: the perm entries, then the rows, are in flight before the (ordered)
-    // adds -- 2 dependent latencies per 8 rows instead of per row
+    // unrolled 8 wide: the rows are in flight before the (ordered) adds
     int j = j0;
     for (; j + 8 <= j1; j += 8) {
-      int pj[8];
       float4 x[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) pj[u] = perm[j + u];
-#pragma unroll
       for (int u = 0; u < 8; ++u)
-        x[u] = *reinterpret_cast<const float4*>(dgr + dg_off(pj[u], v >> 1, rk, c8) + 4 * (v & 1));
+        x[u] = *reinterpret_cast<const float4*>(dgr + dg_off(j + u, v >> 1, rk, c8) + 4 * (v & 1));
 #pragma unroll
       for (int u = 0; u < 8; ++u) add(x[u]);
     }
     for (; j < j1; ++j)
-      add(*reinterpret_cast<const float4*>(dgr + dg_off(perm[j], v >> 1, rk, c8) + 4 * (v & 1)));
+      add(*reinterpret_cast<const float4*>(dgr + dg_off(j, v >> 1, rk, c8) + 4 * (v & 1)));
     const float sv[4] = {s.x, s.y, s.z, s.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -1538,7 +1536,7 @@ inline bool bwd_pipe_enabled() {
 
 template <int O, int KM>
 hipError_t bwd_launch(const Geo& g, const Plan& p, int b, const float* wt, const float* wl,
-                      const float* dy, const int* offsets, const int* perm, float* dxyz,
+                      const float* dy, const int* offsets, float* dxyz,
                       float* dfeats, float* dcenter, float* dwt, float* dwl, char* ws,
                       hipStream_t st) {
   float* dgr = reinterpret_cast<float*>(ws);
@@ -1583,7 +1581,7 @@ hipError_t bwd_launch(const Geo& g, const Plan& p, int b, const float* wt, const
   const long long work = npts * (p.c8 / 4);
   hipLaunchKernelGGL(pc_csr_sum_kernel,
                      dim3((unsigned)std::min<long long>(divupll(work, 256), 1 << 20)), dim3(256),
-                     0, st, npts, rk, g.c, p.c8, g.d, dgr, offsets, perm, dxyz, dfeats);
+                     0, st, npts, rk, g.c, p.c8, g.d, dgr, offsets, dxyz, dfeats);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // the specialised kernel for K <= 9 (the scene-flow estimators' layers); at K = 16 its
   // producers' in-flight gathers (2 x 16 float4) do not fit beside the rest
@@ -1631,6 +1629,7 @@ Geo geo_of(int b, int n, int s, int k, int d, const Plan& p, const float* xyz, c
   g.center = center;
   g.feats = feats;
   g.idx = idx;
+  g.rank = nullptr;
   return g;
 }
 
@@ -1678,7 +1677,7 @@ KDPC_API size_t kdpc_pointconv_bwd_workspace_bytes(int b, int s, int k, int d, i
 KDPC_API int kdpc_pointconv_bwd(int b, int n, int s, int k, int d, int o, const float* xyz,
                                 const float* center, const float* feats, const int* idx,
                                 const float* wt, const float* wl, const float* dy,
-                                const int* offsets, const int* perm, float* dxyz, float* dfeats,
+                                const int* offsets, const int* rank, float* dxyz, float* dfeats,
                                 float* dcenter, float* dwt, float* dwl, void* workspace,
                                 size_t workspace_bytes, void* stream) {
   Plan p;
@@ -1691,11 +1690,12 @@ KDPC_API int kdpc_pointconv_bwd(int b, int n, int s, int k, int d, int o, const 
     if (e == hipSuccess) e = hipMemsetAsync(dwl, 0, sizeof(float) * o * p.c * kW, st);
     return (int)e;
   }
-  KDPC_CHECK_ARG(xyz && center && idx && wt && wl && dy && offsets && perm && dcenter && dwt &&
+  KDPC_CHECK_ARG(xyz && center && idx && wt && wl && dy && offsets && rank && dcenter && dwt &&
                  dwl && (d == 0 || (feats && dfeats)));
   KDPC_CHECK_ARG(workspace && workspace_bytes >= p.dgr + p.dwt_slab + p.dwl_slab + p.wlt);
-  const Geo g = geo_of(b, n, s, k, d, p, xyz, center, feats, idx);
+  Geo g = geo_of(b, n, s, k, d, p, xyz, center, feats, idx);
+  g.rank = rank;
   char* ws = reinterpret_cast<char*>(workspace);
-  return (int)KDPC_PC_DISPATCH(bwd_launch, g, p, b, wt, wl, dy, offsets, perm, dxyz, dfeats,
+  return (int)KDPC_PC_DISPATCH(bwd_launch, g, p, b, wt, wl, dy, offsets, dxyz, dfeats,
                                dcenter, dwt, dwl, ws, st);
 }

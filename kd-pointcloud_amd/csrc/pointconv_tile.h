@@ -29,6 +29,7 @@ struct Geo {
   const float* center;            // (B,S,3)
   const float* feats;             // (B,N,D)
   const int* idx;                 // (B,S,K)
+  const int* rank;                // (B*S*K) CSR slot of each (row, neighbour) (backward only)
 };
 
 __device__ __forceinline__ f32x16 mfma4(float4 a, float4 b, f32x16 c) {
@@ -55,10 +56,16 @@ __device__ __forceinline__ int nbr_of(const Geo& g, int row, int kk) {
 // of a 64-bit address) and hardware bounds checks (an offset past the buffer reads 0).
 constexpr unsigned kOOB = 0x80000000u;  // byte offset that is always out of range
 
-// float offset of pair pos's 8 dG values of chunk ch in the dG buffer: pair-major, each
-// pair's 32 bytes of a chunk sit C8*4 bytes apart and pc_csr_sum reads a pair's whole row
-// contiguously (chunk-major rows -- full-line stores -- measured round 2: data kernel
-// 576 -> 514 us but pc_csr_sum 86 -> 173 us from its 32-byte gathers, a net loss).
+// CSR slot of neighbour kk of row `row` (the dG row it writes), -1 for none / out of range
+__device__ __forceinline__ int slot_of(const Geo& g, int row, int kk) {
+  return g.rank[(long long)row * g.k + kk];
+}
+
+// float offset of dG row `slot`'s 8 values of chunk ch: rows of C8 floats in CSR order (the
+// pair's slot, slot_of), each row's 32 bytes of a chunk sit C8*4 bytes apart; pc_csr_sum
+// reads every point's rows as one contiguous run (chunk-major rows -- full-line stores --
+// measured round 2: data kernel 576 -> 514 us but pc_csr_sum 86 -> 173 us from its 32-byte
+// gathers, a net loss).
 __device__ __forceinline__ long long dg_off(long long pos, int ch, long long /*rk*/, int c8) {
   return pos * c8 + (long long)ch * kCC;
 }

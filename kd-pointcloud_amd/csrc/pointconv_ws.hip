@@ -101,7 +101,7 @@ void pc_bwd_data_ws_kernel(Geo g, const float* __restrict__ wt, const float4* __
   const int pt = t - 256;
   const Srcs src = srcs_of(g);
   float wp[PP][kW], dw[PP][kW];
-  int pr[PP], pk[PP], pn[PP], prc[PP];
+  int pr[PP], pk[PP], pn[PP], ps[PP], prc[PP];
 #pragma unroll
   for (int q = 0; q < PP; ++q) {
     const int p = pt + NT * q;
@@ -110,6 +110,7 @@ void pc_bwd_data_ws_kernel(Geo g, const float* __restrict__ wt, const float4* __
     prc[q] = min(pr[q], TR - 1);
     const bool ok = p < TR * g.k && row0 + pr[q] < g.r;
     pn[q] = ok ? nbr_of(g, row0 + pr[q], pk[q]) : -1;
+    ps[q] = ok ? slot_of(g, row0 + pr[q], pk[q]) : -1;
     const long long pos = (long long)(row0 + pr[q]) * g.k + pk[q];
 #pragma unroll
     for (int v = 0; v < kW / 4; ++v) {
@@ -128,6 +129,7 @@ void pc_bwd_data_ws_kernel(Geo g, const float* __restrict__ wt, const float4* __
   const int xrc = min(xr, TR - 1);
   const bool xok = XI && xp < TR * g.k && row0 + xr < g.r;
   const int xn = xok ? nbr_of(g, row0 + xr, xp - xr * g.k) : -1;
+  const int xsl = xok ? slot_of(g, row0 + xr, xp - xr * g.k) : -1;
   const long long xpos = (long long)(row0 + xr) * g.k + (xp - xr * g.k);
   float xw[kW], xd[kW], xg = 0.f, xgn = 0.f;
   if constexpr (XI) {
@@ -246,8 +248,7 @@ void pc_bwd_data_ws_kernel(Geo g, const float* __restrict__ wt, const float4* __
     // dG rows of this chunk (branch-free buffer stores; nothing to store -> out of range)
 #pragma unroll
     for (int q = 0; q < PP; ++q) {
-      const unsigned pos = (unsigned)((row0 + pr[q]) * g.k + pk[q]);
-      const unsigned off = pn[q] >= 0 ? (unsigned)dg_off(pos, ch, rk_total, g.c8) * 4u : kOOB;
+      const unsigned off = ps[q] >= 0 ? (unsigned)dg_off(ps[q], ch, rk_total, g.c8) * 4u : kOOB;
       __builtin_amdgcn_raw_buffer_store_b128(
           __builtin_bit_cast(f32x4, make_float4(sv[q][0], sv[q][1], sv[q][2], sv[q][3])), dg_rs,
           (int)off, 0, 0);
@@ -260,7 +261,7 @@ void pc_bwd_data_ws_kernel(Geo g, const float* __restrict__ wt, const float4* __
       }
     }
     if constexpr (XI) {
-      const unsigned off = xn >= 0 ? (unsigned)(dg_off(xpos, ch, rk_total, g.c8) + xc) * 4u : kOOB;
+      const unsigned off = xsl >= 0 ? (unsigned)(dg_off(xsl, ch, rk_total, g.c8) + xc) * 4u : kOOB;
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, xs), dg_rs, (int)off, 0, 0);
       if (xn >= 0 && ch == 0 && xc < 3) dcl[xp * 3 + xc] = xs;
     }

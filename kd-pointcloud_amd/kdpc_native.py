@@ -539,13 +539,16 @@ def pointconv_fwd(xyz, center, feats, idx, wt, wl, bias):
 
 
 def pointconv_bwd(xyz, center, feats, idx, wt, wl, dy, csr, need_xyz=True):
-    """Backward of pointconv_fwd for dy (B,S,O) -> (dxyz|None, dfeats, dcenter, dwt, dwl)."""
+    """Backward of pointconv_fwd for dy (B,S,O) -> (dxyz|None, dfeats, dcenter, dwt, dwl).
+    csr: csr_rank_of(idx, N) (offsets + rank; a plain csr_of gets its rank built here)."""
+    if csr.rank is None:
+        csr = csr_rank_of(idx, xyz.shape[1])
     B, N, _ = _gpu(xyz, "xyz").shape
     S, K = idx.shape[1], idx.shape[2]
     O, C = wl.shape[0], 3 + feats.shape[2]
     R = B * S
     return _op("kdpc_pointconv_bwd", "pointconv_bwd", xyz, center, feats, idx, wt, wl, dy,
-               csr.offsets, csr.perm, bool(need_xyz),
+               csr.offsets, csr.rank, bool(need_xyz),
                work=(4 * R * (2 * K * C + 32 * K + 2 * O) + 8 * O * 16 * C,
                      4.0 * R * K * C * 16 + 4.0 * R * 16 * C * O))
 

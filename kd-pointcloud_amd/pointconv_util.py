@@ -371,7 +371,7 @@ class _PointConvLayer(torch.autograd.Function):
         xyz, center, feats, idx, wt, wl = ctx.saved_tensors
         gy = gy.contiguous()
         dxyz, dfeats, dcenter, dwt, dwl = _nat.pointconv_bwd(
-            xyz, center, feats, idx, wt, wl, gy, _nat.csr_of(idx, xyz.shape[1]),
+            xyz, center, feats, idx, wt, wl, gy, _nat.csr_rank_of(idx, xyz.shape[1]),
             need_xyz=ctx.needs_input_grad[0])
         # fixed-order HIP column sum (torch's tall dim-0 reduction gave wrong sums when
         # replayed from a captured graph, tools/graph_diag.py)

@@ -500,12 +500,14 @@ Tensor pointconv_fwd(Tensor xyz, Tensor center, Tensor feats, Tensor idx, Tensor
 
 std::tuple<c10::optional<Tensor>, Tensor, Tensor, Tensor, Tensor> pointconv_bwd(
     Tensor xyz, Tensor center, Tensor feats, Tensor idx, Tensor wt, Tensor wl, Tensor dy,
-    Tensor offsets, Tensor perm, bool need_xyz) {
+    Tensor offsets, Tensor rank, bool need_xyz) {
   for (auto* t : {&xyz, &center, &feats, &wt, &wl, &dy}) dev(*t, kF, "pointconv input");
-  dev(idx, kI, "idx"), dev(offsets, kI, "offsets"), dev(perm, kI, "perm");
+  dev(idx, kI, "idx"), dev(offsets, kI, "offsets"), dev(rank, kI, "rank");
   GUARD(xyz);
   const int64_t b = xyz.size(0), n = xyz.size(1), s = idx.size(1), k = idx.size(2);
   const int64_t d = feats.size(2), o = wl.size(0), c = 3 + d;
+  TORCH_CHECK(offsets.numel() >= b * n + 1 && rank.numel() >= b * s * k,
+              "kdpc: pointconv_bwd: offsets / rank do not match idx");
   const size_t nb = kdpc_pointconv_bwd_workspace_bytes(b, s, k, d, o);
   TORCH_CHECK(nb > 0, "kdpc: pointconv_bwd: invalid sizes");
   Tensor ws = workspace(nb, xyz);
@@ -515,7 +517,7 @@ std::tuple<c10::optional<Tensor>, Tensor, Tensor, Tensor, Tensor> pointconv_bwd(
   Tensor dwt = empty_f({b, s, k, 16}, xyz);
   Tensor dwl = empty_f({o, 16 * c}, xyz);
   check(kdpc_pointconv_bwd(b, n, s, k, d, o, F(xyz), F(center), F(feats), I(idx), F(wt), F(wl),
-                           F(dy), I(offsets), I(perm), need_xyz ? F(dxyz) : nullptr, F(dfeats),
+                           F(dy), I(offsets), I(rank), need_xyz ? F(dxyz) : nullptr, F(dfeats),
                            F(dcenter), F(dwt), F(dwl), ws.data_ptr(), nb, stream_of(xyz)),
         "pointconv_bwd");
   return {need_xyz ? c10::optional<Tensor>(dxyz) : c10::nullopt, dfeats, dcenter, dwt, dwl};
@@ -849,7 +851,7 @@ TORCH_LIBRARY(kdpc, m) {
   m.def("pointconv_fwd(Tensor xyz, Tensor center, Tensor feats, Tensor idx, Tensor wt, "
         "Tensor wl, Tensor bias) -> Tensor");
   m.def("pointconv_bwd(Tensor xyz, Tensor center, Tensor feats, Tensor idx, Tensor wt, "
-        "Tensor wl, Tensor dy, Tensor offsets, Tensor perm, bool need_xyz) "
+        "Tensor wl, Tensor dy, Tensor offsets, Tensor rank, bool need_xyz) "
         "-> (Tensor?, Tensor, Tensor, Tensor, Tensor)");
   m.def("pointconv_contract_fwd(Tensor xyz, Tensor center, Tensor feats, Tensor idx, "
         "Tensor wt) -> Tensor");
