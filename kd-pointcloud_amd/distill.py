@@ -55,12 +55,21 @@ def _core(model):
     return model.module if isinstance(model, torch.nn.parallel.DistributedDataParallel) else model
 
 
+def _plan_fn(model):
+    """The model's coordinate-only precompute: the FPS chain plus the coordinate-only kNN
+    searches and their CSRs (PointConvBidirection.precompute_plan) where the model has it,
+    else the FPS chain alone."""
+    return getattr(model, "precompute_plan", None) or model.precompute_fps
+
+
 class FpsPrefetch:
-    """Runs the encoder's FPS chain (PointConvBidirection.precompute_fps) for an upcoming
-    batch on a side HIP stream.  FPS is one workgroup per cloud for ~2900 dependent steps
-    (2.5 ms per B=8 step, latency-bound on 16 CUs); issued one step ahead it runs beside the
-    current step's kernels instead of in front of them.  Results are identical to computing
-    FPS inside the forward (same kernel, same inputs)."""
+    """Runs the encoder's FPS chain, the coordinate-only kNN searches and their CSRs
+    (PointConvBidirection.precompute_plan) for an upcoming batch on a side HIP stream.  FPS
+    is one workgroup per cloud for ~2900 dependent steps (2.5 ms per B=8 step,
+    latency-bound on 16 CUs); issued one step ahead it runs beside the current step's
+    kernels instead of in front of them, and the 13 searches that depend on coordinates only
+    run after it on the same stream.  Results are identical to computing them inside the
+    forward (same kernels, same inputs)."""
 
     def __init__(self):
         self.stream = None
@@ -79,7 +88,7 @@ class FpsPrefetch:
             self.stream = torch.cuda.Stream(device=pos1.device)
         self.stream.wait_stream(torch.cuda.current_stream(pos1.device))
         with torch.cuda.stream(self.stream):
-            self.fps = _core(model).precompute_fps(pos1, pos2)
+            self.fps = _plan_fn(_core(model))(pos1, pos2)
             self.event = torch.cuda.Event()
             self.event.record(self.stream)
         # the side stream reads pos1/pos2: keep the caching allocator from handing their
@@ -151,7 +160,7 @@ class KDTrainStep:
         color2 = pos2 if color2 is None else color2
         fps = self.prefetch.take(pos1, pos2)
         if fps is None and pos1.is_cuda:  # teacher and student share one FPS chain
-            fps = _core(self.student).precompute_fps(pos1, pos2)
+            fps = _plan_fn(_core(self.student))(pos1, pos2)
         if next_batch is not None:
             self.prefetch.launch(self.student, next_batch[0], next_batch[1])
         kw = {} if fps is None else {"fps_idx": fps}
@@ -212,7 +221,7 @@ class GraphedStep:
     run eagerly on a side stream (they allocate lazily-initialised state: optimizer moments,
     cached attributes, the communicator).
 
-    prefetch_fn (optional, e.g. PointConvBidirection.precompute_fps): a function of the first
+    prefetch_fn (optional, e.g. PointConvBidirection.precompute_plan): a function of the first
     `n_prefetch` inputs whose result loss_fn takes as `fps=`.  The graph then runs it for the
     next batch on a forked stream, beside this batch's forward/backward, into buffers the next
     replay reads.  A call whose batch is not the previous call's `next_batch` recomputes it
@@ -440,8 +449,7 @@ class GraphedStep:
         self.flat_opt.step()
         torch._foreach_copy_(self._steps, [self._flat_step] * len(self._steps))
         if fork is not None:
-            for c, n in zip(self.fps_cur, self.fps_next):
-                c.copy_(n)
+            torch._foreach_copy_(self.fps_cur, self.fps_next)
 
     def _fps_kw(self, fps):
         return {} if self.prefetch_fn is None else {"fps": fps}
@@ -489,8 +497,7 @@ class GraphedStep:
                 hit = (len(ts) == len(cur) and all(a is b for a, b in zip(ts, cur))
                        and ver == tuple(t._version for t in cur))
             if not hit:  # not prefetched by the previous replay: compute it now
-                for c, n in zip(self.fps_cur, self._eager_prefetch()):
-                    c.copy_(n)
+                torch._foreach_copy_(self.fps_cur, self._eager_prefetch())
             nxt = inputs if next_batch is None else next_batch
             for s, t in zip(self.static_next, nxt[:self.n_prefetch]):
                 s.copy_(t, non_blocking=True)
@@ -515,7 +522,7 @@ def graphed_flow_step(model, optimizer, example_inputs, loss_fn=None, warmup=3, 
         flows, fps1, _, _, _, _, _, _ = model(pos1, pos2, pos1, pos2, **kw)
         return loss_fn(flows, flow, fps1)
     return GraphedStep(run, model.parameters(), optimizer, example_inputs, warmup,
-                       prefetch_fn=model.precompute_fps if prefetch else None, overlap=overlap)
+                       prefetch_fn=_plan_fn(model) if prefetch else None, overlap=overlap)
 
 
 def graphed_kd_step(teacher, student, optimizer, example_inputs, gamma=0.3, beta=0.8, layer=3,
@@ -537,4 +544,4 @@ def graphed_kd_step(teacher, student, optimizer, example_inputs, gamma=0.3, beta
             flows, feat1s, feat2s, fps1, fps2, flow, t_flows, t_feat1s, t_feat2s, t_fps1, t_fps2,
             gamma, beta, layer=layer)
     return GraphedStep(run, student.parameters(), optimizer, example_inputs, warmup,
-                       prefetch_fn=student.precompute_fps if prefetch else None, overlap=overlap)
+                       prefetch_fn=_plan_fn(student) if prefetch else None, overlap=overlap)

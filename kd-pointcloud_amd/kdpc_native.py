@@ -379,6 +379,21 @@ def csr_of(idx, n):
     return csr
 
 
+def attach_csr(idx, n, offsets, perm, rank=None):
+    """Cache an inverted index built elsewhere (e.g. on a prefetch stream:
+    PointConvBidirection.precompute_plan) on the index tensor object, as csr_of /
+    csr_rank_of would have: offsets (B*n+1), perm (B*P)[, rank (B*P)] of idx (B, ...)."""
+    p = idx[0].numel() if idx.shape[0] else 0
+    if offsets.numel() != idx.shape[0] * n + 1 or perm.numel() != idx.numel() or \
+            (rank is not None and rank.numel() != idx.numel()):
+        raise ValueError("attach_csr: CSR sizes do not match the index tensor")
+    csr = Csr.__new__(Csr)
+    csr.offsets, csr.perm, csr.rank = offsets, perm, rank
+    csr.n, csr.p = n, p
+    idx._kdpc_csr = csr
+    return csr
+
+
 def csr_rank_of(idx, n):
     """The CSR of idx (csr_of) with its inverse permutation: rank (B*P) int32, the slot of
     every position (perm[rank[i]] == i), built once and cached with the CSR.  A batch prefix

@@ -82,10 +82,87 @@ class PointConvBidirection(nn.Module):
             x = index_points(x, idx)
         return out
 
-    def _encode(self, pc, color, fps_idx=None):
+    # kNN searches of the forward whose inputs are coordinates only (the clouds and their FPS
+    # subsets): 13 of the 19 searches.  The flow-dependent ones (the warping 3-NN and the
+    # levels-0..2 cost volumes, whose query cloud is the warped pc2) stay in the forward.
+    PLAN_KNN = ("enc1", "enc2", "enc3", "enc4", "encup", "cross3", "up2", "up1", "up0",
+                "est3", "est2", "est1", "est0")
+    # the searches whose backward reads the CSR slot of every (row, neighbour) (PointConv and
+    # cost-volume backward: csr_rank_of); the 3-NN blends only need offsets / perm (csr_of)
+    _PLAN_RANKED = frozenset(("enc1", "enc2", "enc3", "enc4", "cross3",
+                              "est3", "est2", "est1", "est0"))
+
+    def precompute_plan(self, xyz1, xyz2, csr=True):
+        """precompute_fps() plus every coordinate-only kNN search of the forward (PLAN_KNN)
+        and, with csr=True, the inverted indices their backward reads (offsets, perm[, rank]),
+        as one flat list of int32 tensors: [4 FPS] + [13 kNN] + [CSR tensors in PLAN_KNN
+        order].  Like the FPS chain it can run for the NEXT batch on a side stream
+        (distill.FpsPrefetch / GraphedStep's forked stream) and be shared by a KD teacher and
+        student; forward(fps_idx=plan) then takes its searches and CSRs from it.  Same
+        kernels on the same inputs as the forward's own searches: identical results."""
+        B = xyz1.shape[0]
+        x = torch.cat([xyz1, xyz2], 0)
+        fps, pcs = [], [x]
+        downs = (self.level1, self.level2, self.level3, self.level4)
+        for down in downs:
+            idx = pointnet2_utils.furthest_point_sample(x, down.npoint)
+            fps.append(idx)
+            x = index_points(x, idx)
+            pcs.append(x)
+        knn, nref = {}, {}
+        for lv, down in enumerate(downs, start=1):
+            knn[f"enc{lv}"] = down.neighbours(pcs[lv - 1], pcs[lv])
+            nref[f"enc{lv}"] = pcs[lv - 1].shape[1]
+        knn["encup"], nref["encup"] = self.upsample.neighbours(pcs[3], pcs[4]), pcs[4].shape[1]
+        knn["cross3"], nref["cross3"] = self.cross3.neighbours(pcs[3]), pcs[3].shape[1]
+        for lv in (2, 1, 0):
+            knn[f"up{lv}"] = self.upsample.neighbours(pcs[lv], pcs[lv + 1])
+            nref[f"up{lv}"] = pcs[lv + 1].shape[1]
+        for lv, est in ((3, self.flow3), (2, self.flow2), (1, self.flow1), (0, self.flow0)):
+            knn[f"est{lv}"] = est.neighbours(pcs[lv][:B])
+            nref[f"est{lv}"] = pcs[lv].shape[1]
+        out = fps + [knn[k] for k in self.PLAN_KNN]
+        if csr:
+            for k in self.PLAN_KNN:
+                c = (kdpc_native.csr_rank_of(knn[k], nref[k]) if k in self._PLAN_RANKED
+                     else kdpc_native.csr_of(knn[k], nref[k]))
+                out += [c.offsets, c.perm] + ([c.rank] if k in self._PLAN_RANKED else [])
+        return out
+
+    def _unpack_plan(self, plan, npts):
+        """(fps list | None, {PLAN_KNN key: idx}) from a precompute_fps() / precompute_plan()
+        result; the CSR tensors of a full plan are attached to their index tensors (the
+        backward's csr_of / csr_rank_of then find them instead of rebuilding)."""
+        if plan is None:
+            return None, {}
+        plan = list(plan)
+        if len(plan) == 4:
+            return plan, {}
+        nk = len(self.PLAN_KNN)
+        knn = dict(zip(self.PLAN_KNN, plan[4:4 + nk]))
+        rest = plan[4 + nk:]
+        if rest:
+            nref = {"encup": npts[4], "cross3": npts[3]}
+            for lv in (1, 2, 3, 4):
+                nref[f"enc{lv}"] = npts[lv - 1]
+            for lv in (0, 1, 2):
+                nref[f"up{lv}"] = npts[lv + 1]
+            for lv in (0, 1, 2, 3):
+                nref[f"est{lv}"] = npts[lv]
+            i = 0
+            for k in self.PLAN_KNN:
+                ranked = k in self._PLAN_RANKED
+                offsets, perm = rest[i], rest[i + 1]
+                rank = rest[i + 2] if ranked else None
+                i += 3 if ranked else 2
+                kdpc_native.attach_csr(knn[k], nref[k], offsets, perm, rank)
+        return plan[:4], knn
+
+    def _encode(self, pc, color, fps_idx=None, knn=None):
         """Shared encoder on the pair batch (2B).  Returns per-level xyz, features, fps idx.
-        fps_idx: optional precompute_fps() result for this batch."""
+        fps_idx: optional precompute_fps() result for this batch; knn: the plan's searches."""
         pre = fps_idx if fps_idx is not None else [None] * 4
+        knn = knn or {}
         feat_l0 = self.level0_1.cl(self.level0.cl(color))
         feat_l0_1 = self.level0_2.cl(feat_l0)
         levels = [(self.level1, self.level1_0, self.level1_1),
@@ -94,25 +171,30 @@ class PointConvBidirection(nn.Module):
         pcs, feats, feats_out, fps = [pc], [feat_l0], [feat_l0_1], []
         x, f = pc, feat_l0_1
         for lv, (down, mix, widen) in enumerate(levels):
-            x, f, idx = down.forward_cl(x, f, pre[lv])
+            x, f, idx = down.forward_cl(x, f, pre[lv], knn.get(f"enc{lv + 1}"))
             f = mix.cl(f)
             pcs.append(x)
             feats.append(f)
             fps.append(idx)
             f = widen.cl(f)
             feats_out.append(f)
-        pc_l4, feat_l4, _ = self.level4.forward_cl(x, f, pre[3])
-        feat_l4_3 = self.deconv4_3.cl(self.upsample.forward_cl(x, pc_l4, feat_l4))
+        pc_l4, feat_l4, _ = self.level4.forward_cl(x, f, pre[3], knn.get("enc4"))
+        feat_l4_3 = self.deconv4_3.cl(self.upsample.forward_cl(x, pc_l4, feat_l4,
+                                                               knn.get("encup")))
         return pcs, feats, feats_out, fps, feat_l4_3
 
     def forward(self, xyz1, xyz2, color1, color2, fps_idx=None):
         """xyz*, color*: (B,N,3).  Returns (flows, fps_pc1_idxs, fps_pc2_idxs, pc1, pc2,
         feat1s, feat2s, crosses) exactly as the reference (models_bid_pointconv.py:198-207):
-        flows/pcs/features as (B,C,N) (views of the point-major tensors)."""
+        flows/pcs/features as (B,C,N) (views of the point-major tensors).
+        fps_idx: optional precompute_fps() or precompute_plan() result for these clouds."""
         B = xyz1.shape[0]
         pc = torch.cat([xyz1, xyz2], 0)
         color = torch.cat([color1, color2], 0)
-        pcs, feats, feats_out, fps, feat_l4_3 = self._encode(pc, color, fps_idx)
+        npts = [pc.shape[1]] + [d.npoint for d in (self.level1, self.level2, self.level3,
+                                                    self.level4)]
+        fps_idx, knn = self._unpack_plan(fps_idx, npts)
+        pcs, feats, feats_out, fps, feat_l4_3 = self._encode(pc, color, fps_idx, knn)
         # pc1 / pc2 halves of a pair-batch tensor through ONE split per tensor: the backward
         # of a split is one concatenation, where two separate slices would each allocate and
         # zero a full-size gradient and copy into it, and then add the two
@@ -128,8 +210,9 @@ class PointConvBidirection(nn.Module):
 
         # ---- level 3 (coarsest): no prior flow
         c_feat_l3 = torch.cat([feats[3], feat_l4_3], dim=-1)
-        f1n, f2n, cross3 = self.cross3.forward_pair(pcs[3], c_feat_l3)
-        feat_est, flow = self.flow3.forward_cl(one(pcs[3]), one(feats[3]), cross3)
+        f1n, f2n, cross3 = self.cross3.forward_pair(pcs[3], c_feat_l3, knn.get("cross3"))
+        feat_est, flow = self.flow3.forward_cl(one(pcs[3]), one(feats[3]), cross3,
+                                               knn_idx=knn.get("est3"))
         flows, crosses, up_feats = [flow], [cross3], []
 
         decoders = [(2, self.cross2, self.flow2, self.deconv3_2),
@@ -138,7 +221,9 @@ class PointConvBidirection(nn.Module):
         for lv, cross, flow_est, deconv in decoders:
             # one 3-NN search per level pair serves all three upsamplings (both clouds'
             # features, and pc1's flow and estimator features: its first B rows)
-            up_idx = self.upsample.neighbours(pcs[lv], pcs[lv + 1])
+            up_idx = knn.get(f"up{lv}")
+            if up_idx is None:
+                up_idx = self.upsample.neighbours(pcs[lv], pcs[lv + 1])
             f_up = deconv.cl(self.upsample.forward_cl(pcs[lv], pcs[lv + 1],
                                                       torch.cat([f1n, f2n], 0), up_idx))
             up_feats.append(f_up)
@@ -151,7 +236,8 @@ class PointConvBidirection(nn.Module):
             f1n, f2n, cost = cross.forward_pair(torch.cat([pc1_lv, pc2_warp], 0), c_feat)
             feat_up = self.upsample.forward_cl(pc1_lv, one(pcs[lv + 1]), feat_est, up_idx1)
             new_feat1 = torch.cat([one(feats[lv]), feat_up], dim=-1)
-            feat_est, flow = flow_est.forward_cl(pc1_lv, new_feat1, cost, up_flow)
+            feat_est, flow = flow_est.forward_cl(pc1_lv, new_feat1, cost, up_flow,
+                                                 knn_idx=knn.get(f"est{lv}"))
             flows.insert(0, flow)
             crosses.insert(0, cost)
 

@@ -471,15 +471,19 @@ class PointConvD(_PointConvBase):
         new_xyz, new_points, fps_idx = self.forward_cl(_cl(xyz), _cl(points))
         return new_xyz.permute(0, 2, 1), new_points.permute(0, 2, 1), fps_idx
 
-    def forward_cl(self, xyz, points, fps_idx=None):
+    def neighbours(self, xyz, new_xyz):
+        """The group_query() kNN of this layer: new_xyz (B,S,3) in xyz (B,N,3)."""
+        return knn_point(self.nsample, xyz.contiguous(), new_xyz.contiguous())
+
+    def forward_cl(self, xyz, points, fps_idx=None, knn_idx=None):
         """Point-major: xyz (B,N,3), points (B,N,D) -> (new_xyz (B,S,3), feats (B,S,out),
         fps_idx (B,S)).  fps_idx: optional precomputed FPS of xyz (the model runs the whole
-        FPS chain ahead, on a side stream)."""
+        FPS chain ahead, on a side stream); knn_idx: optional precomputed neighbours()."""
         xyz = xyz.contiguous()
         if fps_idx is None:
             fps_idx = pointnet2_utils.furthest_point_sample(xyz, self.npoint)
         new_xyz = index_points_gather(xyz, fps_idx)
-        idx = knn_point(self.nsample, xyz, new_xyz)  # group_query()
+        idx = self.neighbours(xyz, new_xyz) if knn_idx is None else knn_idx  # group_query()
         new_points = self._finish(self._linear_features(xyz, new_xyz, points.contiguous(), idx))
         return new_xyz, new_points, fps_idx
 
@@ -672,16 +676,25 @@ class CrossLayerLight(nn.Module):
         """Point-major: pc* (B,N,3), feat* (B,N,C)."""
         return self.forward_pair(torch.cat([pc1, pc2], 0), torch.cat([feat1, feat2], 0))
 
-    def forward_pair(self, xa, fa):
+    def neighbours(self, xa):
+        """The kNN forward_pair() runs on the pair batch xa = cat(pc1, pc2): every point's
+        nsample nearest in the other cloud of its pair."""
+        B = xa.shape[0] // 2
+        xa1, xa2 = xa.split(B)
+        return knn_point(self.nsample, torch.cat([xa2, xa1], 0), xa.contiguous())
+
+    def forward_pair(self, xa, fa, idx=None):
         """Point-major pair batch: xa = cat(pc1, pc2) (2B,N,3), fa = cat(feat1, feat2).
         Both directions of the first cost volume run as ONE batch of 2B (shared weights, no
-        BN between them), then the pc1-side refinement with pos2/mlp2."""
+        BN between them), then the pc1-side refinement with pos2/mlp2.  idx: optional
+        precomputed neighbours(xa)."""
         B = xa.shape[0] // 2
         xa1, xa2 = xa.split(B)
         xb = torch.cat([xa2, xa1], 0)
         # one kNN serves both directions, and its pc1 half is exactly the neighbour set of
         # the refinement cross(pc1, pc2) below (the reference searches it twice)
-        idx = knn_point(self.nsample, xb, xa)
+        if idx is None:
+            idx = knn_point(self.nsample, xb, xa)
         ta = _linear_1x1(self.cross_t11, fa)
         tb = _linear_1x1(self.cross_t22, fa)  # t22 of cat(feat2, feat1) = halves swapped
         tb1, tb2 = tb.split(B)
@@ -982,13 +995,21 @@ class SceneFlowEstimatorResidual(nn.Module):
                                            None if flow is None else _cl(flow))
         return new_points.permute(0, 2, 1), flow.permute(0, 2, 1)
 
-    def forward_cl(self, xyz, feats, cost_volume, flow=None):
-        """Point-major: xyz (B,N,3), feats (B,N,F), cost (B,N,C), flow (B,N,3)."""
+    def neighbours(self, xyz):
+        """The self-kNN every PointConv of this estimator groups with (None without any)."""
+        if not len(self.pointconv_list):
+            return None
+        xyz = xyz.contiguous()
+        return knn_point(self.pointconv_list[0].nsample, xyz, xyz)
+
+    def forward_cl(self, xyz, feats, cost_volume, flow=None, knn_idx=None):
+        """Point-major: xyz (B,N,3), feats (B,N,F), cost (B,N,C), flow (B,N,3).  knn_idx:
+        optional precomputed neighbours(xyz)."""
         new_points = torch.cat([feats, cost_volume], dim=-1)
         # every PointConv here groups the same cloud with the same K: one self-kNN
         xyz = xyz.contiguous()
-        knn_idx = knn_point(self.pointconv_list[0].nsample, xyz, xyz) \
-            if len(self.pointconv_list) else None
+        if knn_idx is None:
+            knn_idx = self.neighbours(xyz)
         for pointconv in self.pointconv_list:
             same = pointconv.nsample == self.pointconv_list[0].nsample
             new_points = pointconv.forward_cl(xyz, new_points, knn_idx if same else None)

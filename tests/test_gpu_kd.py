@@ -130,3 +130,37 @@ def test_reductions_replay_from_graph():
             if not torch.equal(outs[k], want):
                 bad[(seed, k)] = float((outs[k] - want).abs().max())
     assert not bad, bad
+
+
+def test_coordinate_plan_equals_inline_searches():
+    """PointConvBidirection.precompute_plan (FPS chain + the 13 coordinate-only kNN searches
+    + their CSRs, the prefetched work of the training steps) gives the same flows, loss and
+    gradients, bit for bit, as the forward running every search itself; an FPS-only plan
+    (precompute_fps) as well."""
+    import loss_functions as L
+    from models_bid_pointconv import PointConvBidirection
+    torch.manual_seed(3)
+    base = PointConvBidirection().to(DEV).train()
+    p1, p2, fl = _batch(2, 8192, 51)
+    plan = base.precompute_plan(p1, p2)
+    nk = len(PointConvBidirection.PLAN_KNN)
+    assert len(plan) == 4 + nk + sum(3 if k in PointConvBidirection._PLAN_RANKED else 2
+                                     for k in PointConvBidirection.PLAN_KNN)
+    runs = []
+    for pre in (None, base.precompute_fps(p1, p2), [t.clone() for t in plan]):
+        m = copy.deepcopy(base)
+        kw = {} if pre is None else {"fps_idx": pre}
+        out = m(p1, p2, p1, p2, **kw)
+        loss = L.multiScaleLoss(out[0], fl, out[1])
+        loss.backward()
+        torch.cuda.synchronize()
+        runs.append((loss.detach(), [f.detach() for f in out[0]],
+                     {n: p.grad for n, p in m.named_parameters()}))
+    ref = runs[0]
+    for loss, flows, grads in runs[1:]:
+        assert torch.equal(loss, ref[0]), (float(loss), float(ref[0]))
+        for a, b in zip(flows, ref[1]):
+            assert torch.equal(a, b)
+        for n, g in grads.items():
+            assert (g is None) == (ref[2][n] is None), n
+            assert g is None or torch.equal(g, ref[2][n]), n
