@@ -1550,9 +1550,12 @@ hipError_t bwd_launch(const Geo& g, const Plan& p, int b, const float* wt, const
                      O, c16, g.nch, wl, wsw);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  static const bool dat_ws = [] {  // KDPC_PC_DAT_WS=0: the single-role kernels (A/B runs)
+  // Warp-specialised data kernel: opt-in (KDPC_PC_DAT_WS=1).  In the whole training step it
+  // measured level with the pipelined kernel (17.57 vs 17.56 ms/step, round 3), so the
+  // single-role kernel stays the default.
+  static const bool dat_ws = [] {
     const char* v = getenv("KDPC_PC_DAT_WS");
-    return !(v && v[0] == '0');
+    return v && v[0] == '1';
   }();
   bool launched = false;
   // the pipelined kernels store dG through a buffer resource (31-bit byte offsets)
@@ -1585,9 +1588,12 @@ hipError_t bwd_launch(const Geo& g, const Plan& p, int b, const float* wt, const
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // the specialised kernel for K <= 9 (the scene-flow estimators' layers); at K = 16 its
   // producers' in-flight gathers (2 x 16 float4) do not fit beside the rest
-  static const bool ws_env = [] {  // KDPC_PC_WGT_WS=0: the unspecialised kernel (A/B runs)
+  // Warp-specialised weight kernel: opt-in (KDPC_PC_WGT_WS=1).  Faster on the isolated flow0
+  // microbench, slower in the whole step (round 3: 18.19 vs 17.57 ms/step, backward entry
+  // 426 vs 376 us per launch), so the unspecialised kernel stays the default.
+  static const bool ws_env = [] {
     const char* v = getenv("KDPC_PC_WGT_WS");
-    return !(v && v[0] == '0');
+    return v && v[0] == '1';
   }();
   float* wdst = p.rs > 1 ? dwl_slab : dwl;
   bool done = false;

@@ -433,11 +433,24 @@ def three_interpolate_grad(grad_out, idx, weight, m):
 
 
 # ------------------------------------------------------------------ fused cost volume
+# The one-kernel wide cost volume (cost_volume_wide.hip cvw_fused_*: Din = Dout in {128, 256})
+# is opt-in for the model layers (KDPC_CV_WIDE_FUSED=1).  It matches float64 to ~2e-7 on
+# every one of the model's wide calls (tools/cv_insitu.py), but its fp32 rounding differs
+# from the BLAS GEMM's, and on the N=2048 gradient parity fixture that difference moves one
+# LeakyReLU pre-activation of cross1 (|h| = 2e-8) to the other side of 0 from the float64
+# reference (tools/cv_sensitivity.py): the derivative jump (1 vs 0.1) then puts the coarse
+# levels' bias gradients 5e-4 off the reference, over the test's 1e-5.  The default keeps the
+# BLAS-based wide path (cvw_h0 / GEMM / cvw_max kernels), which lands on the reference's side.
+WIDE_FUSED = os.environ.get("KDPC_CV_WIDE_FUSED") == "1"
+
+
 def cost_volume_supported(din, dout, k):
-    """Shapes of the fused cost-volume kernels: Din, Dout in {32, 64} (cost_volume.hip), or
-    Din = Dout in {128, 256} (the fused wide kernels of cost_volume_wide.hip); K <= 32."""
+    """Shapes the model layers run through kdpc_cost_volume_fwd/_bwd: Din, Dout in {32, 64}
+    (cost_volume.hip), plus Din = Dout in {128, 256} (the fused wide kernels of
+    cost_volume_wide.hip) when WIDE_FUSED; K <= 32.  (The C entry points accept the wide
+    shapes either way.)"""
     narrow = din in (32, 64) and dout in (32, 64)
-    wide = din == dout and din in (128, 256)
+    wide = WIDE_FUSED and din == dout and din in (128, 256)
     return (narrow or wide) and 1 <= k <= 32
 
 
