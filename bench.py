@@ -48,9 +48,9 @@ ROOFLINE = {
     "kdpc_pointconv_bwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF,
                            # first name: one launch per entry call (tools count launches by it)
                            ["pc_swizzle_bwd_kernel", "pc_bwd_data_kernel",
-                            "pc_bwd_data_pipe_kernel", "pc_bwd_data_ws_kernel",
+                            "pc_bwd_data_pipe_kernel",
                             "pc_csr_sum_kernel", "pc_bwd_weight_kernel",
-                            "pc_bwd_weight_ws_kernel", "pc_slab_sum_kernel"]),
+                            "pc_slab_sum_kernel"]),
     "kdpc_pointconv_fwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF,
                            ["pc_fwd_kernel", "pc_slab_sum_kernel"]),
     "kdpc_group_rows": ("hbm", "GB/s", HBM_PEAK_GBS, ["group_rows_kernel"]),

@@ -39,7 +39,7 @@ CFLAGS = [
 # per-source extra flags.  cost_volume.hip: no SLP packing (v_pk_fma pairs of independent
 # accumulators force their LDS operands into adjacent registers, hoisted in bulk: the
 # backward kernel went from 182 to >256 VGPRs with it)
-EXTRA_FLAGS = {"cost_volume.hip": ["-fno-slp-vectorize"], "pointconv_ws.hip": ["-fno-slp-vectorize"]}
+EXTRA_FLAGS = {"cost_volume.hip": ["-fno-slp-vectorize"]}
 
 
 def source_files(csrc=CSRC, root=ROOT):

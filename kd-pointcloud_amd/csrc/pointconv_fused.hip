@@ -1195,236 +1195,6 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
     }
 }
 
-// Warp-specialised weight-gradient kernel.  In pc_bwd_weight_kernel every wave runs both
-// phases of a row tile (its MFMAs, then its share of the next tile's A build) between
-// workgroup barriers, so the two waves sharing a SIMD -- same workgroup, same barriers -- run
-// their MFMA phases together (the matrix core serialises them) and their build phases
-// together (the matrix core idles): round-2 stamps, 26 % MFMA issue per wave.  Here waves 0-3
-// only multiply and waves 4-7 only load and build, one per SIMD each: while a consumer wave
-// streams its MFMAs for tile t, the producer wave of the same SIMD gathers tile t+2 and builds
-// tile t+1's A block into the other LDS buffer; one barrier per tile.
-//   consumer wave c: the 32 A columns 32c..32c+31 of the chunk x all O/32 row tiles of dy^T
-//                    (O/32 accumulators), inner index = the tile's 32 rows;
-//   producer thread: (row r, 4 channels 4cq.., 4 weights 4wq..): A[r][c][w] = sum_k G wt, G
-//                    gathered once per wave into its own LDS region, wt in registers; dy rows
-//                    -> dy^T in LDS.
-// Same rows, same inner order (rows 8gb+j / 8gb+4+j per MFMA block, tiles in order) and the
-// same fma chains as pc_bwd_weight_kernel: bit-identical dwl.
-template <int O, int KM, bool EX>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
-void pc_bwd_weight_ws_kernel(Geo g, const float* __restrict__ wt, const float* __restrict__ dy,
-                             float* __restrict__ dwl, int rows_per_split, int nsplit, int xcd_map) {
-  constexpr int TR = 32;                   // rows per tile (MFMA inner dimension)
-  constexpr int TS = TR + 4;               // row stride of the transposed tiles
-  constexpr int MT = O / 32;               // dy^T row tiles = accumulators per consumer wave
-  constexpr int DV = TR * O / (256 * 4);   // dy float4 slots per producer thread
-  static_assert(DV >= 1 && TR * O % 1024 == 0, "dy tile must split into float4 slots");
-  __shared__ __attribute__((aligned(16))) float dyt[2][O * TS];
-  __shared__ __attribute__((aligned(16))) float at[2][kNC * TS];
-  __shared__ __attribute__((aligned(16))) float gls[4][8 * KM * kCC];  // producer waves' G
-
-  const int L = blockIdx.x;
-  int ch, split;
-  if (xcd_map) {  // as pc_bwd_weight_kernel: a split's chunks on one or two XCDs
-    const int per_xcd = (int)gridDim.x >> 3;
-    const int pidx = (L & 7) * per_xcd + (L >> 3);
-    split = pidx / g.nch;
-    ch = pidx % g.nch;
-  } else {
-    ch = L % g.nch;
-    split = L / g.nch;
-  }
-  if (split >= nsplit) return;
-  const int c0 = ch * kCC;
-  const int kk = EX ? KM : g.k;
-  const int rbeg = split * rows_per_split;
-  const int rend = min(g.r, rbeg + rows_per_split);
-  const int ntiles = (rend - rbeg + TR - 1) / TR;
-  if (ntiles <= 0) return;
-  const int t = threadIdx.x, lane = t & 63, half = lane >> 5, l32 = lane & 31;
-  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);  // uniform role branch (see data ws)
-  const bool consumer = wv < 4;
-  const long long c16 = (long long)g.c * kW;
-
-  f32x16 acc[MT];
-#pragma unroll
-  for (int i = 0; i < MT; ++i) acc[i] = zero16();
-
-  // ---- producer state: thread pt -> (row r, channel quad cq, weight quad wq).  Producer
-  // wave pw owns rows 8pw .. 8pw+7 of the tile: it gathers their neighbours' chunk channels
-  // once (slot = (row, neighbour, channel half), 16 bytes, as pc_bwd_weight_kernel), stages
-  // them in a private LDS region and reads them back broadcast to the four weight-quad lanes
-  // of each row -- only this wave touches the region, so no workgroup barrier is needed
-  // between its write and its read (an lgkmcnt wait, and the wave's own LDS order).
-  const int pt = t - 256;
-  const int pw = (pt >> 6) & 3, pl = pt & 63;
-  const int pr = (pt >> 3) & 31, cq = (pt >> 2) & 1, wq = pt & 3;
-  constexpr int NPAIR = 8 * KM;                 // (row, neighbour) pairs per producer wave
-  constexpr int GSW = (2 * NPAIR + 63) / 64;    // gather slots (float4) per lane
-  float* glw = gls[pw];
-  const Srcs src = srcs_of(g);
-  const __amdgpu_buffer_rsrc_t idx_rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<int*>(g.idx), (short)0, (int)((long long)g.r * g.k * 4), 0x00020000);
-  const __amdgpu_buffer_rsrc_t wt_rs = rsrc(wt, (long long)g.r * kk * kW);
-  const __amdgpu_buffer_rsrc_t dy_rs = rsrc(dy, (long long)g.r * O);
-  // The raw indices stay untouched until the gathers that need them: adding the batch base
-  // right after the loads made the wave wait for them -- and, loads retiring in issue order,
-  // for the gathers issued just before -- ahead of every barrier.
-  constexpr int kNoNbr = 1 << 30;
-  int sj[GSW];                 // raw kNN index of each gather slot (tile being loaded next)
-  int sbase[GSW];              // its row's b*N, kNoNbr for none
-  f32x4 gsl[GSW];              // gathered slots (tile in flight)
-  f32x4 wq4[KM];               // wt (4 weights) per neighbour
-  float4 dq[DV];               // dy slots
-  auto load_idx = [&](int tile) {
-#pragma unroll
-    for (int i = 0; i < GSW; ++i) {
-      const int sl = pl + 64 * i, pair = sl >> 1;
-      const int rr = pair / KM, k = pair - rr * KM;
-      const int row = rbeg + tile * TR + 8 * pw + rr;
-      const bool ok = sl < 2 * NPAIR && tile < ntiles && row < rend && k < kk;
-      // unconditional division, then selects (a division under the condition became a branch)
-      const unsigned bq = (unsigned)row / (unsigned)g.s;
-      sbase[i] = ok ? (int)bq * g.n : kNoNbr;
-      unsigned off = ok ? ((unsigned)row * (unsigned)g.k + (unsigned)k) * 4u : kOOB;
-      // opaque to the optimiser: it unswitched the selects into a branch per load (and a
-      // vmcnt(0) drain behind each)
-      asm volatile("" : "+v"(off));
-      sj[i] = (int)__builtin_amdgcn_raw_buffer_load_b32(idx_rs, (int)off, 0, 0);
-    }
-  };
-  // every load unconditional (out-of-range offsets read 0): no branch splits the load queue
-  auto load_tile = [&](int tile) {
-#pragma unroll
-    for (int i = 0; i < GSW; ++i) {
-      const int sl = pl + 64 * i, pair = sl >> 1, h4 = sl & 1;
-      const int rr = pair / KM;
-      const int row = rbeg + tile * TR + 8 * pw + rr;
-      const int nb = sbase[i] + sj[i];
-      const bool live = (unsigned)nb < (unsigned)g.bn;
-      const bool xyzq = c0 == 0 && h4 == 0;  // chunk 0, channels 0..3 = xyz - center, feat 0
-      const int vch = c0 == 0 ? (h4 ? 1 : 0) : c0 - 3 + 4 * h4;  // first feature of the load
-      const unsigned voff = live ? (unsigned)nb * (unsigned)g.d * 4u + (unsigned)vch * 4u : kOOB;
-      const unsigned xoff = (xyzq && live) ? (unsigned)nb * 12u : kOOB;
-      const unsigned coff = (xyzq && live) ? (unsigned)row * 12u : kOOB;
-      const f32x4 v = __builtin_bit_cast(
-          f32x4, __builtin_amdgcn_raw_buffer_load_b128(src.feats, (int)voff, 0, 0));
-      const f32x4 x = __builtin_bit_cast(
-          f32x4, __builtin_amdgcn_raw_buffer_load_b128(src.xyz, (int)xoff, 0, 0));
-      const f32x4 cc = __builtin_bit_cast(
-          f32x4, __builtin_amdgcn_raw_buffer_load_b128(src.center, (int)coff, 0, 0));
-      const int cg = c0 + 4 * h4;
-      const float a0 = xyzq ? 0.f : (cg < g.c ? v[0] : 0.f);
-      const float a1 = xyzq ? 0.f : (cg + 1 < g.c ? v[1] : 0.f);
-      const float a2 = xyzq ? 0.f : (cg + 2 < g.c ? v[2] : 0.f);
-      const float a3 = xyzq ? (3 < g.c ? v[0] : 0.f) : (cg + 3 < g.c ? v[3] : 0.f);
-      gsl[i] = f32x4{a0 + (x[0] - cc[0]), a1 + (x[1] - cc[1]), a2 + (x[2] - cc[2]), a3};
-    }
-    const int row = rbeg + tile * TR + pr;
-    const bool ok = tile < ntiles && row < rend;
-#pragma unroll
-    for (int k = 0; k < KM; ++k) {
-      const unsigned woff = (ok && k < kk) ? (((unsigned)row * (unsigned)kk + k) * kW + 4u * wq) * 4u : kOOB;
-      wq4[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wt_rs, (int)woff, 0, 0));
-    }
-    // dy slot i: row (pt & 31), columns 4 ((pt >> 5) + 8 i) .. +3 (lanes = consecutive rows)
-#pragma unroll
-    for (int i = 0; i < DV; ++i) {
-      const int rw = rbeg + tile * TR + (pt & 31);
-      const int q = (pt >> 5) + 8 * i;
-      const unsigned off = (tile < ntiles && rw < rend) ? ((unsigned)rw * O + 4u * (unsigned)q) * 4u : kOOB;
-      dq[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(dy_rs, (int)off, 0, 0));
-    }
-  };
-  auto build = [&](int buf) {  // registers -> this wave's G region, dy^T and A of buffer buf
-#pragma unroll
-    for (int i = 0; i < GSW; ++i) {
-      const int sl = pl + 64 * i;
-      if (sl < 2 * NPAIR) *reinterpret_cast<f32x4*>(glw + 4 * sl) = gsl[i];
-    }
-    float* dt = dyt[buf];
-#pragma unroll
-    for (int i = 0; i < DV; ++i) {
-      const int r = pt & 31, o = 4 * ((pt >> 5) + 8 * i);
-      dt[(o + 0) * TS + r] = dq[i].x;
-      dt[(o + 1) * TS + r] = dq[i].y;
-      dt[(o + 2) * TS + r] = dq[i].z;
-      dt[(o + 3) * TS + r] = dq[i].w;
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's G stores have landed
-    __builtin_amdgcn_wave_barrier();
-    float a[4][4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-      for (int w = 0; w < 4; ++w) a[c][w] = 0.f;
-    const int rr = pr & 7;
-#pragma unroll
-    for (int k = 0; k < KM; ++k) {
-      if (k < kk) {
-        const f32x4 gv = *reinterpret_cast<const f32x4*>(glw + ((rr * KM + k) * 2 + cq) * 4);
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-#pragma unroll
-          for (int w = 0; w < 4; ++w) a[c][w] = __builtin_fmaf(gv[c], wq4[k][w], a[c][w]);
-      }
-    }
-    float* ab = at[buf];
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-      for (int w = 0; w < 4; ++w) ab[((4 * cq + c) * kW + 4 * wq + w) * TS + pr] = a[c][w];
-  };
-
-  // The two roles run separate loops with the same barrier sequence (one per tile), so
-  // their registers (accumulators vs. in-flight gathers) are never live at the same time.
-  if (!consumer) {
-    // prologue: tile 0 built, tile 1's loads in flight, tile 2's indices
-    load_idx(0);
-    load_tile(0);
-    build(0);
-    load_idx(1);
-    load_tile(1);
-    load_idx(2);
-    __syncthreads();
-    for (int tile = 0; tile < ntiles; ++tile) {
-      if (tile + 1 < ntiles) {
-        build((tile & 1) ^ 1);        // tile + 1 (its loads were issued one iteration ago)
-        load_tile(tile + 2);   // tile + 2 (indices loaded one iteration ago)
-        load_idx(tile + 3);
-      }
-      __syncthreads();
-    }
-    return;
-  }
-  __syncthreads();
-  for (int tile = 0; tile < ntiles; ++tile) {
-    const int cur = tile & 1;
-    const float* dt = dyt[cur];
-    const float* ab = at[cur];
-#pragma unroll
-    for (int gb = 0; gb < TR / 8; ++gb) {
-      const float4 bv = *reinterpret_cast<const float4*>(ab + (wv * 32 + l32) * TS + 8 * gb + 4 * half);
-#pragma unroll
-      for (int i = 0; i < MT; ++i) {
-        const float4 av = *reinterpret_cast<const float4*>(dt + (i * 32 + l32) * TS + 8 * gb + 4 * half);
-        acc[i] = mfma4(av, bv, acc[i]);
-      }
-    }
-    __syncthreads();
-  }
-  const long long col = (long long)c0 * kW + wv * 32 + l32;
-  if (col >= c16) return;
-  float* dst = dwl + (long long)split * O * c16;  // slab index when the rows are split
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int o = i * 32 + (e & 3) + 8 * (e >> 2) + 4 * half;
-      dst[o * c16 + col] = acc[i][e];
-    }
-}
-
 // ------------------------------------------------------------------------------- host
 struct Plan {
   int r, c, nch, c8, tm, rt;  // tm: forward tile rows
@@ -1550,26 +1320,9 @@ hipError_t bwd_launch(const Geo& g, const Plan& p, int b, const float* wt, const
                      O, c16, g.nch, wl, wsw);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  // Warp-specialised data kernel: opt-in (KDPC_PC_DAT_WS=1).  In the whole training step it
-  // measured level with the pipelined kernel (17.57 vs 17.56 ms/step, round 3), so the
-  // single-role kernel stays the default.
-  static const bool dat_ws = [] {
-    const char* v = getenv("KDPC_PC_DAT_WS");
-    return v && v[0] == '1';
-  }();
-  bool launched = false;
   // the pipelined kernels store dG through a buffer resource (31-bit byte offsets)
   const bool dg31 = (long long)p.r * g.k * p.c8 * 4 < (1ll << 31);
-  if constexpr (KM <= 9) {
-    if (dat_ws && dg31) {
-      e = pc_bwd_data_ws(O, g, dim3(divup(p.r, 32), p.bks), wt, wsw, dy, dgr,
-                         p.bks > 1 ? dwt_slab : dwt, dcenter, p.bcps, st);
-      if (e != hipSuccess) return e;
-      launched = true;
-    }
-  }
-  if (launched) {
-  } else if (bwd_pipe_enabled<KM>() && dg31)
+  if (bwd_pipe_enabled<KM>() && dg31)
     hipLaunchKernelGGL((pc_bwd_data_pipe_kernel<O, KM>), dim3(divup(p.r, 32), p.bks), dim3(256),
                        0, st, g, wt, wsw, dy, dgr, p.bks > 1 ? dwt_slab : dwt, dcenter, p.bcps);
   else
@@ -1586,30 +1339,8 @@ hipError_t bwd_launch(const Geo& g, const Plan& p, int b, const float* wt, const
                      dim3((unsigned)std::min<long long>(divupll(work, 256), 1 << 20)), dim3(256),
                      0, st, npts, rk, g.c, p.c8, g.d, dgr, offsets, dxyz, dfeats);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  // the specialised kernel for K <= 9 (the scene-flow estimators' layers); at K = 16 its
-  // producers' in-flight gathers (2 x 16 float4) do not fit beside the rest
-  // Warp-specialised weight kernel: opt-in (KDPC_PC_WGT_WS=1).  Faster on the isolated flow0
-  // microbench, slower in the whole step (round 3: 18.19 vs 17.57 ms/step, backward entry
-  // 426 vs 376 us per launch), so the unspecialised kernel stays the default.
-  static const bool ws_env = [] {
-    const char* v = getenv("KDPC_PC_WGT_WS");
-    return v && v[0] == '1';
-  }();
   float* wdst = p.rs > 1 ? dwl_slab : dwl;
-  bool done = false;
-  if constexpr (KM <= 9) {
-    if (ws_env) {
-      if (g.k == KM)
-        hipLaunchKernelGGL((pc_bwd_weight_ws_kernel<O, KM, true>), dim3(p.wgs), dim3(512), 0, st,
-                           g, wt, dy, wdst, p.rps, p.rs, p.xcd);
-      else
-        hipLaunchKernelGGL((pc_bwd_weight_ws_kernel<O, KM, false>), dim3(p.wgs), dim3(512), 0, st,
-                           g, wt, dy, wdst, p.rps, p.rs, p.xcd);
-      done = true;
-    }
-  }
-  if (done) {
-  } else if (g.k == KM)
+  if (g.k == KM)
     hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM, true>), dim3(p.wgs), dim3(512), 0, st, g, wt,
                        dy, wdst, p.rps, p.rs, p.xcd);
   else

@@ -136,10 +136,4 @@ __device__ __forceinline__ void build_row(const float* gl, int r, int k_n, const
   }
 }
 
-// pointconv_ws.hip: the warp-specialised data kernel (K <= 9, O in {64, 128, 256}),
-// compiled in its own translation unit (no SLP vectorisation; see there)
-hipError_t pc_bwd_data_ws(int o, const Geo& g, dim3 grid, const float* wt, const float4* wsw,
-                          const float* dy, float* dgr, float* dwt, float* dcenter,
-                          int chunks_per_split, hipStream_t st);
-
 }  // namespace kdpc_pc

@@ -343,3 +343,40 @@ def test_idw_blend_vs_fp64(b, s, n, c, warp):
         P._FUSED_IDW = True
     _scale_close(out, out2, name="out vs unfused")
     _scale_close(V.grad, V2.grad, name="dvals vs unfused")
+
+
+@pytest.mark.parametrize("d,n1,n2,bsz,k", [(128, 300, 280, 2, 32), (128, 128, 128, 1, 32),
+                                           (256, 64, 64, 2, 32), (256, 200, 250, 2, 20)])
+def test_one_kernel_wide_cost_volume_equals_blas_path(d, n1, n2, bsz, k):
+    """The one-kernel wide cost volume (cvw_fused_*, reached through kdpc_cost_volume_fwd /
+    _bwd_csr at Din = Dout in {128, 256}; opt-in for the model, KDPC_CV_WIDE_FUSED=1) equals
+    the BLAS-based wide path (_CostVolumeWide) on the same inputs and routing: forward
+    values and every gradient within 2e-5 of the tensor scale."""
+    import kdpc_native as K
+    import pointconv_util as P
+    import synthetic
+    torch.manual_seed(d + n1 + bsz)
+    x1 = torch.from_numpy(synthetic.ft3d_batch(bsz, n1, seed=1)[0]).to(DEV)
+    x2 = torch.from_numpy(synthetic.ft3d_batch(bsz, n2, seed=2)[0]).to(DEV)
+    p1 = torch.randn(bsz, n1, d, device=DEV)
+    p2 = torch.randn(bsz, n2, d, device=DEV)
+    wpos = torch.randn(d, 3, device=DEV) * 0.3
+    bpos = torch.randn(d, device=DEV) * 0.1
+    w1 = torch.randn(d, d, device=DEV) / d ** 0.5
+    b1 = torch.randn(d, device=DEV) * 0.1
+    idx = P._as_idx32(P.knn_point(k, x2, x1)).contiguous()
+    out_f, am_f = K.cost_volume_fwd(x1, x2, idx, p1, p2, wpos, bpos, w1, b1)
+    torch.manual_seed(5)
+    gout = torch.randn_like(out_f)
+    dp1, dp2, dx1, dx2, dpar = K.cost_volume_bwd_csr(x1, x2, idx, p1, p2, wpos, bpos, w1,
+                                                     out_f, am_f, gout)
+    ts = [t.detach().clone().requires_grad_(True) for t in (x1, x2, p1, p2, wpos, bpos, w1, b1)]
+    out_u = P._CostVolumeWide.apply(ts[0], ts[1], idx, *ts[2:], lambda am: am_f)
+    out_u.backward(gout)
+    _scale_close(out_f, out_u, name="out")
+    o = d * d
+    got = [dx1, dx2, dp1, dp2, dpar[o + d:o + 4 * d].view(3, d).t(), dpar[o + 4 * d:],
+           dpar[:o].view(d, d), dpar[o:o + d]]
+    names = ["dx1", "dx2", "dp1", "dp2", "dWpos", "dbpos", "dW1", "db1"]
+    for n, a, t in zip(names, got, ts):
+        _scale_close(a.reshape(t.grad.shape), t.grad, rtol=2e-5, name=n)
