@@ -55,7 +55,9 @@ ROOFLINE = {
                            ["pc_fwd_kernel", "pc_slab_sum_kernel"]),
     "kdpc_group_rows": ("hbm", "GB/s", HBM_PEAK_GBS, ["group_rows_kernel"]),
     "kdpc_group_points": ("hbm", "GB/s", HBM_PEAK_GBS, ["group_points_lds_kernel",
-                                                         "group_points_kernel"]),
+                                                         "group_points_kernel",
+                                                         "transpose_cn_kernel",
+                                                         "group_points_pm_kernel"]),
     # kNN: plain scan (knn_kernel) or the culled scan (ref_sort / query_sort / chunk boxes /
     # knn_cull); work = brute-force-equivalent distance evaluations (8 flops each), bytes =
     # B*(12Nq + 12Nr + 4*Nq*K)

@@ -291,6 +291,22 @@ int kdpc_pointconv_bwd(int b, int n, int s, int k, int d, int o, const float *xy
                        float *dxyz, float *dfeats, float *dcenter, float *dwt, float *dwl,
                        void *workspace, size_t workspace_bytes, void *stream);
 
+/* The two halves of kdpc_pointconv_bwd (same kernels, same results bit for bit), so the weight
+ * gradient -- needed only by the optimizer -- can run on a second stream beside the rest of
+ * the backward: _bwd_data writes dxyz (NULL to skip), dfeats, dcenter, dwt (workspace:
+ * kdpc_pointconv_bwd_workspace_bytes); _bwd_weight writes dwl (workspace:
+ * kdpc_pointconv_bwd_weight_workspace_bytes) and reads only the inputs. */
+int kdpc_pointconv_bwd_data(int b, int n, int s, int k, int d, int o, const float *xyz,
+                            const float *center, const float *feats, const int *idx,
+                            const float *wt, const float *wl, const float *dy, const int *offsets,
+                            const int *rank, float *dxyz, float *dfeats, float *dcenter,
+                            float *dwt, void *workspace, size_t workspace_bytes, void *stream);
+size_t kdpc_pointconv_bwd_weight_workspace_bytes(int b, int s, int k, int d, int o);
+int kdpc_pointconv_bwd_weight(int b, int n, int s, int k, int d, int o, const float *xyz,
+                              const float *center, const float *feats, const int *idx,
+                              const float *wt, const float *dy, float *dwl, void *workspace,
+                              size_t workspace_bytes, void *stream);
+
 /* ---- fused WeightNet over grouped offsets (pointconv_util.py:184-215 as used by
  *      PointConv/PointConvD :217-258, :401-446: weightnet=16, hidden [8, 8], no BN) ------ */
 

@@ -1304,14 +1304,14 @@ inline bool bwd_pipe_enabled() {
   return force >= 0 ? force == 1 : KM <= 9;
 }
 
+// Data half of the backward: dxyz, dfeats, dcenter, dwt (workspace: dG rows | dwt slabs | -
+// | swizzled wl).
 template <int O, int KM>
-hipError_t bwd_launch(const Geo& g, const Plan& p, int b, const float* wt, const float* wl,
-                      const float* dy, const int* offsets, float* dxyz,
-                      float* dfeats, float* dcenter, float* dwt, float* dwl, char* ws,
-                      hipStream_t st) {
+hipError_t bwd_data_launch(const Geo& g, const Plan& p, int b, const float* wt, const float* wl,
+                           const float* dy, const int* offsets, float* dxyz, float* dfeats,
+                           float* dcenter, float* dwt, char* ws, hipStream_t st) {
   float* dgr = reinterpret_cast<float*>(ws);
   float* dwt_slab = reinterpret_cast<float*>(ws + p.dgr);
-  float* dwl_slab = reinterpret_cast<float*>(ws + p.dgr + p.dwt_slab);
   float4* wsw = reinterpret_cast<float4*>(ws + p.dgr + p.dwt_slab + p.dwl_slab);
   const long long rk = (long long)p.r * g.k;
   const int c16 = g.c * kW;
@@ -1338,7 +1338,15 @@ hipError_t bwd_launch(const Geo& g, const Plan& p, int b, const float* wt, const
   hipLaunchKernelGGL(pc_csr_sum_kernel,
                      dim3((unsigned)std::min<long long>(divupll(work, 256), 1 << 20)), dim3(256),
                      0, st, npts, rk, g.c, p.c8, g.d, dgr, offsets, dxyz, dfeats);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
+  return hipGetLastError();
+}
+
+// Weight half: dwl (workspace: its row-split slabs only, dwl_slab bytes).  Reads the same
+// G / wt / dy as the data half and nothing it writes, so it may run on another stream.
+template <int O, int KM>
+hipError_t bwd_weight_launch(const Geo& g, const Plan& p, const float* wt, const float* dy,
+                             float* dwl, char* ws, hipStream_t st) {
+  float* dwl_slab = reinterpret_cast<float*>(ws);
   float* wdst = p.rs > 1 ? dwl_slab : dwl;
   if (g.k == KM)
     hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM, true>), dim3(p.wgs), dim3(512), 0, st, g, wt,
@@ -1346,8 +1354,20 @@ hipError_t bwd_launch(const Geo& g, const Plan& p, int b, const float* wt, const
   else
     hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM, false>), dim3(p.wgs), dim3(512), 0, st, g, wt,
                        dy, wdst, p.rps, p.rs, p.xcd);
-  if ((e = hipGetLastError()) != hipSuccess || p.rs == 1) return e;
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || p.rs == 1) return e;
   return slab_sum(p.rs, (long long)O * g.c * kW, dwl_slab, nullptr, 1, dwl, st);
+}
+
+template <int O, int KM>
+hipError_t bwd_launch(const Geo& g, const Plan& p, int b, const float* wt, const float* wl,
+                      const float* dy, const int* offsets, float* dxyz,
+                      float* dfeats, float* dcenter, float* dwt, float* dwl, char* ws,
+                      hipStream_t st) {
+  hipError_t e = bwd_data_launch<O, KM>(g, p, b, wt, wl, dy, offsets, dxyz, dfeats, dcenter, dwt,
+                                        ws, st);
+  if (e != hipSuccess) return e;
+  return bwd_weight_launch<O, KM>(g, p, wt, dy, dwl, ws + p.dgr + p.dwt_slab, st);
 }
 
 Geo geo_of(int b, int n, int s, int k, int d, const Plan& p, const float* xyz, const float* center,
@@ -1435,4 +1455,49 @@ KDPC_API int kdpc_pointconv_bwd(int b, int n, int s, int k, int d, int o, const 
   char* ws = reinterpret_cast<char*>(workspace);
   return (int)KDPC_PC_DISPATCH(bwd_launch, g, p, b, wt, wl, dy, offsets, dxyz, dfeats,
                                dcenter, dwt, dwl, ws, st);
+}
+
+KDPC_API size_t kdpc_pointconv_bwd_weight_workspace_bytes(int b, int s, int k, int d, int o) {
+  Plan p;
+  return plan_of(b, s, k, d, o, &p) ? std::max<size_t>(p.dwl_slab, 256) : 0;
+}
+
+KDPC_API int kdpc_pointconv_bwd_data(int b, int n, int s, int k, int d, int o, const float* xyz,
+                                     const float* center, const float* feats, const int* idx,
+                                     const float* wt, const float* wl, const float* dy,
+                                     const int* offsets, const int* rank, float* dxyz,
+                                     float* dfeats, float* dcenter, float* dwt, void* workspace,
+                                     size_t workspace_bytes, void* stream) {
+  Plan p;
+  KDPC_CHECK_ARG(n > 0 && b <= 65535 && plan_of(b, s, k, d, o, &p) && fits_buffers(b, n, s, d));
+  hipStream_t st = (hipStream_t)stream;
+  if (p.r == 0) {
+    hipError_t e = hipSuccess;
+    if (dxyz) e = hipMemsetAsync(dxyz, 0, sizeof(float) * b * n * 3, st);
+    if (e == hipSuccess && d > 0) e = hipMemsetAsync(dfeats, 0, sizeof(float) * b * n * d, st);
+    return (int)e;
+  }
+  KDPC_CHECK_ARG(xyz && center && idx && wt && wl && dy && offsets && rank && dcenter && dwt &&
+                 (d == 0 || (feats && dfeats)));
+  KDPC_CHECK_ARG(workspace && workspace_bytes >= p.dgr + p.dwt_slab + p.dwl_slab + p.wlt);
+  Geo g = geo_of(b, n, s, k, d, p, xyz, center, feats, idx);
+  g.rank = rank;
+  char* ws = reinterpret_cast<char*>(workspace);
+  return (int)KDPC_PC_DISPATCH(bwd_data_launch, g, p, b, wt, wl, dy, offsets, dxyz, dfeats,
+                               dcenter, dwt, ws, st);
+}
+
+KDPC_API int kdpc_pointconv_bwd_weight(int b, int n, int s, int k, int d, int o, const float* xyz,
+                                       const float* center, const float* feats, const int* idx,
+                                       const float* wt, const float* dy, float* dwl,
+                                       void* workspace, size_t workspace_bytes, void* stream) {
+  Plan p;
+  KDPC_CHECK_ARG(n > 0 && b <= 65535 && plan_of(b, s, k, d, o, &p) && fits_buffers(b, n, s, d));
+  hipStream_t st = (hipStream_t)stream;
+  if (p.r == 0) return (int)hipMemsetAsync(dwl, 0, sizeof(float) * o * p.c * kW, st);
+  KDPC_CHECK_ARG(xyz && center && idx && wt && dy && dwl && (d == 0 || feats));
+  KDPC_CHECK_ARG(workspace && workspace_bytes >= kdpc_pointconv_bwd_weight_workspace_bytes(b, s, k, d, o));
+  const Geo g = geo_of(b, n, s, k, d, p, xyz, center, feats, idx);
+  char* ws = reinterpret_cast<char*>(workspace);
+  return (int)KDPC_PC_DISPATCH(bwd_weight_launch, g, p, wt, dy, dwl, ws, st);
 }

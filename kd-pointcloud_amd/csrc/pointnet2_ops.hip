@@ -261,6 +261,79 @@ __global__ __launch_bounds__(256) void three_interpolate_kernel(int b, int c, in
   }
 }
 
+// Point-major path for clouds whose channel rows do not fit in LDS (N > 20480 at CG = 1,
+// e.g. BASELINE configs[4]: N = 65536): the (B,C,N) table is first transposed to (B,N,C) in
+// a stream-ordered scratch, then a thread gathers its 4 positions' whole rows (C floats, one
+// or two cache lines each, every byte used) and writes each channel's 4 values as one float4
+// -- a wave's stores to a channel row are 1 KiB contiguous.  The direct kernel above reads
+// one 4-byte value per cache line it brings in.
+template <int C4>
+__global__ __launch_bounds__(256) void transpose_cn_kernel(int n, const float* __restrict__ src,
+                                                           float* __restrict__ dst) {
+  constexpr int C = 4 * C4;
+  __shared__ float tile[C][65];
+  const int bi = blockIdx.y;
+  const int n0 = blockIdx.x * 64;
+  const float* sb = src + (long long)bi * C * n;
+  for (int e = threadIdx.x; e < C * 64; e += 256) {
+    const int c = e / 64, j = e % 64;
+    tile[c][j] = n0 + j < n ? sb[(long long)c * n + n0 + j] : 0.f;
+  }
+  __syncthreads();
+  float* db = dst + ((long long)bi * n + n0) * C;
+  for (int e = threadIdx.x; e < C * 64; e += 256) {
+    const int j = e / C, c = e % C;
+    if (n0 + j < n) db[(long long)j * C + c] = tile[c][j];
+  }
+}
+
+template <int C4>
+__global__ __launch_bounds__(256) void group_points_pm_kernel(int n, int p_total,
+                                                              const float* __restrict__ pt,
+                                                              const int* __restrict__ idx,
+                                                              float* __restrict__ out) {
+  constexpr int C = 4 * C4;
+  const int bi = blockIdx.y;
+  const int p4 = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (p4 >= p_total) return;  // p_total % 4 == 0 (checked by the caller)
+  const int4 q = *reinterpret_cast<const int4*>(idx + (long long)bi * p_total + p4);
+  const float4* rb = reinterpret_cast<const float4*>(pt + (long long)bi * n * C);
+  float* ob = out + (long long)bi * C * p_total + p4;
+#pragma unroll 2
+  for (int c4 = 0; c4 < C4; ++c4) {
+    const float4 a = rb[(long long)q.x * C4 + c4];
+    const float4 b = rb[(long long)q.y * C4 + c4];
+    const float4 c = rb[(long long)q.z * C4 + c4];
+    const float4 d = rb[(long long)q.w * C4 + c4];
+    const f32x4 o0 = {a.x, b.x, c.x, d.x}, o1 = {a.y, b.y, c.y, d.y};
+    const f32x4 o2 = {a.z, b.z, c.z, d.z}, o3 = {a.w, b.w, c.w, d.w};
+    float* o = ob + (long long)(4 * c4) * p_total;
+    __builtin_nontemporal_store(o0, reinterpret_cast<f32x4*>(o));
+    __builtin_nontemporal_store(o1, reinterpret_cast<f32x4*>(o + p_total));
+    __builtin_nontemporal_store(o2, reinterpret_cast<f32x4*>(o + 2ll * p_total));
+    __builtin_nontemporal_store(o3, reinterpret_cast<f32x4*>(o + 3ll * p_total));
+  }
+}
+
+template <int C4>
+hipError_t group_pm_launch(int b, int n, int p_total, const float* points, const int* idx,
+                           float* out, hipStream_t st) {
+  void* pt = nullptr;
+  const size_t bytes = (size_t)b * n * 4 * C4 * sizeof(float);
+  hipError_t e = hipMallocAsync(&pt, bytes, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(transpose_cn_kernel<C4>, dim3(divup(n, 64), b), dim3(256), 0, st, n, points,
+                     (float*)pt);
+  e = hipGetLastError();
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(group_points_pm_kernel<C4>, dim3(divup(p_total / 4, 256), b), dim3(256), 0,
+                       st, n, p_total, (const float*)pt, idx, out);
+    e = hipGetLastError();
+  }
+  const hipError_t f = hipFreeAsync(pt, st);
+  return e != hipSuccess ? e : f;
+}
+
 template <int CG>
 hipError_t launch_group_lds(dim3 grid, size_t lds, hipStream_t st, int c, int n, int p_total,
                             int p_slice, int nslice, int groups, int xcd_units,
@@ -331,6 +404,14 @@ KDPC_API int kdpc_group_points(int b, int c, int n, int npoints, int nsample, co
       default: e = launch_group_lds<1>(grid, lds, st, c, n, pt, p_slice, nslice, groups, xcd_units, points, idx, out);
     }
     return (int)e;
+  }
+  if ((p_total % 4) == 0 && (c == 16 || c == 32 || c == 64)) {
+    const int pt = (int)p_total;
+    switch (c) {
+      case 16: return (int)group_pm_launch<4>(b, n, pt, points, idx, out, st);
+      case 32: return (int)group_pm_launch<8>(b, n, pt, points, idx, out, st);
+      default: return (int)group_pm_launch<16>(b, n, pt, points, idx, out, st);
+    }
   }
   dim3 grid(divup((int)divupll(p_total, 4), 256), divup(c, kGroupCG), b);
   KDPC_CHECK_ARG(grid.y <= 65535);

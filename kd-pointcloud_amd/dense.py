@@ -11,6 +11,8 @@ input-gradient GEMMs are unchanged (they are well shaped).  fp32 throughout.
 import torch
 from torch.autograd import Function
 
+import wgrad
+
 _MIN_ROWS_PER_CHUNK = 2048
 
 
@@ -131,10 +133,14 @@ class _Linear(Function):
                 gx = kdpc_native.dense_small(g2.contiguous(), weight).view(ctx.xshape)
             else:
                 gx = g2.mm(weight).view(ctx.xshape)
-        if ctx.needs_input_grad[1]:
-            gw = splitk_tn(g2.contiguous(), x2)
-        if ctx.has_bias and ctx.needs_input_grad[2]:
-            gb = _colsum(g2)
+        need_w = ctx.needs_input_grad[1]
+        need_b = ctx.has_bias and ctx.needs_input_grad[2]
+        if need_w or need_b:
+            # parameter gradients on the parameter-gradient stream (wgrad.py), beside the
+            # rest of the backward
+            g2c = g2.contiguous()
+            gw, gb = wgrad.run(lambda: (splitk_tn(g2c, x2) if need_w else None,
+                                        _colsum(g2c) if need_b else None), [g2c, x2])
         return gx, gw, gb
 
 

@@ -20,6 +20,7 @@ import torch
 import torch.distributed as dist
 
 import loss_functions
+import wgrad
 
 
 def is_dist():
@@ -30,6 +31,9 @@ def wrap_ddp(model, device=None):
     """Wrap the trained model for DDP when a process group is up (no-op otherwise)."""
     if not is_dist() or dist.get_world_size() == 1:
         return model
+    # DDP's reducer reads each gradient from its own hook during the backward: issue the
+    # parameter gradients in line (wgrad.py)
+    wgrad.enabled = False
     kw = dict(broadcast_buffers=True, static_graph=True, gradient_as_bucket_view=True)
     if device is not None and device.type == "cuda":
         kw["device_ids"] = [device.index]
@@ -429,6 +433,7 @@ class GraphedStep:
             b["left"] -= 1
             if b["left"] == 0:
                 idx = b["idx"]
+                wgrad.join()  # parameter gradients still in flight on their own stream
                 torch._foreach_copy_([self._gviews[i] for i in idx],
                                      [self._used[i].grad for i in idx])
                 self.comm.wait_stream(torch.cuda.current_stream())

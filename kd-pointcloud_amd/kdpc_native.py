@@ -67,6 +67,9 @@ _SIGNATURES = {
     "kdpc_pointconv_fwd": [_c_int] * 6 + [_vp] * 9 + [_c_size, _vp],
     "kdpc_pointconv_bwd_workspace_bytes": [_c_int] * 5,
     "kdpc_pointconv_bwd": [_c_int] * 6 + [_vp] * 15 + [_c_size, _vp],
+    "kdpc_pointconv_bwd_data": [_c_int] * 6 + [_vp] * 14 + [_c_size, _vp],
+    "kdpc_pointconv_bwd_weight_workspace_bytes": [_c_int] * 5,
+    "kdpc_pointconv_bwd_weight": [_c_int] * 6 + [_vp] * 8 + [_c_size, _vp],
     "kdpc_batchnorm_workspace_bytes": [_c_int, _c_int],
     "kdpc_batchnorm_lrelu_fwd": [_c_int, _c_int] + [_vp] * 3 + [_c_float] * 3 + [_vp] * 6
                                 + [_c_size, _vp],
@@ -97,6 +100,7 @@ _RESTYPES = {"kdpc_build_id": ctypes.c_char_p, "kdpc_grad_workspace_bytes": _c_s
              "kdpc_cost_volume_bwd_csr_workspace_bytes": _c_size,
              "kdpc_pointconv_fwd_workspace_bytes": _c_size,
              "kdpc_pointconv_bwd_workspace_bytes": _c_size,
+             "kdpc_pointconv_bwd_weight_workspace_bytes": _c_size,
              "kdpc_weightnet_bwd_workspace_bytes": _c_size,
              "kdpc_wn_wsum_bwd_workspace_bytes": _c_size,
              "kdpc_knn_feature_workspace_bytes": _c_size,
@@ -579,6 +583,38 @@ def pointconv_bwd(xyz, center, feats, idx, wt, wl, dy, csr, need_xyz=True):
                csr.offsets, csr.rank, bool(need_xyz),
                work=(4 * R * (2 * K * C + 32 * K + 2 * O) + 8 * O * 16 * C,
                      4.0 * R * K * C * 16 + 4.0 * R * 16 * C * O))
+
+
+def pointconv_bwd_data(xyz, center, feats, idx, wt, wl, dy, csr, need_xyz=True):
+    """Data half of pointconv_bwd -> (dxyz|None, dfeats, dcenter, dwt)."""
+    if csr.rank is None:
+        csr = csr_rank_of(idx, xyz.shape[1])
+    B, N, _ = _gpu(xyz, "xyz").shape
+    S, K = idx.shape[1], idx.shape[2]
+    O, C = wl.shape[0], 3 + feats.shape[2]
+    R = B * S
+    return _op("kdpc_pointconv_bwd_data", "pointconv_bwd_data", xyz, center, feats, idx, wt, wl,
+               dy, csr.offsets, csr.rank, bool(need_xyz),
+               work=(4 * R * (2 * K * C + 32 * K + O) + 4 * O * 16 * C,
+                     2.0 * R * K * C * 16 + 2.0 * R * 16 * C * O))
+
+
+def pointconv_bwd_weight(xyz, center, feats, idx, wt, dy, o):
+    """Weight half of pointconv_bwd -> dwl (O, 16C); reads only its inputs (may run on a
+    second stream beside the data half)."""
+    B, N, _ = _gpu(xyz, "xyz").shape
+    S, K = idx.shape[1], idx.shape[2]
+    C = 3 + feats.shape[2]
+    R = B * S
+    return _op("kdpc_pointconv_bwd_weight", "pointconv_bwd_weight", xyz, center, feats, idx, wt,
+               dy, int(o),
+               work=(4 * R * (K * C + 16 * K + o) + 4 * o * 16 * C,
+                     2.0 * R * K * C * 16 + 2.0 * R * 16 * C * o))
+
+
+def timing(entry):
+    """True when a LaunchTimer brackets `entry` (bench.py's live roofline)."""
+    return _timer is not None and entry in _timer.names
 
 
 # ------------------------------------------------ 3-NN inverse-distance blend

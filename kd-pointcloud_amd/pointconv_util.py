@@ -21,6 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 import kdpc_native as _nat
+import wgrad
 from dense import conv1x1, linear, linear_1x1, splitk_tn
 from pointnet2 import pointnet2_utils
 
@@ -370,12 +371,21 @@ class _PointConvLayer(torch.autograd.Function):
     def backward(ctx, gy):
         xyz, center, feats, idx, wt, wl = ctx.saved_tensors
         gy = gy.contiguous()
-        dxyz, dfeats, dcenter, dwt, dwl = _nat.pointconv_bwd(
-            xyz, center, feats, idx, wt, wl, gy, _nat.csr_rank_of(idx, xyz.shape[1]),
-            need_xyz=ctx.needs_input_grad[0])
-        # fixed-order HIP column sum (torch's tall dim-0 reduction gave wrong sums when
-        # replayed from a captured graph, tools/graph_diag.py)
-        dbias = _nat.colsum(gy.view(-1, gy.shape[-1])) if ctx.needs_input_grad[6] else None
+        csr = _nat.csr_rank_of(idx, xyz.shape[1])
+        need_b = ctx.needs_input_grad[6]
+        if _nat.timing("kdpc_pointconv_bwd"):  # bench's live roofline brackets the whole entry
+            dxyz, dfeats, dcenter, dwt, dwl = _nat.pointconv_bwd(
+                xyz, center, feats, idx, wt, wl, gy, csr, need_xyz=ctx.needs_input_grad[0])
+            dbias = _nat.colsum(gy.view(-1, gy.shape[-1])) if need_b else None
+        else:
+            dxyz, dfeats, dcenter, dwt = _nat.pointconv_bwd_data(
+                xyz, center, feats, idx, wt, wl, gy, csr, need_xyz=ctx.needs_input_grad[0])
+            # the parameter gradients (weight kernel + fixed-order bias column sum) beside the
+            # rest of the backward, on the parameter-gradient stream (wgrad.py)
+            dwl, dbias = wgrad.run(lambda: (
+                _nat.pointconv_bwd_weight(xyz, center, feats, idx, wt, gy, wl.shape[0]),
+                _nat.colsum(gy.view(-1, gy.shape[-1])) if need_b else None),
+                [xyz, center, feats, idx, wt, gy])
         return (dxyz, dcenter if ctx.needs_input_grad[1] else None, dfeats, None, dwt, dwl, dbias)
 
 

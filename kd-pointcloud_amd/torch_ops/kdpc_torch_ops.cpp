@@ -523,6 +523,48 @@ std::tuple<c10::optional<Tensor>, Tensor, Tensor, Tensor, Tensor> pointconv_bwd(
   return {need_xyz ? c10::optional<Tensor>(dxyz) : c10::nullopt, dfeats, dcenter, dwt, dwl};
 }
 
+std::tuple<c10::optional<Tensor>, Tensor, Tensor, Tensor> pointconv_bwd_data(
+    Tensor xyz, Tensor center, Tensor feats, Tensor idx, Tensor wt, Tensor wl, Tensor dy,
+    Tensor offsets, Tensor rank, bool need_xyz) {
+  for (auto* t : {&xyz, &center, &feats, &wt, &wl, &dy}) dev(*t, kF, "pointconv input");
+  dev(idx, kI, "idx"), dev(offsets, kI, "offsets"), dev(rank, kI, "rank");
+  GUARD(xyz);
+  const int64_t b = xyz.size(0), n = xyz.size(1), s = idx.size(1), k = idx.size(2);
+  const int64_t d = feats.size(2), o = wl.size(0);
+  TORCH_CHECK(offsets.numel() >= b * n + 1 && rank.numel() >= b * s * k,
+              "kdpc: pointconv_bwd_data: offsets / rank do not match idx");
+  const size_t nb = kdpc_pointconv_bwd_workspace_bytes(b, s, k, d, o);
+  TORCH_CHECK(nb > 0, "kdpc: pointconv_bwd_data: invalid sizes");
+  Tensor ws = workspace(nb, xyz);
+  Tensor dxyz = need_xyz ? empty_f({b, n, 3}, xyz) : Tensor();
+  Tensor dfeats = empty_f({b, n, d}, xyz);
+  Tensor dcenter = empty_f({b, s, 3}, xyz);
+  Tensor dwt = empty_f({b, s, k, 16}, xyz);
+  check(kdpc_pointconv_bwd_data(b, n, s, k, d, o, F(xyz), F(center), F(feats), I(idx), F(wt),
+                                F(wl), F(dy), I(offsets), I(rank), need_xyz ? F(dxyz) : nullptr,
+                                F(dfeats), F(dcenter), F(dwt), ws.data_ptr(), nb, stream_of(xyz)),
+        "pointconv_bwd_data");
+  return {need_xyz ? c10::optional<Tensor>(dxyz) : c10::nullopt, dfeats, dcenter, dwt};
+}
+
+Tensor pointconv_bwd_weight(Tensor xyz, Tensor center, Tensor feats, Tensor idx, Tensor wt,
+                            Tensor dy, int64_t o) {
+  for (auto* t : {&xyz, &center, &feats, &wt, &dy}) dev(*t, kF, "pointconv input");
+  dev(idx, kI, "idx");
+  GUARD(xyz);
+  const int64_t b = xyz.size(0), n = xyz.size(1), s = idx.size(1), k = idx.size(2);
+  const int64_t d = feats.size(2), c = 3 + d;
+  TORCH_CHECK(dy.numel() == b * s * o, "kdpc: pointconv_bwd_weight: dy does not match O");
+  const size_t nb = kdpc_pointconv_bwd_weight_workspace_bytes(b, s, k, d, o);
+  TORCH_CHECK(nb > 0, "kdpc: pointconv_bwd_weight: invalid sizes");
+  Tensor ws = workspace(nb, xyz);
+  Tensor dwl = empty_f({o, 16 * c}, xyz);
+  check(kdpc_pointconv_bwd_weight(b, n, s, k, d, o, F(xyz), F(center), F(feats), I(idx), F(wt),
+                                  F(dy), F(dwl), ws.data_ptr(), nb, stream_of(xyz)),
+        "pointconv_bwd_weight");
+  return dwl;
+}
+
 Tensor pointconv_contract_fwd(Tensor xyz, Tensor center, Tensor feats, Tensor idx, Tensor wt) {
   for (auto* t : {&xyz, &center, &feats, &wt}) dev(*t, kF, "pointconv input");
   dev(idx, kI, "idx");
@@ -853,6 +895,11 @@ TORCH_LIBRARY(kdpc, m) {
   m.def("pointconv_bwd(Tensor xyz, Tensor center, Tensor feats, Tensor idx, Tensor wt, "
         "Tensor wl, Tensor dy, Tensor offsets, Tensor rank, bool need_xyz) "
         "-> (Tensor?, Tensor, Tensor, Tensor, Tensor)");
+  m.def("pointconv_bwd_data(Tensor xyz, Tensor center, Tensor feats, Tensor idx, Tensor wt, "
+        "Tensor wl, Tensor dy, Tensor offsets, Tensor rank, bool need_xyz) "
+        "-> (Tensor?, Tensor, Tensor, Tensor)");
+  m.def("pointconv_bwd_weight(Tensor xyz, Tensor center, Tensor feats, Tensor idx, Tensor wt, "
+        "Tensor dy, int o) -> Tensor");
   m.def("pointconv_contract_fwd(Tensor xyz, Tensor center, Tensor feats, Tensor idx, "
         "Tensor wt) -> Tensor");
   m.def("pointconv_contract_bwd(Tensor xyz, Tensor center, Tensor feats, Tensor idx, "
@@ -916,6 +963,8 @@ TORCH_LIBRARY_IMPL(kdpc, CUDA, m) {
   m.impl("cost_volume_wide_h0_bwd", cost_volume_wide_h0_bwd);
   m.impl("pointconv_fwd", pointconv_fwd);
   m.impl("pointconv_bwd", pointconv_bwd);
+  m.impl("pointconv_bwd_data", pointconv_bwd_data);
+  m.impl("pointconv_bwd_weight", pointconv_bwd_weight);
   m.impl("pointconv_contract_fwd", pointconv_contract_fwd);
   m.impl("pointconv_contract_bwd", pointconv_contract_bwd);
   m.impl("weightnet_fwd", weightnet_fwd);

@@ -380,3 +380,32 @@ def test_one_kernel_wide_cost_volume_equals_blas_path(d, n1, n2, bsz, k):
     names = ["dx1", "dx2", "dp1", "dp2", "dWpos", "dbpos", "dW1", "db1"]
     for n, a, t in zip(names, got, ts):
         _scale_close(a.reshape(t.grad.shape), t.grad, rtol=2e-5, name=n)
+
+
+@pytest.mark.parametrize("b,n,s,k,d,o", [(2, 1024, 1024, 9, 125, 128), (2, 2048, 512, 16, 67, 64),
+                                         (1, 300, 77, 16, 131, 256)])
+def test_pointconv_bwd_halves_equal_whole(b, n, s, k, d, o):
+    """kdpc_pointconv_bwd_data + kdpc_pointconv_bwd_weight (the weight half runs on the
+    parameter-gradient stream, wgrad.py) give the outputs of kdpc_pointconv_bwd bit for bit,
+    and the weight half issued on a second stream equals it too."""
+    import kdpc_native as K
+    import pointconv_util as P
+    torch.manual_seed(n + k)
+    xyz = torch.rand(b, n, 3, device=DEV)
+    center = xyz[:, :s].contiguous()
+    feats = torch.randn(b, n, d, device=DEV)
+    idx = P._as_idx32(P.knn_point(k, xyz, center)).contiguous()
+    wt = torch.randn(b, s, k, 16, device=DEV)
+    wl = torch.randn(o, 16 * (3 + d), device=DEV) * 0.05
+    dy = torch.randn(b, s, o, device=DEV)
+    csr = K.csr_rank_of(idx, n)
+    whole = K.pointconv_bwd(xyz, center, feats, idx, wt, wl, dy, csr)
+    data = K.pointconv_bwd_data(xyz, center, feats, idx, wt, wl, dy, csr)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        dwl = K.pointconv_bwd_weight(xyz, center, feats, idx, wt, dy, o)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    for name, a, c in zip(["dxyz", "dfeats", "dcenter", "dwt", "dwl"], whole, list(data) + [dwl]):
+        assert torch.equal(a, c), name

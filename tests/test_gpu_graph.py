@@ -95,3 +95,40 @@ def test_eager_step_after_capture_has_no_stream_mismatch():
         torch.cuda.synchronize()
     bad = [str(w.message) for w in caught if "AccumulateGrad" in str(w.message)]
     assert not bad, bad
+
+
+def test_parameter_gradient_stream_is_bit_identical():
+    """wgrad.py: the parameter gradients issued on their own stream (PointConv weight kernel,
+    dense split-K weight GEMMs, bias column sums) give the same parameters after two eager
+    training steps, bit for bit, as issuing them in line; `.grad` is complete when
+    backward() returns (read straight after it, no synchronisation)."""
+    import wgrad
+    from distill import FlowTrainStep, make_optimizer
+    from models_bid_pointconv import PointConvBidirection
+    import loss_functions as L
+    torch.manual_seed(0)
+    base = PointConvBidirection().to(DEV)
+    batches = [_batch(2, 4096, s) for s in (11, 12)]
+    runs = []
+    prev = wgrad.enabled
+    try:
+        for on in (False, True):
+            wgrad.enabled = on
+            m = copy.deepcopy(base)
+            opt = make_optimizer(m)
+            step = FlowTrainStep(m, opt)
+            for b in batches:
+                step(*b)
+            out = m(*batches[0][:2], *batches[0][:2])
+            loss = L.multiScaleLoss(out[0], batches[0][2], out[1])
+            loss.backward()
+            grads = {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+            runs.append(({n: p.detach().clone() for n, p in m.named_parameters()}, grads))
+    finally:
+        wgrad.enabled = prev
+    (p0, g0), (p1, g1) = runs
+    for n in p0:
+        assert torch.equal(p0[n], p1[n]), n
+    assert g0.keys() == g1.keys()
+    for n in g0:
+        assert torch.equal(g0[n], g1[n]), n

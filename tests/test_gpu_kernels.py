@@ -67,7 +67,9 @@ def test_gather_points(nat):
     np.testing.assert_array_equal(grad, O.gather_points_grad(g, idx, 1000))
 
 
-@pytest.mark.parametrize("c,n,s,k", [(64, 8192, 2048, 16), (7, 513, 37, 9), (3, 100, 5, 3)])
+@pytest.mark.parametrize("c,n,s,k", [(64, 8192, 2048, 16), (7, 513, 37, 9), (3, 100, 5, 3),
+                                     (32, 65536, 2048, 32), (16, 30000, 999, 4),
+                                     (64, 24000, 100, 8)])
 def test_group_points(nat, c, n, s, k):
     rng = np.random.default_rng(c + n)
     pts = rng.normal(size=(2, c, n)).astype(np.float32)

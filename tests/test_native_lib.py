@@ -128,6 +128,8 @@ TORCH_OPS = {
     "cost_volume_wide_max_bwd": "kdpc_cost_volume_wide_max_bwd",
     "cost_volume_wide_h0_bwd": "kdpc_cost_volume_wide_h0_bwd",
     "pointconv_fwd": "kdpc_pointconv_fwd", "pointconv_bwd": "kdpc_pointconv_bwd",
+    "pointconv_bwd_data": "kdpc_pointconv_bwd_data",
+    "pointconv_bwd_weight": "kdpc_pointconv_bwd_weight",
     "pointconv_contract_fwd": "kdpc_pointconv_contract_fwd",
     "pointconv_contract_bwd": "kdpc_pointconv_contract_bwd",
     "weightnet_fwd": "kdpc_weightnet_fwd", "weightnet_bwd": "kdpc_weightnet_bwd",
