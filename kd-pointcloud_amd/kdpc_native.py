@@ -596,7 +596,7 @@ def pointconv_bwd_data(xyz, center, feats, idx, wt, wl, dy, csr, need_xyz=True):
     return _op("kdpc_pointconv_bwd_data", "pointconv_bwd_data", xyz, center, feats, idx, wt, wl,
                dy, csr.offsets, csr.rank, bool(need_xyz),
                work=(4 * R * (2 * K * C + 32 * K + O) + 4 * O * 16 * C,
-                     2.0 * R * K * C * 16 + 2.0 * R * 16 * C * O))
+                     4.0 * R * K * C * 16 + 2.0 * R * 16 * C * O))
 
 
 def pointconv_bwd_weight(xyz, center, feats, idx, wt, dy, o):
@@ -608,8 +608,7 @@ def pointconv_bwd_weight(xyz, center, feats, idx, wt, dy, o):
     R = B * S
     return _op("kdpc_pointconv_bwd_weight", "pointconv_bwd_weight", xyz, center, feats, idx, wt,
                dy, int(o),
-               work=(4 * R * (K * C + 16 * K + o) + 4 * o * 16 * C,
-                     2.0 * R * K * C * 16 + 2.0 * R * 16 * C * o))
+               work=(4 * R * (K * C + 16 * K + o) + 4 * o * 16 * C, 2.0 * R * 16 * C * o))
 
 
 def timing(entry):
