@@ -472,7 +472,35 @@ void cost_volume_bwd_kernel(
 constexpr int kFwdQPW = 8;
 // backward queries per wave: enough waves for ~8 per SIMD over the launch (the workgroups'
 // partial slabs grow with the wave count; the pipeline amortises its prologue over the rest)
-inline int bwd_qpw(int b, int n1) { return std::max(2, (int)divupll((long long)b * n1, 8192)); }
+// backward queries per wave: as many waves as the chip holds at the kernel's occupancy, in
+// ONE round (16 per wave at 8192 waves left the D=32 kernel -- 5 waves per SIMD by its
+// registers -- a 60 %-full second round); at least 2 queries per wave for the pipeline
+template <int DI, int DO>
+int bwd_waves_resident() {
+  static const int w = [] {
+    int blocks = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, cost_volume_bwd_kernel<DI, DO>, 256,
+                                                     0) != hipSuccess || blocks < 1)
+      blocks = 1;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus < 1)
+      cus = 256;
+    return blocks * cus * kWaves;
+  }();
+  return w;
+}
+
+inline int bwd_waves_resident_of(int din, int dout) {
+  if (din == 32 && dout == 32) return bwd_waves_resident<32, 32>();
+  if (din == 32 && dout == 64) return bwd_waves_resident<32, 64>();
+  if (din == 64 && dout == 32) return bwd_waves_resident<64, 32>();
+  return bwd_waves_resident<64, 64>();
+}
+
+inline int bwd_qpw(int b, int n1, int din, int dout) {
+  return std::max(2, (int)divupll((long long)b * n1, bwd_waves_resident_of(din, dout)));
+}
 
 inline int slab_len(int din, int dout) { return dout * din + dout + 4 * din; }
 
@@ -494,7 +522,7 @@ hipError_t bwd_launch(int b, int n1, int n2, int k, const float* x1, const float
                       const unsigned char* amax, const float* dout, float* dp1, float* dp2_rows,
                       float* dx1, float* ddir_rows, const int* rank, float* rows, float* slab,
                       float* dparams, hipStream_t st) {
-  const int qpw = bwd_qpw(b, n1);
+  const int qpw = bwd_qpw(b, n1, DI, DO);
   dim3 grid(divup(n1, kWaves * qpw), b);
   hipLaunchKernelGGL((cost_volume_bwd_kernel<DI, DO>), grid, dim3(256), 0, st, n1, n2, k,
                      qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, dout, dp1,
@@ -636,7 +664,7 @@ KDPC_API size_t kdpc_cost_volume_bwd_workspace_bytes(int b, int n1, int din, int
   if (b <= 0 || n1 <= 0 || !supported(din, dout, 1)) return 0;
   if (!narrow(din, dout, 1))
     return cost_volume_wide_fused_bwd_workspace_floats(b, n1, din) * sizeof(float);
-  const long long nslabs = (long long)divup(n1, kWaves * bwd_qpw(b, n1)) * b;
+  const long long nslabs = (long long)divup(n1, kWaves * bwd_qpw(b, n1, din, dout)) * b;
   const int len = slab_len(din, dout);
   return (size_t)(nslabs * len + colsum_scratch_floats((int)nslabs, len)) * sizeof(float);
 }

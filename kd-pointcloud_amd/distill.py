@@ -16,6 +16,8 @@ train_bid_pointconv.py) MI355X-first:
 The step is model-agnostic (any module returning the reference's 8-tuple), which lets the
 multi-process path be tested on CPU with gloo.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -57,6 +59,38 @@ def make_optimizer(model, lr=1e-3, weight_decay=1e-4, capturable=False):
 
 def _core(model):
     return model.module if isinstance(model, torch.nn.parallel.DistributedDataParallel) else model
+
+
+# KDPC_KD_TEACHER_STREAM=0 runs the frozen teacher's forward in line (A/B runs)
+TEACHER_STREAM = os.environ.get("KDPC_KD_TEACHER_STREAM", "1") != "0"
+_teacher_streams = {}
+
+
+class _TeacherFork:
+    """The frozen teacher's forward (no_grad) on its own stream, beside the student's forward:
+    the two share only their inputs, and at B=4 per GPU neither fills the chip.  join()
+    makes the current stream wait before the teacher's outputs are read (the KD loss).  Same
+    kernels on the same inputs: bit-identical to running the teacher in line."""
+
+    def __init__(self, teacher, args, kw):
+        dev = args[0].device
+        self.cur = self.side = None
+        if TEACHER_STREAM and dev.type == "cuda":
+            self.cur = torch.cuda.current_stream(dev)
+            self.side = _teacher_streams.get(dev.index)
+            if self.side is None:
+                self.side = _teacher_streams[dev.index] = torch.cuda.Stream(device=dev)
+            self.side.wait_stream(self.cur)
+            with torch.cuda.stream(self.side), torch.no_grad():
+                self.out = teacher(*args, **kw)
+        else:
+            with torch.no_grad():
+                self.out = teacher(*args, **kw)
+
+    def join(self):
+        if self.side is not None:
+            self.cur.wait_stream(self.side)
+        return self.out
 
 
 def _plan_fn(model):
@@ -169,12 +203,11 @@ class KDTrainStep:
             self.prefetch.launch(self.student, next_batch[0], next_batch[1])
         kw = {} if fps is None else {"fps_idx": fps}
         self.teacher.eval()
-        with torch.no_grad():
-            t_flows, t_fps1, t_fps2, _, _, t_feat1s, t_feat2s, _ = self.teacher(
-                pos1, pos2, color1, color2, **kw)
+        t_fork = _TeacherFork(self.teacher, (pos1, pos2, color1, color2), kw)
         self.student.train()
         flows, fps1, fps2, _, _, feat1s, feat2s, _ = self.student(pos1, pos2, color1, color2,
                                                                   **kw)
+        t_flows, t_fps1, t_fps2, _, _, t_feat1s, t_feat2s, _ = t_fork.join()
         loss = self.loss_fn(
             flows, feat1s, feat2s, fps1, fps2, flow, t_flows, t_feat1s, t_feat2s, t_fps1, t_fps2,
             self.gamma, self.beta, layer=self.layer)
@@ -541,10 +574,9 @@ def graphed_kd_step(teacher, student, optimizer, example_inputs, gamma=0.3, beta
 
     def run(pos1, pos2, flow, fps=None):
         kw = {} if fps is None else {"fps_idx": fps}
-        with torch.no_grad():
-            t_flows, t_fps1, t_fps2, _, _, t_feat1s, t_feat2s, _ = teacher(pos1, pos2, pos1, pos2,
-                                                                           **kw)
+        t_fork = _TeacherFork(teacher, (pos1, pos2, pos1, pos2), kw)
         flows, fps1, fps2, _, _, feat1s, feat2s, _ = student(pos1, pos2, pos1, pos2, **kw)
+        t_flows, t_fps1, t_fps2, _, _, t_feat1s, t_feat2s, _ = t_fork.join()
         return loss_functions.biDirection_loss_ht(
             flows, feat1s, feat2s, fps1, fps2, flow, t_flows, t_feat1s, t_feat2s, t_fps1, t_fps2,
             gamma, beta, layer=layer)

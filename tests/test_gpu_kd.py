@@ -164,3 +164,36 @@ def test_coordinate_plan_equals_inline_searches():
         for n, g in grads.items():
             assert (g is None) == (ref[2][n] is None), n
             assert g is None or torch.equal(g, ref[2][n]), n
+
+
+def test_teacher_stream_is_bit_identical():
+    """The KD step's frozen-teacher forward on its own stream (distill._TeacherFork, beside the
+    student's forward) gives the same loss and parameters, bit for bit, as running it in
+    line, eagerly and from the captured graph."""
+    import distill
+    from distill import KDTrainStep, graphed_kd_step, make_optimizer
+    from models_bid_pointconv import PointConvBidirection as Net
+    torch.manual_seed(1)
+    teacher = Net().to(DEV)
+    torch.manual_seed(2)
+    base = Net().to(DEV)
+    batches = [_batch(2, 4096, s) for s in (61, 62)]
+    runs = []
+    prev = distill.TEACHER_STREAM
+    try:
+        for on in (False, True):
+            distill.TEACHER_STREAM = on
+            m_e, m_g = copy.deepcopy(base), copy.deepcopy(base)
+            eager = KDTrainStep(teacher, m_e, make_optimizer(m_e, capturable=True))
+            graphed = graphed_kd_step(teacher, m_g, make_optimizer(m_g, capturable=True),
+                                      batches[0], warmup=1)
+            losses = [float(eager(*b)) for b in batches] + [float(graphed(*b)) for b in batches]
+            torch.cuda.synchronize()
+            runs.append((losses, [p.detach().clone() for p in m_e.parameters()],
+                         [p.detach().clone() for p in m_g.parameters()]))
+    finally:
+        distill.TEACHER_STREAM = prev
+    (l0, e0, g0), (l1, e1, g1) = runs
+    assert l0 == l1, (l0, l1)
+    for a, b in zip(e0 + g0, e1 + g1):
+        assert torch.equal(a, b)

@@ -9,8 +9,8 @@ TAG=${TAG:-ab}
 for v in "$@"; do
   name=${v%%:*}
   envs=${v#*:}
-  ( IFS=,; for kv in $envs; do [ -n "$kv" ] && export "$kv"; done
-    timeout -k 10 300 python -u bench.py --sections ${SECTIONS:-train} --no-cpu-baseline \
+  ( IFS=,; for kv in $envs; do [ -n "$kv" ] && export "$kv"; done; IFS=" "
+    timeout -k 10 300 python -u bench.py --sections ${SECTIONS:-train} ${BENCH_EXTRA:-} --no-cpu-baseline \
         --steps ${STEPS:-20} --warmup 3 > gpurun_out/bab_${TAG}_$name.log 2>&1 ) \
     || { echo "STOP $name"; tail -5 gpurun_out/bab_${TAG}_$name.log; exit 1; }
   python - "$name" "gpurun_out/bab_${TAG}_$name.log" <<'PY'
