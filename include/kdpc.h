@@ -334,6 +334,14 @@ int kdpc_weightnet_bwd(int b, int n, int s, int k, const float *xyz, const float
                        float *drel, float *dparams, void *workspace, size_t workspace_bytes,
                        void *stream);
 
+/* drel alone (the same rows, bit-identical to kdpc_weightnet_bwd's): with it the upstream
+ * gradient does not wait for the parameter reduction, which can then run on another stream
+ * (kdpc_weightnet_bwd with drel = NULL). */
+int kdpc_weightnet_bwd_rel(int b, int n, int s, int k, const float *xyz, const float *center,
+                           const int *idx, const float *w0, const float *b0, const float *w1,
+                           const float *b1, const float *w2, const float *b2,
+                           const float *dwt, float *drel, void *stream);
+
 /* ---- WeightNet-weighted neighbour sums: PointConvFlow's point-to-patch and patch-to-patch
  *      cost sums (pointconv_util.py:2039-2112) ----------------------------------------- */
 

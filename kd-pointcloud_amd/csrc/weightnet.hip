@@ -102,6 +102,75 @@ constexpr int kFS = kF + 1;                              // LDS row stride
 constexpr int fD2 = 0, fH1 = fD2 + kOut, fD1 = fH1 + kH1, fH0 = fD1 + kH1, fD0 = fH0 + kH0,
               fRel = fD0 + kH0;
 
+// One row's forward recomputed and back-propagated through the three ReLUs: the factors
+// both backward kernels start from (one definition, so their drel rows are bit-identical).
+struct RowGrad {
+  float rel[3], h0[kH0], h1[kH1], d2[kOut], d1[kH1], d0[kH0];
+};
+__device__ __forceinline__ void row_grad(int r, int s, int k, int n, const float* xyz,
+                                         const float* center, const int* idx, const Params& sp,
+                                         const float* dwt, RowGrad& t) {
+  float o[kOut];
+  rel_of(r, s, k, n, xyz, center, idx, t.rel);
+  dense<kH0, kIn>(sp.w0, sp.b0, t.rel, t.h0);
+  relu(t.h0);
+  dense<kH1, kH0>(sp.w1, sp.b1, t.h0, t.h1);
+  relu(t.h1);
+  dense<kOut, kH1>(sp.w2, sp.b2, t.h1, o);
+  const float4* src = reinterpret_cast<const float4*>(dwt + (long long)r * kOut);
+#pragma unroll
+  for (int v = 0; v < kOut / 4; ++v) {
+    const float4 x = src[v];
+    t.d2[4 * v] = x.x;
+    t.d2[4 * v + 1] = x.y;
+    t.d2[4 * v + 2] = x.z;
+    t.d2[4 * v + 3] = x.w;
+  }
+#pragma unroll
+  for (int q = 0; q < kOut; ++q) t.d2[q] = o[q] > 0.f ? t.d2[q] : 0.f;
+#pragma unroll
+  for (int i = 0; i < kH1; ++i) {
+    float a = 0.f;
+#pragma unroll
+    for (int q = 0; q < kOut; ++q) a = __builtin_fmaf(sp.w2[q * kH1 + i], t.d2[q], a);
+    t.d1[i] = t.h1[i] > 0.f ? a : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < kH0; ++i) {
+    float a = 0.f;
+#pragma unroll
+    for (int q = 0; q < kH1; ++q) a = __builtin_fmaf(sp.w1[q * kH0 + i], t.d1[q], a);
+    t.d0[i] = t.h0[i] > 0.f ? a : 0.f;
+  }
+}
+
+__device__ __forceinline__ void store_drel(int r, const Params& sp, const RowGrad& t,
+                                           float* __restrict__ drel) {
+#pragma unroll
+  for (int i = 0; i < kIn; ++i) {
+    float a = 0.f;
+#pragma unroll
+    for (int q = 0; q < kH0; ++q) a = __builtin_fmaf(sp.w0[q * kIn + i], t.d0[q], a);
+    drel[(long long)r * 3 + i] = a;
+  }
+}
+
+// drel only (one thread per row): the half of the backward the upstream layers wait for;
+// the parameter half (wn_bwd_kernel with drel = nullptr) can then run on another stream.
+__global__ __launch_bounds__(kBlock) void wn_bwd_rel_kernel(int rows, int s, int k, int n,
+                                                            const float* __restrict__ xyz,
+                                                            const float* __restrict__ center,
+                                                            const int* __restrict__ idx,
+                                                            Params sp,
+                                                            const float* __restrict__ dwt,
+                                                            float* __restrict__ drel) {
+  const int r = blockIdx.x * kBlock + threadIdx.x;
+  if (r >= rows) return;
+  RowGrad t;
+  row_grad(r, s, k, n, xyz, center, idx, sp, dwt, t);
+  store_drel(r, sp, t, drel);
+}
+
 __global__ __launch_bounds__(kBlock) void wn_bwd_kernel(int rows, int s, int k, int n,
                                                         const float* __restrict__ xyz,
                                                         const float* __restrict__ center,
@@ -126,50 +195,15 @@ __global__ __launch_bounds__(kBlock) void wn_bwd_kernel(int rows, int s, int k, 
     const int r = t0 + threadIdx.x;
     float* f = fac + threadIdx.x * kFS;
     if (r < rows) {
-      float rel[3], h0[kH0], h1[kH1], o[kOut];
-      rel_of(r, s, k, n, xyz, center, idx, rel);
-      dense<kH0, kIn>(sp.w0, sp.b0, rel, h0);
-      relu(h0);
-      dense<kH1, kH0>(sp.w1, sp.b1, h0, h1);
-      relu(h1);
-      dense<kOut, kH1>(sp.w2, sp.b2, h1, o);
-      float d2[kOut];
-      const float4* src = reinterpret_cast<const float4*>(dwt + (long long)r * kOut);
-#pragma unroll
-      for (int v = 0; v < kOut / 4; ++v) {
-        const float4 x = src[v];
-        d2[4 * v] = x.x;
-        d2[4 * v + 1] = x.y;
-        d2[4 * v + 2] = x.z;
-        d2[4 * v + 3] = x.w;
-      }
-#pragma unroll
-      for (int q = 0; q < kOut; ++q) d2[q] = o[q] > 0.f ? d2[q] : 0.f;
-      float d1[kH1];
-#pragma unroll
-      for (int i = 0; i < kH1; ++i) {
-        float a = 0.f;
-#pragma unroll
-        for (int q = 0; q < kOut; ++q) a = __builtin_fmaf(sp.w2[q * kH1 + i], d2[q], a);
-        d1[i] = h1[i] > 0.f ? a : 0.f;
-      }
-      float d0[kH0];
-#pragma unroll
-      for (int i = 0; i < kH0; ++i) {
-        float a = 0.f;
-#pragma unroll
-        for (int q = 0; q < kH1; ++q) a = __builtin_fmaf(sp.w1[q * kH0 + i], d1[q], a);
-        d0[i] = h0[i] > 0.f ? a : 0.f;
-      }
-      if (drel) {
-#pragma unroll
-        for (int i = 0; i < kIn; ++i) {
-          float a = 0.f;
-#pragma unroll
-          for (int q = 0; q < kH0; ++q) a = __builtin_fmaf(sp.w0[q * kIn + i], d0[q], a);
-          drel[(long long)r * 3 + i] = a;
-        }
-      }
+      RowGrad t;
+      row_grad(r, s, k, n, xyz, center, idx, sp, dwt, t);
+      if (drel) store_drel(r, sp, t, drel);
+      const float (&d2)[kOut] = t.d2;
+      const float (&h1)[kH1] = t.h1;
+      const float (&d1)[kH1] = t.d1;
+      const float (&h0)[kH0] = t.h0;
+      const float (&d0)[kH0] = t.d0;
+      const float (&rel)[3] = t.rel;
 #pragma unroll
       for (int q = 0; q < kOut; ++q) f[fD2 + q] = d2[q];
 #pragma unroll
@@ -216,6 +250,22 @@ KDPC_API int kdpc_weightnet_fwd(int b, int n, int s, int k, const float* xyz, co
   const Params p{w0, b0, w1, b1, w2, b2};
   hipLaunchKernelGGL(wn_fwd_kernel, dim3((unsigned)divupll(rows, kBlock)), dim3(kBlock), 0,
                      (hipStream_t)stream, (int)rows, s, k, n, xyz, center, idx, p, wt);
+  KDPC_RETURN_LAUNCH();
+}
+
+KDPC_API int kdpc_weightnet_bwd_rel(int b, int n, int s, int k, const float* xyz,
+                                    const float* center, const int* idx, const float* w0,
+                                    const float* b0, const float* w1, const float* b1,
+                                    const float* w2, const float* b2, const float* dwt,
+                                    float* drel, void* stream) {
+  KDPC_CHECK_ARG(b >= 0 && n > 0 && s >= 0 && k >= 1);
+  const long long rows = (long long)b * s * k;
+  if (rows == 0) return (int)hipSuccess;
+  KDPC_CHECK_ARG(xyz && center && idx && w0 && b0 && w1 && b1 && w2 && b2 && dwt && drel &&
+                 rows < (1ll << 31) - kBlock);
+  const Params p{w0, b0, w1, b1, w2, b2};
+  hipLaunchKernelGGL(wn_bwd_rel_kernel, dim3((unsigned)divupll(rows, kBlock)), dim3(kBlock), 0,
+                     (hipStream_t)stream, (int)rows, s, k, n, xyz, center, idx, p, dwt, drel);
   KDPC_RETURN_LAUNCH();
 }
 

@@ -93,6 +93,17 @@ class _TeacherFork:
         return self.out
 
 
+def _kd_student_streams(student):
+    """The KD step already runs the teacher's forward on a stream of its own: a fifth stream
+    in the graph (the student's decoder coordinate fork, models_bid_pointconv._CoordFork)
+    exceeds the 4 hardware queues per process and serialises branches onto shared queues
+    (A/B at configs[3]'s slice: 13.4 ms/step without the fork, 14.3 with it,
+    profiles/round03/ab/bab_fkkd_*), so the student searches in line there."""
+    core = _core(student)
+    if hasattr(core, "coord_fork") and TEACHER_STREAM:
+        core.coord_fork = False
+
+
 def _plan_fn(model):
     """The model's coordinate-only precompute: the FPS chain plus the coordinate-only kNN
     searches and their CSRs (PointConvBidirection.precompute_plan) where the model has it,
@@ -192,6 +203,7 @@ class KDTrainStep:
         self.prefetch = FpsPrefetch()
         for p in self.teacher.parameters():
             p.requires_grad_(False)
+        _kd_student_streams(student)
 
     def __call__(self, pos1, pos2, flow, color1=None, color2=None, next_batch=None):
         color1 = pos1 if color1 is None else color1
@@ -571,6 +583,7 @@ def graphed_kd_step(teacher, student, optimizer, example_inputs, gamma=0.3, beta
         p.requires_grad_(False)
     teacher.eval()
     student.train()
+    _kd_student_streams(student)
 
     def run(pos1, pos2, flow, fps=None):
         kw = {} if fps is None else {"fps_idx": fps}

@@ -82,6 +82,7 @@ _SIGNATURES = {
     "kdpc_weightnet_fwd": [_c_int] * 4 + [_vp] * 11,
     "kdpc_weightnet_bwd_workspace_bytes": [],
     "kdpc_weightnet_bwd": [_c_int] * 4 + [_vp] * 13 + [_c_size, _vp],
+    "kdpc_weightnet_bwd_rel": [_c_int] * 4 + [_vp] * 12,
     "kdpc_knn_feature_workspace_bytes": [_c_int] * 3,
     "kdpc_knn_feature": [_c_int] * 5 + [_vp] * 5 + [_c_size, _vp],
     "kdpc_wn_wsum_param_count": [_c_int],
@@ -524,12 +525,13 @@ def cost_volume_wide_max_bwd(gout, out, amax, K):
                _gpu(gout, "gout"), out, amax, K)
 
 
-def cost_volume_wide_h0_bwd(x1, x2, idx, h0, dz):
-    """dz (B*N1*K, Din) dh0 -> dz0 in place; -> dp1 (B,N1,Din), dWpos (Din,3)."""
+def cost_volume_wide_h0_bwd(x1, x2, idx, h0, dz, reduce=True):
+    """dz (B*N1*K, Din) dh0 -> dz0 in place; -> dp1 (B,N1,Din), dWpos (Din,3) (reduce=False:
+    the per-workgroup slab dWpos is the colsum(...).view(Din, 3) of)."""
     din = h0.shape[-1]
     dp1, slab = _op("kdpc_cost_volume_wide_h0_bwd", "cost_volume_wide_h0_bwd", _gpu(x1, "x1"),
                     x2, idx, h0, dz)
-    return dp1, colsum(slab).view(din, 3)
+    return dp1, (colsum(slab).view(din, 3) if reduce else slab)
 
 
 # ------------------------------------------------------------------ PointConv contraction
@@ -651,6 +653,13 @@ def weightnet_bwd(xyz, center, idx, params, dwt, need_rel=False):
     """-> (drel (B,S,K,3) | None, dparams (248,): dW0 | db0 | dW1 | db1 | dW2 | db2)."""
     return _op("kdpc_weightnet_bwd", "weightnet_bwd", _gpu(xyz, "xyz"), center, idx, *params,
                dwt, bool(need_rel))
+
+
+def weightnet_bwd_rel(xyz, center, idx, params, dwt):
+    """drel (B,S,K,3) alone, bit-identical to weightnet_bwd's (the parameter half can then
+    run with need_rel=False on another stream)."""
+    return _op("kdpc_weightnet_bwd_rel", "weightnet_bwd_rel", _gpu(xyz, "xyz"), center, idx,
+               *params, dwt)
 
 
 # ---------------------------------------------- WeightNet-weighted neighbour sums

@@ -11,6 +11,8 @@ output.  MI355X-first restructuring of the forward, with identical per-sample ar
   * only the pc1-side layers (cost volume refinement, scene-flow estimators whose train-mode
     BatchNorm sees pc1 only, warping) run at batch B.
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -20,6 +22,74 @@ from pointconv_util import index_points_gather as index_points, index_points_gro
 from loss_functions import multiScaleLoss  # noqa: F401  (the reference defines it here too)
 import kdpc_native
 from pointnet2 import pointnet2_utils
+
+# KDPC_COORD_FORK=0 runs the decoder's flow-dependent searches in line (A/B runs)
+COORD_FORK = os.environ.get("KDPC_COORD_FORK", "1") != "0"
+_coord_streams = {}  # (device index, forking stream handle) -> side stream
+
+
+class _CoordFork:
+    """The decoder's flow-dependent coordinate work on a second stream.
+
+    At levels 2..0 the cost volume's kNN (every point's nearest in the other cloud, pc2
+    warped by the upsampled flow) depends on the coarser level's flow, so it cannot join the
+    one-step-ahead coordinate plan; but it depends on coordinates only, while the main stream
+    still has the level's feature upsampling (deconv) to run.  cross_neighbours() issues the
+    search on the side stream as soon as the warped cloud exists; ready() makes the main
+    stream wait for it right before the cost volume, and then queues on the side stream the
+    inverted indices that the backward would otherwise build on its critical path (the cost
+    volume's CSR with ranks, the warping blend's CSR); join() (end of the forward) makes the
+    main stream wait for them.  Training forwards only.  Same kernels on the same inputs:
+    bit-identical to the in-line searches
+    (tests/test_gpu_kd.py::test_coordinate_fork_is_bit_identical)."""
+
+    def __init__(self, device, enabled=True):
+        self.cur = self.side = None
+        # training forwards only (the KD step turns it off for its student: distill.py
+        # _kd_student_streams)
+        if enabled and COORD_FORK and device.type == "cuda" and torch.is_grad_enabled():
+            self.cur = torch.cuda.current_stream(device)
+            key = (device.index, self.cur.cuda_stream)
+            self.side = _coord_streams.get(key)
+            if self.side is None:
+                self.side = _coord_streams[key] = torch.cuda.Stream(device=device)
+
+    def cross_neighbours(self, cross, xa, warp_idx):
+        """Issue cross.neighbours(xa) on the side stream -> a handle for ready(), or None
+        (forward_pair then searches in line)."""
+        if self.side is None:
+            return None
+        xa = xa.detach()
+        self.side.wait_stream(self.cur)
+        xa.record_stream(self.side)
+        with torch.cuda.stream(self.side):
+            idx = cross.neighbours(xa)
+        idx.record_stream(self.cur)  # allocated on the side stream, read on the main one
+        return idx, xa.shape[1], warp_idx
+
+    def ready(self, pending):
+        """The main stream waits for the search; the inverted indices the backward will read
+        are then built on the side stream, beside the cost volume."""
+        if pending is None:
+            return None
+        idx, n, warp_idx = pending
+        self.cur.wait_stream(self.side)
+        if torch.is_grad_enabled():
+            keep = []
+            with torch.cuda.stream(self.side):
+                c = kdpc_native.csr_rank_of(idx, n)
+                keep += [c.offsets, c.perm, c.rank]
+                if warp_idx is not None:
+                    warp_idx.record_stream(self.side)
+                    c = kdpc_native.csr_of(warp_idx, n)
+                    keep += [c.offsets, c.perm]
+            for t in keep:
+                t.record_stream(self.cur)
+        return idx
+
+    def join(self):
+        if self.side is not None:
+            self.cur.wait_stream(self.side)
 
 scale = 1.0
 
@@ -81,6 +151,9 @@ class PointConvBidirection(nn.Module):
             out.append(idx)
             x = index_points(x, idx)
         return out
+
+    # the decoder's flow-dependent searches and their CSRs on a side stream (_CoordFork)
+    coord_fork = True
 
     # kNN searches of the forward whose inputs are coordinates only (the clouds and their FPS
     # subsets): 13 of the 19 searches.  The flow-dependent ones (the warping 3-NN and the
@@ -218,28 +291,34 @@ class PointConvBidirection(nn.Module):
         decoders = [(2, self.cross2, self.flow2, self.deconv3_2),
                     (1, self.cross1, self.flow1, self.deconv2_1),
                     (0, self.cross0, self.flow0, self.deconv1_0)]
+        fork = _CoordFork(pc.device, self.coord_fork)
         for lv, cross, flow_est, deconv in decoders:
             # one 3-NN search per level pair serves all three upsamplings (both clouds'
             # features, and pc1's flow and estimator features: its first B rows)
             up_idx = knn.get(f"up{lv}")
             if up_idx is None:
                 up_idx = self.upsample.neighbours(pcs[lv], pcs[lv + 1])
+            up_idx1 = kdpc_native.batch_prefix(up_idx, B)  # pc1 half, CSR shared with up_idx
+            pc1_lv, pc2_lv = one(pcs[lv]), two(pcs[lv])
+            sflow = flow if self.scale == 1.0 else self.scale * flow  # x1.0 is exact
+            # the flow chain first: the cost volume's search can then run on the side
+            # stream while the feature upsampling below runs here
+            up_flow = self.upsample.forward_cl(pc1_lv, one(pcs[lv + 1]), sflow, up_idx1)
+            pc2_warp, warp_idx = self.warping.forward_cl(pc1_lv, pc2_lv, up_flow, with_idx=True)
+            xa = torch.cat([pc1_lv, pc2_warp], 0)
+            pending = fork.cross_neighbours(cross, xa, warp_idx)
             f_up = deconv.cl(self.upsample.forward_cl(pcs[lv], pcs[lv + 1],
                                                       torch.cat([f1n, f2n], 0), up_idx))
             up_feats.append(f_up)
             c_feat = torch.cat([feats[lv], f_up], dim=-1)
-            up_idx1 = kdpc_native.batch_prefix(up_idx, B)  # pc1 half, CSR shared with up_idx
-            pc1_lv, pc2_lv = one(pcs[lv]), two(pcs[lv])
-            sflow = flow if self.scale == 1.0 else self.scale * flow  # x1.0 is exact
-            up_flow = self.upsample.forward_cl(pc1_lv, one(pcs[lv + 1]), sflow, up_idx1)
-            pc2_warp = self.warping.forward_cl(pc1_lv, pc2_lv, up_flow)
-            f1n, f2n, cost = cross.forward_pair(torch.cat([pc1_lv, pc2_warp], 0), c_feat)
             feat_up = self.upsample.forward_cl(pc1_lv, one(pcs[lv + 1]), feat_est, up_idx1)
             new_feat1 = torch.cat([one(feats[lv]), feat_up], dim=-1)
+            f1n, f2n, cost = cross.forward_pair(xa, c_feat, fork.ready(pending))
             feat_est, flow = flow_est.forward_cl(pc1_lv, new_feat1, cost, up_flow,
                                                  knn_idx=knn.get(f"est{lv}"))
             flows.insert(0, flow)
             crosses.insert(0, cost)
+        fork.join()
 
         cn = lambda t: t.permute(0, 2, 1)  # noqa: E731  point-major -> reference (B,C,N) view
         pc1 = [cn(one(p)) for p in pcs]

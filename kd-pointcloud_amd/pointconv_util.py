@@ -324,7 +324,15 @@ class _WeightNetFn(torch.autograd.Function):
     def backward(ctx, dwt):
         xyz, center, idx, *params = ctx.saved_tensors
         need_rel = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
-        drel, dflat = _nat.weightnet_bwd(xyz, center, idx, params, dwt.contiguous(), need_rel)
+        dwt = dwt.contiguous()
+        if wgrad.enabled and xyz.is_cuda:
+            # drel (what the upstream layers wait for) here, the 248-parameter reduction on
+            # the parameter-gradient stream (same kernels' arithmetic: bit-identical)
+            drel = _nat.weightnet_bwd_rel(xyz, center, idx, params, dwt) if need_rel else None
+            dflat = wgrad.run(lambda: _nat.weightnet_bwd(xyz, center, idx, params, dwt)[1],
+                              [xyz, center, idx, dwt, *params])
+        else:
+            drel, dflat = _nat.weightnet_bwd(xyz, center, idx, params, dwt, need_rel)
         dparams = [g.view_as(p) for g, p in
                    zip(dflat.split([p.numel() for p in params]), params)]
         dxyz = dcenter = None
@@ -550,12 +558,14 @@ class _CostVolumeWide(torch.autograd.Function):
         N2, din = x2.shape[1], h0.shape[-1]
         dz1, gsc = _nat.cost_volume_wide_max_bwd(gout.contiguous(), out, amax, K)
         h0f = h0.view(-1, din)
-        dw1 = splitk_tn(dz1, h0f)  # one 262144-deep GEMM ran ~10x below the MFMA rate
-        db1 = _nat.colsum(gsc)
+        # parameter gradients on the parameter-gradient stream (wgrad.py); split-K because
+        # one 262144-deep GEMM ran ~10x below the MFMA rate
+        dw1, db1 = wgrad.run(lambda: (splitk_tn(dz1, h0f), _nat.colsum(gsc)), [dz1, h0f, gsc])
         dz = torch.mm(dz1, w1)  # dh0; becomes dz0 in place
         del dz1
-        dp1, dwpos = _nat.cost_volume_wide_h0_bwd(x1, x2, idx, h0, dz)
-        dbpos = _nat.colsum(dp1.view(-1, din))
+        dp1, slab = _nat.cost_volume_wide_h0_bwd(x1, x2, idx, h0, dz, reduce=False)
+        dwpos, dbpos = wgrad.run(lambda: (_nat.colsum(slab).view(din, 3),
+                                          _nat.colsum(dp1.view(-1, din))), [slab, dp1])
         csr = _nat.csr_of(idx, N2)
         dp2 = _nat.group_rows_grad(dz.view(B, N1 * K, din), csr, B, N2, din)
         ddir = torch.mm(dz, wpos)  # (rows, 3)
@@ -950,14 +960,16 @@ class PointWarping(nn.Module):
             return xyz2
         return self.forward_cl(_cl(xyz1), _cl(xyz2), _cl(flow1)).permute(0, 2, 1)
 
-    def forward_cl(self, x1, x2, flow1=None):
-        """Point-major: x1 (B,N1,3), x2 (B,N2,3), flow1 (B,N1,3) -> warped x2 (B,N2,3)."""
+    def forward_cl(self, x1, x2, flow1=None, with_idx=False):
+        """Point-major: x1 (B,N1,3), x2 (B,N2,3), flow1 (B,N1,3) -> warped x2 (B,N2,3)
+        (with_idx: also the 3-NN index of x2 in x1 + flow1 the blend used)."""
         if flow1 is None:
-            return x2
+            return (x2, None) if with_idx else x2
         xyz1_to_2 = (x1 + flow1).contiguous()
         x2 = x2.contiguous()
         knn_idx = knn_point(3, xyz1_to_2, x2)
-        return _idw_blend(xyz1_to_2, x2, flow1, knn_idx, warp=True)
+        out = _idw_blend(xyz1_to_2, x2, flow1, knn_idx, warp=True)
+        return (out, knn_idx) if with_idx else out
 
 
 class UpsampleFlow(nn.Module):

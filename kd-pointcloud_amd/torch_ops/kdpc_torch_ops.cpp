@@ -624,6 +624,20 @@ std::tuple<c10::optional<Tensor>, Tensor> weightnet_bwd(Tensor xyz, Tensor cente
   return {need_rel ? c10::optional<Tensor>(drel) : c10::nullopt, dparams};
 }
 
+Tensor weightnet_bwd_rel(Tensor xyz, Tensor center, Tensor idx, Tensor w0, Tensor b0, Tensor w1,
+                         Tensor b1, Tensor w2, Tensor b2, Tensor dwt) {
+  for (auto* t : {&xyz, &center, &w0, &b0, &w1, &b1, &w2, &b2, &dwt})
+    dev(*t, kF, "weightnet input");
+  dev(idx, kI, "idx");
+  GUARD(xyz);
+  const int64_t b = xyz.size(0), n = xyz.size(1), s = idx.size(1), k = idx.size(2);
+  Tensor drel = empty_f({b, s, k, 3}, xyz);
+  check(kdpc_weightnet_bwd_rel(b, n, s, k, F(xyz), F(center), I(idx), F(w0), F(b0), F(w1),
+                               F(b1), F(w2), F(b2), F(dwt), F(drel), stream_of(xyz)),
+        "weightnet_bwd_rel");
+  return drel;
+}
+
 // ---------------------------------------------------- WeightNet-weighted neighbour sums
 Tensor wn_wsum_fwd(Tensor dir, c10::optional<Tensor> idx, Tensor v, Tensor w0, Tensor b0,
                    Tensor w1, Tensor b1, Tensor w2, Tensor b2) {
@@ -908,6 +922,8 @@ TORCH_LIBRARY(kdpc, m) {
         "Tensor b1, Tensor w2, Tensor b2) -> Tensor");
   m.def("weightnet_bwd(Tensor xyz, Tensor center, Tensor idx, Tensor w0, Tensor b0, Tensor w1, "
         "Tensor b1, Tensor w2, Tensor b2, Tensor dwt, bool need_rel) -> (Tensor?, Tensor)");
+  m.def("weightnet_bwd_rel(Tensor xyz, Tensor center, Tensor idx, Tensor w0, Tensor b0, "
+        "Tensor w1, Tensor b1, Tensor w2, Tensor b2, Tensor dwt) -> Tensor");
   m.def("wn_wsum_fwd(Tensor dir, Tensor? idx, Tensor v, Tensor w0, Tensor b0, Tensor w1, "
         "Tensor b1, Tensor w2, Tensor b2) -> Tensor");
   m.def("wn_wsum_bwd(Tensor dir, Tensor? idx, Tensor v, Tensor w0, Tensor b0, Tensor w1, "
@@ -969,6 +985,7 @@ TORCH_LIBRARY_IMPL(kdpc, CUDA, m) {
   m.impl("pointconv_contract_bwd", pointconv_contract_bwd);
   m.impl("weightnet_fwd", weightnet_fwd);
   m.impl("weightnet_bwd", weightnet_bwd);
+  m.impl("weightnet_bwd_rel", weightnet_bwd_rel);
   m.impl("knn_feature", knn_feature);
   m.impl("knn_feature_dist", knn_feature_dist);
   m.impl("wn_wsum_fwd", wn_wsum_fwd);

@@ -409,3 +409,30 @@ def test_pointconv_bwd_halves_equal_whole(b, n, s, k, d, o):
     torch.cuda.synchronize()
     for name, a, c in zip(["dxyz", "dfeats", "dcenter", "dwt", "dwl"], whole, list(data) + [dwl]):
         assert torch.equal(a, c), name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("b,n,s,k", [(2, 4096, 1024, 9), (1, 300, 77, 16), (3, 64, 0, 4)])
+def test_weightnet_bwd_rel_equals_whole(b, n, s, k):
+    """kdpc_weightnet_bwd_rel (drel alone, on the backward's stream) equals the drel of
+    kdpc_weightnet_bwd bit for bit, and the parameter half without drel equals the combined
+    launch's dparams (that half runs on the parameter-gradient stream, wgrad.py)."""
+    import kdpc_native as K
+    import pointconv_util as P
+    torch.manual_seed(n + k)
+    wn = P.WeightNet(3, 16).to(DEV)
+    params = [t.detach() for c in wn.mlp_convs for t in (c.weight, c.bias)]
+    xyz = torch.rand(b, n, 3, device=DEV)
+    center = xyz[:, :s].contiguous()
+    if s:
+        idx = P._as_idx32(P.knn_point(k, xyz, center)).contiguous()
+    else:
+        idx = torch.zeros(b, 0, k, dtype=torch.int32, device=DEV)
+    dwt = torch.randn(b, s, k, 16, device=DEV)
+    drel, dflat = K.weightnet_bwd(xyz, center, idx, params, dwt, True)
+    drel2 = K.weightnet_bwd_rel(xyz, center, idx, params, dwt)
+    none, dflat2 = K.weightnet_bwd(xyz, center, idx, params, dwt, False)
+    torch.cuda.synchronize()
+    assert none is None
+    assert torch.equal(drel, drel2)
+    assert torch.equal(dflat, dflat2)

@@ -166,6 +166,51 @@ def test_coordinate_plan_equals_inline_searches():
             assert g is None or torch.equal(g, ref[2][n]), n
 
 
+def test_coordinate_fork_is_bit_identical():
+    """The decoder's flow-dependent searches and inverted indices on the side stream
+    (models_bid_pointconv._CoordFork) give the same flows, loss and gradients, bit for bit, as
+    running them in line: eager, under no_grad, and replayed from the captured train step."""
+    import loss_functions as L
+    import models_bid_pointconv as M
+    from distill import graphed_flow_step, make_optimizer
+    torch.manual_seed(4)
+    base = M.PointConvBidirection().to(DEV).train()
+    batches = [_batch(2, 8192, s) for s in (71, 72)]
+    runs = []
+    prev = M.COORD_FORK
+    try:
+        for on in (False, True):
+            M.COORD_FORK = on
+            m = copy.deepcopy(base)
+            p1, p2, fl = batches[0]
+            out = m(p1, p2, p1, p2)
+            loss = L.multiScaleLoss(out[0], fl, out[1])
+            loss.backward()
+            with torch.no_grad():
+                ev = m.eval()(p1, p2, p1, p2)[0]
+            m.train()
+            mg = copy.deepcopy(base)
+            step = graphed_flow_step(mg, make_optimizer(mg, capturable=True), batches[0],
+                                      warmup=1)
+            gl = [float(step(*b)) for b in batches]
+            torch.cuda.synchronize()
+            runs.append((loss.detach(), [f.detach() for f in out[0]], [f for f in ev],
+                         {n: p.grad for n, p in m.named_parameters()}, gl,
+                         [p.detach().clone() for p in mg.parameters()]))
+    finally:
+        M.COORD_FORK = prev
+    (l0, f0, e0, g0, gl0, p0), (l1, f1, e1, g1, gl1, p1_) = runs
+    assert torch.equal(l0, l1), (float(l0), float(l1))
+    for a, b in zip(f0 + e0, f1 + e1):
+        assert torch.equal(a, b)
+    for n, g in g1.items():
+        assert (g is None) == (g0[n] is None), n
+        assert g is None or torch.equal(g, g0[n]), n
+    assert gl0 == gl1, (gl0, gl1)
+    for a, b in zip(p0, p1_):
+        assert torch.equal(a, b)
+
+
 def test_teacher_stream_is_bit_identical():
     """The KD step's frozen-teacher forward on its own stream (distill._TeacherFork, beside the
     student's forward) gives the same loss and parameters, bit for bit, as running it in

@@ -133,6 +133,7 @@ TORCH_OPS = {
     "pointconv_contract_fwd": "kdpc_pointconv_contract_fwd",
     "pointconv_contract_bwd": "kdpc_pointconv_contract_bwd",
     "weightnet_fwd": "kdpc_weightnet_fwd", "weightnet_bwd": "kdpc_weightnet_bwd",
+    "weightnet_bwd_rel": "kdpc_weightnet_bwd_rel",
     "wn_wsum_fwd": "kdpc_wn_wsum_fwd", "wn_wsum_bwd": "kdpc_wn_wsum_bwd",
     "batchnorm_lrelu_fwd": "kdpc_batchnorm_lrelu_fwd",
     "batchnorm_lrelu_apply": "kdpc_batchnorm_lrelu_apply",
