@@ -93,14 +93,18 @@ class _TeacherFork:
         return self.out
 
 
+# KDPC_KD_COORD_FORK=1: the KD student forks its decoder searches too (A/B runs)
+KD_COORD_FORK = os.environ.get("KDPC_KD_COORD_FORK", "0") == "1"
+
+
 def _kd_student_streams(student):
-    """The KD step already runs the teacher's forward on a stream of its own: a fifth stream
-    in the graph (the student's decoder coordinate fork, models_bid_pointconv._CoordFork)
-    exceeds the 4 hardware queues per process and serialises branches onto shared queues
-    (A/B at configs[3]'s slice: 13.4 ms/step without the fork, 14.3 with it,
-    profiles/round03/ab/bab_fkkd_*), so the student searches in line there."""
+    """The KD step already runs the teacher's forward on a stream of its own, beside the
+    student's; there the student's decoder coordinate fork (models_bid_pointconv._CoordFork)
+    measured slower, with its own stream (13.17-13.66 vs 14.27-14.30 ms/step at configs[3]'s
+    slice, profiles/round03/ab/bab_fkkd_*) and on the parameter-gradient stream alike
+    (13.56-13.66 vs 14.30-14.32, bab_fskd_*), so the student searches in line there."""
     core = _core(student)
-    if hasattr(core, "coord_fork") and TEACHER_STREAM:
+    if hasattr(core, "coord_fork") and TEACHER_STREAM and not KD_COORD_FORK:
         core.coord_fork = False
 
 

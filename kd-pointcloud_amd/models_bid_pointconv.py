@@ -21,11 +21,14 @@ from pointconv_util import (PointConvD, PointWarping, UpsampleFlow, CrossLayerLi
 from pointconv_util import index_points_gather as index_points, index_points_group, square_distance  # noqa: F401
 from loss_functions import multiScaleLoss  # noqa: F401  (the reference defines it here too)
 import kdpc_native
+import wgrad
 from pointnet2 import pointnet2_utils
 
 # KDPC_COORD_FORK=0 runs the decoder's flow-dependent searches in line (A/B runs)
 COORD_FORK = os.environ.get("KDPC_COORD_FORK", "1") != "0"
 _coord_streams = {}  # (device index, forking stream handle) -> side stream
+# KDPC_COORD_OWN_STREAM=1 gives the fork a stream of its own instead of wgrad's (A/B runs)
+SHARED_SIDE_STREAM = os.environ.get("KDPC_COORD_OWN_STREAM") != "1"
 
 
 class _CoordFork:
@@ -49,10 +52,15 @@ class _CoordFork:
         # _kd_student_streams)
         if enabled and COORD_FORK and device.type == "cuda" and torch.is_grad_enabled():
             self.cur = torch.cuda.current_stream(device)
-            key = (device.index, self.cur.cuda_stream)
-            self.side = _coord_streams.get(key)
-            if self.side is None:
-                self.side = _coord_streams[key] = torch.cuda.Stream(device=device)
+            if SHARED_SIDE_STREAM:
+                # the parameter-gradient stream: idle during the forward, and one stream
+                # fewer against the 4 hardware queues of the process
+                self.side = wgrad.side_stream(device)
+            else:
+                key = (device.index, self.cur.cuda_stream)
+                self.side = _coord_streams.get(key)
+                if self.side is None:
+                    self.side = _coord_streams[key] = torch.cuda.Stream(device=device)
 
     def cross_neighbours(self, cross, xa, warp_idx):
         """Issue cross.neighbours(xa) on the side stream -> a handle for ready(), or None
