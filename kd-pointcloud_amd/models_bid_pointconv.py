@@ -29,6 +29,8 @@ COORD_FORK = os.environ.get("KDPC_COORD_FORK", "1") != "0"
 _coord_streams = {}  # (device index, forking stream handle) -> side stream
 # KDPC_COORD_OWN_STREAM=1 gives the fork a stream of its own instead of wgrad's (A/B runs)
 SHARED_SIDE_STREAM = os.environ.get("KDPC_COORD_OWN_STREAM") != "1"
+# KDPC_COORD_FORK_CSR=0 leaves the CSRs to the backward (A/B runs)
+FORK_CSR = os.environ.get("KDPC_COORD_FORK_CSR", "1") != "0"
 
 
 class _CoordFork:
@@ -82,7 +84,7 @@ class _CoordFork:
             return None
         idx, n, warp_idx = pending
         self.cur.wait_stream(self.side)
-        if torch.is_grad_enabled():
+        if torch.is_grad_enabled() and FORK_CSR:
             keep = []
             with torch.cuda.stream(self.side):
                 c = kdpc_native.csr_rank_of(idx, n)
