@@ -64,7 +64,8 @@ ROOFLINE = {
     "kdpc_knn_point": ("hbm", "GB/s", HBM_PEAK_GBS,
                        ["ref_sort_kernel", "query_sort_kernel", "chunk_box_kernel",
                         "knn_cull_kernel", "knn_kernel"]),
-    "kdpc_gather_points": ("hbm", "GB/s", HBM_PEAK_GBS, ["gather_points_kernel"]),
+    "kdpc_gather_points": ("hbm", "GB/s", HBM_PEAK_GBS, ["gather_points_lds_kernel",
+                                                          "gather_points_kernel"]),
     "kdpc_cost_volume_fwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF,
                              ["cost_volume_fwd_kernel", "cvw_fused_fwd_kernel"]),
     "kdpc_cost_volume_bwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF, ["cost_volume_bwd_kernel"]),
@@ -100,7 +101,8 @@ def parse(argv=None):
     ap.add_argument("--mode", choices=["train", "kd"], default="train",
                     help="the headline step (kd: the KD step at --batch is the headline)")
     ap.add_argument("--sections", default="train,kd,configs1,knn",
-                    help="comma list of train, kd, configs1, knn (PMC passes run one each)")
+                    help="comma list of train, kd, configs1, knn, gather_c3, gather_c64 "
+                         "(PMC passes run one each)")
     ap.add_argument("--roofline-kernel", default=PRIMARY_KERNEL)
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -320,8 +322,8 @@ def step_section(args, mode, batch, dev, world, rank):
 
 
 # ----------------------------------------------------------------------- microbenchmarks
-def _time_launches(fn, iters, stream):
-    for _ in range(3):
+def _time_launches(fn, iters, stream, warmup=3):
+    for _ in range(warmup):
         fn()
     e0, e1 = _events(stream)
     for _ in range(iters):
@@ -348,12 +350,13 @@ def configs1_section(dev):
     idx = K.ball_query(0.5, Kn, xyz, centres)
     feats = torch.randn(B, C, N, device=dev)
     wl = "configs1_b8_n8192_s2048_k16_c64"
-    g_ms = _time_launches(lambda: K.group_points(feats, idx), 20, stream)
+    g_ms = _time_launches(lambda: K.group_points(feats, idx), 100, stream, warmup=10)
     g_bytes = B * (4 * C * N + 4 * S * Kn + 4 * C * S * Kn)
     # gather_operation: the model gathers xyz (C=3, index_points_gather); C=64 as well
     xyz_cn = xyz.permute(0, 2, 1).contiguous()
-    ga3_ms = _time_launches(lambda: K.gather_points(xyz_cn, fidx), 50, stream)
-    ga64_ms = _time_launches(lambda: K.gather_points(feats, fidx), 50, stream)
+    # ~3-5 us launches: 20 untimed, then 200 timed back to back
+    ga3_ms = _time_launches(lambda: K.gather_points(xyz_cn, fidx), 200, stream, warmup=20)
+    ga64_ms = _time_launches(lambda: K.gather_points(feats, fidx), 200, stream, warmup=20)
     ga_bytes = lambda c: B * (4 * c * N + 4 * S + 4 * c * S)  # noqa: E731
     return {
         "workload": "B=8 N=8192: FPS 8192->2048, ball_query r=0.5 K=16, grouping C=64 S=2048 "
@@ -365,12 +368,29 @@ def configs1_section(dev):
         "ball_query": {"us_per_call": round(bq_ms * 1e3, 2), "queries": B * S,
                        "bound": "latency (per-query serial scan with early exit)"},
         "grouping_operation": roofline_obj("kdpc_group_points", wl, g_ms, 1, g_bytes, 0),
-        "gather_operation_c3": roofline_obj("kdpc_gather_points", wl, ga3_ms, 1, ga_bytes(3), 0,
-                                            bound="hbm", note="1.0 MB per launch: "
-                                                              "launch-latency-bound"),
-        "gather_operation_c64": roofline_obj("kdpc_gather_points", wl, ga64_ms, 1, ga_bytes(64),
-                                             0, bound="hbm"),
+        # PMC traffic keyed per channel count (the two launches differ 20x in bytes)
+        "gather_operation_c3": roofline_obj("kdpc_gather_points", "configs1_gather_c3", ga3_ms, 1,
+                                            ga_bytes(3), 0, bound="hbm",
+                                            note="1.0 MB per launch (24 rows of 32 KiB): "
+                                                 "launch-latency-bound"),
+        "gather_operation_c64": roofline_obj("kdpc_gather_points", "configs1_gather_c64",
+                                             ga64_ms, 1, ga_bytes(64), 0, bound="hbm"),
     }
+
+
+def gather_section(dev, c):
+    """gather_operation alone at configs[1] (B=8, N=8192, M=2048) for C channels: the
+    single-workload run the per-C PMC passes profile (sections gather_c3 / gather_c64)."""
+    import kdpc_native as K
+    import synthetic
+    B, N, S = 8, 8192, 2048
+    stream = torch.cuda.current_stream(dev)
+    xyz = torch.from_numpy(synthetic.ft3d_batch(B, N, seed=7)[0]).to(dev)
+    fidx = K.furthest_point_sampling(xyz, S)
+    pts = (xyz.permute(0, 2, 1).contiguous() if c == 3 else torch.randn(B, c, N, device=dev))
+    ms = _time_launches(lambda: K.gather_points(pts, fidx), 200, stream, warmup=20)
+    return roofline_obj("kdpc_gather_points", f"configs1_gather_c{c}", ms, 1,
+                        B * (4 * c * N + 4 * S + 4 * c * S), 0, bound="hbm")
 
 
 def knn_section(dev):
@@ -426,6 +446,9 @@ def main(argv=None):
         sub_kd = step_section(args, "kd", args.kd_batch, dev, world, rank)
     cfg1 = configs1_section(dev) if world == 1 and "configs1" in sections else None
     knn = knn_section(dev) if world == 1 and "knn" in sections else None
+    for c in (3, 64):
+        if world == 1 and f"gather_c{c}" in sections:
+            line[f"gather_c{c}"] = gather_section(dev, c)
 
     if head is not None:
         line = {

@@ -6,9 +6,11 @@ Plain hipcc (no torch headers): each csrc/*.hip is compiled to an object in para
 linked into one shared library.  Objects are keyed by a hash of everything that determines
 them (the source, every header, the flags and the hipcc version), never by file times, so a
 build reuses an object only if it would compile to the same thing.  The library exports
-kdpc_build_id() = the hash of the sources it was built from (source_id() below);
-kdpc_native refuses to load a library whose id does not match the sources next to it, so a
-run can never use a stale binary.
+kdpc_build_id() = "<source hash>+<flags hash>+<tool hash>": the sources it was built from
+(source_id()), the target arch and compile flags (flags_id()) and the hipcc version
+(tool_id()).  kdpc_native refuses to load a library whose source or flags part does not match
+the tree next to it (KDPC_ARCH included), and build() relinks unless all three match, so a run
+can never use a stale binary or one built for another arch / with other flags.
 """
 import concurrent.futures
 import glob
@@ -63,6 +65,27 @@ def source_id(csrc=CSRC, root=ROOT):
 def _hipcc_version():
     r = subprocess.run([HIPCC, "--version"], capture_output=True, text=True)
     return r.stdout
+
+
+def flags_id():
+    """Hash of the target arch and every compile flag (per-source extras included); the tree's
+    own include paths enter relative to it (the GPU box runs a copy at another path)."""
+    h = hashlib.sha256()
+    flags = [f.replace(ROOT, "<root>") for f in CFLAGS]
+    h.update(ARCH.encode() + b"\0" + " ".join(flags).encode())
+    for k in sorted(EXTRA_FLAGS):
+        h.update(b"\0" + k.encode() + b"=" + " ".join(EXTRA_FLAGS[k]).encode())
+    return h.hexdigest()[:16]
+
+
+def tool_id(tool=None):
+    """Hash of the hipcc version text."""
+    return hashlib.sha256((tool if tool is not None else _hipcc_version()).encode()).hexdigest()[:16]
+
+
+def build_id(sid=None, tool=None):
+    """The string a library built now from this tree embeds as kdpc_build_id()."""
+    return f"{sid or source_id()}+{flags_id()}+{tool_id(tool)}"
 
 
 def _compile(src, headers_digest, tool):
@@ -129,21 +152,24 @@ def build_torch_ops(verbose=True):
     return TORCH_OPS_LIB
 
 
-def _lib_current(sid):
-    """The shipped library was linked from exactly these sources (its kdpc_build_id string is
-    embedded in the binary): nothing to compile.  The GPU box receives lib/ with the tree (the
+def _lib_current(bid):
+    """The shipped library was linked from exactly these sources, for this arch, with these
+    flags and this hipcc (its kdpc_build_id string is embedded in the binary): nothing to
+    compile.  The GPU box receives lib/ with the tree (the
     driver runs the GPU tests there without building) but not build/, so without this check a
     build() there would recompile every object only to find the link up to date."""
     try:
         with open(LIB, "rb") as f:
-            return sid.encode() in f.read()
+            return bid.encode() in f.read()
     except OSError:
         return False
 
 
 def build(verbose=True):
     sid = source_id()
-    if _lib_current(sid):
+    tool = _hipcc_version()
+    bid = build_id(sid, tool)
+    if _lib_current(bid):
         if verbose:
             print(f"{LIB} is current (sources {sid[:12]})")
         build_torch_ops(verbose)
@@ -155,14 +181,13 @@ def build(verbose=True):
     for p in source_files()[len(srcs):]:
         with open(p, "rb") as f:
             hd.update(f.read())
-    tool = _hipcc_version()
     with concurrent.futures.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
         objs = list(ex.map(lambda s: _compile(s, hd.hexdigest(), tool), srcs))
     # the build id: a one-function host object naming the sources' hash
     idsrc = os.path.join(OBJ, "kdpc_build_id.cpp")
     with open(idsrc, "w") as f:
         f.write('extern "C" __attribute__((visibility("default"))) const char* '
-                f'kdpc_build_id(void) {{ return "{sid}"; }}\n')
+                f'kdpc_build_id(void) {{ return "{bid}"; }}\n')
     idobj = _compile(idsrc, hd.hexdigest(), tool)
     stamp = LIB + ".inputs"
     link_key = "\n".join(objs + [idobj])

@@ -7,20 +7,102 @@ using namespace kdpc;
 
 namespace {
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
 // ---------------------------------------------------------------------------------------
 // gather_points: out[b,c,m] = points[b,c,idx[b,m]]        (reference sampling_gpu.cu:8-24)
-// One thread per output element, m fastest: coalesced idx reads and stores.
-__global__ __launch_bounds__(256) void gather_points_kernel(int b, int c, int n, int m,
+//
+// LDS-staged (kGatherRowLds: rows of N <= 20480): a workgroup owns ONE channel row of one
+// cloud.  It issues its output indices (int4) first, then stages the whole row in LDS with
+// every thread's kGatherStage float4 loads in flight at once (a row is read from HBM exactly
+// once, as coalesced 16-byte loads: with M/N = 1/4 every cache line of the row holds an
+// index anyway), and writes its M outputs as nontemporal float4 stores from random LDS reads.
+// The random 4-byte global gathers of the direct kernel (one L2 request per output) are gone.
+// Workgroups walk (cloud, channel) with the channel fastest, so the C rows that share one
+// index slice run back to back and re-read it from L2.
+constexpr int kGatherStage = 8;   // float4 loads in flight per thread while staging
+constexpr int kGatherOut = 4;     // int4 index loads (16 outputs) in flight per thread
+constexpr int kGatherRowLds = 80 * 1024;
+
+__global__ __launch_bounds__(256) void gather_points_lds_kernel(int c, int n, int m,
+                                                                const float* __restrict__ points,
+                                                                const int* __restrict__ idx,
+                                                                float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float row[];
+  const long long bc = blockIdx.x;             // b * c + channel
+  const int bi = (int)(bc / c);
+  const int* ib = idx + (long long)bi * m;     // m % 4 == 0 (host-checked)
+  float* ob = out + bc * m;
+  const int t = threadIdx.x;
+  int4 q[kGatherOut];
+#pragma unroll
+  for (int u = 0; u < kGatherOut; ++u) {
+    const int p = (t + u * 256) * 4;
+    q[u] = p < m ? *reinterpret_cast<const int4*>(ib + p) : make_int4(0, 0, 0, 0);
+  }
+  const f32x4* src = reinterpret_cast<const f32x4*>(points + bc * n);  // n % 4 == 0
+  f32x4* dst = reinterpret_cast<f32x4*>(row);
+  const int n4 = n >> 2;
+  for (int base = t; base < n4; base += 256 * kGatherStage) {
+    f32x4 r[kGatherStage];
+#pragma unroll
+    for (int u = 0; u < kGatherStage; ++u) {
+      const int e = base + u * 256;
+      if (e < n4) r[u] = __builtin_nontemporal_load(src + e);
+    }
+#pragma unroll
+    for (int u = 0; u < kGatherStage; ++u) {
+      const int e = base + u * 256;
+      if (e < n4) dst[e] = r[u];
+    }
+  }
+  __syncthreads();
+  for (int p0 = 0; p0 < m; p0 += kGatherOut * 1024) {
+    // every LDS read first (indices of unused slots are 0: row[0] is staged), then the
+    // stores: one wait for the index loads, none between the stores
+    f32x4 v[kGatherOut];
+#pragma unroll
+    for (int u = 0; u < kGatherOut; ++u)
+      v[u] = f32x4{row[q[u].x], row[q[u].y], row[q[u].z], row[q[u].w]};
+#pragma unroll
+    for (int u = 0; u < kGatherOut; ++u) {
+      const int p = p0 + (t + u * 256) * 4;
+      if (p < m) __builtin_nontemporal_store(v[u], reinterpret_cast<f32x4*>(ob + p));
+    }
+    const int pn = p0 + kGatherOut * 1024;
+#pragma unroll
+    for (int u = 0; u < kGatherOut; ++u) {
+      const int p = pn + (t + u * 256) * 4;
+      if (p < m) q[u] = *reinterpret_cast<const int4*>(ib + p);
+    }
+  }
+}
+
+// Direct kernel (rows too long for LDS, or n / m not multiples of 4): a thread owns 4
+// consecutive outputs of kGatherCG channels (one index load serves all of them).
+constexpr int kGatherCG = 4;
+
+__global__ __launch_bounds__(256) void gather_points_kernel(int c, int n, int m,
                                                             const float* __restrict__ points,
                                                             const int* __restrict__ idx,
                                                             float* __restrict__ out) {
-  const long long total = (long long)b * c * m;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int p = (int)(e % m);
-    const long long bc = e / m;
-    const int bi = (int)(bc / c);
-    out[e] = points[bc * n + idx[(long long)bi * m + p]];
+  const int bi = blockIdx.z;
+  const int c0 = blockIdx.y * kGatherCG;
+  const int p4 = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (p4 >= m) return;
+  const int* ib = idx + (long long)bi * m;
+  const float* pb = points + ((long long)bi * c + c0) * n;
+  float* ob = out + ((long long)bi * c + c0) * m;
+  const int cg = min(kGatherCG, c - c0);
+  const int np = min(4, m - p4);
+  int q[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) q[j] = j < np ? ib[p4 + j] : 0;
+  for (int cc = 0; cc < cg; ++cc) {
+    const float* r = pb + (long long)cc * n;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j < np) ob[(long long)cc * m + p4 + j] = r[q[j]];
   }
 }
 
@@ -72,7 +154,6 @@ __global__ __launch_bounds__(256) void group_points_kernel(int c, int n, int p_t
 // reading the same index slice run on one XCD (`xcd_units`), keeping those re-reads in its L2.
 constexpr int kRowLdsBytes = 80 * 1024;
 constexpr int kGU = 4;
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <int CG>
 __global__ __launch_bounds__(256) void group_points_lds_kernel(int c, int n, int p_total,
@@ -364,8 +445,20 @@ KDPC_API int kdpc_gather_points(int b, int c, int n, int npoints, const float* p
   const long long total = (long long)b * c * npoints;
   if (total == 0) return (int)hipSuccess;
   KDPC_CHECK_ARG(points && idx && out);
-  hipLaunchKernelGGL(gather_points_kernel, dim3(grid_for(total, 256)), dim3(256), 0,
-                     (hipStream_t)stream, b, c, n, npoints, points, idx, out);
+  hipStream_t st = (hipStream_t)stream;
+  if ((n & 3) == 0 && (npoints & 3) == 0 && (size_t)n * sizeof(float) <= (size_t)kGatherRowLds &&
+      (long long)b * c < (1ll << 31)) {
+    static const hipError_t attr = hipFuncSetAttribute(
+        (const void*)gather_points_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+        kGatherRowLds);
+    if (attr != hipSuccess) return (int)attr;
+    hipLaunchKernelGGL(gather_points_lds_kernel, dim3((unsigned)(b * c)), dim3(256),
+                       (size_t)n * sizeof(float), st, c, n, npoints, points, idx, out);
+    KDPC_RETURN_LAUNCH();
+  }
+  KDPC_CHECK_ARG(b <= 65535 && divup(c, kGatherCG) <= 65535);
+  hipLaunchKernelGGL(gather_points_kernel, dim3(divup(divup(npoints, 4), 256), divup(c, kGatherCG), b),
+                     dim3(256), 0, st, c, n, npoints, points, idx, out);
   KDPC_RETURN_LAUNCH();
 }
 

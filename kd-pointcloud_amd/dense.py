@@ -117,14 +117,14 @@ class _Linear(Function):
             torch.addmm(bias, x2, weight.t(), out=y2)
         else:
             torch.mm(x2, weight.t(), out=y2)
-        ctx.save_for_backward(x2, weight)
+        ctx.save_for_backward(x2, weight, bias)
         ctx.has_bias = bias is not None
         ctx.xshape = x.shape
         return y
 
     @staticmethod
     def backward(ctx, g):
-        x2, weight = ctx.saved_tensors
+        x2, weight, bias = ctx.saved_tensors
         g2 = g.reshape(-1, g.shape[-1])
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
@@ -140,7 +140,8 @@ class _Linear(Function):
             # rest of the backward
             g2c = g2.contiguous()
             gw, gb = wgrad.run(lambda: (splitk_tn(g2c, x2) if need_w else None,
-                                        _colsum(g2c) if need_b else None), [g2c, x2])
+                                        _colsum(g2c) if need_b else None), [g2c, x2],
+                                (weight, bias))
         return gx, gw, gb
 
 

@@ -30,16 +30,19 @@ def is_dist():
 
 
 def wrap_ddp(model, device=None):
-    """Wrap the trained model for DDP when a process group is up (no-op otherwise)."""
+    """Wrap the trained model for DDP when a process group is up (no-op otherwise).
+
+    DDP's reducer reads each gradient from its own hook during the backward, so while a DDP
+    wrapper made here is alive the parameter gradients are issued in line (wgrad.py:
+    wgrad.suspend(), released when the wrapper is garbage-collected)."""
     if not is_dist() or dist.get_world_size() == 1:
         return model
-    # DDP's reducer reads each gradient from its own hook during the backward: issue the
-    # parameter gradients in line (wgrad.py)
-    wgrad.enabled = False
     kw = dict(broadcast_buffers=True, static_graph=True, gradient_as_bucket_view=True)
     if device is not None and device.type == "cuda":
         kw["device_ids"] = [device.index]
-    return torch.nn.parallel.DistributedDataParallel(model, **kw)
+    ddp = torch.nn.parallel.DistributedDataParallel(model, **kw)
+    wgrad.suspend(ddp)
+    return ddp
 
 
 def make_optimizer(model, lr=1e-3, weight_decay=1e-4, capturable=False):
@@ -97,15 +100,33 @@ class _TeacherFork:
 KD_COORD_FORK = os.environ.get("KDPC_KD_COORD_FORK", "0") == "1"
 
 
-def _kd_student_streams(student):
-    """The KD step already runs the teacher's forward on a stream of its own, beside the
-    student's; there the student's decoder coordinate fork (models_bid_pointconv._CoordFork)
-    measured slower, with its own stream (13.17-13.66 vs 14.27-14.30 ms/step at configs[3]'s
-    slice, profiles/round03/ab/bab_fkkd_*) and on the parameter-gradient stream alike
-    (13.56-13.66 vs 14.30-14.32, bab_fskd_*), so the student searches in line there."""
-    core = _core(student)
-    if hasattr(core, "coord_fork") and TEACHER_STREAM and not KD_COORD_FORK:
-        core.coord_fork = False
+class _kd_student_streams:
+    """Context for the KD student's forward.  The KD step already runs the teacher's forward
+    on a stream of its own, beside the student's; there the student's decoder coordinate fork
+    (models_bid_pointconv._CoordFork) measured slower, with its own stream (13.17-13.66 vs
+    14.27-14.30 ms/step at configs[3]'s slice, profiles/round03/ab/bab_fkkd_*) and on the
+    parameter-gradient stream alike (13.56-13.66 vs 14.30-14.32, bab_fskd_*), so the student
+    searches in line inside the KD step (KDPC_KD_COORD_FORK=1 keeps the fork).  Scoped to
+    the step's own forward: the same module trained by a FlowTrainStep keeps its fork."""
+
+    def __init__(self, student):
+        core = _core(student)
+        self.core = core if (hasattr(core, "coord_fork") and TEACHER_STREAM
+                             and not KD_COORD_FORK) else None
+
+    def __enter__(self):
+        if self.core is not None:
+            self.prev = self.core.__dict__.get("coord_fork")
+            self.core.coord_fork = False
+        return self
+
+    def __exit__(self, *exc):
+        if self.core is not None:
+            if self.prev is None:
+                del self.core.coord_fork  # back to the class default
+            else:
+                self.core.coord_fork = self.prev
+        return False
 
 
 def _plan_fn(model):
@@ -207,7 +228,6 @@ class KDTrainStep:
         self.prefetch = FpsPrefetch()
         for p in self.teacher.parameters():
             p.requires_grad_(False)
-        _kd_student_streams(student)
 
     def __call__(self, pos1, pos2, flow, color1=None, color2=None, next_batch=None):
         color1 = pos1 if color1 is None else color1
@@ -221,8 +241,9 @@ class KDTrainStep:
         self.teacher.eval()
         t_fork = _TeacherFork(self.teacher, (pos1, pos2, color1, color2), kw)
         self.student.train()
-        flows, fps1, fps2, _, _, feat1s, feat2s, _ = self.student(pos1, pos2, color1, color2,
-                                                                  **kw)
+        with _kd_student_streams(self.student):
+            flows, fps1, fps2, _, _, feat1s, feat2s, _ = self.student(pos1, pos2, color1,
+                                                                      color2, **kw)
         t_flows, t_fps1, t_fps2, _, _, t_feat1s, t_feat2s, _ = t_fork.join()
         loss = self.loss_fn(
             flows, feat1s, feat2s, fps1, fps2, flow, t_flows, t_feat1s, t_feat2s, t_fps1, t_fps2,
@@ -239,6 +260,35 @@ def epe3d(model, pos1, pos2, flow):
     model.eval()
     flows = model(pos1, pos2, pos1, pos2)[0]
     return torch.norm(flows[0].permute(0, 2, 1) - flow, dim=2).mean()
+
+
+def _capturing(stream):
+    with torch.cuda.stream(stream):
+        return torch.cuda.is_current_stream_capturing()
+
+
+def _join_capture_streams(cap, extra=()):
+    """Make the capture stream wait for every side stream this process forks from a capture
+    (the plan fork, the all-reduce stream, the parameter-gradient stream, the teacher's
+    stream, the decoder coordinate forks) that is still part of the capture.  Every code path
+    joins its streams already; this is the guarantee: on this HIP runtime a capture that ends
+    with unjoined work on a forked stream does not fail cleanly -- hipStreamEndCapture
+    returns hipErrorStreamCaptureUnjoined but still writes a graph handle, and torch's
+    capture_end then crashed in the round-3 KD capture (DESIGN §5,
+    tools/hip_capture_repro.hip `unjoined`, tools/torch_unjoined_capture.py).  Waiting on a
+    stream whose work is already joined adds no work."""
+    import models_bid_pointconv
+    dev = cap.device
+    streams = [s for s in extra if s is not None]
+    streams += [wgrad._side.get(dev.index), _teacher_streams.get(dev.index)]
+    streams += [s for (d, _), s in models_bid_pointconv._coord_streams.items() if d == dev.index]
+    seen = set()
+    for s in streams:
+        if s is None or s.cuda_stream in seen or s.cuda_stream == cap.cuda_stream:
+            continue
+        seen.add(s.cuda_stream)
+        if _capturing(s):
+            cap.wait_stream(s)
 
 
 class GraphedStep:
@@ -361,6 +411,7 @@ class GraphedStep:
                 self._tail(fork)
             else:  # serial: pack only; the all-reduce runs between graph A and graph B
                 self._pack()
+            _join_capture_streams(cap, (fork, self.comm))
         for h in hooks:
             h.remove()
         if self.schedule == "overlap" and any(not b["done"] for b in self.buckets):
@@ -482,7 +533,8 @@ class GraphedStep:
             b["left"] -= 1
             if b["left"] == 0:
                 idx = b["idx"]
-                wgrad.join()  # parameter gradients still in flight on their own stream
+                # only this bucket's parameter gradients still in flight on their own stream
+                wgrad.wait_for([self._used[i] for i in idx])
                 torch._foreach_copy_([self._gviews[i] for i in idx],
                                      [self._used[i].grad for i in idx])
                 self.comm.wait_stream(torch.cuda.current_stream())
@@ -587,12 +639,12 @@ def graphed_kd_step(teacher, student, optimizer, example_inputs, gamma=0.3, beta
         p.requires_grad_(False)
     teacher.eval()
     student.train()
-    _kd_student_streams(student)
 
     def run(pos1, pos2, flow, fps=None):
         kw = {} if fps is None else {"fps_idx": fps}
         t_fork = _TeacherFork(teacher, (pos1, pos2, pos1, pos2), kw)
-        flows, fps1, fps2, _, _, feat1s, feat2s, _ = student(pos1, pos2, pos1, pos2, **kw)
+        with _kd_student_streams(student):
+            flows, fps1, fps2, _, _, feat1s, feat2s, _ = student(pos1, pos2, pos1, pos2, **kw)
         t_flows, t_fps1, t_fps2, _, _, t_feat1s, t_feat2s, _ = t_fork.join()
         return loss_functions.biDirection_loss_ht(
             flows, feat1s, feat2s, fps1, fps2, flow, t_flows, t_feat1s, t_feat2s, t_fps1, t_fps2,

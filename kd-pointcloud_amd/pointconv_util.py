@@ -325,12 +325,12 @@ class _WeightNetFn(torch.autograd.Function):
         xyz, center, idx, *params = ctx.saved_tensors
         need_rel = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
         dwt = dwt.contiguous()
-        if wgrad.enabled and xyz.is_cuda:
+        if wgrad.active() and xyz.is_cuda:
             # drel (what the upstream layers wait for) here, the 248-parameter reduction on
             # the parameter-gradient stream (same kernels' arithmetic: bit-identical)
             drel = _nat.weightnet_bwd_rel(xyz, center, idx, params, dwt) if need_rel else None
             dflat = wgrad.run(lambda: _nat.weightnet_bwd(xyz, center, idx, params, dwt)[1],
-                              [xyz, center, idx, dwt, *params])
+                              [xyz, center, idx, dwt, *params], params)
         else:
             drel, dflat = _nat.weightnet_bwd(xyz, center, idx, params, dwt, need_rel)
         dparams = [g.view_as(p) for g, p in
@@ -372,12 +372,12 @@ class _PointConvLayer(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, xyz, center, feats, idx, wt, wl, bias):
-        ctx.save_for_backward(xyz, center, feats, idx, wt, wl)
+        ctx.save_for_backward(xyz, center, feats, idx, wt, wl, bias)
         return _nat.pointconv_fwd(xyz, center, feats, idx, wt, wl, bias)
 
     @staticmethod
     def backward(ctx, gy):
-        xyz, center, feats, idx, wt, wl = ctx.saved_tensors
+        xyz, center, feats, idx, wt, wl, bias = ctx.saved_tensors
         gy = gy.contiguous()
         csr = _nat.csr_rank_of(idx, xyz.shape[1])
         need_b = ctx.needs_input_grad[6]
@@ -393,7 +393,7 @@ class _PointConvLayer(torch.autograd.Function):
             dwl, dbias = wgrad.run(lambda: (
                 _nat.pointconv_bwd_weight(xyz, center, feats, idx, wt, gy, wl.shape[0]),
                 _nat.colsum(gy.view(-1, gy.shape[-1])) if need_b else None),
-                [xyz, center, feats, idx, wt, gy])
+                [xyz, center, feats, idx, wt, gy], (wl, bias))
         return (dxyz, dcenter if ctx.needs_input_grad[1] else None, dfeats, None, dwt, dwl, dbias)
 
 
@@ -548,24 +548,28 @@ class _CostVolumeWide(torch.autograd.Function):
         out, amax = _nat.cost_volume_wide_max(z1, B, N1, K, w1.shape[0])
         if amax_override is not None:
             amax = amax_override(amax)
-        ctx.save_for_backward(x1, x2, idx, wpos, w1, h0, out, amax)
+        ctx.save_for_backward(x1, x2, idx, wpos, w1, h0, out, amax, bpos, b1)
         return out
 
     @staticmethod
     def backward(ctx, gout):
-        x1, x2, idx, wpos, w1, h0, out, amax = ctx.saved_tensors
+        x1, x2, idx, wpos, w1, h0, out, amax, bpos, b1 = ctx.saved_tensors
         B, N1, K = idx.shape
         N2, din = x2.shape[1], h0.shape[-1]
         dz1, gsc = _nat.cost_volume_wide_max_bwd(gout.contiguous(), out, amax, K)
         h0f = h0.view(-1, din)
         # parameter gradients on the parameter-gradient stream (wgrad.py); split-K because
         # one 262144-deep GEMM ran ~10x below the MFMA rate
-        dw1, db1 = wgrad.run(lambda: (splitk_tn(dz1, h0f), _nat.colsum(gsc)), [dz1, h0f, gsc])
+        dw1, db1 = wgrad.run(lambda: (splitk_tn(dz1, h0f), _nat.colsum(gsc)), [dz1, h0f, gsc],
+                             (w1, b1))
         dz = torch.mm(dz1, w1)  # dh0; becomes dz0 in place
         del dz1
         dp1, slab = _nat.cost_volume_wide_h0_bwd(x1, x2, idx, h0, dz, reduce=False)
-        dwpos, dbpos = wgrad.run(lambda: (_nat.colsum(slab).view(din, 3),
-                                          _nat.colsum(dp1.view(-1, din))), [slab, dp1])
+        # dbpos reads dp1 here, on this stream: dp1 goes back to autograd as p1's gradient,
+        # and p1 has a second consumer, so autograd may accumulate into it in place on this
+        # stream (a side-stream read of it would race that)
+        dbpos = _nat.colsum(dp1.view(-1, din))
+        dwpos = wgrad.run(lambda: _nat.colsum(slab).view(din, 3), [slab], (wpos,))
         csr = _nat.csr_of(idx, N2)
         dp2 = _nat.group_rows_grad(dz.view(B, N1 * K, din), csr, B, N2, din)
         ddir = torch.mm(dz, wpos)  # (rows, 3)
@@ -586,6 +590,21 @@ def set_amax_override(fn):
     None restores the computed routing.  Returns the previous override."""
     global _amax_override
     prev, _amax_override = _amax_override, fn
+    return prev
+
+
+_cv_override = None
+
+
+def set_cv_override(fn):
+    """Test seam: `fn(x1, x2, idx, p1, p2, wpos, bpos, w1, b1) -> out | None` is offered
+    every fused cost-volume call made with gradients enabled, before the kernel runs; a
+    tensor it returns replaces the call's result (None: the kernels run).  The gradient
+    parity test uses it to replay the float64 reference's LeakyReLU decisions for a call
+    whose pre-activations include a near-tie this build's fp32 evaluation cannot place on
+    the reference's side (tests/test_gpu_model.py::_CvReplay).  Returns the previous one."""
+    global _cv_override
+    prev, _cv_override = _cv_override, fn
     return prev
 
 
@@ -628,9 +647,14 @@ def _cost_volume_cl(nsample, x1, x2, p1, p2, pos, mlp, act, knn_idx=None):
     if fn:
         conv = mlp[0].composed_module[0]
         ovr = _amax_override if torch.is_grad_enabled() else None
-        return fn.apply(x1, x2, _as_idx32(knn_idx).contiguous(), p1.contiguous(), p2.contiguous(),
-                        pos.weight.view(din, 3), pos.bias,
-                        conv.weight.view(conv.out_channels, din), conv.bias, ovr)
+        args = (x1, x2, _as_idx32(knn_idx).contiguous(), p1.contiguous(), p2.contiguous(),
+                pos.weight.view(din, 3), pos.bias, conv.weight.view(conv.out_channels, din),
+                conv.bias)
+        if _cv_override is not None and torch.is_grad_enabled():
+            out = _cv_override(*args)
+            if out is not None:
+                return out
+        return fn.apply(*args, ovr)
     direction = index_points_group(x2, knn_idx) - x1.view(B, N1, 1, C)
     grouped_points2 = index_points_group(p2, knn_idx)
     h = act((grouped_points2 + p1.unsqueeze(2)) + _linear_1x1(pos, direction))

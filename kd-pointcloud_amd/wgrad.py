@@ -17,11 +17,23 @@ Ordering (eager and inside a captured HIP graph alike):
     backward() returns -- the optimizer step, a gradient pack or a host read that follows
     needs nothing more;
   * code that reads a parameter gradient DURING the backward (a post-accumulate-grad hook,
-    e.g. GraphedStep's bucket all-reduces) calls join() first.
-`enabled = False` issues everything in line (DDP's reducer reads gradients from its own
-hooks during the backward and is not taught to join).
+    e.g. GraphedStep's bucket all-reduces) calls wait_for(params) first: the current stream
+    waits for the side-stream event recorded after the launch that produced those
+    parameters' gradients (not for everything queued on the side stream so far), or join()
+    for all of it;
+  * autograd's AccumulateGrad runs on the backward's stream right after the layer's backward
+    returns.  With `.grad` None it only takes the new tensor (no kernel reads it), but onto
+    an existing `.grad` (accumulation over micro-batches, zero_grad(set_to_none=False)) it
+    adds on that stream, reading the side stream's result: run() is told which parameters
+    its results are the gradients of, and when any of them already holds a `.grad` the
+    backward's stream waits for the side stream at once (the in-line ordering, for that
+    layer only).
+`enabled = False` issues everything in line; so does any live suspend(owner) (distill.wrap_ddp:
+DDP's reducer reads gradients from its own hooks during the backward and is not taught to
+join) until its owner is garbage-collected.
 """
 import os
+import weakref
 
 import torch
 
@@ -29,6 +41,20 @@ import torch
 enabled = os.environ.get("KDPC_WGRAD_STREAM", "1") != "0"
 _side = {}      # device index -> side stream
 _pending = {}   # (main, side) raw stream handles -> (main, side) joins queued in this backward
+_suspended = weakref.WeakSet()  # objects (DDP wrappers) for whose lifetime run() is in line
+# id(leaf parameter) -> (weak reference to it, side-stream event recorded after the launch
+# that produced its gradient).  The events stay referenced until overwritten (a HIP event destroyed while a
+# graph capture is under way must not be one the capture still tracks).
+_ready = {}
+
+
+def suspend(owner):
+    """Issue parameter gradients in line while `owner` is alive."""
+    _suspended.add(owner)
+
+
+def active():
+    return enabled and len(_suspended) == 0
 
 
 def side_stream(device):
@@ -38,11 +64,12 @@ def side_stream(device):
     return s
 
 
-def run(fn, inputs):
-    """fn() launches parameter-gradient kernels reading `inputs` and returns their results;
-    run it on the side stream.  Call from inside a torch.autograd.Function.backward."""
+def run(fn, inputs, params=()):
+    """fn() launches parameter-gradient kernels reading `inputs` and returns their results,
+    the gradients of `params`; run it on the side stream.  Call from inside a
+    torch.autograd.Function.backward."""
     dev = inputs[0].device
-    if not enabled or dev.type != "cuda":
+    if not active() or dev.type != "cuda":
         return fn()
     main = torch.cuda.current_stream(dev)
     side = side_stream(dev)
@@ -52,6 +79,17 @@ def run(fn, inputs):
     for t in inputs:
         if t is not None:
             t.record_stream(side)
+    if params:
+        ev = torch.cuda.Event()
+        ev.record(side)
+        for p in params:
+            if p is not None:
+                p = _leaf(p)
+                _ready[id(p)] = (weakref.ref(p), ev)
+    if any(_has_grad(p) for p in params):
+        # AccumulateGrad will add onto an existing .grad on `main`: order it after `fn`
+        main.wait_stream(side)
+        return out
     # one join per backward pass: every call queues the (idempotent) callback, the first of
     # them to run at the end of the pass makes `main` wait (a pass that raised and never ran
     # its callbacks leaves nothing stale behind: the next pass queues its own)
@@ -59,6 +97,34 @@ def run(fn, inputs):
     _pending[key] = (main, side)
     torch.autograd.Variable._execution_engine.queue_callback(lambda k=key: _join_pending(k))
     return out
+
+
+def _leaf(p):
+    """The parameter behind `p` (the fused layers receive views of their parameters)."""
+    while not p.is_leaf and p._base is not None:
+        p = p._base
+    return p
+
+
+def _has_grad(p):
+    """`p` (a parameter, or a view of one) already holds a .grad."""
+    if p is None:
+        return False
+    p = _leaf(p)
+    return p.is_leaf and p.grad is not None
+
+
+def wait_for(params, stream=None):
+    """`stream` (default: the current one) waits for the side-stream launches that produced
+    the gradients of `params` -- only those, not the rest of the side stream's queue.
+    Parameters whose gradient was produced in line need nothing."""
+    seen = set()
+    for p in params:
+        hit = _ready.get(id(p))
+        if hit is None or hit[0]() is not p or id(hit[1]) in seen:
+            continue
+        seen.add(id(hit[1]))
+        (stream or torch.cuda.current_stream(p.device)).wait_event(hit[1])
 
 
 def _join_pending(key):

@@ -21,6 +21,7 @@ import numpy as np
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+TIE_REL = 1e-4  # |pre-activation| below TIE_REL x the call's scale counts as a near-tie
 sys.path.insert(0, HERE)
 import make_fixtures as MF  # noqa: E402
 from gradproj import projection  # noqa: E402
@@ -62,25 +63,51 @@ def main(n=2048, full_grads=None, dtype=torch.float64):
     # call order, so the GPU test can replay it (a float64 near-tie may route differently
     # from any fp32 evaluation)
     amax = []
+    # LeakyReLU near-ties of the same calls: the first activation's pre-activation z0
+    # (B, D, K, N1) and the maximum over K of the second activation (B, D, N1), wherever the
+    # float64 value lies within TIE_REL of the call's scale of 0 -- the GPU test replays the
+    # float64 side there when its own evaluation is not clearly on that side (the derivative
+    # jumps from 0.1 to 1 at 0, a discrete choice like the max routing)
+    z0ties, z1ties = [], []
     import torch.nn.functional as TF
     pool = TF.max_pool2d
+
+    def ties(v, tau):
+        """(flat positions, signs, values) of |v| < tau, v of shape (1, D, *rest)."""
+        v = v.detach()[0]
+        hit = (v.abs() < tau).nonzero()
+        vals = v[tuple(hit.t())] if len(hit) else v.new_zeros(0)
+        return hit.numpy().astype(np.int32), np.sign(vals.numpy()).astype(np.int8), vals.numpy()
 
     def recording_pool(x, kernel_size, *a, **k):
         out, ind = pool(x, kernel_size, *a, return_indices=True, **k)
         n = x.shape[3]
         amax.append((ind[:, :, 0, :] // n).permute(0, 2, 1).to(torch.uint8).numpy())
+        scale = float(x.detach().std())
+        z1ties.append(ties(out[:, :, 0, :], TIE_REL * scale) + (scale,))  # (d, n)
         return out
+
+    def z0_hook(mod, inputs):
+        z0 = inputs[0]
+        scale = float(z0.detach().std())
+        z0ties.append(ties(z0, TIE_REL * scale) + (scale,))  # positions (d, k, n)
     try:
         pos1, pos2, flow = (torch.from_numpy(g[k]).to(dtype) for k in ("pos1", "pos2", "flow"))
         teacher = MF._synth(R.teacher.PointConvBidirection(), seed=1).to(dtype).eval()
         student = MF._synth(R.student.PointConvBidirection(), seed=2).to(dtype).train()
         with torch.no_grad():
             t_out = teacher(pos1, pos2, pos1, pos2)
+        CL = sys.modules["pointconv_util2"].CrossLayerLight
+        hooks = [m.relu.register_forward_pre_hook(z0_hook) for m in student.modules()
+                 if isinstance(m, CL)]
         TF.max_pool2d = recording_pool
         try:
             s_out = student(pos1, pos2, pos1, pos2)
         finally:
             TF.max_pool2d = pool
+            for h in hooks:
+                h.remove()
+        assert len(z0ties) == len(amax) == len(z1ties), (len(z0ties), len(amax))
         flows, f1i, f2i, _, _, feat1s, feat2s, _ = s_out
         kd = R.loss.biDirection_loss_ht(flows, feat1s, feat2s, f1i, f2i, flow, t_out[0],
                                         t_out[5], t_out[6], t_out[1], t_out[2], 0.3, 0.8, layer=3)
@@ -108,6 +135,16 @@ def main(n=2048, full_grads=None, dtype=torch.float64):
     out["n_amax"] = np.array(len(amax))
     for j, a in enumerate(amax):
         out[f"amax{j}"] = a
+    # near-ties, per call: z0 positions as (n, k, d) and z1-max positions as (n, d) in the
+    # build's point-major layout, the float64 sign and value, and the call's scale
+    out["tie_rel"] = np.array(TIE_REL)
+    for j, ((p0, s0, v0, c0), (p1, s1, v1, c1)) in enumerate(zip(z0ties, z1ties)):
+        out[f"z0tie{j}_nkd"] = p0[:, ::-1].copy()
+        out[f"z0tie{j}_sign"], out[f"z0tie{j}_val"], out[f"z0tie{j}_scale"] = s0, v0, np.array(c0)
+        out[f"z1tie{j}_nd"] = p1[:, ::-1].copy()
+        out[f"z1tie{j}_sign"], out[f"z1tie{j}_val"], out[f"z1tie{j}_scale"] = s1, v1, np.array(c1)
+    print("LeakyReLU near-ties per call (z0, z1 max):",
+          [(len(a[0]), len(b[0])) for a, b in zip(z0ties, z1ties)])
     if full_grads:  # every gradient element (diagnostics: tools/grad_gap.py), not committed
         np.savez_compressed(full_grads, **{k: p.grad.numpy() for k, p in student.named_parameters()
                                            if p.grad is not None})

@@ -15,11 +15,21 @@ def _batch(b, n, seed):
     return tuple(torch.from_numpy(a).to(DEV) for a in synthetic.ft3d_batch(b, n, seed=seed))
 
 
-@pytest.mark.parametrize("mode", ["train", "kd"])
-def test_graphed_step_equals_eager(mode):
+@pytest.mark.parametrize("mode", ["train", "kd", "kd_fork", "kd_fork_own"])
+def test_graphed_step_equals_eager(mode, monkeypatch):
+    """kd_fork: the KD student keeps its decoder coordinate fork (models_bid_pointconv.
+    _CoordFork) on the parameter-gradient stream beside the teacher's stream; kd_fork_own:
+    on a stream of its own (five streams in the captured graph: capture, plan fork, teacher,
+    coordinate fork, parameter gradients) -- the round-3 capture_end segfault case."""
+    import distill
+    import models_bid_pointconv
     from distill import (FlowTrainStep, KDTrainStep, graphed_flow_step, graphed_kd_step,
                          make_optimizer)
     from models_bid_pointconv import PointConvBidirection
+    if mode.startswith("kd_fork"):
+        monkeypatch.setattr(distill, "KD_COORD_FORK", True)
+        monkeypatch.setattr(models_bid_pointconv, "SHARED_SIDE_STREAM", mode == "kd_fork")
+        mode = "kd"
     torch.manual_seed(0)
     base = PointConvBidirection().to(DEV)
     teacher = PointConvBidirection().to(DEV) if mode == "kd" else None
@@ -132,3 +142,67 @@ def test_parameter_gradient_stream_is_bit_identical():
     assert g0.keys() == g1.keys()
     for n in g0:
         assert torch.equal(g0[n], g1[n]), n
+
+
+def test_parameter_gradient_stream_accumulates_onto_existing_grads():
+    """Two backward() calls without zero_grad (gradient accumulation): the second pass's
+    AccumulateGrad adds onto the first pass's .grad on the backward's stream, so wgrad.run
+    must order those layers' side-stream kernels before it.  Bit-identical to
+    issuing the parameter gradients in line."""
+    import wgrad
+    from models_bid_pointconv import PointConvBidirection
+    import loss_functions as L
+    torch.manual_seed(0)
+    base = PointConvBidirection().to(DEV)
+    batches = [_batch(2, 4096, s) for s in (21, 22)]
+    runs = []
+    prev = wgrad.enabled
+    try:
+        for on in (False, True):
+            wgrad.enabled = on
+            m = copy.deepcopy(base).train()
+            for b in batches:  # no zero_grad in between
+                out = m(*b[:2], *b[:2])
+                L.multiScaleLoss(out[0], b[2], out[1]).backward()
+            runs.append({n: p.grad.clone() for n, p in m.named_parameters()
+                         if p.grad is not None})
+    finally:
+        wgrad.enabled = prev
+    g0, g1 = runs
+    assert g0.keys() == g1.keys()
+    for n in g0:
+        assert torch.equal(g0[n], g1[n]), n
+
+
+def test_capture_joins_forked_side_streams():
+    """distill._join_capture_streams: work left unjoined on one of the process's side streams
+    (here the KD teacher's stream) at the end of a captured step is joined into the capture
+    stream before capture_end -- an unjoined capture crashes this runtime's capture_end
+    instead of raising (tools/hip_capture_repro.hip `unjoined`) -- and the graph replays it."""
+    import distill
+    from distill import GraphedStep, make_optimizer
+    from models_bid_pointconv import PointConvBidirection
+    import loss_functions as L
+    torch.manual_seed(0)
+    model = PointConvBidirection().to(DEV).train()
+    opt = make_optimizer(model, capturable=True)
+    b = _batch(1, 1024, 31)
+    dev = torch.device(DEV, torch.cuda.current_device())
+    side = distill._teacher_streams.get(dev.index)
+    if side is None:
+        side = distill._teacher_streams[dev.index] = torch.cuda.Stream(device=dev)
+    marks = torch.zeros(4, device=DEV)
+
+    def run(pos1, pos2, flow):
+        out = model(pos1, pos2, pos1, pos2)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            marks.add_(1.0)  # never joined by this function
+        return L.multiScaleLoss(out[0], flow, out[1])
+    step = GraphedStep(run, model.parameters(), opt, b, warmup=1)
+    torch.cuda.synchronize()
+    before = float(marks[0])
+    for _ in range(3):
+        step(*b)
+    torch.cuda.synchronize()
+    assert float(marks[0]) == before + 3.0

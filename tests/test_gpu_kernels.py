@@ -55,16 +55,23 @@ def test_fps_duplicates_and_exhaustion(nat):
                                   O.furthest_point_sample(same, 16)[0])
 
 
-def test_gather_points(nat):
-    rng = np.random.default_rng(0)
-    pts = rng.normal(size=(3, 19, 1000)).astype(np.float32)
-    idx = rng.integers(0, 1000, (3, 333)).astype(np.int32)
+# (b, c, n, m): the LDS-staged kernel (n, m multiples of 4, a row <= 80 KiB: configs[1] at
+# C=64 and C=3, the largest row, m > 4096 outputs per row = two output rounds, tiny rows) and
+# the direct kernel (m or n not a multiple of 4, rows longer than 20480)
+@pytest.mark.parametrize("b,c,n,m", [(3, 19, 1000, 333), (8, 64, 8192, 2048), (8, 3, 8192, 2048),
+                                     (2, 5, 20480, 4096), (1, 6, 16384, 8192), (2, 4, 100, 12),
+                                     (1, 7, 20484, 64), (2, 3, 1001, 40)])
+def test_gather_points(nat, b, c, n, m):
+    rng = np.random.default_rng(n + m)
+    pts = rng.normal(size=(b, c, n)).astype(np.float32)
+    idx = rng.integers(0, n, (b, m)).astype(np.int32)
+    idx[:, 0], idx[:, -1] = 0, n - 1  # both ends of the row
     out = nat.gather_points(_t(pts), _t(idx)).cpu().numpy()
     np.testing.assert_array_equal(out, O.gather_points(pts, idx))
-    g = rng.normal(size=(3, 19, 333)).astype(np.float32)
-    csr = nat.csr_of(_t(idx), 1000)
-    grad = nat.csr_sum_channels(_t(g), csr, 3, 19, 1000).cpu().numpy()
-    np.testing.assert_array_equal(grad, O.gather_points_grad(g, idx, 1000))
+    g = rng.normal(size=(b, c, m)).astype(np.float32)
+    csr = nat.csr_of(_t(idx), n)
+    grad = nat.csr_sum_channels(_t(g), csr, b, c, n).cpu().numpy()
+    np.testing.assert_array_equal(grad, O.gather_points_grad(g, idx, n))
 
 
 @pytest.mark.parametrize("c,n,s,k", [(64, 8192, 2048, 16), (7, 513, 37, 9), (3, 100, 5, 3),

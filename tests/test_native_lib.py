@@ -84,11 +84,29 @@ def test_ctypes_signatures_match_header():
 
 
 def test_library_built_from_these_sources():
-    """kdpc_build_id() is the hash of the sources next to the library: the loader refuses a
-    stale binary (a changed kernel source without a rebuild)."""
+    """kdpc_build_id() is the hash of the sources next to the library, of the arch + flags and
+    of the hipcc version: the loader refuses a stale binary (a changed kernel source without
+    a rebuild) and one built for another arch or with other flags."""
     import build_native
     lib = kdpc_native.load_library()
-    assert lib.kdpc_build_id().decode() == build_native.source_id()
+    assert lib.kdpc_build_id().decode() == build_native.build_id()
+    assert build_native._lib_current(build_native.build_id())
+
+
+def test_other_arch_or_flags_change_the_build_id(monkeypatch):
+    """Rebuilding for another arch (KDPC_ARCH) or with other flags must not reuse the shipped
+    library (the id used to cover the sources only)."""
+    import build_native
+    base = build_native.build_id(tool="hipcc x")
+    monkeypatch.setattr(build_native, "ARCH", "gfx942")
+    assert build_native.build_id(tool="hipcc x") != base
+    assert not build_native._lib_current(build_native.build_id())
+    monkeypatch.undo()
+    monkeypatch.setattr(build_native, "EXTRA_FLAGS", {"fps.hip": ["-O1"]})
+    assert build_native.build_id(tool="hipcc x") != base
+    monkeypatch.undo()
+    assert build_native.build_id(tool="hipcc y") != base
+    assert build_native.build_id(tool="hipcc x") == base
 
 
 def test_stale_library_is_refused(tmp_path):
