@@ -131,6 +131,13 @@ int kdpc_knn_point_ws(int b, int n, int s, int k, const float *xyz, const float 
                       int *idx, float *dist, void *workspace, size_t workspace_bytes,
                       void *stream);
 
+/* kdpc_knn_point_ws on the culled path (needs kdpc_knn_workspace_bytes(b, n, s) > 0) that
+ * also adds the number of query-ref distance evaluations it issues to *evals (device u64):
+ * the roofline's work count (bench.py configs[4]).  Same idx as kdpc_knn_point_ws. */
+int kdpc_knn_point_evals(int b, int n, int s, int k, const float *xyz, const float *new_xyz,
+                         int *idx, void *workspace, size_t workspace_bytes,
+                         unsigned long long *evals, void *stream);
+
 /* kNN in feature space (CrossLayerLightFG's knn_point over (B,N,D) features,
  * pointconv_util.py:1871-1957 with square_distance + topk :73-107): ref (B,N,D),
  * query (B,S,D) -> idx (B,S,K) int32 ascending by (dist, index), dist (B,S,K) if non-null,

@@ -514,16 +514,27 @@ __device__ __noinline__ void shrink_buffer(float2* buf, int& cnt, float& thr, in
   if (tk < ord_key(INFINITY)) thr = fminf(thr, from_ord_key(tk + 1u));
 }
 
-template <int QW>
+// STATS: also count the distance evaluations the wave issues (visited 64-ref chunks x 64
+// lanes x QW queries, plus the kWin-ref seed window per query) into *evals -- the work the
+// culled scan really performs, for the roofline (kdpc_knn_point_evals; never on the
+// product path).
+//
+// (Measured and rejected, round 4: an XCD-aware block order giving each XCD one contiguous
+// run of cell-sorted query blocks -- configs[4] 1270 -> 1527 us: contiguous regions carry
+// unequal work (point density varies), while the default round-robin deal gives every XCD a
+// uniform sample of the cloud.)
+template <int QW, bool STATS>
 __global__ __launch_bounds__(256) void knn_cull_kernel(
     int n, int s, int k, int* __restrict__ idx, float* __restrict__ dist,
     const float4* __restrict__ rs, const int* __restrict__ ri, const float4* __restrict__ cbox,
-    const float4* __restrict__ qrec, const int* __restrict__ qwin) {
+    const float4* __restrict__ qrec, const int* __restrict__ qwin,
+    unsigned long long* __restrict__ evals) {
   __shared__ float2 cand_buf[4][QW][kBuf];
-  const int b = blockIdx.y;
+  const int b = blockIdx.y, bx = blockIdx.x;
   const int wave = threadIdx.x >> 6;
   const int lane = lane_id();
-  const int qbase = (blockIdx.x * 4 + wave) * QW;  // sorted query positions
+  const int qbase = (bx * 4 + wave) * QW;  // sorted query positions
+  unsigned visits = 0;
   const int nch = divup(n, kWave);
   const float4* rb = rs + (long long)b * n;
   const int* ib = ri + (long long)b * n;
@@ -559,6 +570,7 @@ __global__ __launch_bounds__(256) void knn_cull_kernel(
     float4 r = rb[j < n ? j : cc * kWave];
     int gi = ib[j < n ? j : cc * kWave];
     while (true) {
+      if (STATS) ++visits;
       const bool valid = j < n;
       const bool more = todo != 0ull;
       const int cn = more ? cbase + __ffsll((long long)todo) - 1 : cc;
@@ -629,6 +641,13 @@ __global__ __launch_bounds__(256) void knn_cull_kernel(
     run(__ballot(need2) & need_m & ~near_m, cbase);
   }
 
+  if (STATS && lane == 0) {
+    int live = 0;
+#pragma unroll
+    for (int q = 0; q < QW; ++q) live += qbase + q < s ? 1 : 0;
+    if (live > 0)
+      atomicAdd(evals, (unsigned long long)visits * kWave * QW + (unsigned long long)kWin * live);
+  }
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (int q = 0; q < QW; ++q) {
@@ -735,6 +754,29 @@ KDPC_API size_t kdpc_knn_workspace_bytes(int b, int n, int s) {
   return seed_ws(b, n, s, nullptr).bytes;
 }
 
+namespace {
+int knn_culled(int b, int n, int s, int k, const float* xyz, const float* new_xyz, int* idx,
+               float* dist, void* workspace, unsigned long long* evals, hipStream_t st) {
+  const SeedWs w = seed_ws(b, n, s, workspace);
+  hipLaunchKernelGGL(ref_sort_kernel, dim3(b), dim3(kSortThreads), 0, st, n, xyz, w.bbox, w.roff,
+                     w.rs, w.ri);
+  hipLaunchKernelGGL(chunk_box_kernel, dim3(divup(divup(n, kWave), 4), b), dim3(256), 0, st, n,
+                     w.rs, w.cbox);
+  hipLaunchKernelGGL(query_sort_kernel, dim3(b), dim3(kSortThreads), 0, st, s, n, new_xyz,
+                     w.bbox, w.roff, w.qrec, w.qwin);
+  static_assert(KNN_QW == 4 || KNN_QW == 8, "KNN_QW");
+  constexpr int QW = KNN_QW;
+  const dim3 grid(divup(s, 4 * QW), b);
+  if (evals)
+    hipLaunchKernelGGL((knn_cull_kernel<QW, true>), grid, dim3(256), 0, st, n, s, k, idx, dist,
+                       w.rs, w.ri, w.cbox, w.qrec, w.qwin, evals);
+  else
+    hipLaunchKernelGGL((knn_cull_kernel<QW, false>), grid, dim3(256), 0, st, n, s, k, idx, dist,
+                       w.rs, w.ri, w.cbox, w.qrec, w.qwin, evals);
+  KDPC_RETURN_LAUNCH();
+}
+}  // namespace
+
 // kdpc_knn_point with scratch for the seeded threshold (identical results).
 KDPC_API int kdpc_knn_point_ws(int b, int n, int s, int k, const float* xyz,
                                const float* new_xyz, int* idx, float* dist, void* workspace,
@@ -745,19 +787,20 @@ KDPC_API int kdpc_knn_point_ws(int b, int n, int s, int k, const float* xyz,
   if (need == 0 || workspace == nullptr)
     return kdpc_knn_point(b, n, s, k, xyz, new_xyz, idx, dist, stream);
   KDPC_CHECK_ARG(xyz && new_xyz && idx && workspace_bytes >= need);
-  hipStream_t st = (hipStream_t)stream;
-  const SeedWs w = seed_ws(b, n, s, workspace);
-  hipLaunchKernelGGL(ref_sort_kernel, dim3(b), dim3(kSortThreads), 0, st, n, xyz, w.bbox, w.roff,
-                     w.rs, w.ri);
-  hipLaunchKernelGGL(chunk_box_kernel, dim3(divup(divup(n, kWave), 4), b), dim3(256), 0, st, n,
-                     w.rs, w.cbox);
-  hipLaunchKernelGGL(query_sort_kernel, dim3(b), dim3(kSortThreads), 0, st, s, n, new_xyz,
-                     w.bbox, w.roff, w.qrec, w.qwin);
-  if (KNN_QW == 8)
-    hipLaunchKernelGGL(knn_cull_kernel<8>, dim3(divup(s, 32), b), dim3(256), 0, st, n, s, k, idx,
-                       dist, w.rs, w.ri, w.cbox, w.qrec, w.qwin);
-  else
-    hipLaunchKernelGGL(knn_cull_kernel<4>, dim3(divup(s, 16), b), dim3(256), 0, st, n, s, k, idx,
-                       dist, w.rs, w.ri, w.cbox, w.qrec, w.qwin);
-  KDPC_RETURN_LAUNCH();
+  return knn_culled(b, n, s, k, xyz, new_xyz, idx, dist, workspace, nullptr,
+                    (hipStream_t)stream);
+}
+
+// kdpc_knn_point_ws (culled scan only) that also adds the number of distance evaluations it
+// issues to *evals (a device u64): the roofline's work count.  Same results.
+KDPC_API int kdpc_knn_point_evals(int b, int n, int s, int k, const float* xyz,
+                                  const float* new_xyz, int* idx, void* workspace,
+                                  size_t workspace_bytes, unsigned long long* evals,
+                                  void* stream) {
+  KDPC_CHECK_ARG(b >= 1 && n > 0 && s >= 1 && k >= 1 && k <= 64 && k <= n && b <= 65535);
+  const size_t need = kdpc_knn_workspace_bytes(b, n, s);
+  KDPC_CHECK_ARG(need > 0 && xyz && new_xyz && idx && evals && workspace &&
+                 workspace_bytes >= need);
+  return knn_culled(b, n, s, k, xyz, new_xyz, idx, nullptr, workspace, evals,
+                    (hipStream_t)stream);
 }

@@ -47,6 +47,7 @@ _SIGNATURES = {
     "kdpc_cost_volume_wide_slab_rows": [],
     "kdpc_cost_volume_wide_h0_bwd": [_c_int] * 5 + [_vp] * 8,
     "kdpc_knn_point_ws": [_c_int] * 4 + [_vp] * 5 + [_c_size, _vp],
+    "kdpc_knn_point_evals": [_c_int] * 4 + [_vp] * 4 + [_c_size, _vp, _vp],
     "kdpc_group_rows": [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp],
     "kdpc_csr_workspace_bytes": [_c_int, _c_int, _c_int],
     "kdpc_csr_build": [_c_int, _c_int, _c_int, _vp, _vp, _c_size, _vp, _vp, _vp],
@@ -317,6 +318,27 @@ def knn_point(nsample, xyz, new_xyz, return_dist=False, seeded=True):
         return _op("kdpc_knn_point", "knn_point_dist", int(nsample), xyz, new_xyz, seeded,
                    work=work)
     return _op("kdpc_knn_point", "knn_point", int(nsample), xyz, new_xyz, seeded, work=work)
+
+
+def knn_point_evals(nsample, xyz, new_xyz):
+    """The culled kNN scan through the bare C ABI (kdpc_knn_point_evals) -> (idx (B,S,K) i32,
+    number of query-ref distance evaluations it issued).  Measurement only (bench.py's
+    configs[4] roofline): the same indices as knn_point; needs a problem large enough for the
+    culled path."""
+    lib = load_library()
+    B, N, _ = _gpu(xyz, "xyz").shape
+    S = new_xyz.shape[1]
+    ws_bytes = lib.kdpc_knn_workspace_bytes(B, N, S)
+    if ws_bytes == 0:
+        raise KdpcError("knn_point_evals: the problem is too small for the culled scan")
+    xyz, new_xyz = xyz.contiguous(), new_xyz.contiguous()
+    idx = torch.empty((B, S, nsample), dtype=torch.int32, device=xyz.device)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=xyz.device)
+    cnt = torch.zeros(1, dtype=torch.int64, device=xyz.device)
+    _check(lib.kdpc_knn_point_evals(B, N, S, int(nsample), xyz.data_ptr(), new_xyz.data_ptr(),
+                                    idx.data_ptr(), ws.data_ptr(), ws_bytes, cnt.data_ptr(),
+                                    _stream(xyz)), "kdpc_knn_point_evals")
+    return idx, int(cnt.item())
 
 
 def knn_feature(nsample, ref, query, return_dist=False):

@@ -691,7 +691,9 @@ def test_kd_step_matches_reference(golden):
     """distilTrain.py:164-182 through distill.KDTrainStep (the product training step: shared
     FPS chain, teacher eval/no_grad, student train, biDirection_loss_ht, backward, Adam) on
     the N=2048 trace fixture with the reference's neighbours replayed: the loss at 1e-5 and
-    the gradients the optimizer sees vs the float64 reference at 1e-5."""
+    the gradients the optimizer sees vs the float64 reference at 1e-5, with the float64
+    run's discrete cost-volume decisions (max routing, LeakyReLU near-ties) replayed as in
+    test_model_matches_reference_with_reference_neighbours."""
     import pointconv_util as P
     from distill import KDTrainStep, make_optimizer
     from models_bid_lighttoken_res import PointConvBidirection as Student
@@ -711,10 +713,15 @@ def test_kd_step_matches_reference(golden):
     opt.step = recording_step
     before = {n: p.detach().clone() for n, p in student.named_parameters()}
     prev = P.set_knn_override(_KnnReplay(g))
+    routing = _CvReplay(g64)
+    prev_a, prev_c = P.set_amax_override(routing), P.set_cv_override(routing.cv)
     try:
         loss = KDTrainStep(teacher, student, opt)(_t(g["pos1"]), _t(g["pos2"]), _t(g["flow"]))
     finally:
         P.set_knn_override(prev)
+        P.set_amax_override(prev_a)
+        P.set_cv_override(prev_c)
+    assert routing.pos == len(routing.recs)  # every max of the student was replayed
     _close(loss, g["kd"], name="KD loss")
 
     class _View:  # the recorded gradients, shaped like the module for _check_grads_vs_f64

@@ -10,5 +10,9 @@ timeout -k 10 900 $PT tests/test_gpu_model.py tests/test_gpu_graph.py tests/test
 rc=$?; tail -4 gpurun_out/r4c_tests.log; grep -n "gradient error vs float64\|FAILED" gpurun_out/r4c_tests.log | head; [ $rc -eq 0 ] || exit $rc
 for c in joined unjoined; do
   timeout -k 5 120 python -u tools/torch_unjoined_capture.py $c > gpurun_out/r4c_torch_$c.log 2>&1
-  rc=$?; echo "torch capture $c rc=$rc"; tail -25 gpurun_out/r4c_torch_$c.log; [ $rc -eq 0 ] || exit $rc
+  rc=$?; echo "torch capture $c rc=$rc"; tail -25 gpurun_out/r4c_torch_$c.log; [ $rc -eq 0 ] || break
 done
+timeout -k 10 300 $PT tests/test_gpu_kernels.py -k "knn or gather" > gpurun_out/r4c_knn.log 2>&1
+rc=$?; tail -3 gpurun_out/r4c_knn.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u bench.py --sections knn,configs1 --no-cpu-baseline > gpurun_out/r4c_bench_knn.log 2>&1
+rc=$?; tail -1 gpurun_out/r4c_bench_knn.log | cut -c1-3000; exit $rc

@@ -95,6 +95,17 @@ int main(int argc, char** argv) {
     CK(hipStreamSynchronize(A));
     printf("done\n");
     return 0;
+  } else if (!strcmp(c, "external_event_destroyed") || !strcmp(c, "external_event_kept")) {
+    // the capturing stream waits on an event recorded on a stream that is NOT part of the
+    // capture (torch: cur.wait_stream(idle_side) inside a capture), then the event is
+    // destroyed before the graph is instantiated (a Python temporary)
+    hipLaunchKernelGGL(bump, 1, 64, 0, D, buf + 192);
+    hipEvent_t e;
+    CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    CK(hipEventRecord(e, D));
+    CK(hipStreamWaitEvent(A, e, 0));
+    hipLaunchKernelGGL(bump, 1, 64, 0, A, buf);
+    if (!strcmp(c, "external_event_destroyed")) CK(hipEventDestroy(e));
   } else if (!strcmp(c, "stream_destroyed_in_capture")) {
     hipStream_t E;
     CK(hipStreamCreateWithFlags(&E, hipStreamNonBlocking));

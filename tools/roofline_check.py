@@ -18,14 +18,20 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+EXCLUDE = {"kdpc_knn_point": ("true>",)}  # knn_cull_kernel<QW, true>: the STATS variant
+
+
 def main():
     import bench
     d, bench_file = sys.argv[1], sys.argv[2]
     line = None
-    for ln in open(bench_file):
-        ln = ln.strip()
-        if ln.startswith("{") and '"metric"' in ln:
-            line = json.loads(ln)
+    for ln in open(bench_file):  # the last JSON object line (a single-section run has no
+        ln = ln.strip()           # "metric": its line holds only that section's record)
+        if ln.startswith("{"):
+            try:
+                line = json.loads(ln)
+            except ValueError:
+                pass
     trace = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)[0]
     rows = list(csv.DictReader(open(trace)))
     out = {}
@@ -39,9 +45,20 @@ def main():
 
     for key, r in objs(line or {}, ""):
         kernels = bench.ROOFLINE[r["kernel"]][3]
-        head = kernels[0]
-        n = sum(1 for x in rows if head in x["Kernel_Name"])
-        tot = sum(int(x["End_Timestamp"]) - int(x["Start_Timestamp"]) for x in rows
+        sel = rows
+        wgs = r.get("grid_workgroups")
+        if wgs:  # one entry timed at two shapes in one run (gather C=3 / C=64): by grid size
+            sel = [x for x in rows if int(x["Grid_Size_X"]) * int(x["Grid_Size_Y"]) *
+                   int(x["Grid_Size_Z"]) // max(1, int(x["Workgroup_Size_X"]) *
+                   int(x["Workgroup_Size_Y"]) * int(x["Workgroup_Size_Z"])) == wgs]
+        # the counting launch of the kNN evaluation count (kdpc_knn_point_evals) is not part
+        # of the timed launches
+        skip = EXCLUDE.get(r["kernel"], ())
+        sel = [x for x in sel if not any(p in x["Kernel_Name"] for p in skip)]
+        # launches of the entry = launches of the first of its kernels (list order) present
+        head = next((k for k in kernels if any(k in x["Kernel_Name"] for x in sel)), kernels[0])
+        n = sum(1 for x in sel if head in x["Kernel_Name"])
+        tot = sum(int(x["End_Timestamp"]) - int(x["Start_Timestamp"]) for x in sel
                   if any(k in x["Kernel_Name"] for k in kernels))
         rp = tot / max(n, 1) / 1e3
         out[key] = {"entry": r["kernel"], "hip_kernels": kernels, "rocprof_launches": n,

@@ -25,6 +25,12 @@ try:
             x.mul_(2)
         if case == "joined":
             cap.wait_stream(side)
+        if case == "external":  # wait on a stream that is not part of the capture
+            idle = torch.cuda.Stream()
+            cap.wait_stream(idle)
+            cap.wait_stream(side)
+            import gc
+            gc.collect()
     print("capture_end returned", flush=True)
     g.replay()
     torch.cuda.synchronize()
