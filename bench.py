@@ -66,13 +66,19 @@ ROOFLINE = {
                         "knn_cull_kernel", "knn_kernel"]),
     "kdpc_gather_points": ("hbm", "GB/s", HBM_PEAK_GBS, ["gather_points_lds_kernel",
                                                           "gather_points_kernel"]),
-    "kdpc_cost_volume_fwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF,
-                             ["cost_volume_fwd_kernel", "cvw_fused_fwd_kernel"]),
+    # cost volume, D <= 64 (cost_volume.hip) and the wide levels D in {128, 256} (the one-kernel
+    # MFMA path of cost_volume_wide.hip) as separate entries (kdpc_native labels them by D)
+    "kdpc_cost_volume_fwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF, ["cost_volume_fwd_kernel"]),
+    "kdpc_cost_volume_fwd_wide": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF,
+                                  ["cvw_fused_fwd_kernel"]),
     "kdpc_cost_volume_bwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF, ["cost_volume_bwd_kernel"]),
     # the model's backward: rows in CSR order + contiguous per-point sums (+ the slab colsum)
     "kdpc_cost_volume_bwd_csr": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF,
-                                 ["cv_rows_sum_kernel", "cost_volume_bwd_kernel",
-                                  "cvw_fused_bwd_kernel", "cvw_transpose_kernel"]),
+                                 ["cost_volume_bwd_kernel", "cv_rows_sum_kernel<32>",
+                                  "cv_rows_sum_kernel<64>"]),
+    "kdpc_cost_volume_bwd_csr_wide": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF,
+                                      ["cvw_fused_bwd_kernel", "cvw_transpose_kernel",
+                                       "cv_rows_sum_kernel<128>", "cv_rows_sum_kernel<256>"]),
     "kdpc_idw_blend_fwd": ("hbm", "GB/s", HBM_PEAK_GBS, ["idw_fwd_kernel"]),
 }
 # the step's dominant entry point (rocprofv3 step profile, profiles/)
@@ -270,6 +276,7 @@ def step_section(args, mode, batch, dev, world, rank):
     t0 = time.perf_counter()
     for i in range(args.warmup, args.warmup + args.steps):
         step(*batches[i % nb], **nxt(i))
+    t_issue = time.perf_counter() - t0  # host time to issue the K steps (graph replays)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -306,7 +313,9 @@ def step_section(args, mode, batch, dev, world, rank):
     res = {"value": round(pairs / dt, 3), "unit": "pairs/s", "ms_per_step": round(ms, 3),
            "steps": args.steps, "warmup": args.warmup, "batch_per_gpu": batch,
            "global_batch": world * batch, "step": step_kind,
-           "host_enqueue_ms": round(min(host) * 1e3, 3), "roofline": roof,
+           "host_enqueue_ms": round(min(host) * 1e3, 3),
+           "host_issue_ms_per_step": round(t_issue / args.steps * 1e3, 3),
+           "roofline": roof,
            "step_roofline": {
                "bound": "mfma", "unit": "TFLOP/s", "peak": FP32_MFMA_PEAK_TF,
                "achieved": round(batch * STEP_FLOPS_PER_PAIR / (ms * 1e-3) / 1e12, 2),

@@ -30,6 +30,14 @@ inline int rows_per_block(long long r) {
   const long long nb = std::min<long long>(kMaxSlabs, std::max<long long>(1, divupll(r, 256)));
   return (int)divupll(r, nb);
 }
+// the backward reduction: up to 2048 blocks of >= 64 rows (round 4: 256 blocks of 256 rows
+// left one workgroup per CU walking 32 dependent row steps -- ~1.2 TB/s at R = 65536; the
+// order of the sums changes with the block size, the backward makes no discrete choice)
+constexpr int kMaxSlabsBwd = 2048;
+inline int rows_per_block_bwd(long long r) {
+  const long long nb = std::min<long long>(kMaxSlabsBwd, std::max<long long>(1, divupll(r, 64)));
+  return (int)divupll(r, nb);
+}
 
 // thread layout inside a block: channel group cg (4 channels), row lane rl
 struct Lay {
@@ -186,18 +194,31 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(int r, int c, int
       mu[i] = mean[4 * L.cg + i];
       is[i] = invstd[4 * L.cg + i];
     }
-    for (int row = r0 + L.rl; row < r1; row += L.lanes) {
-      const long long o = (long long)row * c;
-      const float4 g = reinterpret_cast<const float4*>(dya + o)[L.cg];
-      const float4 a = reinterpret_cast<const float4*>(ya + o)[L.cg];
-      const float4 v = reinterpret_cast<const float4*>(x + o)[L.cg];
-      const float gs[4] = {g.x, g.y, g.z, g.w}, as[4] = {a.x, a.y, a.z, a.w};
-      const float xs[4] = {v.x, v.y, v.z, v.w};
+    // kU rows' loads issued together, then accumulated in row order (same sums as one row
+    // at a time)
+    constexpr int kU = 4;
+    for (int row0 = r0 + L.rl; row0 < r1; row0 += kU * L.lanes) {
+      float4 g[kU], a[kU], v[kU];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float dy = as[i] > 0.f ? gs[i] : gs[i] * slope;
-        s1[i] += dy;
-        s2[i] = __builtin_fmaf(dy, (xs[i] - mu[i]) * is[i], s2[i]);
+      for (int u = 0; u < kU; ++u) {
+        const int row = row0 + u * L.lanes;
+        const long long o = (long long)(row < r1 ? row : r0) * c;
+        g[u] = reinterpret_cast<const float4*>(dya + o)[L.cg];
+        a[u] = reinterpret_cast<const float4*>(ya + o)[L.cg];
+        v[u] = reinterpret_cast<const float4*>(x + o)[L.cg];
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        if (row0 + u * L.lanes >= r1) break;
+        const float gs[4] = {g[u].x, g[u].y, g[u].z, g[u].w};
+        const float as[4] = {a[u].x, a[u].y, a[u].z, a[u].w};
+        const float xs[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float dy = as[i] > 0.f ? gs[i] : gs[i] * slope;
+          s1[i] += dy;
+          s2[i] = __builtin_fmaf(dy, (xs[i] - mu[i]) * is[i], s2[i]);
+        }
       }
     }
 #pragma unroll
@@ -268,8 +289,11 @@ inline int ew_grid(long long n4) {
 KDPC_API size_t kdpc_batchnorm_workspace_bytes(int r, int c) {
   if (r <= 0 || c <= 0) return 0;
   const long long nblk = divupll(r, rows_per_block(r));
-  // slab (nblk, 3, C) | column sums (2C) | colsum scratch
-  return (size_t)(nblk * 3 * c + 2 * c + colsum_scratch_floats((int)nblk, 2 * c)) * sizeof(float);
+  const long long nbb = divupll(r, rows_per_block_bwd(r));
+  // forward: slab (nblk, 3, C); backward: slab (nbb, 2, C) | column sums (2C) | colsum scratch
+  const long long fwd = nblk * 3 * c;
+  const long long bwd = nbb * 2 * c + 2 * c + colsum_scratch_floats((int)nbb, 2 * c);
+  return (size_t)std::max(fwd, bwd) * sizeof(float);
 }
 
 // Train-mode forward.  x, y (R, C) row-major; C % 4 == 0 and C <= 1024; mean/invstd (C)
@@ -326,7 +350,7 @@ KDPC_API int kdpc_batchnorm_lrelu_bwd(int r, int c, const float* dy_act, const f
                  workspace);
   KDPC_CHECK_ARG(workspace_bytes >= kdpc_batchnorm_workspace_bytes(r, c));
   hipStream_t st = (hipStream_t)stream;
-  const int rpb = rows_per_block(r);
+  const int rpb = rows_per_block_bwd(r);
   const int nblk = (int)divupll(r, rpb);
   const int lanes = kBlock / (c / 4);
   float* slab = reinterpret_cast<float*>(workspace);
@@ -334,7 +358,7 @@ KDPC_API int kdpc_batchnorm_lrelu_bwd(int r, int c, const float* dy_act, const f
                      r, c, rpb, slope, dy_act, y_act, x, mean, invstd, slab);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  float* sums = slab + (size_t)nblk * 3 * c;  // [sum dy (C) | sum dy*xhat (C)]
+  float* sums = slab + (size_t)nblk * 2 * c;  // [sum dy (C) | sum dy*xhat (C)]
   if ((e = colsum(nblk, 2 * c, slab, sums, sums + 2 * c, st)) != hipSuccess) return (int)e;
   const long long n4 = (long long)r * c / 4;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(n4)), dim3(kBlock), 0, st, n4, c / 4,

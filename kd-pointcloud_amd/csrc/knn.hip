@@ -354,6 +354,33 @@ __device__ __forceinline__ void seed_thresholds(int n, int k, int b, int qbase, 
   }
 }
 
+// A query's K results (lane r holds rank r) written at row offset o: for K % 4 == 0 (every
+// K of the models) lane t < K/4 collects ranks 4t..4t+3 by shuffles and writes them as one
+// 16-byte store, so a row is K/4 full-width stores instead of K 4-byte ones.
+__device__ __forceinline__ void store_row(int* __restrict__ idx, float* __restrict__ dist,
+                                          long long o, int k, int li, float ld) {
+  const int lane = lane_id();
+  const bool aligned = ((reinterpret_cast<unsigned long long>(idx) |
+                         reinterpret_cast<unsigned long long>(dist)) & 15ull) == 0ull;
+  if ((k & 3) == 0 && aligned) {
+    int iv[4];
+    float dv[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      iv[e] = __shfl(li, 4 * (lane & 15) + e, kWave);
+      dv[e] = __shfl(ld, 4 * (lane & 15) + e, kWave);
+    }
+    if (lane < (k >> 2)) {
+      *reinterpret_cast<int4*>(idx + o + 4 * lane) = make_int4(iv[0], iv[1], iv[2], iv[3]);
+      if (dist)
+        *reinterpret_cast<float4*>(dist + o + 4 * lane) = make_float4(dv[0], dv[1], dv[2], dv[3]);
+    }
+  } else if (lane < k) {
+    idx[o + lane] = li;
+    if (dist) dist[o + lane] = ld;
+  }
+}
+
 template <int QW>
 __global__ __launch_bounds__(256) void knn_kernel(int n, int s, int k,
                                                   const float* __restrict__ xyz,
@@ -418,14 +445,8 @@ __global__ __launch_bounds__(256) void knn_kernel(int n, int s, int k,
   }
 
 #pragma unroll
-  for (int q = 0; q < QW; ++q) {
-    const int qi = qbase + q;
-    if (qi < s && lane < k) {
-      const long long o = ((long long)b * s + qi) * k + lane;
-      idx[o] = li[q];
-      if (dist) dist[o] = ld[q];
-    }
-  }
+  for (int q = 0; q < QW; ++q)
+    if (qbase + q < s) store_row(idx, dist, ((long long)b * s + qbase + q) * k, k, li[q], ld[q]);
 }
 
 constexpr int kBuf = 128;  // candidate slots per query (LDS)
@@ -665,13 +686,8 @@ __global__ __launch_bounds__(256) void knn_cull_kernel(
   }
   sort64_multi<QW>(ld, li);
 #pragma unroll
-  for (int q = 0; q < QW; ++q) {
-    if (qbase + q < s && lane < k) {
-      const long long o = ((long long)b * s + qid[q]) * k + lane;
-      idx[o] = li[q];
-      if (dist) dist[o] = ld[q];
-    }
-  }
+  for (int q = 0; q < QW; ++q)
+    if (qbase + q < s) store_row(idx, dist, ((long long)b * s + qid[q]) * k, k, li[q], ld[q]);
 }
 
 struct SeedWs {

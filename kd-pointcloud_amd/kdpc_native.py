@@ -490,7 +490,9 @@ def cost_volume_fwd(x1, x2, idx, p1, p2, wpos, bpos, w1, b1):
     B, N1, _ = _gpu(x1, "x1").shape
     K = idx.shape[2]
     din, dout = p1.shape[2], w1.shape[0]
-    return _op("kdpc_cost_volume_fwd", "cost_volume_fwd", x1, x2, idx, p1, p2, wpos, bpos, w1,
+    # the wide shapes (the one-kernel MFMA path) are timed under their own label
+    entry = "kdpc_cost_volume_fwd_wide" if din >= 128 else "kdpc_cost_volume_fwd"
+    return _op(entry, "cost_volume_fwd", x1, x2, idx, p1, p2, wpos, bpos, w1,
                b1, work=(4 * B * N1 * (3 + K + din + K * din + 2 * dout) + B * N1 * dout,
                          2.0 * B * N1 * K * din * dout))
 
@@ -517,7 +519,8 @@ def cost_volume_bwd_csr(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout):
     csr = csr_rank_of(idx, N2)
     # reads x1, idx, rank, p1, the K gathered p2 rows, out, gout, amax, offsets; writes dp1,
     # dx1 and the per-point dp2 / dx2 (the CSR-ordered rows in between are not counted)
-    return _op("kdpc_cost_volume_bwd_csr", "cost_volume_bwd_csr", x1, x2, idx, p1, p2,
+    entry = "kdpc_cost_volume_bwd_csr_wide" if din >= 128 else "kdpc_cost_volume_bwd_csr"
+    return _op(entry, "cost_volume_bwd_csr", x1, x2, idx, p1, p2,
                wpos, bpos, w1, out, amax, gout, csr.offsets, csr.rank,
                work=(4 * B * N1 * (3 + 2 * K + din + K * din + 2 * dout + din + 3)
                      + B * N1 * dout + 4 * B * N2 * (din + 4) + 4,

@@ -16,6 +16,8 @@ model code and checkpoints load unchanged.  The implementation is MI355X-first:
     (B,C,K,N) Conv2d without the transposes.
 Dense GEMMs run on rocBLAS/hipBLASLt through torch; nothing here has a CPU fallback.
 """
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -506,6 +508,11 @@ class PointConvD(_PointConvBase):
         return new_xyz, new_points, fps_idx
 
 
+# KDPC_CV_BWD_PLAIN=1: the D <= 64 backward writes its per-neighbour rows in (query,
+# neighbour) order and sums them through the CSR's perm (A/B runs; bit-identical)
+_CV_BWD_PLAIN = os.environ.get("KDPC_CV_BWD_PLAIN") == "1"
+
+
 class _CostVolume(torch.autograd.Function):
     """Fused cost volume (csrc/cost_volume.hip): x1 (B,N1,3), x2 (B,N2,3), idx (B,N1,K),
     p1 (B,N1,D), p2 (B,N2,D) channel-last -> (B,N1,Dout) channel-last."""
@@ -524,9 +531,17 @@ class _CostVolume(torch.autograd.Function):
         B, N1, K = idx.shape
         N2 = x2.shape[1]
         din, dout = p1.shape[2], w1.shape[0]
-        # per-neighbour rows straight into the CSR order of idx, summed per point inside
-        dp1, dp2, dx1, dx2, dpar = _nat.cost_volume_bwd_csr(
-            x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout.contiguous())
+        if _CV_BWD_PLAIN and din <= 64:
+            # A/B: rows in (query, neighbour) order, summed per point through perm
+            dp1, rows, dx1, drows, dpar = _nat.cost_volume_bwd(
+                x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout.contiguous())
+            csr = _nat.csr_of(idx, N2)
+            dp2 = _nat.group_rows_grad(rows.view(B, N1 * K, din), csr, B, N2, din)
+            dx2 = _nat.group_rows_grad(drows.view(B, N1 * K, 3), csr, B, N2, 3)
+        else:
+            # per-neighbour rows straight into the CSR order of idx, summed per point inside
+            dp1, dp2, dx1, dx2, dpar = _nat.cost_volume_bwd_csr(
+                x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout.contiguous())
         o = dout * din
         dw1 = dpar[:o].view(dout, din)
         db1 = dpar[o:o + dout]
