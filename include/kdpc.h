@@ -455,6 +455,11 @@ size_t kdpc_colsum_workspace_bytes(int nrows, int len);
 int kdpc_colsum(int nrows, int len, const float *src, float *dst, void *workspace,
                 size_t workspace_bytes, void *stream);
 
+/* out (m, c) = -sum_{j<k} in (m, k, c) in ascending j: the center gradient -sum_k drel of the
+ * grouped relative offsets (replaces the torch reduction of pointconv_util.py's WeightNet
+ * backward: `-drel.sum(2)`). */
+int kdpc_neg_sum_k(int m, int k, int c, const float *in, float *out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

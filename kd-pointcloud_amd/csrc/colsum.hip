@@ -110,3 +110,32 @@ KDPC_API int kdpc_colsum(int nrows, int len, const float* src, float* dst, void*
   return (int)kdpc::colsum(nrows, len, src, dst, reinterpret_cast<float*>(workspace),
                            (hipStream_t)stream);
 }
+
+// ------------------------------------------------------------------------------------------
+// out[i][c] = -sum_{j<k} in[i][j][c] (ascending j): the center gradient of a grouped
+// relative-offset layer, dcenter = -sum_k drel (WeightNet backward), in one launch (torch's
+// `-x.sum(2)` was a strided reduction plus a negation: two launches per layer).
+namespace {
+__global__ __launch_bounds__(256) void neg_sum_k_kernel(long long m, int k, int c,
+                                                        const float* __restrict__ in,
+                                                        float* __restrict__ out) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= m * c) return;
+  const long long i = e / c;
+  const int ch = (int)(e - i * c);
+  const float* p = in + i * k * c + ch;
+  float s = 0.f;
+  for (int j = 0; j < k; ++j) s = __fadd_rn(s, p[(long long)j * c]);
+  out[e] = -s;
+}
+}  // namespace
+
+KDPC_API int kdpc_neg_sum_k(int m, int k, int c, const float* in, float* out,
+                            void* stream) {
+  KDPC_CHECK_ARG(m >= 0 && k >= 1 && c >= 1);
+  if (m == 0) return (int)hipSuccess;
+  KDPC_CHECK_ARG(in && out);
+  hipLaunchKernelGGL(neg_sum_k_kernel, dim3((unsigned)divupll((long long)m * c, 256)), dim3(256),
+                     0, (hipStream_t)stream, (long long)m, k, c, in, out);
+  KDPC_RETURN_LAUNCH();
+}

@@ -79,6 +79,7 @@ _SIGNATURES = {
                                 + [_c_size, _vp],
     "kdpc_colsum_workspace_bytes": [_c_int, _c_int],
     "kdpc_colsum": [_c_int, _c_int, _vp, _vp, _vp, _c_size, _vp],
+    "kdpc_neg_sum_k": [_c_int, _c_int, _c_int, _vp, _vp, _vp],
     "kdpc_weightnet_param_count": [],
     "kdpc_weightnet_fwd": [_c_int] * 4 + [_vp] * 11,
     "kdpc_weightnet_bwd_workspace_bytes": [],
@@ -756,6 +757,11 @@ def dense_small_out(x2, m, bias, y2):
     N = m.shape[1]
     _op("kdpc_dense_small", "dense_small_out", x2.contiguous(), m.contiguous(), bias, y2,
         work=(4 * (R * K + R * N + K * N), 2.0 * R * K * N))
+
+
+def neg_sum_k(x):
+    """x (..., K, C) -> -x.sum(-2) (..., C), ascending-K order, one launch."""
+    return _op("kdpc_neg_sum_k", "neg_sum_k", _gpu(x, "x").contiguous())
 
 
 def colsum(x2):

@@ -344,7 +344,7 @@ class _WeightNetFn(torch.autograd.Function):
             if ctx.needs_input_grad[0]:
                 dxyz = _nat.group_rows_grad(drel.view(B, S * K, 3), _nat.csr_of(idx, N), B, N, 3)
             if ctx.needs_input_grad[1]:
-                dcenter = -drel.sum(2)
+                dcenter = _nat.neg_sum_k(drel)  # -drel.sum(2), one launch
         return (dxyz, dcenter, None, *dparams)
 
 

@@ -718,6 +718,20 @@ std::tuple<Tensor, Tensor, Tensor> batchnorm_lrelu_bwd(Tensor dy, Tensor y, Tens
   return {dx, dw, db};
 }
 
+Tensor neg_sum_k(Tensor x) {
+  dev(x, kF, "x");
+  TORCH_CHECK(x.dim() >= 2, "kdpc: neg_sum_k expects (..., K, C)");
+  GUARD(x);
+  const int64_t k = x.size(-2), c = x.size(-1);
+  const int64_t m = k * c == 0 ? 0 : x.numel() / (k * c);
+  std::vector<int64_t> shape(x.sizes().begin(), x.sizes().end() - 2);
+  shape.push_back(c);
+  Tensor out = at::empty(shape, x.options());
+  TORCH_CHECK(m < (int64_t(1) << 31), "kdpc: neg_sum_k: too many rows");
+  check(kdpc_neg_sum_k((int)m, k, c, F(x), F(out), stream_of(x)), "neg_sum_k");
+  return out;
+}
+
 Tensor colsum(Tensor x) {
   dev(x, kF, "src");
   TORCH_CHECK(x.dim() == 2, "kdpc: colsum expects a (rows, len) tensor");
@@ -942,6 +956,7 @@ TORCH_LIBRARY(kdpc, m) {
   m.def("idw_blend_bwd_coords(Tensor ref, Tensor qry, Tensor vals, Tensor idx, Tensor dout, "
         "bool warp) -> (Tensor, Tensor)");
   m.def("dense_tn_small(Tensor a, Tensor b) -> Tensor");
+  m.def("neg_sum_k(Tensor x) -> Tensor");
   m.def("dense_small(Tensor x, Tensor m, Tensor? bias) -> Tensor");
   m.def("dense_small_out(Tensor x, Tensor m, Tensor? bias, Tensor(a!) y) -> ()");
 }
@@ -998,6 +1013,7 @@ TORCH_LIBRARY_IMPL(kdpc, CUDA, m) {
   m.impl("idw_blend_bwd_vals", idw_blend_bwd_vals);
   m.impl("idw_blend_bwd_coords", idw_blend_bwd_coords);
   m.impl("dense_tn_small", dense_tn_small);
+  m.impl("neg_sum_k", neg_sum_k);
   m.impl("dense_small", dense_small);
   m.impl("dense_small_out", dense_small_out);
 }

@@ -464,3 +464,18 @@ def test_dense_small_vs_float64(nat, r, k, n, bias):
     assert ((got.double() - want).abs() <= bound).all()
     y = dense.linear(x, m.t().contiguous(), b)
     assert torch.equal(y, got)
+
+
+@pytest.mark.parametrize("shape", [(3, 100, 9, 3), (2, 5, 16, 7), (1, 1, 1, 3), (8, 2048, 16, 3)])
+def test_neg_sum_k(nat, shape):
+    """-x.sum(-2) in ascending-K order (the WeightNet center gradient), one launch."""
+    g = torch.Generator(device="cpu").manual_seed(sum(shape))
+    x = torch.randn(*shape, generator=g)
+    got = nat.neg_sum_k(x.to(DEV)).cpu()
+    want = -x.double().sum(-2)
+    assert got.shape == want.shape
+    seq = torch.zeros(want.shape)
+    for j in range(shape[-2]):
+        seq = seq + x[..., j, :]
+    np.testing.assert_array_equal(got.numpy(), (-seq).numpy())  # the fixed order, bit for bit
+    np.testing.assert_allclose(got.double().numpy(), want.numpy(), rtol=1e-5, atol=1e-6)

@@ -159,6 +159,7 @@ TORCH_OPS = {
     "idw_blend_fwd": "kdpc_idw_blend_fwd", "idw_blend_bwd_vals": "kdpc_idw_blend_bwd_vals",
     "idw_blend_bwd_coords": "kdpc_idw_blend_bwd_coords",
     "dense_tn_small": "kdpc_dense_tn_small", "dense_small": "kdpc_dense_small",
+    "neg_sum_k": "kdpc_neg_sum_k",
     "dense_small_out": "kdpc_dense_small",
 }
 
