@@ -460,6 +460,13 @@ int kdpc_colsum(int nrows, int len, const float *src, float *dst, void *workspac
  * backward: `-drel.sum(2)`). */
 int kdpc_neg_sum_k(int m, int k, int c, const float *in, float *out, void *stream);
 
+/* n byte copies dst[i] <- src[i] (bytes[i] a multiple of 4, 4-byte aligned pointers) in
+ * ceil(n/128) launches.  Replaces torch._foreach_copy_ in the graphed training step (the
+ * gradient pack into the flat buffer and the plan prefetch hand-over); no reference
+ * counterpart: the reference steps its optimizer per parameter (train.py:150-160). */
+int kdpc_copy_segments(int n, const void *const *src, void *const *dst, const long long *bytes,
+                       void *stream);
+
 #ifdef __cplusplus
 }
 #endif

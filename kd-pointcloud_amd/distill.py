@@ -21,6 +21,7 @@ import os
 import torch
 import torch.distributed as dist
 
+import kdpc_native as _nat
 import loss_functions
 import wgrad
 
@@ -492,7 +493,15 @@ class GraphedStep:
                 self._offs.append(off)
                 off += k
         self.G = G
-        self._steps = steps
+        # the per-parameter Adam step counters become views of one buffer: the tail keeps
+        # them in sync with the flat optimizer's counter in one launch instead of a
+        # foreach copy over ~240 scalars
+        S = torch.empty(len(used), device=steps[0].device, dtype=steps[0].dtype)
+        with torch.no_grad():
+            S.copy_(torch.stack([st.reshape(()) for st in steps]))
+        for i, p in enumerate(used):
+            opt.state[p]["step"] = S[i].view_as(steps[i])
+        self._steps = S
         flat = torch.nn.Parameter(P)
         flat.grad = G
         fo = torch.optim.Adam([flat], lr=self._lr, betas=grp["betas"], eps=grp["eps"],
@@ -535,8 +544,8 @@ class GraphedStep:
                 idx = b["idx"]
                 # only this bucket's parameter gradients still in flight on their own stream
                 wgrad.wait_for([self._used[i] for i in idx])
-                torch._foreach_copy_([self._gviews[i] for i in idx],
-                                     [self._used[i].grad for i in idx])
+                _nat.copy_segments([self._gviews[i] for i in idx],
+                                   [self._used[i].grad for i in idx])
                 self.comm.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(self.comm):
                     dist.all_reduce(self.G[b["lo"]:b["hi"]])
@@ -544,7 +553,7 @@ class GraphedStep:
         return [p.register_post_accumulate_grad_hook(hook) for p in self._used]
 
     def _pack(self):
-        torch._foreach_copy_(self._gviews, [p.grad for p in self._used])
+        _nat.copy_segments(self._gviews, [p.grad for p in self._used])
 
     def _tail(self, fork, pack=True):
         """Flat Adam step (+ the prefetched FPS handed over), inside a graph."""
@@ -553,9 +562,9 @@ class GraphedStep:
         # an eager optimizer step in between advanced the per-parameter counters
         self._flat_step.copy_(self._steps[0])
         self.flat_opt.step()
-        torch._foreach_copy_(self._steps, [self._flat_step] * len(self._steps))
+        self._steps.copy_(self._flat_step.reshape(1).expand_as(self._steps))
         if fork is not None:
-            torch._foreach_copy_(self.fps_cur, self.fps_next)
+            _nat.copy_segments(self.fps_cur, [t.contiguous() for t in self.fps_next])
 
     def _fps_kw(self, fps):
         return {} if self.prefetch_fn is None else {"fps": fps}

@@ -80,6 +80,7 @@ _SIGNATURES = {
     "kdpc_colsum_workspace_bytes": [_c_int, _c_int],
     "kdpc_colsum": [_c_int, _c_int, _vp, _vp, _vp, _c_size, _vp],
     "kdpc_neg_sum_k": [_c_int, _c_int, _c_int, _vp, _vp, _vp],
+    "kdpc_copy_segments": [_c_int, _vp, _vp, _vp, _vp],
     "kdpc_weightnet_param_count": [],
     "kdpc_weightnet_fwd": [_c_int] * 4 + [_vp] * 11,
     "kdpc_weightnet_bwd_workspace_bytes": [],
@@ -762,6 +763,13 @@ def dense_small_out(x2, m, bias, y2):
 def neg_sum_k(x):
     """x (..., K, C) -> -x.sum(-2) (..., C), ascending-K order, one launch."""
     return _op("kdpc_neg_sum_k", "neg_sum_k", _gpu(x, "x").contiguous())
+
+
+def copy_segments(dst, src):
+    """dst[i].copy_(src[i]) for same-size contiguous tensors, ceil(n/128) launches."""
+    dst, src = list(dst), list(src)
+    _op("kdpc_copy_segments", "copy_segments", dst, src,
+        work=(2.0 * sum(s.numel() * s.element_size() for s in src), 0.0))
 
 
 def colsum(x2):

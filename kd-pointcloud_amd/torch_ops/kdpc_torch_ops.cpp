@@ -732,6 +732,30 @@ Tensor neg_sum_k(Tensor x) {
   return out;
 }
 
+// dst[i] <- src[i] for same-size contiguous tensors on one device, one launch per 128 pairs
+void copy_segments(at::TensorList dst, at::TensorList src) {
+  TORCH_CHECK(dst.size() == src.size(), "kdpc: copy_segments: ", dst.size(), " destinations, ",
+              src.size(), " sources");
+  if (dst.empty()) return;
+  std::vector<const void*> sp;
+  std::vector<void*> dp;
+  std::vector<long long> nb;
+  for (size_t i = 0; i < dst.size(); ++i) {
+    const Tensor &d = dst[i], &s = src[i];
+    TORCH_CHECK(d.is_cuda() && s.is_cuda(), "kdpc: copy_segments: tensors must be on the GPU");
+    same_device(dst[0], d, "dst"), same_device(dst[0], s, "src");
+    TORCH_CHECK(d.is_contiguous() && s.is_contiguous() && d.dtype() == s.dtype() &&
+                    d.numel() == s.numel(),
+                "kdpc: copy_segments: pair ", i, " must be contiguous, same dtype and size");
+    sp.push_back(s.data_ptr());
+    dp.push_back(d.data_ptr());
+    nb.push_back((long long)s.nbytes());
+  }
+  GUARD(dst[0]);
+  check(kdpc_copy_segments((int)dst.size(), sp.data(), dp.data(), nb.data(), stream_of(dst[0])),
+        "copy_segments");
+}
+
 Tensor colsum(Tensor x) {
   dev(x, kF, "src");
   TORCH_CHECK(x.dim() == 2, "kdpc: colsum expects a (rows, len) tensor");
@@ -957,6 +981,7 @@ TORCH_LIBRARY(kdpc, m) {
         "bool warp) -> (Tensor, Tensor)");
   m.def("dense_tn_small(Tensor a, Tensor b) -> Tensor");
   m.def("neg_sum_k(Tensor x) -> Tensor");
+  m.def("copy_segments(Tensor(a!)[] dst, Tensor[] src) -> ()");
   m.def("dense_small(Tensor x, Tensor m, Tensor? bias) -> Tensor");
   m.def("dense_small_out(Tensor x, Tensor m, Tensor? bias, Tensor(a!) y) -> ()");
 }
@@ -1014,6 +1039,7 @@ TORCH_LIBRARY_IMPL(kdpc, CUDA, m) {
   m.impl("idw_blend_bwd_coords", idw_blend_bwd_coords);
   m.impl("dense_tn_small", dense_tn_small);
   m.impl("neg_sum_k", neg_sum_k);
+  m.impl("copy_segments", copy_segments);
   m.impl("dense_small", dense_small);
   m.impl("dense_small_out", dense_small_out);
 }

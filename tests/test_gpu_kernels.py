@@ -479,3 +479,37 @@ def test_neg_sum_k(nat, shape):
         seq = seq + x[..., j, :]
     np.testing.assert_array_equal(got.numpy(), (-seq).numpy())  # the fixed order, bit for bit
     np.testing.assert_allclose(got.double().numpy(), want.numpy(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("count", [1, 127, 128, 129, 300])
+def test_copy_segments(nat, count):
+    """Many copies in ceil(n/128) launches: every pair bit-exact, bytes around each
+    destination untouched (odd sizes, 4-byte-aligned views, int and float, empty ones)."""
+    g = torch.Generator(device="cpu").manual_seed(count)
+    sizes = torch.randint(0, 3000, (count,), generator=g).tolist()
+    sizes[0] = 1
+    total = sum(sizes) + 5 * count + 8
+    dst_buf = torch.full((total,), -7.0, device=DEV)
+    src, dst, off = [], [], 1  # offset 1: 4-byte but not 16-byte aligned views
+    for i, k in enumerate(sizes):
+        if i % 3 == 2:
+            s = torch.randint(-2**31, 2**31 - 1, (k,), generator=g, dtype=torch.int32).to(DEV)
+            d = dst_buf[off:off + k].view(torch.int32)
+        else:
+            s = torch.randn(k, generator=g).to(DEV)
+            d = dst_buf[off:off + k]
+        src.append(s)
+        dst.append(d)
+        off += k + 1 + (i % 4)
+    nat.copy_segments(dst, src)
+    torch.cuda.synchronize()
+    for s, d in zip(src, dst):
+        assert torch.equal(s, d)
+    mask = torch.ones(total, dtype=torch.bool)
+    off = 1
+    for i, k in enumerate(sizes):
+        mask[off:off + k] = False
+        off += k + 1 + (i % 4)
+    assert (dst_buf.cpu()[mask] == -7.0).all()
+    with pytest.raises(RuntimeError):
+        nat.copy_segments([dst_buf[:4]], [src[0][:3] if sizes[0] >= 3 else torch.zeros(3, device=DEV)])

@@ -160,6 +160,7 @@ TORCH_OPS = {
     "idw_blend_bwd_coords": "kdpc_idw_blend_bwd_coords",
     "dense_tn_small": "kdpc_dense_tn_small", "dense_small": "kdpc_dense_small",
     "neg_sum_k": "kdpc_neg_sum_k",
+    "copy_segments": "kdpc_copy_segments",
     "dense_small_out": "kdpc_dense_small",
 }
 
