@@ -341,6 +341,9 @@ class GraphedStep:
 
     def __init__(self, loss_fn, params, optimizer, example_inputs, warmup=3, prefetch_fn=None,
                  n_prefetch=2, overlap=None):
+        if warmup < 1:
+            raise ValueError("GraphedStep needs warmup >= 1: the last warm-up backward records "
+                             "the gradient order the flat buffers are laid out in")
         self.loss_fn = loss_fn
         self.opt = optimizer
         self.params = [p for p in params if p.requires_grad]

@@ -126,3 +126,13 @@ def _check(kd):
             torch.testing.assert_close(v, bn_state[k], rtol=0, atol=0)
             continue
         torch.testing.assert_close(v, sd[k], rtol=1e-6, atol=1e-6, msg=k)
+
+
+def test_graphed_step_requires_warmup():
+    """GraphedStep lays the flat buffers out in the order the last warm-up backward finalised
+    the gradients: warmup=0 is refused up front with a clear message (CPU, no capture)."""
+    import distill
+    p = torch.nn.Parameter(torch.zeros(3))
+    with pytest.raises(ValueError, match="warmup >= 1"):
+        distill.GraphedStep(lambda x: p.sum(), [p], torch.optim.SGD([p], lr=0.1),
+                            (torch.zeros(1),), warmup=0)
