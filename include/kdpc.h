@@ -314,6 +314,41 @@ int kdpc_pointconv_bwd_weight(int b, int n, int s, int k, int d, int o, const fl
                               const float *wt, const float *dy, float *dwl, void *workspace,
                               size_t workspace_bytes, void *stream);
 
+/* Tiled PointConv backward: the same gradients with the dG rows summed per (32-row tile,
+ * destination point) inside the data kernel (one partial row each instead of one row per
+ * (row, neighbour) pair), then per point through the CSR of the partial rows.  The rows of
+ * a tile come from a row order that keeps them close in space (kdpc_morton_order), so a
+ * tile's 32K pairs name few distinct points.  Sums in a fixed order (pairs of a destination
+ * in ascending pair order within a tile, tiles ascending): deterministic, rounding differs
+ * from the untiled entry points.  Same as kdpc_pointconv_bwd(_data) (pointconv_util.py:
+ * 217-258 backward) otherwise; same workspace.
+ *
+ * kdpc_morton_order: order (B,S) = each batch element's S <= 8192 centers (B,S,3) sorted by
+ *   their Morton code (6 bits per axis over the element's bounding box), ties by index.
+ * kdpc_pc_tile_plan: for idx (B,S,K) (K <= 16, values in [0,N)) and an optional order (NULL
+ *   = identity), per tile t of T = B*ceil(S/32): trow (T*32) global rows or -1, tpair
+ *   (T*32K) the tile's pairs (p = row_in_tile*K + k) sorted by (destination, p), -1 padded,
+ *   tsoff (T*(32K+1)) each destination's first sorted position (then the pair count), tkey
+ *   (T*32K) the destinations (-1 padded).  offsets / tdst = kdpc_csr_build / kdpc_csr_rank
+ *   of tkey viewed as (B, ceil(S/32)*32K) over N keys. */
+int kdpc_morton_order(int b, int s, const float *xyz, int *order, void *stream);
+int kdpc_pc_tile_plan(int b, int s, int n, int k, const int *idx, const int *order, int *trow,
+                      int *tpair, int *tsoff, int *tkey, void *stream);
+int kdpc_pointconv_bwd_data_tiled(int b, int n, int s, int k, int d, int o, const float *xyz,
+                                  const float *center, const float *feats, const int *idx,
+                                  const float *wt, const float *wl, const float *dy,
+                                  const int *offsets, const int *trow, const int *tpair,
+                                  const int *tsoff, const int *tdst, float *dxyz, float *dfeats,
+                                  float *dcenter, float *dwt, void *workspace,
+                                  size_t workspace_bytes, void *stream);
+int kdpc_pointconv_bwd_tiled(int b, int n, int s, int k, int d, int o, const float *xyz,
+                             const float *center, const float *feats, const int *idx,
+                             const float *wt, const float *wl, const float *dy,
+                             const int *offsets, const int *trow, const int *tpair,
+                             const int *tsoff, const int *tdst, float *dxyz, float *dfeats,
+                             float *dcenter, float *dwt, float *dwl, void *workspace,
+                             size_t workspace_bytes, void *stream);
+
 /* ---- fused WeightNet over grouped offsets (pointconv_util.py:184-215 as used by
  *      PointConv/PointConvD :217-258, :401-446: weightnet=16, hidden [8, 8], no BN) ------ */
 

@@ -559,7 +559,12 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
 // and LDS work fills the MFMAs' 64-cycle issue shadows of the same wave.  One barrier per
 // chunk.  Identical arithmetic to pc_bwd_data_kernel (same fma order in every sum), so the
 // two produce bit-identical dG / dwt / dcenter.
-template <int O, int KM>
+// TP (tiled plan, tile_plan.hip): the tile's rows come from g.trow, and instead of one dG
+// row per pair the kernel writes one partial row per (tile, destination point): each chunk's
+// pair values go to LDS (red), and the next step sums every destination's pairs in
+// ascending pair order (g.tpair / g.tsoff) into registers, stored at the step's store slot
+// (partial row g.tdst).  The forward arithmetic per pair is unchanged.
+template <int O, int KM, bool TP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* __restrict__ wsw,
                              const float* __restrict__ dy, float* __restrict__ dgr,
@@ -582,7 +587,21 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
   __shared__ __attribute__((aligned(16))) float dyl[(O / 4) * kBlk];
   __shared__ __attribute__((aligned(16))) float dal[2][32 * kDaS];
   __shared__ float dcl[TR * KM * 3];  // every pair slot (invalid ones write zeros)
+  // TP: the chunk's per-pair dG values (double-buffered by chunk parity) and the tile's
+  // pairs in (destination, pair) order
+  constexpr int TRK = TR * KM;
+  constexpr int NJ = TP ? (2 * TRK + NT - 1) / NT : 1;  // (destination, half) items/thread
+  __shared__ __attribute__((aligned(16))) float red[TP ? 2 : 1][TP ? TRK * kCC : 4];
+  __shared__ int tpl[TP ? TRK : 1], tsl[TP ? TRK + 1 : 1], tdl[TP ? TRK : 1];
   const int row0 = blockIdx.x * TR;
+  // global row of tile row r (< TR), -1 for none
+  auto grow = [&](int r) -> int {
+    if constexpr (TP) {
+      return g.trow[(long long)blockIdx.x * TR + r];
+    } else {
+      return row0 + r < g.r ? row0 + r : -1;
+    }
+  };
   const int split = blockIdx.y;
   const int ch0 = split * chunks_per_split;
   const int ch1 = min(g.nch, ch0 + chunks_per_split);
@@ -592,21 +611,22 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
 
   for (int e = t; e < 32 * O; e += NT) {
     const int r = e / O, o = e % O;
-    const int row = row0 + r;
-    dyl[(o >> 2) * kBlk + r * 4 + (o & 3)] = row < g.r ? dy[(long long)row * O + o] : 0.f;
+    const int row = grow(r);
+    dyl[(o >> 2) * kBlk + r * 4 + (o & 3)] = row >= 0 ? dy[(long long)row * O + o] : 0.f;
   }
   float wp[PP][kW], dw[PP][kW];
-  int pr[PP], pk[PP], pn[PP], ps[PP], prc[PP];
+  int pr[PP], pk[PP], pn[PP], ps[PP], prc[PP], prow[PP];
 #pragma unroll
   for (int q = 0; q < PP; ++q) {
     const int p = t + NT * q;
     pr[q] = p / g.k;
     pk[q] = p - pr[q] * g.k;
     prc[q] = min(pr[q], TR - 1);  // dA row read by this slot (any row when the pair is dead)
-    const bool ok = p < TR * g.k && row0 + pr[q] < g.r;
-    pn[q] = ok ? nbr_of(g, row0 + pr[q], pk[q]) : -1;
-    ps[q] = ok ? slot_of(g, row0 + pr[q], pk[q]) : -1;
-    const long long pos = (long long)(row0 + pr[q]) * g.k + pk[q];
+    prow[q] = p < TR * g.k ? grow(pr[q]) : -1;
+    const bool ok = prow[q] >= 0;
+    pn[q] = ok ? nbr_of(g, prow[q], pk[q]) : -1;
+    ps[q] = (ok && !TP) ? slot_of(g, prow[q], pk[q]) : -1;
+    const long long pos = (long long)prow[q] * g.k + pk[q];
 #pragma unroll
     for (int v = 0; v < kW / 4; ++v) {
       const float4 x = ok ? reinterpret_cast<const float4*>(wt + pos * kW)[v]
@@ -622,10 +642,23 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
   const int xp = PP * NT + t / kCC, xc = t % kCC;
   const int xr = XI ? xp / g.k : 0;
   const int xrc = min(xr, TR - 1);
-  const bool xok = XI && xp < TR * g.k && row0 + xr < g.r;
-  const int xn = xok ? nbr_of(g, row0 + xr, xp - xr * g.k) : -1;
-  const int xsl = xok ? slot_of(g, row0 + xr, xp - xr * g.k) : -1;
-  const long long xpos = (long long)(row0 + xr) * g.k + (xp - xr * g.k);
+  const int xrow = (XI && xp < TR * g.k) ? grow(xrc) : -1;
+  const bool xok = xrow >= 0;
+  const int xn = xok ? nbr_of(g, xrow, xp - xr * g.k) : -1;
+  const int xsl = (xok && !TP) ? slot_of(g, xrow, xp - xr * g.k) : -1;
+  const long long xpos = (long long)xrow * g.k + (xp - xr * g.k);
+  // TP: the tile's plan in LDS (sorted pairs tpl, destination starts tsl, partial rows tdl);
+  // thread t owns the (destination, half) items t + NT j.  Registers are the constraint here
+  // (the untiled kernel holds 232 VGPRs), so nothing of it lives in registers across steps.
+  if constexpr (TP) {
+    const long long tb = (long long)blockIdx.x;
+    const int trk = TR * g.k;
+    for (int i = t; i < TRK; i += NT) {
+      tpl[i] = i < trk ? g.tpair[tb * trk + i] : -1;
+      tdl[i] = i < trk ? g.tdst[tb * trk + i] : -1;
+    }
+    for (int i = t; i <= TRK; i += NT) tsl[i] = i <= trk ? g.tsoff[tb * (trk + 1) + i] : 0;
+  }
   float xw[kW], xd[kW], xg = 0.f, xgn = 0.f, xs = 0.f;
   if constexpr (XI) {
 #pragma unroll
@@ -645,7 +678,7 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
     const bool live = xn >= 0;
     const unsigned fo = (live && cg >= 3 && cg < g.c) ? ((unsigned)xn * (unsigned)g.d + (unsigned)(cg - 3)) * 4u : kOOB;
     const unsigned xo = (live && cg < 3) ? ((unsigned)xn * 3u + (unsigned)cg) * 4u : kOOB;
-    const unsigned co = (live && cg < 3) ? ((unsigned)(row0 + xr) * 3u + (unsigned)cg) * 4u : kOOB;
+    const unsigned co = (live && cg < 3) ? ((unsigned)xrow * 3u + (unsigned)cg) * 4u : kOOB;
     return bload(src.feats, fo) + (bload(src.xyz, xo) - bload(src.center, co));
   };
 
@@ -664,7 +697,7 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
       const f32x4 hi = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                                      src.feats, (int)(fo + hi_ch), 0, 0));
       const unsigned xo = (c0 && live) ? (unsigned)nb * 12u : kOOB;
-      const unsigned co = (c0 && live) ? (unsigned)(row0 + pr[q]) * 12u : kOOB;
+      const unsigned co = (c0 && live) ? (unsigned)prow[q] * 12u : kOOB;
       const f32x4 x = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                                     src.xyz, (int)xo, 0, 0));
       const f32x4 cc = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
@@ -725,6 +758,22 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
   auto store_dg = [&](int ch) {
     const bool on = ch >= 0;
     const int chs = on ? ch : 0;
+    if constexpr (TP) {
+      // every destination's sum, left by reduce() at its first pair's LDS slot
+      const float* rb = red[(chs - ch0) & 1];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int it = t + NT * j, sl = min(it >> 1, TR * g.k - 1);
+        const int b0 = tsl[sl], e0 = tsl[sl + 1], d = tdl[sl];
+        const bool ok = on && (it >> 1) < TR * g.k && e0 > b0 && d >= 0;
+        const int p0 = tpl[min(b0, TRK - 1)];
+        const float4 v =
+            *reinterpret_cast<const float4*>(rb + max(p0, 0) * kCC + 4 * (it & 1));
+        const unsigned off = ok ? (unsigned)(d * g.c8 + chs * kCC + 4 * (it & 1)) * 4u : kOOB;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(f32x4, v), dg_rs, (int)off,
+                                               0, 0);
+      }
+    } else {
 #pragma unroll
     for (int q = 0; q < PP; ++q) {
       const unsigned off = (on && ps[q] >= 0) ? (unsigned)dg_off(ps[q], chs, rk_total, g.c8) * 4u : kOOB;
@@ -738,6 +787,42 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
     if constexpr (XI) {
       const unsigned off = (on && xsl >= 0) ? (unsigned)(dg_off(xsl, chs, rk_total, g.c8) + xc) * 4u : kOOB;
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, xsh), dg_rs, (int)off, 0, 0);
+    }
+    }
+  };
+  // TP: every destination's pairs of one chunk summed in ascending pair order (LDS only: no
+  // memory operation inside the data-dependent loop, so the load counting stays exact)
+  // (each sum overwrites its first pair's values: no other item reads them)
+  auto reduce = [&](float* rb) {
+    for (int j = 0; j < NJ; ++j) {
+      const int it = t + NT * j;
+      if ((it >> 1) >= TR * g.k) break;
+      const int h4 = (it & 1) * 4;
+      const int b0 = tsl[it >> 1], e0 = tsl[(it >> 1) + 1];
+      if (e0 - b0 <= 1) continue;  // none, or a single pair: its value is its sum
+      auto add = [](float4& a, const float4& x) {
+        a.x = __fadd_rn(a.x, x.x);
+        a.y = __fadd_rn(a.y, x.y);
+        a.z = __fadd_rn(a.z, x.z);
+        a.w = __fadd_rn(a.w, x.w);
+      };
+      float4 v = *reinterpret_cast<const float4*>(rb + tpl[b0] * kCC + h4);
+      int i = b0 + 1;
+      // four pairs' reads in flight per round (the adds stay in pair order): a group is up
+      // to ~K+ pairs and a wave waits for its largest group
+      for (; i + 4 <= e0; i += 4) {
+        const int q0 = tpl[i], q1 = tpl[i + 1], q2 = tpl[i + 2], q3 = tpl[i + 3];
+        const float4 x0 = *reinterpret_cast<const float4*>(rb + q0 * kCC + h4);
+        const float4 x1 = *reinterpret_cast<const float4*>(rb + q1 * kCC + h4);
+        const float4 x2 = *reinterpret_cast<const float4*>(rb + q2 * kCC + h4);
+        const float4 x3 = *reinterpret_cast<const float4*>(rb + q3 * kCC + h4);
+        add(v, x0);
+        add(v, x1);
+        add(v, x2);
+        add(v, x3);
+      }
+      for (; i < e0; ++i) add(v, *reinterpret_cast<const float4*>(rb + tpl[i] * kCC + h4));
+      *reinterpret_cast<float4*>(rb + tpl[b0] * kCC + h4) = v;
     }
   };
   constexpr int SI = NOG - PF > 0 ? NOG - PF - 1 : 0;  // step issuing the last B load
@@ -803,6 +888,9 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
       gather(ch + 1, gn);
       if constexpr (XI) xgn = gather_x(ch + 1);
     }
+    if constexpr (TP) {
+      if (ch > ch0) reduce(red[(ch - 1 - ch0) & 1]);
+    }
     f32x16 acc = zero16();
     float sv[PP][kCC];
     const int prev = ch > ch0 ? ch - 1 : -1;
@@ -816,11 +904,18 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
 #pragma unroll
         for (int cl = 0; cl < 3; ++cl) dcl[(t + NT * q) * 3 + cl] = sv[q][cl];
       }
+      if constexpr (TP) {
+        float4* rp = reinterpret_cast<float4*>(red[buf] + (t + NT * q) * kCC);
+        rp[0] = make_float4(sv[q][0], sv[q][1], sv[q][2], sv[q][3]);
+        rp[1] = make_float4(sv[q][4], sv[q][5], sv[q][6], sv[q][7]);
+      } else {
 #pragma unroll
-      for (int c = 0; c < kCC; ++c) svh[q][c] = sv[q][c];
+        for (int c = 0; c < kCC; ++c) svh[q][c] = sv[q][c];
+      }
     }
     if constexpr (XI) {
       xsh = xs;
+      if constexpr (TP) red[buf][xp * kCC + xc] = xs;
       if (xn >= 0 && c0 == 0 && xc < 3) dcl[xp * 3 + xc] = xs;
     }
     if (more) {
@@ -838,11 +933,14 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
       for (int c = 0; c < kCC; ++c) gv[q][c] = gn[q][c];
     xg = xgn;
   }
-  if (ch0 < ch1) store_dg(ch1 - 1);
+  if (ch0 < ch1) {
+    if constexpr (TP) reduce(red[(ch1 - 1 - ch0) & 1]);
+    store_dg(ch1 - 1);
+  }
   if (ch0 == 0 && t < TR * 3) {
     const int r = t / 3, i = t - (t / 3) * 3;
-    const int row = row0 + r;
-    if (row < g.r) {
+    const int row = grow(r);
+    if (row >= 0) {
       float s = 0.f;
       for (int k = 0; k < g.k; ++k) s = __fadd_rn(s, dcl[(r * g.k + k) * 3 + i]);  // slot p
       dcenter[(long long)row * 3 + i] = -s;
@@ -852,7 +950,7 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
 #pragma unroll
   for (int q = 0; q < PP; ++q) {
     if (pn[q] < 0) continue;
-    const long long pos = (long long)(row0 + pr[q]) * g.k + pk[q];
+    const long long pos = (long long)prow[q] * g.k + pk[q];
     float4* dst = reinterpret_cast<float4*>(dwt_dst + pos * kW);
 #pragma unroll
     for (int v = 0; v < kW / 4; ++v)
@@ -1259,7 +1357,9 @@ bool plan_of(int b, int s, int k, int d, int o, Plan* p) {
   p->wgs = divup(p->nch * p->rs, 8) * 8;  // XCD fill: a multiple of 8 workgroups
   const size_t c16 = (size_t)p->c * kW;
   p->fwd_slab = p->ks > 1 ? align256((size_t)p->ks * p->r * o * 4) : 0;
-  p->dgr = align256((size_t)p->r * k * p->c8 * 4);
+  // dG rows: one per pair, or (tiled) one per (32-row tile, destination): at most 32K per
+  // tile, tiles per batch element
+  p->dgr = align256((size_t)b * divup(s, 32) * 32 * k * p->c8 * 4);
   p->dwt_slab = p->bks > 1 ? align256((size_t)p->bks * p->r * k * kW * 4) : 0;
   p->dwl_slab = p->rs > 1 ? align256((size_t)p->rs * o * c16 * 4) : 0;
   p->wlt = align256((size_t)p->nch * kNC * o * 4);  // swizzled B, padded to whole chunks
@@ -1313,7 +1413,6 @@ hipError_t bwd_data_launch(const Geo& g, const Plan& p, int b, const float* wt, 
   float* dgr = reinterpret_cast<float*>(ws);
   float* dwt_slab = reinterpret_cast<float*>(ws + p.dgr);
   float4* wsw = reinterpret_cast<float4*>(ws + p.dgr + p.dwt_slab + p.dwl_slab);
-  const long long rk = (long long)p.r * g.k;
   const int c16 = g.c * kW;
   const long long nsw = (long long)g.nch * 4 * (O / 8) * 64;
   hipLaunchKernelGGL(pc_swizzle_bwd_kernel, dim3((unsigned)divupll(nsw, 256)), dim3(256), 0, st,
@@ -1322,8 +1421,13 @@ hipError_t bwd_data_launch(const Geo& g, const Plan& p, int b, const float* wt, 
   if (e != hipSuccess) return e;
   // the pipelined kernels store dG through a buffer resource (31-bit byte offsets)
   const bool dg31 = (long long)p.r * g.k * p.c8 * 4 < (1ll << 31);
-  if (bwd_pipe_enabled<KM>() && dg31)
-    hipLaunchKernelGGL((pc_bwd_data_pipe_kernel<O, KM>), dim3(divup(p.r, 32), p.bks), dim3(256),
+  const long long rk = (long long)p.r * g.k;
+  if (g.trow)  // tiled plan (checked by the entry point: dG partial rows fit 31 bits)
+    hipLaunchKernelGGL((pc_bwd_data_pipe_kernel<O, KM, true>),
+                       dim3((unsigned)((long long)b * divup(g.s, 32)), p.bks), dim3(256), 0, st,
+                       g, wt, wsw, dy, dgr, p.bks > 1 ? dwt_slab : dwt, dcenter, p.bcps);
+  else if (bwd_pipe_enabled<KM>() && dg31)
+    hipLaunchKernelGGL((pc_bwd_data_pipe_kernel<O, KM, false>), dim3(divup(p.r, 32), p.bks), dim3(256),
                        0, st, g, wt, wsw, dy, dgr, p.bks > 1 ? dwt_slab : dwt, dcenter, p.bcps);
   else
     hipLaunchKernelGGL((pc_bwd_data_kernel<O, KM>), dim3(divup(p.r, bwd_tile_rows<KM>()), p.bks),
@@ -1387,6 +1491,7 @@ Geo geo_of(int b, int n, int s, int k, int d, const Plan& p, const float* xyz, c
   g.feats = feats;
   g.idx = idx;
   g.rank = nullptr;
+  g.trow = g.tpair = g.tsoff = g.tdst = nullptr;
   return g;
 }
 
@@ -1499,5 +1604,61 @@ KDPC_API int kdpc_pointconv_bwd_weight(int b, int n, int s, int k, int d, int o,
   KDPC_CHECK_ARG(workspace && workspace_bytes >= kdpc_pointconv_bwd_weight_workspace_bytes(b, s, k, d, o));
   const Geo g = geo_of(b, n, s, k, d, p, xyz, center, feats, idx);
   char* ws = reinterpret_cast<char*>(workspace);
+  return (int)KDPC_PC_DISPATCH(bwd_weight_launch, g, p, wt, dy, dwl, ws, st);
+}
+
+// Tiled backward (tile_plan.hip): offsets = the CSR of the plan's partial-row keys over the
+// B*N points (kdpc_csr_build of tkey viewed as (B, ceil(S/32)*32K)), tdst its kdpc_csr_rank.
+namespace {
+bool tiled_ok(int b, int s, int k, const Plan& p) {
+  return (long long)b * divup(s, 32) * 32 * k * p.c8 * 4 < (1ll << 31);
+}
+}  // namespace
+
+KDPC_API int kdpc_pointconv_bwd_data_tiled(int b, int n, int s, int k, int d, int o,
+                                           const float* xyz, const float* center,
+                                           const float* feats, const int* idx, const float* wt,
+                                           const float* wl, const float* dy, const int* offsets,
+                                           const int* trow, const int* tpair, const int* tsoff,
+                                           const int* tdst, float* dxyz, float* dfeats,
+                                           float* dcenter, float* dwt, void* workspace,
+                                           size_t workspace_bytes, void* stream) {
+  Plan p;
+  KDPC_CHECK_ARG(n > 0 && b <= 65535 && plan_of(b, s, k, d, o, &p) && fits_buffers(b, n, s, d) &&
+                 tiled_ok(b, s, k, p));
+  if (p.r == 0)
+    return kdpc_pointconv_bwd_data(b, n, s, k, d, o, xyz, center, feats, idx, wt, wl, dy, offsets,
+                                   nullptr, dxyz, dfeats, dcenter, dwt, workspace,
+                                   workspace_bytes, stream);
+  KDPC_CHECK_ARG(xyz && center && idx && wt && wl && dy && offsets && trow && tpair && tsoff &&
+                 tdst && dcenter && dwt && (d == 0 || (feats && dfeats)));
+  KDPC_CHECK_ARG(workspace && workspace_bytes >= p.dgr + p.dwt_slab + p.dwl_slab + p.wlt);
+  Geo g = geo_of(b, n, s, k, d, p, xyz, center, feats, idx);
+  g.trow = trow, g.tpair = tpair, g.tsoff = tsoff, g.tdst = tdst;
+  char* ws = reinterpret_cast<char*>(workspace);
+  hipStream_t st = (hipStream_t)stream;
+  return (int)KDPC_PC_DISPATCH(bwd_data_launch, g, p, b, wt, wl, dy, offsets, dxyz, dfeats,
+                               dcenter, dwt, ws, st);
+}
+
+KDPC_API int kdpc_pointconv_bwd_tiled(int b, int n, int s, int k, int d, int o, const float* xyz,
+                                      const float* center, const float* feats, const int* idx,
+                                      const float* wt, const float* wl, const float* dy,
+                                      const int* offsets, const int* trow, const int* tpair,
+                                      const int* tsoff, const int* tdst, float* dxyz,
+                                      float* dfeats, float* dcenter, float* dwt, float* dwl,
+                                      void* workspace, size_t workspace_bytes, void* stream) {
+  Plan p;
+  KDPC_CHECK_ARG(n > 0 && b <= 65535 && plan_of(b, s, k, d, o, &p) && fits_buffers(b, n, s, d) &&
+                 tiled_ok(b, s, k, p));
+  KDPC_CHECK_ARG(dwl);
+  const int e = kdpc_pointconv_bwd_data_tiled(b, n, s, k, d, o, xyz, center, feats, idx, wt, wl,
+                                              dy, offsets, trow, tpair, tsoff, tdst, dxyz, dfeats,
+                                              dcenter, dwt, workspace, workspace_bytes, stream);
+  if (e != (int)hipSuccess) return e;
+  hipStream_t st = (hipStream_t)stream;
+  if (p.r == 0) return (int)hipMemsetAsync(dwl, 0, sizeof(float) * o * p.c * kW, st);
+  const Geo g = geo_of(b, n, s, k, d, p, xyz, center, feats, idx);
+  char* ws = reinterpret_cast<char*>(workspace) + p.dgr + p.dwt_slab;
   return (int)KDPC_PC_DISPATCH(bwd_weight_launch, g, p, wt, dy, dwl, ws, st);
 }

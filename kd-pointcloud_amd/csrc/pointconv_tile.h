@@ -30,6 +30,13 @@ struct Geo {
   const float* feats;             // (B,N,D)
   const int* idx;                 // (B,S,K)
   const int* rank;                // (B*S*K) CSR slot of each (row, neighbour) (backward only)
+  // tiled backward (tile_plan.hip; null otherwise): per 32-row tile its global rows
+  // (trow, -1 = none), its pairs sorted by (destination, pair) (tpair), each destination's
+  // first sorted position (tsoff, stride 32K+1) and partial-row slot (tdst, stride 32K)
+  const int* trow;
+  const int* tpair;
+  const int* tsoff;
+  const int* tdst;
 };
 
 __device__ __forceinline__ f32x16 mfma4(float4 a, float4 b, f32x16 c) {

@@ -69,6 +69,10 @@ _SIGNATURES = {
     "kdpc_pointconv_bwd_workspace_bytes": [_c_int] * 5,
     "kdpc_pointconv_bwd": [_c_int] * 6 + [_vp] * 15 + [_c_size, _vp],
     "kdpc_pointconv_bwd_data": [_c_int] * 6 + [_vp] * 14 + [_c_size, _vp],
+    "kdpc_pointconv_bwd_data_tiled": [_c_int] * 6 + [_vp] * 17 + [_c_size, _vp],
+    "kdpc_pointconv_bwd_tiled": [_c_int] * 6 + [_vp] * 18 + [_c_size, _vp],
+    "kdpc_morton_order": [_c_int, _c_int, _vp, _vp, _vp],
+    "kdpc_pc_tile_plan": [_c_int] * 4 + [_vp] * 7,
     "kdpc_pointconv_bwd_weight_workspace_bytes": [_c_int] * 5,
     "kdpc_pointconv_bwd_weight": [_c_int] * 6 + [_vp] * 8 + [_c_size, _vp],
     "kdpc_batchnorm_workspace_bytes": [_c_int, _c_int],
@@ -442,6 +446,90 @@ def csr_rank_of(idx, n):
             csr.rank = _op("kdpc_csr_rank", "csr_rank", _gpu(idx2d, "idx"), csr.offsets,
                            csr.perm, n)
     return csr
+
+
+# ------------------------------------------------------------- tiled PointConv backward
+# The PointConv backward with the dG rows summed per (32-row tile, destination) inside the
+# data kernel (csrc/tile_plan.hip, pointconv_fused.hip): rows of a tile in Morton order of
+# their centers, so their 32K neighbours name few distinct points (self-kNN K=9: ~69 of 288
+# at N=8192).  Used for K <= 9 (the estimators' layers); KDPC_PC_TILED=0 keeps the per-pair
+# rows for A/B runs.
+TILED_PC = os.environ.get("KDPC_PC_TILED", "1") != "0"
+TILED_MAX_K = 9
+
+
+class TilePlan:
+    """Per-tile rows / sorted pairs / destination starts, plus the CSR of the partial rows
+    (offsets over the B*n points, tdst = the partial-row slot of every (tile, destination))."""
+    __slots__ = ("trow", "tpair", "tsoff", "offsets", "tdst", "n")
+
+
+def tiled_supported(idx, center):
+    return TILED_PC and idx.shape[-1] <= TILED_MAX_K and center.shape[1] <= 8192
+
+
+def tile_plan_of(idx, center, n):
+    """The tile plan of idx (B,S,K) over n points with rows ordered by their centers (B,S,3),
+    cached on the index tensor object (a batch prefix takes its parent's tiles)."""
+    tp = getattr(idx, "_kdpc_tplan", None)
+    if tp is not None and tp.n == n:
+        return tp
+    parent = getattr(idx, "_kdpc_parent", None)
+    if parent is not None:
+        pidx, b = parent
+        pp = getattr(pidx, "_kdpc_tplan", None)
+        if pp is not None and pp.n == n:
+            nt = b * ((idx.shape[1] + 31) // 32)
+            tp = TilePlan()
+            tp.trow, tp.tpair, tp.tsoff = pp.trow[:nt], pp.tpair[:nt], pp.tsoff[:nt]
+            tp.offsets, tp.tdst = pp.offsets[:b * n + 1], pp.tdst[:b]
+            tp.n = n
+            idx._kdpc_tplan = tp
+            return tp
+    idx = _gpu(idx, "idx")
+    order = _op("kdpc_morton_order", "morton_order", _gpu(center, "center").contiguous())
+    trow, tpair, tsoff, tkey = _op("kdpc_pc_tile_plan", "pc_tile_plan", idx, order, n)
+    offsets, perm = _op("kdpc_csr_build", "csr_build", tkey, n)
+    tdst = _op("kdpc_csr_rank", "csr_rank", tkey, offsets, perm, n)
+    return attach_tile_plan(idx, n, trow, tpair, tsoff, offsets, tdst.view(tkey.shape))
+
+
+def attach_tile_plan(idx, n, trow, tpair, tsoff, offsets, tdst):
+    """Cache a tile plan built elsewhere (PointConvBidirection.precompute_plan) on idx."""
+    B, S, K = idx.shape
+    nt = B * ((S + 31) // 32)
+    if trow.shape != (nt, 32) or tpair.shape != (nt, 32 * K) or \
+            tsoff.shape != (nt, 32 * K + 1) or offsets.numel() != B * n + 1 or \
+            tdst.numel() != nt * 32 * K:
+        raise ValueError("attach_tile_plan: plan sizes do not match the index tensor")
+    tp = TilePlan()
+    tp.trow, tp.tpair, tp.tsoff, tp.offsets, tp.tdst, tp.n = trow, tpair, tsoff, offsets, tdst, n
+    try:
+        idx._kdpc_tplan = tp
+    except AttributeError:
+        pass
+    return tp
+
+
+def tile_plan_tensors(tp):
+    return [tp.trow, tp.tpair, tp.tsoff, tp.offsets, tp.tdst]
+
+
+def pointconv_bwd_tiled(xyz, center, feats, idx, wt, wl, dy, tp, need_xyz=True, weight=True):
+    """pointconv_bwd / pointconv_bwd_data (weight=False) through a tile plan ->
+    (dxyz|None, dfeats, dcenter, dwt, dwl|None)."""
+    B, N, _ = _gpu(xyz, "xyz").shape
+    S, K = idx.shape[1], idx.shape[2]
+    O, C = wl.shape[0], 3 + feats.shape[2]
+    R = B * S
+    # timed under the untiled entries' labels: the bench's live roofline brackets "the
+    # PointConv backward" whichever C entry point runs it (kdpc_pointconv_bwd(_data)_tiled)
+    entry = "kdpc_pointconv_bwd" if weight else "kdpc_pointconv_bwd_data"
+    return _op(entry, "pointconv_bwd_tiled", xyz, center, feats, idx, wt, wl, dy,
+               tp.offsets, tp.trow, tp.tpair, tp.tsoff, tp.tdst, bool(need_xyz), bool(weight),
+               work=(4 * R * (2 * K * C + 32 * K + (2 if weight else 1) * O) +
+                     (8 if weight else 4) * O * 16 * C,
+                     4.0 * R * K * C * 16 + (4.0 if weight else 2.0) * R * 16 * C * O))
 
 
 def group_rows_grad(grad_out, csr, B, N, C):

@@ -172,8 +172,13 @@ class PointConvBidirection(nn.Module):
                 "est3", "est2", "est1", "est0")
     # the searches whose backward reads the CSR slot of every (row, neighbour) (PointConv and
     # cost-volume backward: csr_rank_of); the 3-NN blends only need offsets / perm (csr_of)
+    # the estimators' self-kNN (K=9): their PointConv backward runs tiled
+    # (kdpc_native.tile_plan_of: rows + tile plan + the CSR of the partial rows) and their
+    # WeightNet backward reads offsets / perm
+    _PLAN_TILED = (frozenset(("est3", "est2", "est1", "est0")) if kdpc_native.TILED_PC
+                   else frozenset())
     _PLAN_RANKED = frozenset(("enc1", "enc2", "enc3", "enc4", "cross3",
-                              "est3", "est2", "est1", "est0"))
+                              "est3", "est2", "est1", "est0")) - _PLAN_TILED
 
     def precompute_plan(self, xyz1, xyz2, csr=True):
         """precompute_fps() plus every coordinate-only kNN search of the forward (PLAN_KNN)
@@ -192,7 +197,7 @@ class PointConvBidirection(nn.Module):
             fps.append(idx)
             x = index_points(x, idx)
             pcs.append(x)
-        knn, nref = {}, {}
+        knn, nref, ctr = {}, {}, {}
         for lv, down in enumerate(downs, start=1):
             knn[f"enc{lv}"] = down.neighbours(pcs[lv - 1], pcs[lv])
             nref[f"enc{lv}"] = pcs[lv - 1].shape[1]
@@ -204,12 +209,16 @@ class PointConvBidirection(nn.Module):
         for lv, est in ((3, self.flow3), (2, self.flow2), (1, self.flow1), (0, self.flow0)):
             knn[f"est{lv}"] = est.neighbours(pcs[lv][:B])
             nref[f"est{lv}"] = pcs[lv].shape[1]
+            ctr[f"est{lv}"] = pcs[lv][:B]
         out = fps + [knn[k] for k in self.PLAN_KNN]
         if csr:
             for k in self.PLAN_KNN:
                 c = (kdpc_native.csr_rank_of(knn[k], nref[k]) if k in self._PLAN_RANKED
                      else kdpc_native.csr_of(knn[k], nref[k]))
                 out += [c.offsets, c.perm] + ([c.rank] if k in self._PLAN_RANKED else [])
+                if k in self._PLAN_TILED:
+                    out += kdpc_native.tile_plan_tensors(
+                        kdpc_native.tile_plan_of(knn[k], ctr[k], nref[k]))
         return out
 
     def _unpack_plan(self, plan, npts):
@@ -239,6 +248,9 @@ class PointConvBidirection(nn.Module):
                 rank = rest[i + 2] if ranked else None
                 i += 3 if ranked else 2
                 kdpc_native.attach_csr(knn[k], nref[k], offsets, perm, rank)
+                if k in self._PLAN_TILED:
+                    kdpc_native.attach_tile_plan(knn[k], nref[k], *rest[i:i + 5])
+                    i += 5
         return plan[:4], knn
 
     def _encode(self, pc, color, fps_idx=None, knn=None):

@@ -381,15 +381,28 @@ class _PointConvLayer(torch.autograd.Function):
     def backward(ctx, gy):
         xyz, center, feats, idx, wt, wl, bias = ctx.saved_tensors
         gy = gy.contiguous()
-        csr = _nat.csr_rank_of(idx, xyz.shape[1])
+        # K <= 9 (the estimators): dG summed per (Morton-ordered row tile, destination) in
+        # the data kernel (kdpc_native.tile_plan_of); else one dG row per pair + the kNN CSR
+        tp = (_nat.tile_plan_of(idx, center, xyz.shape[1])
+              if _nat.tiled_supported(idx, center) else None)
+        csr = _nat.csr_rank_of(idx, xyz.shape[1]) if tp is None else None
         need_b = ctx.needs_input_grad[6]
+        need_x = ctx.needs_input_grad[0]
         if _nat.timing("kdpc_pointconv_bwd"):  # bench's live roofline brackets the whole entry
-            dxyz, dfeats, dcenter, dwt, dwl = _nat.pointconv_bwd(
-                xyz, center, feats, idx, wt, wl, gy, csr, need_xyz=ctx.needs_input_grad[0])
+            if tp is not None:
+                dxyz, dfeats, dcenter, dwt, dwl = _nat.pointconv_bwd_tiled(
+                    xyz, center, feats, idx, wt, wl, gy, tp, need_xyz=need_x)
+            else:
+                dxyz, dfeats, dcenter, dwt, dwl = _nat.pointconv_bwd(
+                    xyz, center, feats, idx, wt, wl, gy, csr, need_xyz=need_x)
             dbias = _nat.colsum(gy.view(-1, gy.shape[-1])) if need_b else None
         else:
-            dxyz, dfeats, dcenter, dwt = _nat.pointconv_bwd_data(
-                xyz, center, feats, idx, wt, wl, gy, csr, need_xyz=ctx.needs_input_grad[0])
+            if tp is not None:
+                dxyz, dfeats, dcenter, dwt, _ = _nat.pointconv_bwd_tiled(
+                    xyz, center, feats, idx, wt, wl, gy, tp, need_xyz=need_x, weight=False)
+            else:
+                dxyz, dfeats, dcenter, dwt = _nat.pointconv_bwd_data(
+                    xyz, center, feats, idx, wt, wl, gy, csr, need_xyz=need_x)
             # the parameter gradients (weight kernel + fixed-order bias column sum) beside the
             # rest of the backward, on the parameter-gradient stream (wgrad.py)
             dwl, dbias = wgrad.run(lambda: (

@@ -547,6 +547,79 @@ std::tuple<c10::optional<Tensor>, Tensor, Tensor, Tensor> pointconv_bwd_data(
   return {need_xyz ? c10::optional<Tensor>(dxyz) : c10::nullopt, dfeats, dcenter, dwt};
 }
 
+// ---- tiled PointConv backward (tile_plan.hip)
+Tensor morton_order(Tensor xyz) {
+  dev(xyz, kF, "xyz");
+  TORCH_CHECK(xyz.dim() == 3 && xyz.size(2) == 3 && xyz.size(1) <= 8192,
+              "kdpc: morton_order expects (B,S<=8192,3)");
+  GUARD(xyz);
+  Tensor order = at::empty({xyz.size(0), xyz.size(1)}, xyz.options().dtype(at::kInt));
+  check(kdpc_morton_order(xyz.size(0), xyz.size(1), F(xyz), I(order), stream_of(xyz)),
+        "morton_order");
+  return order;
+}
+
+std::tuple<Tensor, Tensor, Tensor, Tensor> pc_tile_plan(Tensor idx, c10::optional<Tensor> order,
+                                                        int64_t n) {
+  dev(idx, kI, "idx");
+  TORCH_CHECK(idx.dim() == 3, "kdpc: pc_tile_plan expects idx (B,S,K)");
+  const int64_t b = idx.size(0), s = idx.size(1), k = idx.size(2);
+  const int* op = nullptr;
+  if (order.has_value()) {
+    dev(*order, kI, "order"), same_device(idx, *order, "order");
+    TORCH_CHECK(order->numel() == b * s, "kdpc: pc_tile_plan: order must be (B,S)");
+    op = I(*order);
+  }
+  GUARD(idx);
+  const int64_t t = b * ((s + 31) / 32), trk = 32 * k;
+  auto io = idx.options();
+  Tensor trow = at::empty({t, 32}, io), tpair = at::empty({t, trk}, io);
+  Tensor tsoff = at::empty({t, trk + 1}, io), tkey = at::empty({b, t / std::max<int64_t>(b, 1) * trk}, io);
+  check(kdpc_pc_tile_plan(b, s, n, k, I(idx), op, I(trow), I(tpair), I(tsoff), I(tkey),
+                          stream_of(idx)),
+        "pc_tile_plan");
+  return {trow, tpair, tsoff, tkey};
+}
+
+std::tuple<c10::optional<Tensor>, Tensor, Tensor, Tensor, c10::optional<Tensor>> pointconv_bwd_tiled(
+    Tensor xyz, Tensor center, Tensor feats, Tensor idx, Tensor wt, Tensor wl, Tensor dy,
+    Tensor offsets, Tensor trow, Tensor tpair, Tensor tsoff, Tensor tdst, bool need_xyz,
+    bool weight) {
+  for (auto* t : {&xyz, &center, &feats, &wt, &wl, &dy}) dev(*t, kF, "pointconv input");
+  for (auto* t : {&idx, &offsets, &trow, &tpair, &tsoff, &tdst}) dev(*t, kI, "tile plan");
+  GUARD(xyz);
+  const int64_t b = xyz.size(0), n = xyz.size(1), s = idx.size(1), k = idx.size(2);
+  const int64_t d = feats.size(2), o = wl.size(0), c = 3 + d;
+  const int64_t tiles = b * ((s + 31) / 32);
+  TORCH_CHECK(offsets.numel() >= b * n + 1 && trow.numel() >= tiles * 32 &&
+                  tpair.numel() >= tiles * 32 * k && tsoff.numel() >= tiles * (32 * k + 1) &&
+                  tdst.numel() >= tiles * 32 * k,
+              "kdpc: pointconv_bwd_tiled: the tile plan does not match idx");
+  const size_t nb = kdpc_pointconv_bwd_workspace_bytes(b, s, k, d, o);
+  TORCH_CHECK(nb > 0, "kdpc: pointconv_bwd_tiled: invalid sizes");
+  Tensor ws = workspace(nb, xyz);
+  Tensor dxyz = need_xyz ? empty_f({b, n, 3}, xyz) : Tensor();
+  Tensor dfeats = empty_f({b, n, d}, xyz);
+  Tensor dcenter = empty_f({b, s, 3}, xyz);
+  Tensor dwt = empty_f({b, s, k, 16}, xyz);
+  Tensor dwl = weight ? empty_f({o, 16 * c}, xyz) : Tensor();
+  if (weight)
+    check(kdpc_pointconv_bwd_tiled(b, n, s, k, d, o, F(xyz), F(center), F(feats), I(idx), F(wt),
+                                   F(wl), F(dy), I(offsets), I(trow), I(tpair), I(tsoff),
+                                   I(tdst), need_xyz ? F(dxyz) : nullptr, F(dfeats), F(dcenter),
+                                   F(dwt), F(dwl), ws.data_ptr(), nb, stream_of(xyz)),
+          "pointconv_bwd_tiled");
+  else
+    check(kdpc_pointconv_bwd_data_tiled(b, n, s, k, d, o, F(xyz), F(center), F(feats), I(idx),
+                                        F(wt), F(wl), F(dy), I(offsets), I(trow), I(tpair),
+                                        I(tsoff), I(tdst), need_xyz ? F(dxyz) : nullptr,
+                                        F(dfeats), F(dcenter), F(dwt), ws.data_ptr(), nb,
+                                        stream_of(xyz)),
+          "pointconv_bwd_data_tiled");
+  return {need_xyz ? c10::optional<Tensor>(dxyz) : c10::nullopt, dfeats, dcenter, dwt,
+          weight ? c10::optional<Tensor>(dwl) : c10::nullopt};
+}
+
 Tensor pointconv_bwd_weight(Tensor xyz, Tensor center, Tensor feats, Tensor idx, Tensor wt,
                             Tensor dy, int64_t o) {
   for (auto* t : {&xyz, &center, &feats, &wt, &dy}) dev(*t, kF, "pointconv input");
@@ -952,6 +1025,11 @@ TORCH_LIBRARY(kdpc, m) {
         "-> (Tensor?, Tensor, Tensor, Tensor)");
   m.def("pointconv_bwd_weight(Tensor xyz, Tensor center, Tensor feats, Tensor idx, Tensor wt, "
         "Tensor dy, int o) -> Tensor");
+  m.def("morton_order(Tensor xyz) -> Tensor");
+  m.def("pc_tile_plan(Tensor idx, Tensor? order, int n) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("pointconv_bwd_tiled(Tensor xyz, Tensor center, Tensor feats, Tensor idx, Tensor wt, "
+        "Tensor wl, Tensor dy, Tensor offsets, Tensor trow, Tensor tpair, Tensor tsoff, "
+        "Tensor tdst, bool need_xyz, bool weight) -> (Tensor?, Tensor, Tensor, Tensor, Tensor?)");
   m.def("pointconv_contract_fwd(Tensor xyz, Tensor center, Tensor feats, Tensor idx, "
         "Tensor wt) -> Tensor");
   m.def("pointconv_contract_bwd(Tensor xyz, Tensor center, Tensor feats, Tensor idx, "
@@ -1021,6 +1099,9 @@ TORCH_LIBRARY_IMPL(kdpc, CUDA, m) {
   m.impl("pointconv_bwd", pointconv_bwd);
   m.impl("pointconv_bwd_data", pointconv_bwd_data);
   m.impl("pointconv_bwd_weight", pointconv_bwd_weight);
+  m.impl("morton_order", morton_order);
+  m.impl("pc_tile_plan", pc_tile_plan);
+  m.impl("pointconv_bwd_tiled", pointconv_bwd_tiled);
   m.impl("pointconv_contract_fwd", pointconv_contract_fwd);
   m.impl("pointconv_contract_bwd", pointconv_contract_bwd);
   m.impl("weightnet_fwd", weightnet_fwd);

@@ -436,3 +436,115 @@ def test_weightnet_bwd_rel_equals_whole(b, n, s, k):
     assert none is None
     assert torch.equal(drel, drel2)
     assert torch.equal(dflat, dflat2)
+
+
+def _tiled_inputs(b, n, s, k, d, o, knn, seed):
+    import pointconv_util as P
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    xyz = torch.rand(b, n, 3, generator=g).to(DEV)
+    center = xyz[:, :s].contiguous()
+    if knn:
+        idx = P._as_idx32(P.knn_point(k, xyz, center)).contiguous()
+    else:  # random neighbours, repeats within a row included
+        idx = torch.randint(0, n, (b, s, k), generator=g, dtype=torch.int32).to(DEV)
+    feats = torch.randn(b, n, d, generator=g).to(DEV)
+    wt = torch.randn(b, s, k, 16, generator=g).to(DEV)
+    wl = (torch.randn(o, 16 * (3 + d), generator=g) / (16 * (3 + d)) ** 0.5).to(DEV)
+    dy = torch.randn(b, s, o, generator=g).to(DEV)
+    return xyz, center, feats, idx, wt, wl, dy
+
+
+@pytest.mark.parametrize("b,n,s,k,d,o,knn,morton", [
+    (2, 2048, 2048, 9, 125, 128, True, True), (2, 1024, 1024, 9, 61, 128, True, False),
+    (2, 2048, 2048, 9, 125, 128, True, False),
+    (3, 700, 333, 9, 61, 256, False, True), (1, 300, 300, 5, 0, 64, True, True),
+    (2, 2048, 512, 16, 67, 64, True, True), (1, 100, 37, 1, 4, 64, False, True),
+    (2, 8192, 8192, 9, 128, 128, True, True)])
+def test_pointconv_bwd_tiled(b, n, s, k, d, o, knn, morton):
+    """The tiled backward (dG summed per (row tile, destination) in the data kernel, then per
+    point through the partial rows' CSR): dwt, dcenter and dwl bit-equal to the untiled entry
+    points (same per-pair arithmetic), dxyz / dfeats within 1e-5 of the tensor scale of an
+    fp64 evaluation, and run-to-run bit-identical.  Morton-ordered and identity row tiles,
+    kNN and random (repeating) neighbours, S not a multiple of 32, K up to 16."""
+    import kdpc_native as K
+    xyz, center, feats, idx, wt, wl, dy = _tiled_inputs(b, n, s, k, d, o, knn, n + k + d)
+    if morton:
+        tp = K.tile_plan_of(idx, center, n)
+    else:
+        trow, tpair, tsoff, tkey = K.load_ops().pc_tile_plan(idx, None, n)
+        offsets, perm = K.load_ops().csr_build(tkey, n)
+        tdst = K.load_ops().csr_rank(tkey, offsets, perm, n)
+        tp = K.attach_tile_plan(idx, n, trow, tpair, tsoff, offsets, tdst.view(tkey.shape))
+    got = K.pointconv_bwd_tiled(xyz, center, feats, idx, wt, wl, dy, tp)
+    again = K.pointconv_bwd_tiled(xyz, center, feats, idx, wt, wl, dy, tp)
+    data = K.pointconv_bwd_tiled(xyz, center, feats, idx, wt, wl, dy, tp, weight=False)
+    ref = K.pointconv_bwd(xyz, center, feats, idx, wt, wl, dy, K.csr_rank_of(idx, n))
+    for name, a, c in zip(["dxyz", "dfeats", "dcenter", "dwt", "dwl"], got, again):
+        assert torch.equal(a, c), ("run-to-run", name)
+    for name, a, c in zip(["dxyz", "dfeats", "dcenter", "dwt"], got, data):
+        assert torch.equal(a, c), ("data half", name)
+    for name, i in (("dcenter", 2), ("dwl", 4)):
+        assert torch.equal(got[i], ref[i]), name
+    # dwt of a pair is summed over its channels by one thread, or -- for the tile's 32K-256
+    # left-over pairs -- by 8 lanes and a butterfly: a row's tile position picks the order,
+    # so Morton-ordered tiles round some pairs differently (the untiled kernel does the same
+    # under any row permutation); identity-ordered tiles are bit-identical
+    if morton:
+        _scale_close(got[3], ref[3], rtol=1e-6, name="dwt")
+    else:
+        assert torch.equal(got[3], ref[3]), "dwt"
+    X, F = xyz.double().requires_grad_(True), feats.double().requires_grad_(True)
+    il = idx.long()
+    bi = torch.arange(b, device=DEV).view(b, 1, 1)
+    G = torch.cat([X[bi, il] - center.double().unsqueeze(2), F[bi, il]], dim=-1)
+    A = torch.matmul(G.transpose(2, 3), wt.double()).reshape(b, s, -1)
+    (A @ wl.double().t()).backward(dy.double())
+    _scale_close(got[0], X.grad, name="dxyz")
+    if d:
+        _scale_close(got[1], F.grad, name="dfeats")
+
+
+def test_tile_plan_structure():
+    """kdpc_morton_order is a per-element permutation sorted by the Morton code of its
+    centers; kdpc_pc_tile_plan's tiles hold those rows, every valid pair exactly once sorted
+    by (destination, pair), and destination groups that match the partial-row CSR."""
+    import kdpc_native as K
+    b, n, s, k = 2, 500, 333, 9
+    xyz, center, _, idx, _, _, _ = _tiled_inputs(b, n, s, k, 4, 64, True, 7)
+    ops = K.load_ops()
+    order = ops.morton_order(center).cpu().numpy()
+    c = center.cpu().numpy()
+    for e in range(b):
+        assert sorted(order[e].tolist()) == list(range(s))
+        lo, hi = c[e].min(0), c[e].max(0)
+        q = np.clip(np.floor((c[e] - lo) * (np.float32(64) / (hi - lo))), 0, 63).astype(np.int64)
+        code = np.zeros(s, np.int64)
+        for bit in range(6):
+            for dd in range(3):
+                code |= ((q[:, dd] >> bit) & 1) << (3 * bit + dd)
+        assert (np.diff(code[order[e]]) >= 0).all()
+    tp = K.tile_plan_of(idx, center, n)
+    trow, tpair, tsoff = (t.cpu().numpy() for t in (tp.trow, tp.tpair, tp.tsoff))
+    offsets, tdst = tp.offsets.cpu().numpy(), tp.tdst.cpu().numpy().reshape(-1)
+    il = idx.cpu().numpy().reshape(b * s, k)
+    tb = (s + 31) // 32
+    seen = np.zeros(b * n + 1, np.int64)
+    for t in range(b * tb):
+        e, rows = t // tb, trow[t]
+        want_rows = [e * s + r for r in order[e][(t % tb) * 32:(t % tb) * 32 + 32]]
+        assert rows[:len(want_rows)].tolist() == want_rows and (rows[len(want_rows):] == -1).all()
+        pairs = [(il[rows[p // k], p % k], p) for p in range(32 * k) if rows[p // k] >= 0]
+        pairs.sort()
+        nv = len(pairs)
+        assert tpair[t][:nv].tolist() == [p for _, p in pairs] and (tpair[t][nv:] == -1).all()
+        dests = sorted(set(j for j, _ in pairs))
+        for sl, j in enumerate(dests):
+            beg, end = tsoff[t][sl], tsoff[t][sl + 1]
+            assert all(pairs[i][0] == j for i in range(beg, end))
+            assert end - beg == sum(1 for jj, _ in pairs if jj == j)
+            pos = tdst[t * 32 * k + sl]
+            assert offsets[e * n + j] <= pos < offsets[e * n + j + 1]
+            seen[e * n + j] += 1
+        assert (tsoff[t][len(dests):] == nv).all()
+        assert (tdst[t * 32 * k + len(dests):(t + 1) * 32 * k] == -1).all()
+    assert (np.diff(offsets) == seen[:-1]).all()

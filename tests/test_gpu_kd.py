@@ -144,7 +144,8 @@ def test_coordinate_plan_equals_inline_searches():
     p1, p2, fl = _batch(2, 8192, 51)
     plan = base.precompute_plan(p1, p2)
     nk = len(PointConvBidirection.PLAN_KNN)
-    assert len(plan) == 4 + nk + sum(3 if k in PointConvBidirection._PLAN_RANKED else 2
+    assert len(plan) == 4 + nk + sum((3 if k in PointConvBidirection._PLAN_RANKED else 2) +
+                                     (5 if k in PointConvBidirection._PLAN_TILED else 0)
                                      for k in PointConvBidirection.PLAN_KNN)
     runs = []
     for pre in (None, base.precompute_fps(p1, p2), [t.clone() for t in plan]):

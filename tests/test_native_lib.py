@@ -161,6 +161,8 @@ TORCH_OPS = {
     "dense_tn_small": "kdpc_dense_tn_small", "dense_small": "kdpc_dense_small",
     "neg_sum_k": "kdpc_neg_sum_k",
     "copy_segments": "kdpc_copy_segments",
+    "morton_order": "kdpc_morton_order", "pc_tile_plan": "kdpc_pc_tile_plan",
+    "pointconv_bwd_tiled": "kdpc_pointconv_bwd_tiled",
     "dense_small_out": "kdpc_dense_small",
 }
 
