@@ -188,9 +188,13 @@ class LaunchTimer:
     torch stream (the stream the kernel runs on) and accumulates per-launch algorithmic
     bytes/flops supplied by the op wrappers.  Used by bench.py for the live roofline."""
 
-    def __init__(self, names):
+    def __init__(self, names, lead_cycles=0):
         self.names = set(names)
         self.records = []  # (name, start_event, end_event, bytes, flops)
+        # a GPU spin of this many cycles before each bracketed launch: the host then enqueues
+        # the start event, the entry's kernels and the end event while the GPU is busy, so a
+        # host-bound step's issue gaps do not land inside the bracket
+        self.lead_cycles = lead_cycles
 
     def summary(self):
         torch.cuda.synchronize()
@@ -258,6 +262,8 @@ def _op(entry, op, *args, work=None):
     if t is not None and entry in t.names:
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
+        if t.lead_cycles:
+            torch.cuda._sleep(t.lead_cycles)
         e0.record()
         out = fn(*args)
         e1.record()

@@ -6,7 +6,9 @@ For each roofline object in the bench line (the headline `roofline`, `kd_step.ro
 `configs1.*`, `roofline_knn`, ...): rocprof per-launch duration = the summed durations of its
 entry's HIP kernels / launches of its first kernel, next to the live HIP-event average
 (avg_launch_us).  Profile a single-section bench command (`--sections train`, `kd`,
-`configs1` or `knn`): the rocprof sums cover every launch in the process.
+`configs1` or `knn`): the rocprof sums cover every launch in the process, except for the
+train / KD entries, which count the launches inside the measurement window bench.py marks
+with two spin kernels (torch.cuda._sleep).
 """
 import csv
 import glob
@@ -34,6 +36,11 @@ def main():
                 pass
     trace = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)[0]
     rows = list(csv.DictReader(open(trace)))
+    # bench.py brackets the train / KD sections' measurement steps with spin kernels: their
+    # entries are compared on the launches inside that window only
+    spins = sorted(int(x["Start_Timestamp"]) for x in rows if "spin_kernel" in x["Kernel_Name"])
+    window = (spins[0], spins[-1]) if len(spins) >= 2 else None  # (bench also spins before
+    # every bracketed launch: those lie inside the window)
     out = {}
 
     def objs(d, path):
@@ -46,6 +53,8 @@ def main():
     for key, r in objs(line or {}, ""):
         kernels = bench.ROOFLINE[r["kernel"]][3]
         sel = rows
+        if window and key in ("roofline", "kd_step.roofline"):
+            sel = [x for x in rows if window[0] < int(x["Start_Timestamp"]) < window[1]]
         wgs = r.get("grid_workgroups")
         if wgs:  # one entry timed at two shapes in one run (gather C=3 / C=64): by grid size
             sel = [x for x in rows if int(x["Grid_Size_X"]) * int(x["Grid_Size_Y"]) *
