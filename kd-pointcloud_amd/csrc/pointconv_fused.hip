@@ -235,7 +235,13 @@ __global__ __launch_bounds__(256) void pc_slab_sum_kernel(int nslabs, long long 
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < len;
        e += (long long)gridDim.x * blockDim.x) {
     float v = 0.f;
-    for (int s = 0; s < nslabs; ++s) v = __fadd_rn(v, slab[(long long)s * len + e]);
+    int s = 0;
+    for (; s + 4 <= nslabs; s += 4) {  // four slabs' loads in flight, adds in slab order
+      const float x0 = slab[(long long)s * len + e], x1 = slab[(long long)(s + 1) * len + e];
+      const float x2 = slab[(long long)(s + 2) * len + e], x3 = slab[(long long)(s + 3) * len + e];
+      v = __fadd_rn(__fadd_rn(__fadd_rn(__fadd_rn(v, x0), x1), x2), x3);
+    }
+    for (; s < nslabs; ++s) v = __fadd_rn(v, slab[(long long)s * len + e]);
     if (bias) v = __fadd_rn(v, bias[e % o]);
     dst[e] = v;
   }

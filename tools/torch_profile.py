@@ -67,6 +67,10 @@ def main():
         rows.sort(reverse=True)
         for t, c, k, st in rows[:120]:
             f.write(f"{t:9.1f} {c:6.1f} {k:28s} {st}\n")
+        f.write("\n\n==== by call site, most launches first\n")
+        rows.sort(key=lambda x: -x[1])
+        for t, c, k, st in rows[:120]:
+            f.write(f"{t:9.1f} {c:6.1f} {k:28s} {st}\n")
     print("wrote", args.out)
 
 
