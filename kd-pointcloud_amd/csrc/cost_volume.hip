@@ -198,8 +198,8 @@ __global__ __launch_bounds__(256) void cost_volume_fwd_kernel(
 // Row-per-lane (direction gradients): lane l32 = neighbour row, the two halves split the
 // channels.  D_IN = 32: the halves of L split the rows and the dW1 rows, nothing idles.
 
-template <int D_IN, int D_OUT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D_IN == 32 ? 2 : 1)))
+template <int D_IN, int D_OUT, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 void cost_volume_bwd_kernel(
     int n1, int n2, int k, int queries_per_wave, const float* __restrict__ x1,
     const float* __restrict__ x2, const int* __restrict__ idx, const float* __restrict__ p1,
@@ -471,12 +471,12 @@ constexpr int kFwdQPW = 8;
 // backward queries per wave: as many waves as the chip holds at the kernel's occupancy, in
 // ONE round (16 per wave at 8192 waves left the D=32 kernel -- 5 waves per SIMD by its
 // registers -- a 60 %-full second round); at least 2 queries per wave for the pipeline
-template <int DI, int DO>
+template <int DI, int DO, int W>
 int bwd_waves_resident() {
   static const int w = [] {
     int blocks = 0, dev = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, cost_volume_bwd_kernel<DI, DO>, 256,
-                                                     0) != hipSuccess || blocks < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, cost_volume_bwd_kernel<DI, DO, W>,
+                                                     256, 0) != hipSuccess || blocks < 1)
       blocks = 1;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
@@ -487,15 +487,34 @@ int bwd_waves_resident() {
   return w;
 }
 
-inline int bwd_waves_resident_of(int din, int dout) {
-  if (din == 32 && dout == 32) return bwd_waves_resident<32, 32>();
-  if (din == 32 && dout == 64) return bwd_waves_resident<32, 64>();
-  if (din == 64 && dout == 32) return bwd_waves_resident<64, 32>();
-  return bwd_waves_resident<64, 64>();
+// waves per SIMD the kernel is compiled for: 2 for D_IN = 32 (183 VGPRs), 1 for D_IN = 64;
+// KDPC_CV_BWD_WPE=3|4 picks a higher-occupancy build of the D = 32 kernel (A/B runs: the
+// compiler then spills to reach 168 / 128 VGPRs)
+template <int DI>
+constexpr int bwd_wpe_default() { return DI == 32 ? 2 : 1; }
+
+inline int bwd_wpe_env() {
+  static const int w = [] {
+    const char* v = getenv("KDPC_CV_BWD_WPE");
+    return v && (v[0] == '3' || v[0] == '4') ? v[0] - '0' : 0;
+  }();
+  return w;
 }
 
-inline int bwd_qpw(int b, int n1, int din, int dout) {
-  return std::max(2, (int)divupll((long long)b * n1, bwd_waves_resident_of(din, dout)));
+template <int DI, int DO, int W>
+inline int bwd_qpw(int b, int n1) {
+  return std::max(2, (int)divupll((long long)b * n1, bwd_waves_resident<DI, DO, W>()));
+}
+
+inline int bwd_qpw_of(int b, int n1, int din, int dout) {
+  if (din == 32 && dout == 32) {
+    if (bwd_wpe_env() == 3) return bwd_qpw<32, 32, 3>(b, n1);
+    if (bwd_wpe_env() == 4) return bwd_qpw<32, 32, 4>(b, n1);
+    return bwd_qpw<32, 32, 2>(b, n1);
+  }
+  if (din == 32 && dout == 64) return bwd_qpw<32, 64, 2>(b, n1);
+  if (din == 64 && dout == 32) return bwd_qpw<64, 32, 1>(b, n1);
+  return bwd_qpw<64, 64, 1>(b, n1);
 }
 
 inline int slab_len(int din, int dout) { return dout * din + dout + 4 * din; }
@@ -511,16 +530,16 @@ hipError_t fwd_launch(int b, int n1, int n2, int k, const float* x1, const float
   return hipGetLastError();
 }
 
-template <int DI, int DO>
-hipError_t bwd_launch(int b, int n1, int n2, int k, const float* x1, const float* x2,
-                      const int* idx, const float* p1, const float* p2, const float* wpos,
-                      const float* bpos, const float* w1, const float* out,
-                      const unsigned char* amax, const float* dout, float* dp1, float* dp2_rows,
-                      float* dx1, float* ddir_rows, const int* rank, float* rows, float* slab,
-                      float* dparams, hipStream_t st) {
-  const int qpw = bwd_qpw(b, n1, DI, DO);
+template <int DI, int DO, int W>
+hipError_t bwd_launch_w(int b, int n1, int n2, int k, const float* x1, const float* x2,
+                        const int* idx, const float* p1, const float* p2, const float* wpos,
+                        const float* bpos, const float* w1, const float* out,
+                        const unsigned char* amax, const float* dout, float* dp1,
+                        float* dp2_rows, float* dx1, float* ddir_rows, const int* rank,
+                        float* rows, float* slab, float* dparams, hipStream_t st) {
+  const int qpw = bwd_qpw<DI, DO, W>(b, n1);
   dim3 grid(divup(n1, kWaves * qpw), b);
-  hipLaunchKernelGGL((cost_volume_bwd_kernel<DI, DO>), grid, dim3(256), 0, st, n1, n2, k,
+  hipLaunchKernelGGL((cost_volume_bwd_kernel<DI, DO, W>), grid, dim3(256), 0, st, n1, n2, k,
                      qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, dout, dp1,
                      dp2_rows, dx1, ddir_rows, rank, rows, slab);
   hipError_t e = hipGetLastError();
@@ -530,56 +549,107 @@ hipError_t bwd_launch(int b, int n1, int n2, int k, const float* x1, const float
   return colsum(nslab, len, slab, dparams, slab + (size_t)nslab * len, st);
 }
 
+template <int DI, int DO>
+hipError_t bwd_launch(int b, int n1, int n2, int k, const float* x1, const float* x2,
+                      const int* idx, const float* p1, const float* p2, const float* wpos,
+                      const float* bpos, const float* w1, const float* out,
+                      const unsigned char* amax, const float* dout, float* dp1, float* dp2_rows,
+                      float* dx1, float* ddir_rows, const int* rank, float* rows, float* slab,
+                      float* dparams, hipStream_t st) {
+#define KDPC_CV_BWD_ARGS b, n1, n2, k, x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, dout, dp1, \
+                         dp2_rows, dx1, ddir_rows, rank, rows, slab, dparams, st
+  if constexpr (DI == 32 && DO == 32) {
+    if (bwd_wpe_env() == 3) return bwd_launch_w<32, 32, 3>(KDPC_CV_BWD_ARGS);
+    if (bwd_wpe_env() == 4) return bwd_launch_w<32, 32, 4>(KDPC_CV_BWD_ARGS);
+  }
+  return bwd_launch_w<DI, DO, bwd_wpe_default<DI>()>(KDPC_CV_BWD_ARGS);
+#undef KDPC_CV_BWD_ARGS
+}
+
 // Per-point sums of the ranked rows: key e = b*N2 + j owns the contiguous slots
 // [offsets[e], offsets[e+1]) (ascending position: the CSR order of every other gather-sum,
 // so dP2 / dx2 are bit-identical to summing the (n, k)-ordered rows through perm).
 // One thread per (key, 4-column chunk) of the D+4 wide rows; chunk D/4 is d(dir) -> dx2.
-constexpr int kSumU = 8;
 __device__ __forceinline__ float4 vadd(float4 a, float4 b) {
   return make_float4(__fadd_rn(a.x, b.x), __fadd_rn(a.y, b.y), __fadd_rn(a.z, b.z),
                      __fadd_rn(a.w, b.w));
 }
+// The sums stream the rows through LDS: a workgroup owns KB consecutive keys,
+// whose segments are one contiguous run of rows; windows of WR rows are read with
+// contiguous float4 loads (the whole workgroup, 16 per thread, the next window in flight
+// while this one is summed) into LDS, then every (key, chunk) thread adds the rows of its
+// segment inside the window in ascending
+// order (round 4; the round-3 kernel, one thread per (key, chunk) reading rows straight from
+// memory, read each row as 144-byte pieces of ~7 segments per load instruction and waited on
+// its longest segment per wave: ~2.6 TB/s at cross0).
 template <int D>
-__global__ __launch_bounds__(256) void cv_rows_sum_kernel(long long nkeys,
-                                                          const float* __restrict__ rows,
-                                                          const int* __restrict__ offsets,
-                                                          float* __restrict__ dp2,
-                                                          float* __restrict__ dx2) {
+__global__ __launch_bounds__(256) void cv_rows_sum_lds_kernel(long long nkeys,
+                                                              const float* __restrict__ rows,
+                                                              const int* __restrict__ offsets,
+                                                              float* __restrict__ dp2,
+                                                              float* __restrict__ dx2) {
   constexpr int CH = D / 4 + 1;
+  constexpr int KB = 256 / CH;          // keys per workgroup
+  constexpr int WR = 4096 / CH;         // rows per LDS window (64 KiB)
+  __shared__ float4 win[WR * CH];
   const float4* src = reinterpret_cast<const float4*>(rows);
-  const long long total = nkeys * CH;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (long long)gridDim.x * blockDim.x) {
-    const long long key = e / CH;
-    const int ch = (int)(e - key * CH);
-    const int j0 = offsets[key], j1 = offsets[key + 1];
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    int j = j0;
-    for (; j + kSumU <= j1; j += kSumU) {
-      float4 v[kSumU];
+  const long long k0 = (long long)blockIdx.x * KB;
+  const int t = threadIdx.x;
+  const int kl = t / CH, ch = t - (t / CH) * CH;
+  const long long key = k0 + kl;
+  const bool mine = kl < KB && key < nkeys;
+  const long long kend = std::min<long long>(k0 + KB, nkeys);
+  const int s0 = offsets[k0], s1 = offsets[kend];
+  const int j0 = mine ? offsets[key] : 0, j1 = mine ? offsets[key + 1] : 0;
+  constexpr int NPT = (WR * CH + 255) / 256;  // float4 loads per thread and window
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 nx[NPT];  // the next window, in flight while the current one is summed
+  auto fetch = [&](int w) {
+    const long long base = (long long)w * CH;
+    const int n = min(WR, s1 - w) * CH;
 #pragma unroll
-      for (int u = 0; u < kSumU; ++u) v[u] = src[(long long)(j + u) * CH + ch];
+    for (int q = 0; q < NPT; ++q) {
+      const int i = t + 256 * q;
+      nx[q] = i < n ? src[base + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  if (s0 < s1) fetch(s0);
+  for (int w = s0; w < s1; w += WR) {
+    const int nr = min(WR, s1 - w);
 #pragma unroll
-      for (int u = 0; u < kSumU; ++u) acc = vadd(acc, v[u]);
+    for (int q = 0; q < NPT; ++q)
+      if (t + 256 * q < WR * CH) win[t + 256 * q] = nx[q];
+    __syncthreads();
+    if (w + WR < s1) fetch(w + WR);
+    const int a = max(j0, w) - w, b = min(j1, w + nr) - w;
+    int j = a;
+    for (; j + 8 <= b; j += 8) {  // eight rows' LDS reads in flight, adds in row order
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = win[(j + u) * CH + ch];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = vadd(acc, v[u]);
     }
-    for (; j < j1; ++j) acc = vadd(acc, src[(long long)j * CH + ch]);
-    if (ch < D / 4) {
-      reinterpret_cast<float4*>(dp2)[key * (D / 4) + ch] = acc;
-    } else {
-      float* o = dx2 + key * 3;
-      o[0] = acc.x;
-      o[1] = acc.y;
-      o[2] = acc.z;
-    }
+    for (; j < b; ++j) acc = vadd(acc, win[j * CH + ch]);
+    __syncthreads();
+  }
+  if (!mine) return;
+  if (ch < D / 4) {
+    reinterpret_cast<float4*>(dp2)[key * (D / 4) + ch] = acc;
+  } else {
+    float* o = dx2 + key * 3;
+    o[0] = acc.x;
+    o[1] = acc.y;
+    o[2] = acc.z;
   }
 }
 
 template <int D>
 hipError_t rows_sum_launch(long long nkeys, const float* rows, const int* offsets, float* dp2,
                            float* dx2, hipStream_t st) {
-  const long long work = nkeys * (D / 4 + 1);
-  hipLaunchKernelGGL((cv_rows_sum_kernel<D>),
-                     dim3((unsigned)std::min<long long>(divupll(work, 256), 1 << 20)), dim3(256),
+  constexpr int KB = 256 / (D / 4 + 1);
+  if (nkeys <= 0) return hipSuccess;
+  hipLaunchKernelGGL((cv_rows_sum_lds_kernel<D>), dim3((unsigned)divupll(nkeys, KB)), dim3(256),
                      0, st, nkeys, rows, offsets, dp2, dx2);
   return hipGetLastError();
 }
@@ -660,7 +730,7 @@ KDPC_API size_t kdpc_cost_volume_bwd_workspace_bytes(int b, int n1, int din, int
   if (b <= 0 || n1 <= 0 || !supported(din, dout, 1)) return 0;
   if (!narrow(din, dout, 1))
     return cost_volume_wide_fused_bwd_workspace_floats(b, n1, din) * sizeof(float);
-  const long long nslabs = (long long)divup(n1, kWaves * bwd_qpw(b, n1, din, dout)) * b;
+  const long long nslabs = (long long)divup(n1, kWaves * bwd_qpw_of(b, n1, din, dout)) * b;
   const int len = slab_len(din, dout);
   return (size_t)(nslabs * len + colsum_scratch_floats((int)nslabs, len)) * sizeof(float);
 }
