@@ -210,7 +210,6 @@ void cost_volume_bwd_kernel(
     float* __restrict__ ddir_rows, const int* __restrict__ rank, float* __restrict__ rows,
     float* __restrict__ slab) {
   constexpr int LD = D_IN + 1;            // odd row stride: row-per-lane reads hit 32 banks
-  constexpr int RS = D_IN + 4;            // ranked row: dP2 (D_IN) | d(dir) (3) | 0
   constexpr int RPP = 64 / D_IN;          // layout-L rows per pass
   constexpr int RT = kRows / RPP;         // layout-L passes
   constexpr int TI = D_IN / 32;           // 32-column tiles of dh0
@@ -258,6 +257,9 @@ void cost_volume_bwd_kernel(
   // ranked rows (rank != null): row (n, r) goes to slot rank[n, r] of the CSR of idx, so the
   // per-point sums read each segment contiguously (cv_rows_sum_kernel)
   const bool ranked = rank != nullptr;
+  // ranked rows: dP2 rows (P, D_IN) -- whole 128 / 256-byte lines -- then the d(dir) rows
+  // (P, 4) (round 3 interleaved them as (P, D_IN + 4): every 144-byte row straddled lines)
+  float* dirs = ranked ? rows + (long long)gridDim.y * n1 * k * D_IN : nullptr;
   const __amdgpu_buffer_rsrc_t rkr = rsrc_of(ranked ? rank + (long long)b * n1 * k : idx,
                                              ranked ? (long long)n1 * k * 4 : 0);
 
@@ -378,7 +380,7 @@ void cost_volume_bwd_kernel(
       if (ranked) {
         const int sa = __builtin_amdgcn_readlane(rkv, r0);
         const int slot = RPP == 2 ? (sub ? __builtin_amdgcn_readlane(rkv, r0 + 1) : sa) : sa;
-        if (slot >= 0) rows[(long long)slot * RS + c] = v;
+        if (slot >= 0) rows[(long long)slot * D_IN + c] = v;
       } else {
         dp2n[r * D_IN] = v;
       }
@@ -408,7 +410,7 @@ void cost_volume_bwd_kernel(
     const bool row = lane < k;  // lanes >= 32 never (k <= 32)
     if (row && ranked) {
       if (rkv >= 0)
-        *reinterpret_cast<float4*>(rows + (long long)rkv * RS + D_IN) = make_float4(g0, g1, g2, 0.f);
+        *reinterpret_cast<float4*>(dirs + (long long)rkv * 4) = make_float4(g0, g1, g2, 0.f);
     } else if (row) {
       float* dd = ddir_rows + (((long long)b * n1 + n) * k + lane) * 3;
       dd[0] = g0;
@@ -585,6 +587,7 @@ __device__ __forceinline__ float4 vadd(float4 a, float4 b) {
 template <int D>
 __global__ __launch_bounds__(256) void cv_rows_sum_lds_kernel(long long nkeys,
                                                               const float* __restrict__ rows,
+                                                              const float* __restrict__ dirs,
                                                               const int* __restrict__ offsets,
                                                               float* __restrict__ dp2,
                                                               float* __restrict__ dx2) {
@@ -592,7 +595,9 @@ __global__ __launch_bounds__(256) void cv_rows_sum_lds_kernel(long long nkeys,
   constexpr int KB = 256 / CH;          // keys per workgroup
   constexpr int WR = 4096 / CH;         // rows per LDS window (64 KiB)
   __shared__ float4 win[WR * CH];
+  constexpr int DQ = D / 4;
   const float4* src = reinterpret_cast<const float4*>(rows);
+  const float4* srd = reinterpret_cast<const float4*>(dirs);
   const long long k0 = (long long)blockIdx.x * KB;
   const int t = threadIdx.x;
   const int kl = t / CH, ch = t - (t / CH) * CH;
@@ -604,21 +609,25 @@ __global__ __launch_bounds__(256) void cv_rows_sum_lds_kernel(long long nkeys,
   constexpr int NPT = (WR * CH + 255) / 256;  // float4 loads per thread and window
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   float4 nx[NPT];  // the next window, in flight while the current one is summed
+  // window element i < nr*DQ: dP2 chunk i % DQ of row i / DQ; then the nr d(dir) rows
   auto fetch = [&](int w) {
-    const long long base = (long long)w * CH;
-    const int n = min(WR, s1 - w) * CH;
+    const int nr = min(WR, s1 - w);
 #pragma unroll
     for (int q = 0; q < NPT; ++q) {
       const int i = t + 256 * q;
-      nx[q] = i < n ? src[base + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      nx[q] = i < nr * DQ ? src[(long long)w * DQ + i]
+                          : (i < nr * CH ? srd[w + (i - nr * DQ)] : make_float4(0.f, 0.f, 0.f, 0.f));
     }
   };
   if (s0 < s1) fetch(s0);
   for (int w = s0; w < s1; w += WR) {
     const int nr = min(WR, s1 - w);
 #pragma unroll
-    for (int q = 0; q < NPT; ++q)
-      if (t + 256 * q < WR * CH) win[t + 256 * q] = nx[q];
+    for (int q = 0; q < NPT; ++q) {
+      const int i = t + 256 * q;
+      if (i < nr * CH)
+        win[i < nr * DQ ? (i / DQ) * CH + i % DQ : (i - nr * DQ) * CH + DQ] = nx[q];
+    }
     __syncthreads();
     if (w + WR < s1) fetch(w + WR);
     const int a = max(j0, w) - w, b = min(j1, w + nr) - w;
@@ -645,22 +654,22 @@ __global__ __launch_bounds__(256) void cv_rows_sum_lds_kernel(long long nkeys,
 }
 
 template <int D>
-hipError_t rows_sum_launch(long long nkeys, const float* rows, const int* offsets, float* dp2,
-                           float* dx2, hipStream_t st) {
+hipError_t rows_sum_launch(long long nkeys, const float* rows, const float* dirs,
+                           const int* offsets, float* dp2, float* dx2, hipStream_t st) {
   constexpr int KB = 256 / (D / 4 + 1);
   if (nkeys <= 0) return hipSuccess;
   hipLaunchKernelGGL((cv_rows_sum_lds_kernel<D>), dim3((unsigned)divupll(nkeys, KB)), dim3(256),
-                     0, st, nkeys, rows, offsets, dp2, dx2);
+                     0, st, nkeys, rows, dirs, offsets, dp2, dx2);
   return hipGetLastError();
 }
 
-hipError_t rows_sum(int din, long long nkeys, const float* rows, const int* offsets, float* dp2,
-                    float* dx2, hipStream_t st) {
+hipError_t rows_sum(int din, long long nkeys, const float* rows, const float* dirs,
+                    const int* offsets, float* dp2, float* dx2, hipStream_t st) {
   switch (din) {
-    case 32: return rows_sum_launch<32>(nkeys, rows, offsets, dp2, dx2, st);
-    case 64: return rows_sum_launch<64>(nkeys, rows, offsets, dp2, dx2, st);
-    case 128: return rows_sum_launch<128>(nkeys, rows, offsets, dp2, dx2, st);
-    case 256: return rows_sum_launch<256>(nkeys, rows, offsets, dp2, dx2, st);
+    case 32: return rows_sum_launch<32>(nkeys, rows, dirs, offsets, dp2, dx2, st);
+    case 64: return rows_sum_launch<64>(nkeys, rows, dirs, offsets, dp2, dx2, st);
+    case 128: return rows_sum_launch<128>(nkeys, rows, dirs, offsets, dp2, dx2, st);
+    case 256: return rows_sum_launch<256>(nkeys, rows, dirs, offsets, dp2, dx2, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -788,5 +797,6 @@ KDPC_API int kdpc_cost_volume_bwd_csr(int b, int n1, int n2, int k, int din, int
                               amax, dout_grad, dp1, nullptr, dx1, nullptr, rank, rows, slab,
                               dparams, st);
   if (e != hipSuccess) return (int)e;
-  return (int)rows_sum(din, (long long)b * n2, rows, offsets, dp2, dx2, st);
+  return (int)rows_sum(din, (long long)b * n2, rows, rows + (size_t)b * n1 * k * din, offsets, dp2,
+                       dx2, st);
 }

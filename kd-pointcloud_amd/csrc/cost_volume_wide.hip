@@ -433,7 +433,7 @@ __global__ __launch_bounds__(2 * D) void cvw_fused_bwd_kernel(
     float* __restrict__ ddir_rows, const int* __restrict__ rank, float* __restrict__ rows,
     float* __restrict__ slab) {
   using G = WideGeo<D>;
-  constexpr int RS = D + 4;  // ranked row: dP2 (D) | d(dir) (3) | 0 (cost_volume.hip)
+  // ranked rows: dP2 rows (P, D), then d(dir) rows (P, 4) (cost_volume.hip)
   using W = WideBwd<D>;
   constexpr int NG2 = G::NT / 32;  // channel groups of the direction pass
   constexpr int CPG = D / NG2;     // channels per group
@@ -601,7 +601,7 @@ __global__ __launch_bounds__(2 * D) void cvw_fused_bwd_kernel(
         const float4 v = *reinterpret_cast<const float4*>(H + r * G::LD + 4 * c4);
         const float4 dr = dirs[p][r];
         if (ranked) {
-          if (r < k && rk[i] >= 0) *reinterpret_cast<float4*>(rows + (long long)rk[i] * RS + 4 * c4) = v;
+          if (r < k && rk[i] >= 0) *reinterpret_cast<float4*>(rows + (long long)rk[i] * D + 4 * c4) = v;
         } else if (r < k) {
           *reinterpret_cast<float4*>(d2 + (long long)r * D) = v;
         }
@@ -676,7 +676,8 @@ __global__ __launch_bounds__(2 * D) void cvw_fused_bwd_kernel(
       const bool row = l32 < k;
       if (row && ranked) {
         if (rkd >= 0)
-          *reinterpret_cast<float4*>(rows + (long long)rkd * RS + D) = make_float4(v.x, v.y, v.z, 0.f);
+          *reinterpret_cast<float4*>(rows + (long long)b * n1 * k * D + (long long)rkd * 4) =
+              make_float4(v.x, v.y, v.z, 0.f);
       } else if (row) {
         float* dd = ddir_rows + ((long long)q * k + l32) * 3;
         dd[0] = v.x;
