@@ -61,7 +61,13 @@ __device__ __forceinline__ unsigned long long wave_argmax_key(unsigned hi, unsig
   return ((unsigned long long)vmax << 32) | lbest;
 }
 
-template <int BLOCK, int PPT, bool LDS_XYZ>
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// FULL: every thread owns exactly PPT points (N = T * PPT, T = BLOCK; the model's 8192 ->
+// 2048 case): no ownership selects, and the distance of two points at a time on packed f32
+// ops (v_pk_add / v_pk_mul / v_pk_fma: the same IEEE operations per element as dist3, so the
+// same bits).  The step is VALU-bound: ~11 -> ~7 instructions per point.
+template <int BLOCK, int PPT, bool LDS_XYZ, bool FULL>
 __global__ __launch_bounds__(BLOCK) void fps_kernel(int n, int m, int T, int log2T,
                                                     const float* __restrict__ xyz,
                                                     float* __restrict__ temp,
@@ -109,15 +115,36 @@ __global__ __launch_bounds__(BLOCK) void fps_kernel(int n, int m, int T, int log
   for (int j = 1; j < m; ++j) {
     float best = -1.f;
     int bestk = 0;
+    if constexpr (FULL) {
+      const f32x2 X = {x1, x1}, Y = {y1, y1}, Z = {z1, z1};
 #pragma unroll
-    for (int p = 0; p < PPT; ++p) {
-      const float d = dist3(x1, y1, z1, px[p], py[p], pz[p]);
-      const float d2 = fminf(d, pt[p]);
-      const bool own = tid < T && tid + p * T < n;
-      pt[p] = own ? d2 : pt[p];
-      const bool better = own && d2 > best;
-      bestk = better ? tid + p * T : bestk;
-      best = better ? d2 : best;
+      for (int q = 0; q < PPT / 2; ++q) {
+        const f32x2 dx = f32x2{px[2 * q], px[2 * q + 1]} - X;
+        const f32x2 dy = f32x2{py[2 * q], py[2 * q + 1]} - Y;
+        const f32x2 dz = f32x2{pz[2 * q], pz[2 * q + 1]} - Z;
+        const f32x2 d =
+            __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {  // points in the reference's scan order
+          const int p = 2 * q + e;
+          const float d2 = fminf(d[e], pt[p]);
+          pt[p] = d2;
+          const bool better = d2 > best;
+          bestk = better ? tid + p * T : bestk;
+          best = better ? d2 : best;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < PPT; ++p) {
+        const float d = dist3(x1, y1, z1, px[p], py[p], pz[p]);
+        const float d2 = fminf(d, pt[p]);
+        const bool own = tid < T && tid + p * T < n;
+        pt[p] = own ? d2 : pt[p];
+        const bool better = own && d2 > best;
+        bestk = better ? tid + p * T : bestk;
+        best = better ? d2 : best;
+      }
     }
     const unsigned hi = best >= 0.f ? __float_as_uint(best) : 0u;
     const unsigned lo = best >= 0.f ? (tiekey | (unsigned)bestk) : 0u;
@@ -204,16 +231,27 @@ hipError_t launch_reg(int b, int n, int m, int T, int log2T, const float* xyz, f
                       int* idx, hipStream_t st) {
   const size_t slot_bytes = 2 * kMaxSlots * sizeof(unsigned long long);
   const size_t lds = slot_bytes + (size_t)n * 3 * sizeof(float);
+  const bool full = PPT % 2 == 0 && T == BLOCK && n == T * PPT;
   if (lds <= 160 * 1024) {
-    auto k = fps_kernel<BLOCK, PPT, true>;
     // once per process and instantiation (thread-safe static initialisation)
-    static const hipError_t attr =
-        hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    static const hipError_t attr = [] {
+      hipError_t e = hipFuncSetAttribute((const void*)fps_kernel<BLOCK, PPT, true, false>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      if (e == hipSuccess && PPT % 2 == 0)
+        e = hipFuncSetAttribute((const void*)fps_kernel<BLOCK, PPT, true, PPT % 2 == 0>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      return e;
+    }();
     if (attr != hipSuccess) return attr;
-    hipLaunchKernelGGL(k, dim3(b), dim3(BLOCK), lds, st, n, m, T, log2T, xyz, temp, idx);
+    if (full)
+      hipLaunchKernelGGL((fps_kernel<BLOCK, PPT, true, PPT % 2 == 0>), dim3(b), dim3(BLOCK), lds,
+                         st, n, m, T, log2T, xyz, temp, idx);
+    else
+      hipLaunchKernelGGL((fps_kernel<BLOCK, PPT, true, false>), dim3(b), dim3(BLOCK), lds, st, n,
+                         m, T, log2T, xyz, temp, idx);
   } else {
-    hipLaunchKernelGGL((fps_kernel<BLOCK, PPT, false>), dim3(b), dim3(BLOCK), slot_bytes, st, n,
-                       m, T, log2T, xyz, temp, idx);
+    hipLaunchKernelGGL((fps_kernel<BLOCK, PPT, false, false>), dim3(b), dim3(BLOCK), slot_bytes,
+                       st, n, m, T, log2T, xyz, temp, idx);
   }
   return hipGetLastError();
 }
