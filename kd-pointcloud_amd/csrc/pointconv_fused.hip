@@ -1313,6 +1313,20 @@ inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 inline int km_of(int k) { return k <= 9 ? 9 : 16; }
 
 // every gathered table must be addressable by a 31-bit byte offset (buffer loads)
+// CUs the weight half may fill when it runs on its own stream (kdpc_pointconv_bwd_weight):
+// its workgroups hold 90-158 KB of LDS each, one per CU for the whole kernel, so a launch
+// sized for all 256 CUs shuts the main stream's kernels out until it finishes (round-4
+// trace: a 17 us BatchNorm reduction waited 458 us behind the level-0 weight kernel).
+// KDPC_PC_WGT_CUS overrides (A/B runs).
+inline int side_weight_cus() {
+  static const int w = [] {
+    const char* v = getenv("KDPC_PC_WGT_CUS");
+    const int x = v ? atoi(v) : 0;
+    return x >= 8 && x <= kCUs ? x : kCUs;
+  }();
+  return w;
+}
+
 inline bool fits_buffers(long long b, long long n, long long s, int d) {
   const long long lim = 1ll << 31;
   return b * n * 4 * std::max(d, 3) < lim && b * s * 12 < lim;
@@ -1324,7 +1338,7 @@ void channel_split(int nch, int tiles, int* ks, int* cps) {
   *ks = divup(nch, *cps);
 }
 
-bool plan_of(int b, int s, int k, int d, int o, Plan* p) {
+bool plan_of(int b, int s, int k, int d, int o, Plan* p, int wcus = kCUs) {
   if (b < 0 || s < 0 || k < 1 || k > kKMax || d < 0 || !(o == 64 || o == 128 || o == 256))
     return false;
   const long long r = (long long)b * s;
@@ -1345,10 +1359,10 @@ bool plan_of(int b, int s, int k, int d, int o, Plan* p) {
   // slower.  (round 1, unpipelined: 2-3 co-resident workgroups per CU ran slower than one.)
   const int trw = km_of(k) <= 9 ? (o == 256 ? 32 : 64) : (o == 64 ? 64 : 32);
   const int t32 = std::max(1, divup(p->r, trw));
-  const int cap = std::max(1, std::min(t32, kCUs / p->nch));
+  const int cap = std::max(1, std::min(t32, wcus / p->nch));
   auto cost = [&](int rs) {
     const int rps = divup(t32, rs);
-    const int per = divup(p->nch * divup(t32, rps), kCUs);
+    const int per = divup(p->nch * divup(t32, rps), wcus);
     return (double)per * (rps + 2);  // + the pipeline's prologue
   };
   int best = 1, best8 = 0;
@@ -1570,7 +1584,7 @@ KDPC_API int kdpc_pointconv_bwd(int b, int n, int s, int k, int d, int o, const 
 
 KDPC_API size_t kdpc_pointconv_bwd_weight_workspace_bytes(int b, int s, int k, int d, int o) {
   Plan p;
-  return plan_of(b, s, k, d, o, &p) ? std::max<size_t>(p.dwl_slab, 256) : 0;
+  return plan_of(b, s, k, d, o, &p, side_weight_cus()) ? std::max<size_t>(p.dwl_slab, 256) : 0;
 }
 
 KDPC_API int kdpc_pointconv_bwd_data(int b, int n, int s, int k, int d, int o, const float* xyz,
@@ -1603,7 +1617,7 @@ KDPC_API int kdpc_pointconv_bwd_weight(int b, int n, int s, int k, int d, int o,
                                        const float* wt, const float* dy, float* dwl,
                                        void* workspace, size_t workspace_bytes, void* stream) {
   Plan p;
-  KDPC_CHECK_ARG(n > 0 && b <= 65535 && plan_of(b, s, k, d, o, &p) && fits_buffers(b, n, s, d));
+  KDPC_CHECK_ARG(n > 0 && b <= 65535 && plan_of(b, s, k, d, o, &p, side_weight_cus()) && fits_buffers(b, n, s, d));
   hipStream_t st = (hipStream_t)stream;
   if (p.r == 0) return (int)hipMemsetAsync(dwl, 0, sizeof(float) * o * p.c * kW, st);
   KDPC_CHECK_ARG(xyz && center && idx && wt && dy && dwl && (d == 0 || feats));
