@@ -332,6 +332,14 @@ int kdpc_pointconv_bwd_weight(int b, int n, int s, int k, int d, int o, const fl
  *   (T*32K) the destinations (-1 padded).  offsets / tdst = kdpc_csr_build / kdpc_csr_rank
  *   of tkey viewed as (B, ceil(S/32)*32K) over N keys. */
 int kdpc_morton_order(int b, int s, const float *xyz, int *order, void *stream);
+/* kdpc_pointconv_fwd with the rows of each 64-row tile taken from a tile plan's trow (two
+ * consecutive 32-row tiles; ntrow = its entry count): the same outputs bit for bit, the
+ * neighbour gathers of a tile spatially close.  K must be 9 or 16. */
+int kdpc_pointconv_fwd_tiled(int b, int n, int s, int k, int d, int o, const float *xyz,
+                             const float *center, const float *feats, const int *idx,
+                             const float *wt, const float *wl, const float *bias,
+                             const int *trow, int ntrow, float *y, void *workspace,
+                             size_t workspace_bytes, void *stream);
 int kdpc_pc_tile_plan(int b, int s, int n, int k, const int *idx, const int *order, int *trow,
                       int *tpair, int *tsoff, int *tkey, void *stream);
 int kdpc_pointconv_bwd_data_tiled(int b, int n, int s, int k, int d, int o, const float *xyz,

@@ -41,7 +41,10 @@ namespace {
 // ------------------------------------------------------------------------------ forward
 // grid (row tiles, channel splits); a split > 1 writes a partial tile to slab[split].
 // 256 threads.  Tile = 32*MT rows; output tiles 32x32 spread over the 4 waves.
-template <int O, int KM, bool EX>
+// TP: the tile's rows come from the backward's tile plan (g.trow: Morton-ordered 32-row
+// tiles, two per 64-row forward tile), so a tile's neighbour gathers hit few distinct points;
+// every row's arithmetic is unchanged (bit-identical outputs).
+template <int O, int KM, bool EX, bool TP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 void pc_fwd_kernel(Geo g, const float* __restrict__ wt, const float* __restrict__ wl,
                    const float* __restrict__ bias, float* __restrict__ y,
@@ -60,6 +63,14 @@ void pc_fwd_kernel(Geo g, const float* __restrict__ wt, const float* __restrict_
   __shared__ __attribute__((aligned(16))) float al[MT][(kNC / 4) * kBlk];
 
   const int row0 = blockIdx.x * TM;
+  // global row of tile row r, -1 for none
+  auto grow = [&](int r) -> int {
+    if constexpr (TP) {
+      return row0 + r < g.ntrow ? g.trow[row0 + r] : -1;
+    } else {
+      return row0 + r < g.r ? row0 + r : -1;
+    }
+  };
   const int kk = EX ? KM : g.k;  // exact-K instantiation: constant trip counts
   const int split = blockIdx.y;
   const int ch0 = split * chunks_per_split;
@@ -77,10 +88,10 @@ void pc_fwd_kernel(Geo g, const float* __restrict__ wt, const float* __restrict_
   float wr[RPT][KM];
 #pragma unroll
   for (int q = 0; q < RPT; ++q) {
-    const int row = row0 + rr + 16 * q;
+    const int row = grow(rr + 16 * q);
 #pragma unroll
     for (int k = 0; k < KM; ++k)
-      wr[q][k] = (row < g.r && k < kk) ? wt[((long long)row * kk + k) * kW + w] : 0.f;
+      wr[q][k] = (row >= 0 && k < kk) ? wt[((long long)row * kk + k) * kW + w] : 0.f;
   }
   const Srcs src = srcs_of(g);
   // gather slots: (row, neighbour) rk = (t >> 1) + 128 i, channels 4*h4 .. 4*h4+3 of the
@@ -92,11 +103,12 @@ void pc_fwd_kernel(Geo g, const float* __restrict__ wt, const float* __restrict_
   for (int i = 0; i < GS; ++i) {
     const int rk = (t >> 1) + 128 * i;
     const int r = rk / kk;
-    const int nb = rk < tk ? nbr_of(g, row0 + r, rk - r * kk) : -1;
+    const int row = rk < tk ? grow(r) : -1;
+    const int nb = row >= 0 ? nbr_of(g, row, rk - r * kk) : -1;
     nbf[i] = feat_off(g, nb);
     float v[4];
 #pragma unroll
-    for (int e2 = 0; e2 < 4; ++e2) v[e2] = g_fetch(g, src, nb, row0 + r, ch0 * kCC + 4 * h4 + e2);
+    for (int e2 = 0; e2 < 4; ++e2) v[e2] = g_fetch(g, src, nb, row, ch0 * kCC + 4 * h4 + e2);
     gr[i] = make_float4(v[0], v[1], v[2], v[3]);
   }
   f32x16 acc[MPW][NPW];
@@ -216,8 +228,8 @@ void pc_fwd_kernel(Geo g, const float* __restrict__ wt, const float* __restrict_
     for (int i = 0; i < MPW; ++i)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int row = row0 + (m0 + i) * 32 + (e & 3) + 8 * (e >> 2) + 4 * half;
-        if (row < g.r) {
+        const int row = grow((m0 + i) * 32 + (e & 3) + 8 * (e >> 2) + 4 * half);
+        if (row >= 0) {
           if (slab)
             slab[((long long)split * g.r + row) * O + n] = acc[i][j][e];
           else
@@ -1397,12 +1409,18 @@ hipError_t slab_sum(int nslabs, long long len, const float* slab, const float* b
 template <int O, int KM>
 hipError_t fwd_launch(const Geo& g, const Plan& p, const float* wt, const float* wl,
                       const float* bias, float* y, float* slab, hipStream_t st) {
-  if (g.k == KM)
-    hipLaunchKernelGGL((pc_fwd_kernel<O, KM, true>), dim3(p.rt, p.ks), dim3(256), 0, st, g, wt, wl,
-                       bias, y, p.ks > 1 ? slab : nullptr, p.cps);
-  else
-    hipLaunchKernelGGL((pc_fwd_kernel<O, KM, false>), dim3(p.rt, p.ks), dim3(256), 0, st, g, wt, wl,
-                       bias, y, p.ks > 1 ? slab : nullptr, p.cps);
+  float* sl = p.ks > 1 ? slab : nullptr;
+  if (g.trow) {  // tiled plan: exact-K only (the estimators' K = 9)
+    const unsigned rt = (unsigned)divup(g.ntrow, p.tm);
+    hipLaunchKernelGGL((pc_fwd_kernel<O, KM, true, true>), dim3(rt, p.ks), dim3(256), 0, st, g,
+                       wt, wl, bias, y, sl, p.cps);
+  } else if (g.k == KM) {
+    hipLaunchKernelGGL((pc_fwd_kernel<O, KM, true, false>), dim3(p.rt, p.ks), dim3(256), 0, st, g,
+                       wt, wl, bias, y, sl, p.cps);
+  } else {
+    hipLaunchKernelGGL((pc_fwd_kernel<O, KM, false, false>), dim3(p.rt, p.ks), dim3(256), 0, st,
+                       g, wt, wl, bias, y, sl, p.cps);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || p.ks == 1) return e;
   return slab_sum(p.ks, (long long)p.r * O, slab, bias, O, y, st);
@@ -1512,6 +1530,7 @@ Geo geo_of(int b, int n, int s, int k, int d, const Plan& p, const float* xyz, c
   g.idx = idx;
   g.rank = nullptr;
   g.trow = g.tpair = g.tsoff = g.tdst = nullptr;
+  g.ntrow = 0;
   return g;
 }
 
@@ -1681,4 +1700,26 @@ KDPC_API int kdpc_pointconv_bwd_tiled(int b, int n, int s, int k, int d, int o, 
   const Geo g = geo_of(b, n, s, k, d, p, xyz, center, feats, idx);
   char* ws = reinterpret_cast<char*>(workspace) + p.dgr + p.dwt_slab;
   return (int)KDPC_PC_DISPATCH(bwd_weight_launch, g, p, wt, dy, dwl, ws, st);
+}
+
+// Forward through the backward's tile plan (rows of each 64-row tile = two consecutive
+// 32-row plan tiles): same outputs as kdpc_pointconv_fwd, bit for bit.  K must be 9 or 16
+// (the exact-K kernels); trow (ntrow = tiles * 32 entries) from kdpc_pc_tile_plan.
+KDPC_API int kdpc_pointconv_fwd_tiled(int b, int n, int s, int k, int d, int o, const float* xyz,
+                                      const float* center, const float* feats, const int* idx,
+                                      const float* wt, const float* wl, const float* bias,
+                                      const int* trow, int ntrow, float* y, void* workspace,
+                                      size_t workspace_bytes, void* stream) {
+  Plan p;
+  KDPC_CHECK_ARG(n > 0 && b <= 65535 && plan_of(b, s, k, d, o, &p) && fits_buffers(b, n, s, d));
+  KDPC_CHECK_ARG(k == km_of(k) && ntrow >= 0 && ntrow == b * divup(s, 32) * 32);
+  if (p.r == 0) return (int)hipSuccess;
+  KDPC_CHECK_ARG(xyz && center && idx && wt && wl && bias && y && trow && (d == 0 || feats));
+  KDPC_CHECK_ARG(workspace_bytes >= p.fwd_slab && (p.fwd_slab == 0 || workspace));
+  Geo g = geo_of(b, n, s, k, d, p, xyz, center, feats, idx);
+  g.trow = trow;
+  g.ntrow = ntrow;
+  float* slab = reinterpret_cast<float*>(workspace);
+  hipStream_t st = (hipStream_t)stream;
+  return (int)KDPC_PC_DISPATCH(fwd_launch, g, p, wt, wl, bias, y, slab, st);
 }

@@ -37,6 +37,7 @@ struct Geo {
   const int* tpair;
   const int* tsoff;
   const int* tdst;
+  int ntrow;  // entries of trow (tiles * 32)
 };
 
 __device__ __forceinline__ f32x16 mfma4(float4 a, float4 b, f32x16 c) {

@@ -66,6 +66,7 @@ _SIGNATURES = {
     "kdpc_pointconv_supported": [_c_int] * 3,
     "kdpc_pointconv_fwd_workspace_bytes": [_c_int] * 5,
     "kdpc_pointconv_fwd": [_c_int] * 6 + [_vp] * 9 + [_c_size, _vp],
+    "kdpc_pointconv_fwd_tiled": [_c_int] * 6 + [_vp] * 8 + [_c_int, _vp, _vp, _c_size, _vp],
     "kdpc_pointconv_bwd_workspace_bytes": [_c_int] * 5,
     "kdpc_pointconv_bwd": [_c_int] * 6 + [_vp] * 15 + [_c_size, _vp],
     "kdpc_pointconv_bwd_data": [_c_int] * 6 + [_vp] * 14 + [_c_size, _vp],
@@ -461,6 +462,8 @@ def csr_rank_of(idx, n):
 # at N=8192).  Used for K <= 9 (the estimators' layers); KDPC_PC_TILED=0 keeps the per-pair
 # rows for A/B runs.
 TILED_PC = os.environ.get("KDPC_PC_TILED", "1") != "0"
+# the forward through the same row tiles (bit-identical; KDPC_PC_TILED_FWD=0 for A/B)
+TILED_FWD = TILED_PC and os.environ.get("KDPC_PC_TILED_FWD", "1") != "0"
 TILED_MAX_K = 9
 
 
@@ -519,6 +522,17 @@ def attach_tile_plan(idx, n, trow, tpair, tsoff, offsets, tdst):
 
 def tile_plan_tensors(tp):
     return [tp.trow, tp.tpair, tp.tsoff, tp.offsets, tp.tdst]
+
+
+def pointconv_fwd_tiled(xyz, center, feats, idx, wt, wl, bias, tp):
+    """pointconv_fwd with the rows of each tile from the tile plan tp (bit-identical)."""
+    B, N, _ = _gpu(xyz, "xyz").shape
+    S, K = idx.shape[1], idx.shape[2]
+    O, C = wl.shape[0], 3 + feats.shape[2]
+    R = B * S
+    return _op("kdpc_pointconv_fwd", "pointconv_fwd_tiled", xyz, center, feats, idx, wt, wl,
+               bias, tp.trow, work=(4 * R * (K + K * C + 16 * K + O) + 4 * O * 16 * C,
+                                    2.0 * R * K * C * 16 + 2.0 * R * 16 * C * O))
 
 
 def pointconv_bwd_tiled(xyz, center, feats, idx, wt, wl, dy, tp, need_xyz=True, weight=True):

@@ -375,6 +375,11 @@ class _PointConvLayer(torch.autograd.Function):
     @staticmethod
     def forward(ctx, xyz, center, feats, idx, wt, wl, bias):
         ctx.save_for_backward(xyz, center, feats, idx, wt, wl, bias)
+        if _nat.TILED_FWD and _nat.tiled_supported(idx, center) and \
+                idx.shape[-1] == _nat.TILED_MAX_K:
+            # the backward's Morton-ordered row tiles: the same rows, spatially close gathers
+            tp = _nat.tile_plan_of(idx, center, xyz.shape[1])
+            return _nat.pointconv_fwd_tiled(xyz, center, feats, idx, wt, wl, bias, tp)
         return _nat.pointconv_fwd(xyz, center, feats, idx, wt, wl, bias)
 
     @staticmethod

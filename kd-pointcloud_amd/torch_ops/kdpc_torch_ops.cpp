@@ -498,6 +498,26 @@ Tensor pointconv_fwd(Tensor xyz, Tensor center, Tensor feats, Tensor idx, Tensor
   return y;
 }
 
+Tensor pointconv_fwd_tiled(Tensor xyz, Tensor center, Tensor feats, Tensor idx, Tensor wt,
+                           Tensor wl, Tensor bias, Tensor trow) {
+  for (auto* t : {&xyz, &center, &feats, &wt, &wl, &bias}) dev(*t, kF, "pointconv input");
+  dev(idx, kI, "idx"), dev(trow, kI, "trow");
+  GUARD(xyz);
+  const int64_t b = xyz.size(0), n = xyz.size(1), s = idx.size(1), k = idx.size(2);
+  const int64_t d = feats.size(2), o = wl.size(0);
+  TORCH_CHECK(kdpc_pointconv_supported(k, d, o), "kdpc: pointconv shape (K=", k, ", D=", d,
+              ", O=", o, ") not supported");
+  TORCH_CHECK(trow.numel() == b * ((s + 31) / 32) * 32, "kdpc: pointconv_fwd_tiled: trow size");
+  const size_t nb = kdpc_pointconv_fwd_workspace_bytes(b, s, k, d, o);
+  Tensor ws = workspace(nb, xyz);
+  Tensor y = empty_f({b, s, o}, xyz);
+  check(kdpc_pointconv_fwd_tiled(b, n, s, k, d, o, F(xyz), F(center), F(feats), I(idx), F(wt),
+                                 F(wl), F(bias), I(trow), (int)trow.numel(), F(y), ws.data_ptr(),
+                                 nb, stream_of(xyz)),
+        "pointconv_fwd_tiled");
+  return y;
+}
+
 std::tuple<c10::optional<Tensor>, Tensor, Tensor, Tensor, Tensor> pointconv_bwd(
     Tensor xyz, Tensor center, Tensor feats, Tensor idx, Tensor wt, Tensor wl, Tensor dy,
     Tensor offsets, Tensor rank, bool need_xyz) {
@@ -1026,6 +1046,8 @@ TORCH_LIBRARY(kdpc, m) {
   m.def("pointconv_bwd_weight(Tensor xyz, Tensor center, Tensor feats, Tensor idx, Tensor wt, "
         "Tensor dy, int o) -> Tensor");
   m.def("morton_order(Tensor xyz) -> Tensor");
+  m.def("pointconv_fwd_tiled(Tensor xyz, Tensor center, Tensor feats, Tensor idx, Tensor wt, "
+        "Tensor wl, Tensor bias, Tensor trow) -> Tensor");
   m.def("pc_tile_plan(Tensor idx, Tensor? order, int n) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("pointconv_bwd_tiled(Tensor xyz, Tensor center, Tensor feats, Tensor idx, Tensor wt, "
         "Tensor wl, Tensor dy, Tensor offsets, Tensor trow, Tensor tpair, Tensor tsoff, "
@@ -1100,6 +1122,7 @@ TORCH_LIBRARY_IMPL(kdpc, CUDA, m) {
   m.impl("pointconv_bwd_data", pointconv_bwd_data);
   m.impl("pointconv_bwd_weight", pointconv_bwd_weight);
   m.impl("morton_order", morton_order);
+  m.impl("pointconv_fwd_tiled", pointconv_fwd_tiled);
   m.impl("pc_tile_plan", pc_tile_plan);
   m.impl("pointconv_bwd_tiled", pointconv_bwd_tiled);
   m.impl("pointconv_contract_fwd", pointconv_contract_fwd);

@@ -475,6 +475,10 @@ def test_pointconv_bwd_tiled(b, n, s, k, d, o, knn, morton):
         offsets, perm = K.load_ops().csr_build(tkey, n)
         tdst = K.load_ops().csr_rank(tkey, offsets, perm, n)
         tp = K.attach_tile_plan(idx, n, trow, tpair, tsoff, offsets, tdst.view(tkey.shape))
+    if k in (9, 16):  # the forward through the same tiles: bit-identical rows
+        bias = torch.randn(o, device=DEV)
+        assert torch.equal(K.pointconv_fwd_tiled(xyz, center, feats, idx, wt, wl, bias, tp),
+                           K.pointconv_fwd(xyz, center, feats, idx, wt, wl, bias))
     got = K.pointconv_bwd_tiled(xyz, center, feats, idx, wt, wl, dy, tp)
     again = K.pointconv_bwd_tiled(xyz, center, feats, idx, wt, wl, dy, tp)
     data = K.pointconv_bwd_tiled(xyz, center, feats, idx, wt, wl, dy, tp, weight=False)

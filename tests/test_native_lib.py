@@ -163,6 +163,7 @@ TORCH_OPS = {
     "copy_segments": "kdpc_copy_segments",
     "morton_order": "kdpc_morton_order", "pc_tile_plan": "kdpc_pc_tile_plan",
     "pointconv_bwd_tiled": "kdpc_pointconv_bwd_tiled",
+    "pointconv_fwd_tiled": "kdpc_pointconv_fwd_tiled",
     "dense_small_out": "kdpc_dense_small",
 }
 

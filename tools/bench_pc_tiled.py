@@ -59,6 +59,12 @@ def main():
                      a.iters)
         t_t = timeit(lambda: K.pointconv_bwd_tiled(xyz, xyz, feats, idx, wt, wl, dy, tp,
                                                    weight=False), a.iters)
+        bias = torch.randn(o, generator=g).to(DEV)
+        f_u = timeit(lambda: K.pointconv_fwd(xyz, xyz, feats, idx, wt, wl, bias), a.iters)
+        f_t = timeit(lambda: K.pointconv_fwd_tiled(xyz, xyz, feats, idx, wt, wl, bias, tp),
+                     a.iters)
+        print(name, {"fwd_untiled_us": round(f_u, 1), "fwd_tiled_us": round(f_t, 1)},
+              flush=True)
         print(name, {"untiled_us": round(t_u, 1), "tiled_us": round(t_t, 1),
                      "dG_rows_untiled": b * n * k, "dG_rows_tiled": nrows}, flush=True)
 
