@@ -467,7 +467,17 @@ void cost_volume_bwd_kernel(
   for (int e = threadIdx.x; e < SLAB; e += blockDim.x) sb[e] = rw[e];
 }
 
-constexpr int kFwdQPW = 8;
+// forward queries per wave: 16 (A/B, tools/gpu_r4t.sh: cross0 191.6 -> 185.3 us, cross1
+// 146.9 -> 136.9 us against 8; 32+ leaves SIMDs idle at the tail).  KDPC_CV_FWD_QPW overrides
+// for A/B runs: the per-query arithmetic does not depend on which wave runs the query.
+inline int fwd_qpw() {
+  static const int q = [] {
+    const char* v = getenv("KDPC_CV_FWD_QPW");
+    const int x = v ? atoi(v) : 0;
+    return x >= 2 && x <= 256 ? x : 16;
+  }();
+  return q;
+}
 // backward queries per wave: enough waves for ~8 per SIMD over the launch (the workgroups'
 // partial slabs grow with the wave count; the pipeline amortises its prologue over the rest)
 // backward queries per wave: as many waves as the chip holds at the kernel's occupancy, in
@@ -526,9 +536,10 @@ hipError_t fwd_launch(int b, int n1, int n2, int k, const float* x1, const float
                       const int* idx, const float* p1, const float* p2, const float* wpos,
                       const float* bpos, const float* w1, const float* b1, float* out,
                       unsigned char* amax, hipStream_t st) {
-  dim3 grid(divup(n1, kWaves * kFwdQPW), b);
+  const int qpw = fwd_qpw();
+  dim3 grid(divup(n1, kWaves * qpw), b);
   hipLaunchKernelGGL((cost_volume_fwd_kernel<DI, DO>), grid, dim3(256), 0, st, n1, n2, k,
-                     kFwdQPW, x1, x2, idx, p1, p2, wpos, bpos, w1, b1, out, amax);
+                     qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, b1, out, amax);
   return hipGetLastError();
 }
 
