@@ -737,8 +737,25 @@ __global__ __launch_bounds__(256) void cvw_transpose_kernel(int d, const float* 
   if (e < d * d) w1t[e] = w1[(e % d) * d + e / d];
 }
 
-inline int fused_qpw(long long nq) {  // ~512 workgroups
-  return (int)std::max<long long>(2, divupll(nq, 512));
+// queries per workgroup (KDPC_CVW_WGS overrides the workgroup target for A/B runs: the
+// per-query arithmetic does not depend on it, the backward's parameter-gradient slab count
+// does, so dW1 / dWpos regroup their sums -- bit-identical only at equal settings)
+inline int cvw_target_wgs() {
+  static const int w = [] {
+    const char* v = getenv("KDPC_CVW_WGS");
+    const int x = v ? atoi(v) : 0;
+    return x >= 64 && x <= 8192 ? x : 0;
+  }();
+  return w;
+}
+
+// A/B at the model's calls (B=16 pair batch, K=32; tools/gpu_r4u.sh): forward D=128 512
+// workgroups (108.5 us; 256: 140), D=256 256 (173.6 vs 180.7 at 512); backward 256 for both
+// (cross2 251 vs 256 us, cross3 394 vs 428 us)
+inline int fused_qpw(long long nq, int d, bool bwd) {
+  const int env = cvw_target_wgs();
+  const int target = env ? env : (bwd || d == 256 ? 256 : 512);
+  return (int)std::max<long long>(2, divupll(nq, target));
 }
 
 }  // namespace
@@ -755,7 +772,7 @@ hipError_t cost_volume_wide_fused_fwd(int b, int n1, int n2, int k, int d, const
                                       const float* w1, const float* b1, float* out,
                                       unsigned char* amax, hipStream_t st) {
   const long long nq = (long long)b * n1;
-  const int qpw = fused_qpw(nq);
+  const int qpw = fused_qpw(nq, d, false);
   const dim3 grid((unsigned)divupll(nq, qpw));
   if (d == 128)
     hipLaunchKernelGGL(cvw_fused_fwd_kernel<128>, grid, dim3(256), 0, st, b, n1, n2, k, qpw, x1,
@@ -768,7 +785,7 @@ hipError_t cost_volume_wide_fused_fwd(int b, int n1, int n2, int k, int d, const
 
 size_t cost_volume_wide_fused_bwd_workspace_floats(int b, int n1, int d) {
   const long long nq = (long long)b * n1;
-  const long long nwg = divupll(nq, fused_qpw(nq));
+  const long long nwg = divupll(nq, fused_qpw(nq, d, true));
   const long long len = (long long)d * d + 5 * d;
   return (size_t)(nwg * len + colsum_scratch_floats((int)nwg, len) + (long long)d * d);
 }
@@ -782,7 +799,7 @@ hipError_t cost_volume_wide_fused_bwd(int b, int n1, int n2, int k, int d, const
                                       const int* rank, float* rows, float* ws,
                                       float* dparams, hipStream_t st) {
   const long long nq = (long long)b * n1;
-  const int qpw = fused_qpw(nq);
+  const int qpw = fused_qpw(nq, d, true);
   const int nwg = (int)divupll(nq, qpw);
   const long long len = (long long)d * d + 5 * d;
   float* slab = ws;
