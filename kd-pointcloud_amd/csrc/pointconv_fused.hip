@@ -1339,13 +1339,26 @@ inline int side_weight_cus() {
   return w;
 }
 
+// workgroups the backward data kernel's channel splits aim for (KDPC_PC_BWD_TARGET_WG
+// overrides for A/B runs; backward-only: the dwt split partials regroup).  A/B round 4
+// (tools/gpu_r4w.sh, tiled data half): 512 beats 256 / 1024 / 2048 at flow2 (112 vs 125-135
+// us) and ties at flow0 / flow1.
+inline int bwd_target_wg() {
+  static const int w = [] {
+    const char* v = getenv("KDPC_PC_BWD_TARGET_WG");
+    const int x = v ? atoi(v) : 0;
+    return x >= 64 && x <= 8192 ? x : kTargetWG;
+  }();
+  return w;
+}
+
 inline bool fits_buffers(long long b, long long n, long long s, int d) {
   const long long lim = 1ll << 31;
   return b * n * 4 * std::max(d, 3) < lim && b * s * 12 < lim;
 }
 
-void channel_split(int nch, int tiles, int* ks, int* cps) {
-  int s = tiles > 0 ? std::min(nch, std::max(1, divup(kTargetWG, tiles))) : 1;
+void channel_split(int nch, int tiles, int* ks, int* cps, int target = kTargetWG) {
+  int s = tiles > 0 ? std::min(nch, std::max(1, divup(target, tiles))) : 1;
   *cps = divup(nch, s);
   *ks = divup(nch, *cps);
 }
@@ -1362,7 +1375,7 @@ bool plan_of(int b, int s, int k, int d, int o, Plan* p, int wcus = kCUs) {
   p->tm = km_of(k) <= 9 ? 64 : 32;
   p->rt = divup(p->r, p->tm);
   channel_split(p->nch, p->rt, &p->ks, &p->cps);
-  channel_split(p->nch, divup(p->r, 32), &p->bks, &p->bcps);
+  channel_split(p->nch, divup(p->r, 32), &p->bks, &p->bcps, bwd_target_wg());
   // bwd-weight row splits: every (chunk, split) workgroup carries the same MFMA work and
   // all of them are resident at once (one 512-thread workgroup per CU: the pipelined kernel
   // double-buffers its operands in 90-158 KB of LDS), so the kernel takes (workgroups on the
