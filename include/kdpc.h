@@ -313,6 +313,13 @@ int kdpc_pointconv_bwd_weight(int b, int n, int s, int k, int d, int o, const fl
                               const float *center, const float *feats, const int *idx,
                               const float *wt, const float *dy, float *dwl, void *workspace,
                               size_t workspace_bytes, void *stream);
+/* The weight half plus the Linear's bias gradient dbias (O) = column sums of dy, from the
+ * same MFMAs (a padding column of the contraction set to 1; requires (3 + d) % 8 != 0).
+ * Same workspace as kdpc_pointconv_bwd_weight. */
+int kdpc_pointconv_bwd_weight_bias(int b, int n, int s, int k, int d, int o, const float *xyz,
+                                   const float *center, const float *feats, const int *idx,
+                                   const float *wt, const float *dy, float *dwl, float *dbias,
+                                   void *workspace, size_t workspace_bytes, void *stream);
 
 /* Tiled PointConv backward: the same gradients with the dG rows summed per (32-row tile,
  * destination point) inside the data kernel (one partial row each instead of one row per

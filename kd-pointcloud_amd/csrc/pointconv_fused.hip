@@ -1084,7 +1084,8 @@ constexpr int wgt_tile_rows() { return O == 256 || (O == 128 && KM > 9) ? 32 : 6
 template <int O, int KM, bool EX>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
 void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __restrict__ dy,
-                          float* __restrict__ dwl, int rows_per_split, int nsplit, int xcd_map) {
+                          float* __restrict__ dwl, int rows_per_split, int nsplit, int xcd_map,
+                          float* __restrict__ dbias) {
   constexpr int TR = wgt_tile_rows<O, KM>();
   constexpr int TS = TR + 4;               // row stride of the transposed tiles
   constexpr int NT = 512;                  // threads: 2 waves per SIMD
@@ -1252,6 +1253,11 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
       for (int k = 0; k < KM; ++k) wc[p2][k] = wr[p2][k];
   };
   // A block of the tile staged in gl / wc -> at[buf] (transposed: column-major rows)
+  // bias gradient for free (dbias != null): the first padding channel's w = 0 column of A
+  // (always 0 otherwise: C % 8 != 0 puts it in the last chunk) is set to 1, so that column
+  // of the MFMA output is sum_r dy[r, o] -- the rows past the split read dy = 0
+  const int ones_col = (dbias != nullptr && ch == g.nch - 1 && g.c % kCC != 0)
+                           ? (g.c % kCC) * kW : -1;
   auto build = [&](int buf) {
     float* ab = at[buf];
 #pragma unroll
@@ -1259,7 +1265,8 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
       float a[kCC];
       build_row<KM>(gl, rb + RS * p2, kk, wc[p2], a);
 #pragma unroll
-      for (int c = 0; c < kCC; ++c) ab[(c * kW + w) * TS + rb + RS * p2] = a[c];
+      for (int c = 0; c < kCC; ++c)
+        ab[(c * kW + w) * TS + rb + RS * p2] = c * kW + w == ones_col ? 1.f : a[c];
     }
   };
 
@@ -1300,6 +1307,13 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
     __syncthreads();
   }
   const long long col = (long long)c0 * kW + nt * 32 + l32;
+  if (ones_col >= 0 && col == (long long)c0 * kW + ones_col) {
+    float* bd = dbias + (long long)split * O;  // slab index when the rows are split
+#pragma unroll
+    for (int i = 0; i < MPW; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) bd[(m0 + i) * 32 + (e & 3) + 8 * (e >> 2) + 4 * half] = acc[i][e];
+  }
   if (col >= c16) return;
   float* dst = dwl + (long long)split * O * c16;  // slab index when the rows are split
 #pragma unroll
@@ -1500,18 +1514,23 @@ hipError_t bwd_data_launch(const Geo& g, const Plan& p, int b, const float* wt, 
 // G / wt / dy as the data half and nothing it writes, so it may run on another stream.
 template <int O, int KM>
 hipError_t bwd_weight_launch(const Geo& g, const Plan& p, const float* wt, const float* dy,
-                             float* dwl, char* ws, hipStream_t st) {
+                             float* dwl, char* ws, hipStream_t st, float* dbias = nullptr) {
   float* dwl_slab = reinterpret_cast<float*>(ws);
   float* wdst = p.rs > 1 ? dwl_slab : dwl;
+  // bias slab after the dwl slabs (kdpc_pointconv_bwd_weight_workspace_bytes)
+  float* bias_slab = reinterpret_cast<float*>(ws + p.dwl_slab);
+  float* bdst = dbias == nullptr ? nullptr : (p.rs > 1 ? bias_slab : dbias);
   if (g.k == KM)
     hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM, true>), dim3(p.wgs), dim3(512), 0, st, g, wt,
-                       dy, wdst, p.rps, p.rs, p.xcd);
+                       dy, wdst, p.rps, p.rs, p.xcd, bdst);
   else
     hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM, false>), dim3(p.wgs), dim3(512), 0, st, g, wt,
-                       dy, wdst, p.rps, p.rs, p.xcd);
+                       dy, wdst, p.rps, p.rs, p.xcd, bdst);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || p.rs == 1) return e;
-  return slab_sum(p.rs, (long long)O * g.c * kW, dwl_slab, nullptr, 1, dwl, st);
+  if ((e = slab_sum(p.rs, (long long)O * g.c * kW, dwl_slab, nullptr, 1, dwl, st)) != hipSuccess)
+    return e;
+  return dbias == nullptr ? hipSuccess : slab_sum(p.rs, O, bias_slab, nullptr, 1, dbias, st);
 }
 
 template <int O, int KM>
@@ -1616,7 +1635,9 @@ KDPC_API int kdpc_pointconv_bwd(int b, int n, int s, int k, int d, int o, const 
 
 KDPC_API size_t kdpc_pointconv_bwd_weight_workspace_bytes(int b, int s, int k, int d, int o) {
   Plan p;
-  return plan_of(b, s, k, d, o, &p, side_weight_cus()) ? std::max<size_t>(p.dwl_slab, 256) : 0;
+  return plan_of(b, s, k, d, o, &p, side_weight_cus())
+             ? std::max<size_t>(p.dwl_slab + (p.rs > 1 ? align256((size_t)p.rs * o * 4) : 0), 256)
+             : 0;
 }
 
 KDPC_API int kdpc_pointconv_bwd_data(int b, int n, int s, int k, int d, int o, const float* xyz,
@@ -1735,4 +1756,29 @@ KDPC_API int kdpc_pointconv_fwd_tiled(int b, int n, int s, int k, int d, int o, 
   float* slab = reinterpret_cast<float*>(workspace);
   hipStream_t st = (hipStream_t)stream;
   return (int)KDPC_PC_DISPATCH(fwd_launch, g, p, wt, wl, bias, y, slab, st);
+}
+
+// Weight half plus the bias gradient (column sums of dy) from the same MFMAs: a padding
+// column of A set to 1 (needs C % 8 != 0, i.e. a padding channel in the last chunk).
+KDPC_API int kdpc_pointconv_bwd_weight_bias(int b, int n, int s, int k, int d, int o,
+                                            const float* xyz, const float* center,
+                                            const float* feats, const int* idx, const float* wt,
+                                            const float* dy, float* dwl, float* dbias,
+                                            void* workspace, size_t workspace_bytes,
+                                            void* stream) {
+  Plan p;
+  KDPC_CHECK_ARG(n > 0 && b <= 65535 && plan_of(b, s, k, d, o, &p, side_weight_cus()) &&
+                 fits_buffers(b, n, s, d) && (3 + d) % kCC != 0);
+  hipStream_t st = (hipStream_t)stream;
+  if (p.r == 0) {
+    hipError_t e = hipMemsetAsync(dwl, 0, sizeof(float) * o * p.c * kW, st);
+    if (e == hipSuccess) e = hipMemsetAsync(dbias, 0, sizeof(float) * o, st);
+    return (int)e;
+  }
+  KDPC_CHECK_ARG(xyz && center && idx && wt && dy && dwl && dbias && (d == 0 || feats));
+  KDPC_CHECK_ARG(workspace &&
+                 workspace_bytes >= kdpc_pointconv_bwd_weight_workspace_bytes(b, s, k, d, o));
+  const Geo g = geo_of(b, n, s, k, d, p, xyz, center, feats, idx);
+  char* ws = reinterpret_cast<char*>(workspace);
+  return (int)KDPC_PC_DISPATCH(bwd_weight_launch, g, p, wt, dy, dwl, ws, st, dbias);
 }

@@ -73,6 +73,7 @@ _SIGNATURES = {
     "kdpc_pointconv_bwd_data_tiled": [_c_int] * 6 + [_vp] * 17 + [_c_size, _vp],
     "kdpc_pointconv_bwd_tiled": [_c_int] * 6 + [_vp] * 18 + [_c_size, _vp],
     "kdpc_morton_order": [_c_int, _c_int, _vp, _vp, _vp],
+    "kdpc_pointconv_bwd_weight_bias": [_c_int] * 6 + [_vp] * 9 + [_c_size, _vp],
     "kdpc_pc_tile_plan": [_c_int] * 4 + [_vp] * 7,
     "kdpc_pointconv_bwd_weight_workspace_bytes": [_c_int] * 5,
     "kdpc_pointconv_bwd_weight": [_c_int] * 6 + [_vp] * 8 + [_c_size, _vp],
@@ -462,6 +463,9 @@ def csr_rank_of(idx, n):
 # at N=8192).  Used for K <= 9 (the estimators' layers); KDPC_PC_TILED=0 keeps the per-pair
 # rows for A/B runs.
 TILED_PC = os.environ.get("KDPC_PC_TILED", "1") != "0"
+# the PointConv bias gradient from the weight kernel's MFMAs (KDPC_PC_BIAS_IN_WEIGHT=0: the
+# fixed-order column sum of dy instead, for A/B)
+BIAS_IN_WEIGHT = os.environ.get("KDPC_PC_BIAS_IN_WEIGHT", "1") != "0"
 # the forward through the same row tiles (bit-identical; KDPC_PC_TILED_FWD=0 for A/B)
 TILED_FWD = TILED_PC and os.environ.get("KDPC_PC_TILED_FWD", "1") != "0"
 TILED_MAX_K = 9
@@ -750,6 +754,23 @@ def pointconv_bwd_weight(xyz, center, feats, idx, wt, dy, o):
     return _op("kdpc_pointconv_bwd_weight", "pointconv_bwd_weight", xyz, center, feats, idx, wt,
                dy, int(o),
                work=(4 * R * (K * C + 16 * K + o) + 4 * o * 16 * C, 2.0 * R * 16 * C * o))
+
+
+
+def pointconv_bwd_weight_bias(xyz, center, feats, idx, wt, dy, o):
+    """pointconv_bwd_weight plus the bias gradient (column sums of dy) from the same MFMAs
+    -> (dwl (O, 16C), dbias (O,)); needs C = 3 + D with C % 8 != 0 (bias_in_weight)."""
+    B, N, _ = _gpu(xyz, "xyz").shape
+    S, K = idx.shape[1], idx.shape[2]
+    C = 3 + feats.shape[2]
+    R = B * S
+    return _op("kdpc_pointconv_bwd_weight", "pointconv_bwd_weight_bias", xyz, center, feats, idx,
+               wt, dy, o, work=(4 * R * (K * C + 16 * K + o) + 4 * o * 16 * C,
+                                2.0 * R * K * C * 16 + 2.0 * R * 16 * C * o))
+
+
+def bias_in_weight(feats):
+    return BIAS_IN_WEIGHT and (3 + feats.shape[-1]) % 8 != 0
 
 
 def timing(entry):

@@ -410,10 +410,16 @@ class _PointConvLayer(torch.autograd.Function):
                     xyz, center, feats, idx, wt, wl, gy, csr, need_xyz=need_x)
             # the parameter gradients (weight kernel + fixed-order bias column sum) beside the
             # rest of the backward, on the parameter-gradient stream (wgrad.py)
-            dwl, dbias = wgrad.run(lambda: (
-                _nat.pointconv_bwd_weight(xyz, center, feats, idx, wt, gy, wl.shape[0]),
-                _nat.colsum(gy.view(-1, gy.shape[-1])) if need_b else None),
-                [xyz, center, feats, idx, wt, gy], (wl, bias))
+            if need_b and _nat.bias_in_weight(feats):
+                # the bias gradient from the weight kernel's MFMAs (a ones column of A)
+                dwl, dbias = wgrad.run(lambda: _nat.pointconv_bwd_weight_bias(
+                    xyz, center, feats, idx, wt, gy, wl.shape[0]),
+                    [xyz, center, feats, idx, wt, gy], (wl, bias))
+            else:
+                dwl, dbias = wgrad.run(lambda: (
+                    _nat.pointconv_bwd_weight(xyz, center, feats, idx, wt, gy, wl.shape[0]),
+                    _nat.colsum(gy.view(-1, gy.shape[-1])) if need_b else None),
+                    [xyz, center, feats, idx, wt, gy], (wl, bias))
         return (dxyz, dcenter if ctx.needs_input_grad[1] else None, dfeats, None, dwt, dwl, dbias)
 
 

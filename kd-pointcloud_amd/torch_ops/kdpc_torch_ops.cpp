@@ -658,6 +658,28 @@ Tensor pointconv_bwd_weight(Tensor xyz, Tensor center, Tensor feats, Tensor idx,
   return dwl;
 }
 
+std::tuple<Tensor, Tensor> pointconv_bwd_weight_bias(Tensor xyz, Tensor center, Tensor feats,
+                                                     Tensor idx, Tensor wt, Tensor dy,
+                                                     int64_t o) {
+  for (auto* t : {&xyz, &center, &feats, &wt, &dy}) dev(*t, kF, "pointconv input");
+  dev(idx, kI, "idx");
+  GUARD(xyz);
+  const int64_t b = xyz.size(0), n = xyz.size(1), s = idx.size(1), k = idx.size(2);
+  const int64_t d = feats.size(2), c = 3 + d;
+  TORCH_CHECK(dy.numel() == b * s * o, "kdpc: pointconv_bwd_weight_bias: dy does not match O");
+  TORCH_CHECK(c % 8 != 0, "kdpc: pointconv_bwd_weight_bias needs C % 8 != 0");
+  const size_t nb = kdpc_pointconv_bwd_weight_workspace_bytes(b, s, k, d, o);
+  TORCH_CHECK(nb > 0, "kdpc: pointconv_bwd_weight_bias: invalid sizes");
+  Tensor ws = workspace(nb, xyz);
+  Tensor dwl = empty_f({o, 16 * c}, xyz);
+  Tensor dbias = empty_f({o}, xyz);
+  check(kdpc_pointconv_bwd_weight_bias(b, n, s, k, d, o, F(xyz), F(center), F(feats), I(idx),
+                                       F(wt), F(dy), F(dwl), F(dbias), ws.data_ptr(), nb,
+                                       stream_of(xyz)),
+        "pointconv_bwd_weight_bias");
+  return {dwl, dbias};
+}
+
 Tensor pointconv_contract_fwd(Tensor xyz, Tensor center, Tensor feats, Tensor idx, Tensor wt) {
   for (auto* t : {&xyz, &center, &feats, &wt}) dev(*t, kF, "pointconv input");
   dev(idx, kI, "idx");
@@ -1046,6 +1068,8 @@ TORCH_LIBRARY(kdpc, m) {
   m.def("pointconv_bwd_weight(Tensor xyz, Tensor center, Tensor feats, Tensor idx, Tensor wt, "
         "Tensor dy, int o) -> Tensor");
   m.def("morton_order(Tensor xyz) -> Tensor");
+  m.def("pointconv_bwd_weight_bias(Tensor xyz, Tensor center, Tensor feats, Tensor idx, "
+        "Tensor wt, Tensor dy, int o) -> (Tensor, Tensor)");
   m.def("pointconv_fwd_tiled(Tensor xyz, Tensor center, Tensor feats, Tensor idx, Tensor wt, "
         "Tensor wl, Tensor bias, Tensor trow) -> Tensor");
   m.def("pc_tile_plan(Tensor idx, Tensor? order, int n) -> (Tensor, Tensor, Tensor, Tensor)");
@@ -1122,6 +1146,7 @@ TORCH_LIBRARY_IMPL(kdpc, CUDA, m) {
   m.impl("pointconv_bwd_data", pointconv_bwd_data);
   m.impl("pointconv_bwd_weight", pointconv_bwd_weight);
   m.impl("morton_order", morton_order);
+  m.impl("pointconv_bwd_weight_bias", pointconv_bwd_weight_bias);
   m.impl("pointconv_fwd_tiled", pointconv_fwd_tiled);
   m.impl("pc_tile_plan", pc_tile_plan);
   m.impl("pointconv_bwd_tiled", pointconv_bwd_tiled);

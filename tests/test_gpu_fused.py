@@ -552,3 +552,21 @@ def test_tile_plan_structure():
         assert (tsoff[t][len(dests):] == nv).all()
         assert (tdst[t * 32 * k + len(dests):(t + 1) * 32 * k] == -1).all()
     assert (np.diff(offsets) == seen[:-1]).all()
+
+
+@pytest.mark.parametrize("b,n,s,k,d,o", [(2, 2048, 2048, 9, 128, 128), (2, 1024, 512, 16, 60, 64),
+                                         (1, 300, 77, 16, 131, 256), (3, 700, 333, 9, 6, 64)])
+def test_pointconv_weight_bias(b, n, s, k, d, o):
+    """kdpc_pointconv_bwd_weight_bias: dwl bit-identical to kdpc_pointconv_bwd_weight, dbias
+    (a ones column of the contraction through the same MFMAs) within 1e-5 of the scale of an
+    fp64 column sum of dy; refused for C % 8 == 0."""
+    import kdpc_native as K
+    xyz, center, feats, idx, wt, wl, dy = _tiled_inputs(b, n, s, k, d, o, True, n + k + d + 1)
+    dwl, dbias = K.pointconv_bwd_weight_bias(xyz, center, feats, idx, wt, dy, o)
+    assert torch.equal(dwl, K.pointconv_bwd_weight(xyz, center, feats, idx, wt, dy, o))
+    _scale_close(dbias, dy.double().sum((0, 1)), name="dbias")
+    again = K.pointconv_bwd_weight_bias(xyz, center, feats, idx, wt, dy, o)
+    assert torch.equal(again[1], dbias)
+    with pytest.raises(RuntimeError):
+        f8 = torch.randn(b, n, 5, device=DEV)  # C = 8
+        K.pointconv_bwd_weight_bias(xyz, center, f8, idx, wt, dy, o)

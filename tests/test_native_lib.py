@@ -164,6 +164,7 @@ TORCH_OPS = {
     "morton_order": "kdpc_morton_order", "pc_tile_plan": "kdpc_pc_tile_plan",
     "pointconv_bwd_tiled": "kdpc_pointconv_bwd_tiled",
     "pointconv_fwd_tiled": "kdpc_pointconv_fwd_tiled",
+    "pointconv_bwd_weight_bias": "kdpc_pointconv_bwd_weight_bias",
     "dense_small_out": "kdpc_dense_small",
 }
 
