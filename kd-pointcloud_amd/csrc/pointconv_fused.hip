@@ -1348,7 +1348,7 @@ inline int side_weight_cus() {
   static const int w = [] {
     const char* v = getenv("KDPC_PC_WGT_CUS");
     const int x = v ? atoi(v) : 0;
-    return x >= 8 && x <= kCUs ? x : kCUs;
+    return x >= 8 && x <= 4 * kCUs ? x : kCUs;  // > 256: several rounds of workgroups
   }();
   return w;
 }

@@ -409,7 +409,7 @@ def _colsum_order_ref(x):
     if nrows <= 256:
         return quarters(x)
     cb = -(-ln // 64)
-    g = max(2, -(-1024 // cb))
+    g = max(2, -(-512 // cb))  # kLevel1WGDefault
     g = max(1, min(min(g, -(-nrows // 64)), 1024))
     rpw = -(-nrows // g)
     slabs = -(-nrows // rpw)
