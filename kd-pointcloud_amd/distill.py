@@ -281,7 +281,8 @@ def _join_capture_streams(cap, extra=()):
     import models_bid_pointconv
     dev = cap.device
     streams = [s for s in extra if s is not None]
-    streams += [wgrad._side.get(dev.index), _teacher_streams.get(dev.index)]
+    streams += list(wgrad._pool.get(dev.index, [wgrad._side.get(dev.index)]))
+    streams += [_teacher_streams.get(dev.index)]
     streams += [s for (d, _), s in models_bid_pointconv._coord_streams.items() if d == dev.index]
     seen = set()
     for s in streams:

@@ -4,8 +4,8 @@ A layer's backward produces two kinds of output: the gradients of its inputs, wh
 next (upstream) backward op waits for, and the gradients of its parameters, which only the
 optimizer reads.  The second kind -- the PointConv weight-gradient kernel (pc_bwd_weight,
 ~1.8 ms of a B=8 training step), the dense layers' split-K weight GEMMs and every bias column
-sum -- is issued here on a second HIP stream, forked from the backward's stream at that
-point, so it runs beside the rest of the backward instead of in front of it.  Same kernels on
+sum -- is issued here on side HIP streams (two, round-robin), forked from the backward's
+stream at that point, so it runs beside the rest of the backward instead of in front of it.  Same kernels on
 the same inputs: the gradients are bit-identical to issuing them in line.
 
 Ordering (eager and inside a captured HIP graph alike):
@@ -39,7 +39,15 @@ import torch
 
 # KDPC_WGRAD_STREAM=0 issues every parameter gradient in line (A/B runs)
 enabled = os.environ.get("KDPC_WGRAD_STREAM", "1") != "0"
-_side = {}      # device index -> side stream
+# parameter-gradient streams per device, used round-robin by run(): two, so that the
+# parameter-gradient kernels of consecutive layers can run beside each other as well as beside
+# the backward (round-4 A/B, tools/gpu_r4aa.sh, three runs each: 1 stream 16.07-16.21 ms,
+# 2 streams 15.89-16.04, 3 streams 16.01-16.29; KD 12.83-12.89 / 12.67-12.72 / 12.82-12.97).
+# KDPC_WGRAD_STREAMS overrides (A/B runs).
+_NSTREAMS = max(1, int(os.environ.get("KDPC_WGRAD_STREAMS", "2")))
+_side = {}      # device index -> the first side stream (the decoder coordinate fork's)
+_pool = {}      # device index -> [side streams]
+_turn = {}      # device index -> next pool entry
 _pending = {}   # (main, side) raw stream handles -> (main, side) joins queued in this backward
 _suspended = weakref.WeakSet()  # objects (DDP wrappers) for whose lifetime run() is in line
 # id(leaf parameter) -> (weak reference to it, side-stream event recorded after the launch
@@ -64,6 +72,22 @@ def side_stream(device):
     return s
 
 
+def side_streams(device):
+    """Every parameter-gradient stream of `device` (the first is side_stream(device))."""
+    pool = _pool.get(device.index)
+    if pool is None:
+        pool = _pool[device.index] = [side_stream(device)] + [
+            torch.cuda.Stream(device=device) for _ in range(_NSTREAMS - 1)]
+    return pool
+
+
+def _next_side(device):
+    pool = side_streams(device)
+    i = _turn.get(device.index, 0)
+    _turn[device.index] = (i + 1) % len(pool)
+    return pool[i]
+
+
 def run(fn, inputs, params=()):
     """fn() launches parameter-gradient kernels reading `inputs` and returns their results,
     the gradients of `params`; run it on the side stream.  Call from inside a
@@ -72,7 +96,7 @@ def run(fn, inputs, params=()):
     if not active() or dev.type != "cuda":
         return fn()
     main = torch.cuda.current_stream(dev)
-    side = side_stream(dev)
+    side = _next_side(dev)
     side.wait_stream(main)
     with torch.cuda.stream(side):
         out = fn()
@@ -136,6 +160,5 @@ def _join_pending(key):
 def join(device=None):
     """The current stream waits for every parameter-gradient kernel issued so far."""
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else device
-    s = _side.get(dev.index)
-    if s is not None:
+    for s in _pool.get(dev.index, [s for s in (_side.get(dev.index),) if s is not None]):
         torch.cuda.current_stream(dev).wait_stream(s)
