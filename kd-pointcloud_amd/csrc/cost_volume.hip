@@ -381,7 +381,7 @@ void cost_volume_bwd_kernel(
         const int sa = __builtin_amdgcn_readlane(rkv, r0);
         const int slot = RPP == 2 ? (sub ? __builtin_amdgcn_readlane(rkv, r0 + 1) : sa) : sa;
         if (slot >= 0) rows[(long long)slot * D_IN + c] = v;
-      } else {
+      } else if (dp2_rows) {
         dp2n[r * D_IN] = v;
       }
       dp1_acc = __fadd_rn(dp1_acc, v);
@@ -411,7 +411,7 @@ void cost_volume_bwd_kernel(
     if (row && ranked) {
       if (rkv >= 0)
         *reinterpret_cast<float4*>(dirs + (long long)rkv * 4) = make_float4(g0, g1, g2, 0.f);
-    } else if (row) {
+    } else if (row && ddir_rows) {
       float* dd = ddir_rows + (((long long)b * n1 + n) * k + lane) * 3;
       dd[0] = g0;
       dd[1] = g1;
@@ -552,6 +552,10 @@ hipError_t bwd_launch_w(int b, int n1, int n2, int k, const float* x1, const flo
                         float* rows, float* slab, float* dparams, hipStream_t st) {
   const int qpw = bwd_qpw<DI, DO, W>(b, n1);
   dim3 grid(divup(n1, kWaves * qpw), b);
+  // diagnostic (tools/bench_cv_bwd.py): KDPC_CV_BWD_DIAG_NOROWS=1 drops the per-neighbour row
+  // stores of the plain entry, timing the kernel's arithmetic without its scatter
+  static const bool norows = getenv("KDPC_CV_BWD_DIAG_NOROWS") != nullptr;
+  if (norows && rank == nullptr) dp2_rows = ddir_rows = nullptr;
   hipLaunchKernelGGL((cost_volume_bwd_kernel<DI, DO, W>), grid, dim3(256), 0, st, n1, n2, k,
                      qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, dout, dp1,
                      dp2_rows, dx1, ddir_rows, rank, rows, slab);
@@ -685,6 +689,120 @@ hipError_t rows_sum(int din, long long nkeys, const float* rows, const float* di
   }
 }
 
+// Pull form of the per-point sums (D_IN == D_OUT in {32, 64}, K <= 32; round 4).  The ranked
+// path writes one dz0 row per (query, neighbour) pair at its CSR slot and sums the rows per
+// point: B*N1*K*(D+4)*4 bytes out to HBM and back (604 MB each way at cross0, B=16 clouds of
+// 8192, K=32).  Here the backward kernel writes no rows, and one wave per reference point j
+// walks its CSR segment (perm: the positions (n, k) naming j, ascending) and recomputes each
+// pair's row from the query's inputs, which stay cache-resident (one cloud's P1 / out / dout
+// rows at a time, ~3.5 MB at D=32):
+//   h0  = LeakyReLU((P2[j] + P1[n]) + (Wpos (x2[j] - x1[n]) + bpos))   the forward's exact
+//         arithmetic, so every LeakyReLU branch is the forward's
+//   dh0 = sum over d ascending with am[n, d] == k of g'[n, d] W1[d, :],
+//         g' = dout * LeakyReLU'(out)        (one term per output channel routed to row k)
+//   dz0 = dh0 * LeakyReLU'(h0);   dP2[j] = the segment's sum;   dx2[j] = Wpos^T dP2[j]
+// D = 32 runs two pairs per step (the wave's halves take alternate pairs; the two partial sums
+// are added at the end).  Fixed order throughout: deterministic.  Rounding differs from the
+// ranked path's (per-pair d(dir) sums; MFMA vs fma-chain dh0 when two channels route to one row).
+template <int D>
+__global__ __launch_bounds__(256) void cv_pull_kernel(
+    int k, int n2, long long nkeys, const float* __restrict__ x1, const float* __restrict__ x2,
+    const float* __restrict__ p1, const float* __restrict__ p2, const float* __restrict__ wpos,
+    const float* __restrict__ bpos, const float* __restrict__ w1, const float* __restrict__ out,
+    const unsigned char* __restrict__ amax, const float* __restrict__ dout,
+    const int* __restrict__ offsets, const int* __restrict__ perm, float* __restrict__ dp2,
+    float* __restrict__ dx2) {
+  constexpr int RPP = 64 / D;  // pairs per step
+  constexpr int U = 4;         // steps whose loads are in flight together
+  __shared__ float w1s[D * D];
+  for (int e = threadIdx.x; e < D * D; e += blockDim.x) w1s[e] = w1[e];
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = lane_id();
+  const int c = lane % D, sub = lane / D;
+  const long long key = (long long)blockIdx.x * kWaves + wave;
+  if (key >= nkeys) return;
+  const float w0 = wpos[c * 3 + 0], wy = wpos[c * 3 + 1], wz = wpos[c * 3 + 2], bp = bpos[c];
+  const float pj = p2[key * D + c];
+  const float xj0 = x2[key * 3 + 0], xj1 = x2[key * 3 + 1], xj2 = x2[key * 3 + 2];
+  const int s0 = offsets[key], s1 = offsets[key + 1];
+  float acc = 0.f;
+  for (int cs = s0; cs < s1; cs += 64) {  // chunks of 64 pairs: lane l holds pair cs + l
+    const int cn = min(64, s1 - cs);
+    const int pl = lane < cn ? perm[cs + lane] : 0;
+    for (int i0 = 0; i0 < cn; i0 += RPP * U) {
+      float p1v[U], ov[U], gv[U], q0[U], q1[U], q2[U];
+      int am[U], kk[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + RPP * u + sub;
+        const int gp = __shfl(pl, i < cn ? i : 0, kWave);
+        const int ng = gp / k;  // b*N1 + n
+        kk[u] = gp - ng * k;
+        const long long ro = (long long)ng * D + c;
+        p1v[u] = p1[ro];
+        ov[u] = out[ro];
+        gv[u] = dout[ro];
+        am[u] = amax[ro];
+        q0[u] = x1[ng * 3 + 0];
+        q1[u] = x1[ng * 3 + 1];
+        q2[u] = x1[ng * 3 + 2];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + RPP * u + sub;
+        const float dx = xj0 - q0[u], dy = xj1 - q1[u], dzz = xj2 - q2[u];
+        const float pos = __fadd_rn(__builtin_fmaf(wz, dzz, __builtin_fmaf(wy, dy, __fmul_rn(w0, dx))), bp);
+        const float h = lrelu(__fadd_rn(__fadd_rn(pj, p1v[u]), pos));
+        const float gd = gv[u] * (ov[u] > 0.f ? 1.f : kSlope);
+        const unsigned long long m = __ballot(am[u] == kk[u]);
+        // the half's routing mask is uniform over the half, so the whole half runs each step
+        unsigned long long hm = D == 64 ? m : ((m >> (32 * sub)) & 0xFFFFFFFFull);
+        float dh = 0.f;
+        while (hm) {
+          const int d = __builtin_ctzll(hm);
+          hm &= hm - 1;
+          dh = __builtin_fmaf(__shfl(gd, sub * D + d, kWave), w1s[d * D + c], dh);
+        }
+        const float dz = dh * (h > 0.f ? 1.f : kSlope);
+        if (i < cn) acc = __fadd_rn(acc, dz);
+      }
+    }
+  }
+  if (RPP == 2) acc = __fadd_rn(acc, __shfl_xor(acc, 32, kWave));
+  float g0 = wpos[c * 3 + 0] * acc, g1 = wy * acc, g2 = wz * acc;
+#pragma unroll
+  for (int o = D / 2; o >= 1; o >>= 1) {
+    g0 = __fadd_rn(g0, __shfl_xor(g0, o, kWave));
+    g1 = __fadd_rn(g1, __shfl_xor(g1, o, kWave));
+    g2 = __fadd_rn(g2, __shfl_xor(g2, o, kWave));
+  }
+  if (sub == 0) dp2[key * D + c] = acc;
+  if (lane == 0) {
+    dx2[key * 3 + 0] = g0;
+    dx2[key * 3 + 1] = g1;
+    dx2[key * 3 + 2] = g2;
+  }
+}
+
+hipError_t pull_sum(int d, int k, int n2, long long nkeys, const float* x1, const float* x2,
+                    const float* p1, const float* p2, const float* wpos, const float* bpos,
+                    const float* w1, const float* out, const unsigned char* amax,
+                    const float* dout, const int* offsets, const int* perm, float* dp2,
+                    float* dx2, hipStream_t st) {
+  if (nkeys <= 0) return hipSuccess;
+  const dim3 grid((unsigned)divupll(nkeys, kWaves));
+#define KDPC_CV_PULL(DD)                                                                    \
+  if (d == DD) {                                                                            \
+    hipLaunchKernelGGL((cv_pull_kernel<DD>), grid, dim3(256), 0, st, k, n2, nkeys, x1, x2, p1, \
+                       p2, wpos, bpos, w1, out, amax, dout, offsets, perm, dp2, dx2);          \
+    return hipGetLastError();                                                               \
+  }
+  KDPC_CV_PULL(32)
+  KDPC_CV_PULL(64)
+#undef KDPC_CV_PULL
+  return hipErrorInvalidValue;
+}
+
 bool narrow(int din, int dout, int k) {
   return (din == 32 || din == 64) && (dout == 32 || dout == 64) && k >= 1 && k <= 32;
 }
@@ -810,4 +928,37 @@ KDPC_API int kdpc_cost_volume_bwd_csr(int b, int n1, int n2, int k, int din, int
   if (e != hipSuccess) return (int)e;
   return (int)rows_sum(din, (long long)b * n2, rows, rows + (size_t)b * n1 * k * din, offsets, dp2,
                        dx2, st);
+}
+
+// Backward with the per-point sums in pull form (cv_pull_kernel): offsets (B*N2+1) / perm
+// (B*N1*K) of the CSR of idx over the N2 points (kdpc_csr_build).  No per-neighbour rows are
+// written; D_IN == D_OUT in {32, 64} only (kdpc_cost_volume_bwd_pull_supported).  Outputs as
+// kdpc_cost_volume_bwd_csr (dp2 / dx2 within rounding of it); workspace as
+// kdpc_cost_volume_bwd_workspace_bytes.
+KDPC_API int kdpc_cost_volume_bwd_pull_supported(int din, int dout, int k) {
+  return din == dout && (din == 32 || din == 64) && k >= 1 && k <= 32;
+}
+
+KDPC_API int kdpc_cost_volume_bwd_pull(int b, int n1, int n2, int k, int din, int dout,
+                                       const float* x1, const float* x2, const int* idx,
+                                       const float* p1, const float* p2, const float* wpos,
+                                       const float* bpos, const float* w1, const float* out,
+                                       const unsigned char* amax, const float* dout_grad,
+                                       const int* offsets, const int* perm, float* dp1,
+                                       float* dp2, float* dx1, float* dx2, void* workspace,
+                                       size_t workspace_bytes, float* dparams, void* stream) {
+  KDPC_CHECK_ARG(b > 0 && n1 > 0 && n2 > 0 && b <= 65535 &&
+                 kdpc_cost_volume_bwd_pull_supported(din, dout, k));
+  KDPC_CHECK_ARG((long long)b * n1 * k < (1ll << 31));
+  KDPC_CHECK_ARG(x1 && x2 && idx && p1 && p2 && wpos && bpos && w1 && out && amax && dout_grad &&
+                 offsets && perm && dp1 && dp2 && dx1 && dx2 && workspace && dparams);
+  KDPC_CHECK_ARG(workspace_bytes >= kdpc_cost_volume_bwd_workspace_bytes(b, n1, din, dout));
+  hipStream_t st = (hipStream_t)stream;
+  // rank == rows == null and no plain row buffers: the backward writes dp1 / dx1 / slabs only
+  hipError_t e = bwd_dispatch(b, n1, n2, k, din, dout, x1, x2, idx, p1, p2, wpos, bpos, w1, out,
+                              amax, dout_grad, dp1, nullptr, dx1, nullptr, nullptr, nullptr,
+                              (float*)workspace, dparams, st);
+  if (e != hipSuccess) return (int)e;
+  return (int)pull_sum(din, k, n2, (long long)b * n2, x1, x2, p1, p2, wpos, bpos, w1, out, amax,
+                       dout_grad, offsets, perm, dp2, dx2, st);
 }

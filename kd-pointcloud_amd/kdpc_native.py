@@ -63,6 +63,8 @@ _SIGNATURES = {
     "kdpc_cost_volume_bwd": [_c_int] * 6 + [_vp] * 16 + [_c_size, _vp, _vp],
     "kdpc_cost_volume_bwd_csr_workspace_bytes": [_c_int] * 5,
     "kdpc_cost_volume_bwd_csr": [_c_int] * 6 + [_vp] * 18 + [_c_size, _vp, _vp],
+    "kdpc_cost_volume_bwd_pull_supported": [_c_int] * 3,
+    "kdpc_cost_volume_bwd_pull": [_c_int] * 6 + [_vp] * 18 + [_c_size, _vp, _vp],
     "kdpc_pointconv_supported": [_c_int] * 3,
     "kdpc_pointconv_fwd_workspace_bytes": [_c_int] * 5,
     "kdpc_pointconv_fwd": [_c_int] * 6 + [_vp] * 9 + [_c_size, _vp],
@@ -638,6 +640,30 @@ def cost_volume_bwd_csr(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout):
                wpos, bpos, w1, out, amax, gout, csr.offsets, csr.rank,
                work=(4 * B * N1 * (3 + 2 * K + din + K * din + 2 * dout + din + 3)
                      + B * N1 * dout + 4 * B * N2 * (din + 4) + 4,
+                     4.0 * B * N1 * K * din * dout))
+
+
+@functools.lru_cache(maxsize=None)
+def cost_volume_bwd_pull_supported(din, dout, k):
+    return bool(load_library().kdpc_cost_volume_bwd_pull_supported(din, dout, k))
+
+
+def cost_volume_bwd_pull(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout):
+    """-> dp1 (B,N1,Din), dp2 (B,N2,Din), dx1 (B,N1,3), dx2 (B,N2,3), dparams: the backward
+    with the per-point sums in pull form (csrc/cost_volume.hip cv_pull_kernel: one wave per
+    reference point recomputes the dz0 rows of its CSR segment; no per-neighbour rows in HBM).
+    Din == Dout in {32, 64} (cost_volume_bwd_pull_supported)."""
+    B, N1, _ = _gpu(x1, "x1").shape
+    N2, K = x2.shape[1], idx.shape[2]
+    din, dout = p1.shape[2], w1.shape[0]
+    csr = csr_of(idx, N2)
+    # reads x1, idx, p1, the K gathered p2 rows, out, gout, amax (backward kernel); offsets,
+    # perm, p2, x2 and the per-pair query rows p1 / out / gout / amax / x1 (pull kernel, cache-
+    # resident per cloud; counted once); writes dp1, dx1, dp2, dx2
+    return _op("kdpc_cost_volume_bwd_pull", "cost_volume_bwd_pull", x1, x2, idx, p1, p2,
+               wpos, bpos, w1, out, amax, gout, csr.offsets, csr.perm,
+               work=(4 * B * N1 * (3 + 2 * K + din + K * din + 2 * dout + din + 3)
+                     + B * N1 * dout + 4 * B * N2 * (2 * din + 7) + 4,
                      4.0 * B * N1 * K * din * dout))
 
 

@@ -17,7 +17,7 @@ import torch
 import torch.nn as nn
 
 from pointconv_util import (PointConvD, PointWarping, UpsampleFlow, CrossLayerLight as CrossLayer,
-                            SceneFlowEstimatorResidual, Conv1d)
+                            SceneFlowEstimatorResidual, Conv1d, cost_volume_bwd_uses_rank)
 from pointconv_util import index_points_gather as index_points, index_points_group, square_distance  # noqa: F401
 from loss_functions import multiScaleLoss  # noqa: F401  (the reference defines it here too)
 import kdpc_native
@@ -75,20 +75,25 @@ class _CoordFork:
         with torch.cuda.stream(self.side):
             idx = cross.neighbours(xa)
         idx.record_stream(self.cur)  # allocated on the side stream, read on the main one
-        return idx, xa.shape[1], warp_idx
+        return idx, xa.shape[1], warp_idx, cross.pos1.out_channels
 
     def ready(self, pending):
         """The main stream waits for the search; the inverted indices the backward will read
         are then built on the side stream, beside the cost volume."""
         if pending is None:
             return None
-        idx, n, warp_idx = pending
+        idx, n, warp_idx, d = pending
         self.cur.wait_stream(self.side)
         if torch.is_grad_enabled() and FORK_CSR:
             keep = []
             with torch.cuda.stream(self.side):
-                c = kdpc_native.csr_rank_of(idx, n)
-                keep += [c.offsets, c.perm, c.rank]
+                # the pull-form backward (D <= 64) reads offsets / perm only
+                if cost_volume_bwd_uses_rank(d, idx.shape[-1]):
+                    c = kdpc_native.csr_rank_of(idx, n)
+                    keep += [c.offsets, c.perm, c.rank]
+                else:
+                    c = kdpc_native.csr_of(idx, n)
+                    keep += [c.offsets, c.perm]
                 if warp_idx is not None:
                     warp_idx.record_stream(self.side)
                     c = kdpc_native.csr_of(warp_idx, n)

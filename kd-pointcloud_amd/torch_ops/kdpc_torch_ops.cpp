@@ -432,6 +432,36 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> cost_volume_bwd_csr(
   return {dp1, dp2, dx1, dx2, dparams};
 }
 
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> cost_volume_bwd_pull(
+    Tensor x1, Tensor x2, Tensor idx, Tensor p1, Tensor p2, Tensor wpos, Tensor bpos, Tensor w1,
+    Tensor out, Tensor amax, Tensor gout, Tensor offsets, Tensor perm) {
+  for (auto* t : {&x1, &x2, &p1, &p2, &wpos, &bpos, &w1, &out, &gout})
+    dev(*t, kF, "cost volume input");
+  dev(idx, kI, "idx"), dev(amax, at::kByte, "amax"), dev(offsets, kI, "offsets");
+  dev(perm, kI, "perm");
+  GUARD(x1);
+  const int64_t b = x1.size(0), n1 = x1.size(1), n2 = x2.size(1), k = idx.size(2);
+  const int64_t din = p1.size(2), dout = w1.size(0);
+  TORCH_CHECK(kdpc_cost_volume_bwd_pull_supported(din, dout, k),
+              "kdpc: cost_volume_bwd_pull: unsupported shape");
+  TORCH_CHECK(offsets.numel() >= b * n2 + 1 && perm.numel() >= b * n1 * k,
+              "kdpc: cost_volume_bwd_pull: offsets / perm do not match idx");
+  Tensor dp1 = empty_f({b, n1, din}, x1);
+  Tensor dp2 = empty_f({b, n2, din}, x1);
+  Tensor dx1 = empty_f({b, n1, 3}, x1);
+  Tensor dx2 = empty_f({b, n2, 3}, x1);
+  Tensor dparams = empty_f({dout * din + dout + 4 * din}, x1);
+  const size_t nb = kdpc_cost_volume_bwd_workspace_bytes(b, n1, din, dout);
+  TORCH_CHECK(nb > 0, "kdpc: cost_volume_bwd_pull: unsupported shape");
+  Tensor ws = workspace(nb, x1);
+  check(kdpc_cost_volume_bwd_pull(b, n1, n2, k, din, dout, F(x1), F(x2), I(idx), F(p1), F(p2),
+                                  F(wpos), F(bpos), F(w1), F(out), amax.data_ptr<uint8_t>(),
+                                  F(gout), I(offsets), I(perm), F(dp1), F(dp2), F(dx1), F(dx2),
+                                  ws.data_ptr(), nb, F(dparams), stream_of(x1)),
+        "cost_volume_bwd_pull");
+  return {dp1, dp2, dx1, dx2, dparams};
+}
+
 Tensor cost_volume_wide_h0(Tensor x1, Tensor x2, Tensor idx, Tensor p1, Tensor p2, Tensor wpos,
                            Tensor bpos) {
   for (auto* t : {&x1, &x2, &p1, &p2, &wpos, &bpos}) dev(*t, kF, "cost volume input");
@@ -1050,6 +1080,9 @@ TORCH_LIBRARY(kdpc, m) {
   m.def("cost_volume_bwd_csr(Tensor x1, Tensor x2, Tensor idx, Tensor p1, Tensor p2, "
         "Tensor wpos, Tensor bpos, Tensor w1, Tensor out, Tensor amax, Tensor gout, "
         "Tensor offsets, Tensor rank) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
+  m.def("cost_volume_bwd_pull(Tensor x1, Tensor x2, Tensor idx, Tensor p1, Tensor p2, "
+        "Tensor wpos, Tensor bpos, Tensor w1, Tensor out, Tensor amax, Tensor gout, "
+        "Tensor offsets, Tensor perm) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("cost_volume_wide_h0(Tensor x1, Tensor x2, Tensor idx, Tensor p1, Tensor p2, "
         "Tensor wpos, Tensor bpos) -> Tensor");
   m.def("cost_volume_wide_max(Tensor z1, int b, int n1, int k, int dout) -> (Tensor, Tensor)");
@@ -1137,6 +1170,7 @@ TORCH_LIBRARY_IMPL(kdpc, CUDA, m) {
   m.impl("cost_volume_fwd", cost_volume_fwd);
   m.impl("cost_volume_bwd", cost_volume_bwd);
   m.impl("cost_volume_bwd_csr", cost_volume_bwd_csr);
+  m.impl("cost_volume_bwd_pull", cost_volume_bwd_pull);
   m.impl("cost_volume_wide_h0", cost_volume_wide_h0);
   m.impl("cost_volume_wide_max", cost_volume_wide_max);
   m.impl("cost_volume_wide_max_bwd", cost_volume_wide_max_bwd);

@@ -93,6 +93,49 @@ def test_cost_volume_bwd_csr_bitwise(din, dout, n1, n2, bsz, k):
     assert torch.count_nonzero(r[1][:, -1]) == 0 and torch.count_nonzero(r[3][:, -1]) == 0
 
 
+@pytest.mark.parametrize("din,k,n1,n2,bsz,clustered", [
+    (32, 32, 1000, 900, 2, False), (64, 32, 513, 700, 3, False), (32, 17, 300, 300, 1, False),
+    (64, 9, 257, 600, 2, False), (32, 32, 2048, 2048, 2, True), (64, 32, 1024, 1500, 2, True)])
+def test_cost_volume_bwd_pull_matches_ranked(din, k, n1, n2, bsz, clustered):
+    """kdpc_cost_volume_bwd_pull (each reference point recomputes the dz0 rows of its CSR
+    segment, no per-neighbour rows) against the ranked path: dp1 / dx1 / dparams come from the
+    same backward kernel (bit-identical); dp2 / dx2 are the same sums in another rounding
+    (d(dir) summed after Wpos^T instead of per pair; halves of the segment added last).
+    clustered: real kNN indices (segments of very different lengths, hot points with > 64
+    pairs: the pull kernel's 64-pair chunks).  A point no query picks gets exact zeros."""
+    import kdpc_native as K
+    g = torch.Generator(device="cpu").manual_seed(din * 11 + k)
+    x1 = torch.rand(bsz, n1, 3, generator=g).to(DEV)
+    x2 = torch.rand(bsz, n2, 3, generator=g).to(DEV)
+    if clustered:
+        x2[:, : n2 // 8] *= 0.05  # a dense clump: its points are picked by many queries
+        idx = K.knn_point(k, x2[:, :-1].contiguous(), x1)
+    else:
+        idx = torch.randint(0, n2 - 1, (bsz, n1, k), generator=g, dtype=torch.int32).to(DEV)
+    p1 = torch.randn(bsz, n1, din, generator=g).to(DEV)
+    p2 = torch.randn(bsz, n2, din, generator=g).to(DEV)
+    wpos = (torch.randn(din, 3, generator=g) * 0.3).to(DEV)
+    bpos = (torch.randn(din, generator=g) * 0.1).to(DEV)
+    w1 = (torch.randn(din, din, generator=g) / din ** 0.5).to(DEV)
+    b1 = (torch.randn(din, generator=g) * 0.1).to(DEV)
+    out, amax = K.cost_volume_fwd(x1, x2, idx, p1, p2, wpos, bpos, w1, b1)
+    gout = torch.randn(bsz, n1, din, generator=g).to(DEV)
+    assert K.cost_volume_bwd_pull_supported(din, din, k)
+    r = K.cost_volume_bwd_csr(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout)
+    q = K.cost_volume_bwd_pull(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout)
+    torch.cuda.synchronize()
+    for name, a, b in zip(["dp1", "dx1", "dparams"], [q[0], q[2], q[4]], [r[0], r[2], r[4]]):
+        assert torch.equal(a, b), name
+    for name, a, b in zip(["dp2", "dx2"], [q[1], q[3]], [r[1], r[3]]):
+        scale = b.abs().max().item()
+        err = (a - b).abs().max().item()
+        assert err <= 1e-5 * scale, (name, err, scale)  # fp32 sums of <= ~200 terms
+    assert torch.count_nonzero(q[1][:, -1]) == 0 and torch.count_nonzero(q[3][:, -1]) == 0
+    # deterministic: a second call is bit-identical
+    q2 = K.cost_volume_bwd_pull(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout)
+    assert all(torch.equal(a, b) for a, b in zip(q, q2))
+
+
 def test_csr_rank_marks_out_of_range():
     """kdpc_csr_rank: perm[rank[i]] == i for in-range positions, -1 for the others."""
     import kdpc_native as K

@@ -52,7 +52,7 @@ def main():
         b1 = torch.randn(do, generator=g).to(DEV)
         gout = torch.randn(B, N1, do, generator=g).to(DEV)
         out, amax = K.cost_volume_fwd(x1, x2, idx, p1, p2, wpos, bpos, w1, b1)
-        csr = K.csr_rank_of(idx, N2)
+        csr = K.csr_rank_of(idx, N2)  # offsets / perm / rank cached: kernels only below
 
         def plain():
             dp1, rows, dx1, drows, dpar = K.cost_volume_bwd(x1, x2, idx, p1, p2, wpos, bpos, w1,
@@ -69,8 +69,15 @@ def main():
         t_bwd = timeit(lambda: K.cost_volume_bwd(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax,
                                                  gout), a.iters)
         t_ranked = timeit(ranked, a.iters)
-        print(name, {"plain_bwd_plus_sums_us": round(t_plain, 1), "plain_bwd_us": round(t_bwd, 1),
-                     "ranked_us": round(t_ranked, 1), "bit_identical": same}, flush=True)
+        res = {"plain_bwd_plus_sums_us": round(t_plain, 1), "plain_bwd_us": round(t_bwd, 1),
+               "ranked_us": round(t_ranked, 1), "bit_identical": same}
+        if K.cost_volume_bwd_pull_supported(di, do, Kn):
+            def pull():
+                return K.cost_volume_bwd_pull(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout)
+            q = pull()
+            res["pull_us"] = round(timeit(pull, a.iters), 1)
+            res["pull_max_rel_dp2"] = ((q[1] - r2[1]).abs().max() / r2[1].abs().max()).item()
+        print(name, res, flush=True)
 
 
 if __name__ == "__main__":
