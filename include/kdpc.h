@@ -225,11 +225,11 @@ int kdpc_cost_volume_bwd_csr(int b, int n1, int n2, int k, int din, int dout, co
 /* Backward with the per-reference-point sums in pull form: offsets (B*N2+1) / perm (B*N1*K)
  * of the CSR of idx over the N2 points (kdpc_csr_build).  No per-neighbour rows are written:
  * one wave per reference point recomputes the dz0 rows of its CSR segment (the forward's
- * arithmetic for h0, so every LeakyReLU branch is the forward's).  Din == Dout in {32, 64},
- * K <= 32 (kdpc_cost_volume_bwd_pull_supported).  Outputs as kdpc_cost_volume_bwd_csr (dp1,
- * dx1, dparams bit-identical; dp2 / dx2 within rounding); workspace:
- * kdpc_cost_volume_bwd_workspace_bytes.  Replaces the same backward as kdpc_cost_volume_bwd
- * (reference pointconv_util.py:1826-1850 autograd). */
+ * arithmetic for h0, so every LeakyReLU branch is the forward's).  Din == Dout in
+ * {32, 64, 128, 256}, K <= 32 (kdpc_cost_volume_bwd_pull_supported).  Outputs as
+ * kdpc_cost_volume_bwd_csr (dp1, dx1, dparams bit-identical; dp2 / dx2 within rounding);
+ * workspace: kdpc_cost_volume_bwd_workspace_bytes.  Replaces the same backward as
+ * kdpc_cost_volume_bwd (reference pointconv_util.py:1826-1850 autograd). */
 int kdpc_cost_volume_bwd_pull_supported(int din, int dout, int k);
 int kdpc_cost_volume_bwd_pull(int b, int n1, int n2, int k, int din, int dout, const float *x1,
                               const float *x2, const int *idx, const float *p1, const float *p2,

@@ -689,7 +689,7 @@ hipError_t rows_sum(int din, long long nkeys, const float* rows, const float* di
   }
 }
 
-// Pull form of the per-point sums (D_IN == D_OUT in {32, 64}, K <= 32; round 4).  The ranked
+// Pull form of the per-point sums (D_IN == D_OUT in {32, 64, 128, 256}, K <= 32; round 4).  The ranked
 // path writes one dz0 row per (query, neighbour) pair at its CSR slot and sums the rows per
 // point: B*N1*K*(D+4)*4 bytes out to HBM and back (604 MB each way at cross0, B=16 clouds of
 // 8192, K=32).  Here the backward kernel writes no rows, and one wave per reference point j
@@ -702,7 +702,7 @@ hipError_t rows_sum(int din, long long nkeys, const float* rows, const float* di
 //         g' = dout * LeakyReLU'(out)        (one term per output channel routed to row k)
 //   dz0 = dh0 * LeakyReLU'(h0);   dP2[j] = the segment's sum;   dx2[j] = Wpos^T dP2[j]
 // D = 32 runs two pairs per step (the wave's halves take alternate pairs; the two partial sums
-// are added at the end).  Fixed order throughout: deterministic.  Rounding differs from the
+// are added at the end); D >= 128 gives each lane D/64 channels and reads W1 rows from L2.  Fixed order throughout: deterministic.  Rounding differs from the
 // ranked path's (per-pair d(dir) sums; MFMA vs fma-chain dh0 when two channels route to one row).
 template <int D>
 __global__ __launch_bounds__(256) void cv_pull_kernel(
@@ -712,37 +712,53 @@ __global__ __launch_bounds__(256) void cv_pull_kernel(
     const unsigned char* __restrict__ amax, const float* __restrict__ dout,
     const int* __restrict__ offsets, const int* __restrict__ perm, float* __restrict__ dp2,
     float* __restrict__ dx2) {
-  constexpr int RPP = 64 / D;  // pairs per step
-  constexpr int U = 4;         // steps whose loads are in flight together
-  __shared__ float w1s[D * D];
-  for (int e = threadIdx.x; e < D * D; e += blockDim.x) w1s[e] = w1[e];
-  __syncthreads();
+  constexpr int RPP = D < 64 ? 64 / D : 1;  // pairs per step
+  constexpr int CPL = D > 64 ? D / 64 : 1;  // channels per lane: c = lane % D + 64 j
+  constexpr int DL = D < 64 ? D : 64;       // lanes per pair
+  constexpr int U = D > 128 ? 2 : 4;        // steps whose loads are in flight together
+  constexpr bool W1_LDS = D <= 64;          // D >= 128: W1 rows from L2 (~1 row per pair)
+  __shared__ float w1s[W1_LDS ? D * D : 1];
+  if constexpr (W1_LDS) {
+    for (int e = threadIdx.x; e < D * D; e += blockDim.x) w1s[e] = w1[e];
+    __syncthreads();
+  }
   const int wave = threadIdx.x >> 6, lane = lane_id();
-  const int c = lane % D, sub = lane / D;
+  const int c0 = lane % DL, sub = lane / DL;
   const long long key = (long long)blockIdx.x * kWaves + wave;
   if (key >= nkeys) return;
-  const float w0 = wpos[c * 3 + 0], wy = wpos[c * 3 + 1], wz = wpos[c * 3 + 2], bp = bpos[c];
-  const float pj = p2[key * D + c];
+  float w0[CPL], wy[CPL], wz[CPL], bp[CPL], pj[CPL], acc[CPL];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const int c = c0 + 64 * j;
+    w0[j] = wpos[c * 3 + 0];
+    wy[j] = wpos[c * 3 + 1];
+    wz[j] = wpos[c * 3 + 2];
+    bp[j] = bpos[c];
+    pj[j] = p2[key * D + c];
+    acc[j] = 0.f;
+  }
   const float xj0 = x2[key * 3 + 0], xj1 = x2[key * 3 + 1], xj2 = x2[key * 3 + 2];
   const int s0 = offsets[key], s1 = offsets[key + 1];
-  float acc = 0.f;
   for (int cs = s0; cs < s1; cs += 64) {  // chunks of 64 pairs: lane l holds pair cs + l
     const int cn = min(64, s1 - cs);
     const int pl = lane < cn ? perm[cs + lane] : 0;
     for (int i0 = 0; i0 < cn; i0 += RPP * U) {
-      float p1v[U], ov[U], gv[U], q0[U], q1[U], q2[U];
-      int am[U], kk[U];
+      float p1v[U][CPL], ov[U][CPL], gv[U][CPL], q0[U], q1[U], q2[U];
+      int am[U][CPL], kk[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int i = i0 + RPP * u + sub;
         const int gp = __shfl(pl, i < cn ? i : 0, kWave);
         const int ng = gp / k;  // b*N1 + n
         kk[u] = gp - ng * k;
-        const long long ro = (long long)ng * D + c;
-        p1v[u] = p1[ro];
-        ov[u] = out[ro];
-        gv[u] = dout[ro];
-        am[u] = amax[ro];
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) {
+          const long long ro = (long long)ng * D + c0 + 64 * j;
+          p1v[u][j] = p1[ro];
+          ov[u][j] = out[ro];
+          gv[u][j] = dout[ro];
+          am[u][j] = amax[ro];
+        }
         q0[u] = x1[ng * 3 + 0];
         q1[u] = x1[ng * 3 + 1];
         q2[u] = x1[ng * 3 + 2];
@@ -751,32 +767,53 @@ __global__ __launch_bounds__(256) void cv_pull_kernel(
       for (int u = 0; u < U; ++u) {
         const int i = i0 + RPP * u + sub;
         const float dx = xj0 - q0[u], dy = xj1 - q1[u], dzz = xj2 - q2[u];
-        const float pos = __fadd_rn(__builtin_fmaf(wz, dzz, __builtin_fmaf(wy, dy, __fmul_rn(w0, dx))), bp);
-        const float h = lrelu(__fadd_rn(__fadd_rn(pj, p1v[u]), pos));
-        const float gd = gv[u] * (ov[u] > 0.f ? 1.f : kSlope);
-        const unsigned long long m = __ballot(am[u] == kk[u]);
-        // the half's routing mask is uniform over the half, so the whole half runs each step
-        unsigned long long hm = D == 64 ? m : ((m >> (32 * sub)) & 0xFFFFFFFFull);
-        float dh = 0.f;
-        while (hm) {
-          const int d = __builtin_ctzll(hm);
-          hm &= hm - 1;
-          dh = __builtin_fmaf(__shfl(gd, sub * D + d, kWave), w1s[d * D + c], dh);
+        float dh[CPL];
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) dh[j] = 0.f;
+        // output channels d = 64 j' + bit routed to this row, ascending d; the routing mask is
+        // uniform over the lanes of one pair, so they run each step together
+#pragma unroll
+        for (int jo = 0; jo < CPL; ++jo) {
+          const float gd = gv[u][jo] * (ov[u][jo] > 0.f ? 1.f : kSlope);
+          const unsigned long long m = __ballot(am[u][jo] == kk[u]);
+          unsigned long long hm = DL == 64 ? m : ((m >> (DL * sub)) & ((1ull << DL) - 1ull));
+          while (hm) {
+            const int bit = __builtin_ctzll(hm);
+            hm &= hm - 1;
+            const float g = __shfl(gd, sub * DL + bit, kWave);
+            const int d = 64 * jo + bit;
+#pragma unroll
+            for (int j = 0; j < CPL; ++j)
+              dh[j] = __builtin_fmaf(g, W1_LDS ? w1s[d * D + c0 + 64 * j] : w1[d * D + c0 + 64 * j], dh[j]);
+          }
         }
-        const float dz = dh * (h > 0.f ? 1.f : kSlope);
-        if (i < cn) acc = __fadd_rn(acc, dz);
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) {
+          const float pos = __fadd_rn(__builtin_fmaf(wz[j], dzz, __builtin_fmaf(wy[j], dy, __fmul_rn(w0[j], dx))), bp[j]);
+          const float h = lrelu(__fadd_rn(__fadd_rn(pj[j], p1v[u][j]), pos));
+          const float dz = dh[j] * (h > 0.f ? 1.f : kSlope);
+          if (i < cn) acc[j] = __fadd_rn(acc[j], dz);
+        }
       }
     }
   }
-  if (RPP == 2) acc = __fadd_rn(acc, __shfl_xor(acc, 32, kWave));
-  float g0 = wpos[c * 3 + 0] * acc, g1 = wy * acc, g2 = wz * acc;
+  if (RPP == 2) acc[0] = __fadd_rn(acc[0], __shfl_xor(acc[0], 32, kWave));
+  float g0 = 0.f, g1 = 0.f, g2 = 0.f;
 #pragma unroll
-  for (int o = D / 2; o >= 1; o >>= 1) {
+  for (int j = 0; j < CPL; ++j) {
+    g0 = __builtin_fmaf(w0[j], acc[j], g0);
+    g1 = __builtin_fmaf(wy[j], acc[j], g1);
+    g2 = __builtin_fmaf(wz[j], acc[j], g2);
+  }
+#pragma unroll
+  for (int o = DL / 2; o >= 1; o >>= 1) {
     g0 = __fadd_rn(g0, __shfl_xor(g0, o, kWave));
     g1 = __fadd_rn(g1, __shfl_xor(g1, o, kWave));
     g2 = __fadd_rn(g2, __shfl_xor(g2, o, kWave));
   }
-  if (sub == 0) dp2[key * D + c] = acc;
+  if (sub == 0)
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) dp2[key * D + c0 + 64 * j] = acc[j];
   if (lane == 0) {
     dx2[key * 3 + 0] = g0;
     dx2[key * 3 + 1] = g1;
@@ -799,6 +836,8 @@ hipError_t pull_sum(int d, int k, int n2, long long nkeys, const float* x1, cons
   }
   KDPC_CV_PULL(32)
   KDPC_CV_PULL(64)
+  KDPC_CV_PULL(128)
+  KDPC_CV_PULL(256)
 #undef KDPC_CV_PULL
   return hipErrorInvalidValue;
 }
@@ -936,7 +975,8 @@ KDPC_API int kdpc_cost_volume_bwd_csr(int b, int n1, int n2, int k, int din, int
 // kdpc_cost_volume_bwd_csr (dp2 / dx2 within rounding of it); workspace as
 // kdpc_cost_volume_bwd_workspace_bytes.
 KDPC_API int kdpc_cost_volume_bwd_pull_supported(int din, int dout, int k) {
-  return din == dout && (din == 32 || din == 64) && k >= 1 && k <= 32;
+  return din == dout && (din == 32 || din == 64 || din == 128 || din == 256) && k >= 1 &&
+         k <= 32 && supported(din, dout, k);
 }
 
 KDPC_API int kdpc_cost_volume_bwd_pull(int b, int n1, int n2, int k, int din, int dout,

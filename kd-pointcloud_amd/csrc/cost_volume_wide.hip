@@ -602,7 +602,7 @@ __global__ __launch_bounds__(2 * D) void cvw_fused_bwd_kernel(
         const float4 dr = dirs[p][r];
         if (ranked) {
           if (r < k && rk[i] >= 0) *reinterpret_cast<float4*>(rows + (long long)rk[i] * D + 4 * c4) = v;
-        } else if (r < k) {
+        } else if (r < k && dp2_rows) {  // null: the pull-form caller sums per point itself
           *reinterpret_cast<float4*>(d2 + (long long)r * D) = v;
         }
         sp.x = __fadd_rn(sp.x, v.x);
@@ -678,7 +678,7 @@ __global__ __launch_bounds__(2 * D) void cvw_fused_bwd_kernel(
         if (rkd >= 0)
           *reinterpret_cast<float4*>(rows + (long long)b * n1 * k * D + (long long)rkd * 4) =
               make_float4(v.x, v.y, v.z, 0.f);
-      } else if (row) {
+      } else if (row && ddir_rows) {
         float* dd = ddir_rows + ((long long)q * k + l32) * 3;
         dd[0] = v.x;
         dd[1] = v.y;

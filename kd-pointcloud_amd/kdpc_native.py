@@ -652,7 +652,7 @@ def cost_volume_bwd_pull(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout):
     """-> dp1 (B,N1,Din), dp2 (B,N2,Din), dx1 (B,N1,3), dx2 (B,N2,3), dparams: the backward
     with the per-point sums in pull form (csrc/cost_volume.hip cv_pull_kernel: one wave per
     reference point recomputes the dz0 rows of its CSR segment; no per-neighbour rows in HBM).
-    Din == Dout in {32, 64} (cost_volume_bwd_pull_supported)."""
+    Din == Dout in {32, 64, 128, 256} (cost_volume_bwd_pull_supported)."""
     B, N1, _ = _gpu(x1, "x1").shape
     N2, K = x2.shape[1], idx.shape[2]
     din, dout = p1.shape[2], w1.shape[0]

@@ -538,12 +538,20 @@ _CV_BWD_PLAIN = os.environ.get("KDPC_CV_BWD_PLAIN") == "1"
 # KDPC_CV_BWD_PULL=0: the ranked path (rows at their CSR slots, summed per point) instead of
 # the pull form (kdpc_cost_volume_bwd_pull: no per-neighbour rows in HBM) for Din == Dout
 _CV_BWD_PULL = os.environ.get("KDPC_CV_BWD_PULL", "1") != "0"
+# KDPC_CV_BWD_PULL_WIDE=1: the pull form for the wide levels too (D in {128, 256}; A/B)
+_CV_BWD_PULL_WIDE = os.environ.get("KDPC_CV_BWD_PULL_WIDE", "0") == "1"
+
+
+def _cv_bwd_pull(din, dout, k):
+    if not _CV_BWD_PULL or (din > 64 and not _CV_BWD_PULL_WIDE):
+        return False
+    return _nat.cost_volume_bwd_pull_supported(din, dout, k)
 
 
 def cost_volume_bwd_uses_rank(d, k):
     """Whether the backward of a (d -> d, K = k) cost volume reads the CSR's rank (the ranked
     path) or only offsets / perm (the pull form)."""
-    return not (_CV_BWD_PULL and not _CV_BWD_PLAIN and _nat.cost_volume_bwd_pull_supported(d, d, k))
+    return not (not _CV_BWD_PLAIN and _cv_bwd_pull(d, d, k))
 
 
 class _CostVolume(torch.autograd.Function):
@@ -571,7 +579,7 @@ class _CostVolume(torch.autograd.Function):
             csr = _nat.csr_of(idx, N2)
             dp2 = _nat.group_rows_grad(rows.view(B, N1 * K, din), csr, B, N2, din)
             dx2 = _nat.group_rows_grad(drows.view(B, N1 * K, 3), csr, B, N2, 3)
-        elif _CV_BWD_PULL and _nat.cost_volume_bwd_pull_supported(din, dout, K):
+        elif _cv_bwd_pull(din, dout, K):
             # each reference point recomputes the dz0 rows naming it (no rows through HBM)
             dp1, dp2, dx1, dx2, dpar = _nat.cost_volume_bwd_pull(
                 x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout.contiguous())

@@ -95,7 +95,9 @@ def test_cost_volume_bwd_csr_bitwise(din, dout, n1, n2, bsz, k):
 
 @pytest.mark.parametrize("din,k,n1,n2,bsz,clustered", [
     (32, 32, 1000, 900, 2, False), (64, 32, 513, 700, 3, False), (32, 17, 300, 300, 1, False),
-    (64, 9, 257, 600, 2, False), (32, 32, 2048, 2048, 2, True), (64, 32, 1024, 1500, 2, True)])
+    (64, 9, 257, 600, 2, False), (32, 32, 2048, 2048, 2, True), (64, 32, 1024, 1500, 2, True),
+    (128, 32, 300, 280, 2, False), (256, 20, 200, 250, 2, False), (128, 32, 512, 512, 2, True),
+    (256, 32, 256, 256, 2, True)])
 def test_cost_volume_bwd_pull_matches_ranked(din, k, n1, n2, bsz, clustered):
     """kdpc_cost_volume_bwd_pull (each reference point recomputes the dz0 rows of its CSR
     segment, no per-neighbour rows) against the ranked path: dp1 / dx1 / dparams come from the

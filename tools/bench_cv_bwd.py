@@ -19,6 +19,8 @@ DEV = "cuda"
 SHAPES = {  # the model's two narrow calls at B=8 pairs: both directions as one batch of 16
     "cross0 (B16 N8192 K32 D32)": (16, 8192, 8192, 32, 32, 32),
     "cross1 (B16 N2048 K32 D64)": (16, 2048, 2048, 32, 64, 64),
+    "cross2 (B16 N512 K32 D128)": (16, 512, 512, 32, 128, 128),
+    "cross3 (B16 N256 K32 D256)": (16, 256, 256, 32, 256, 256),
 }
 
 
