@@ -228,6 +228,8 @@ int kdpc_cost_volume_bwd_csr(int b, int n1, int n2, int k, int din, int dout, co
  * arithmetic for h0, so every LeakyReLU branch is the forward's).  Din == Dout in
  * {32, 64, 128, 256}, K <= 32 (kdpc_cost_volume_bwd_pull_supported).  Outputs as
  * kdpc_cost_volume_bwd_csr (dp1, dx1, dparams bit-identical; dp2 / dx2 within rounding);
+ * order (B*N2, nullable): per-cloud order the reference points are walked in (e.g.
+ * kdpc_morton_order of x2; results do not depend on it).
  * workspace: kdpc_cost_volume_bwd_workspace_bytes.  Replaces the same backward as
  * kdpc_cost_volume_bwd (reference pointconv_util.py:1826-1850 autograd). */
 int kdpc_cost_volume_bwd_pull_supported(int din, int dout, int k);
@@ -236,7 +238,8 @@ int kdpc_cost_volume_bwd_pull(int b, int n1, int n2, int k, int din, int dout, c
                               const float *wpos, const float *bpos, const float *w1,
                               const float *out, const unsigned char *amax,
                               const float *dout_grad, const int *offsets, const int *perm,
-                              float *dp1, float *dp2, float *dx1, float *dx2, void *workspace,
+                              const int *order, float *dp1, float *dp2, float *dx1, float *dx2,
+                              void *workspace,
                               size_t workspace_bytes, float *dparams, void *stream);
 
 /* ---- unfused wide cost volume (same layers, the widths kdpc_cost_volume_fwd does not take,

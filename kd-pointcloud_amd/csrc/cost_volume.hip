@@ -704,9 +704,10 @@ hipError_t rows_sum(int din, long long nkeys, const float* rows, const float* di
 // D = 32 runs two pairs per step (the wave's halves take alternate pairs; the two partial sums
 // are added at the end); D >= 128 gives each lane D/64 channels and reads W1 rows from L2.  Fixed order throughout: deterministic.  Rounding differs from the
 // ranked path's (per-pair d(dir) sums; MFMA vs fma-chain dh0 when two channels route to one row).
-template <int D>
+template <int D, int UU>
 __global__ __launch_bounds__(256) void cv_pull_kernel(
-    int k, int n2, long long nkeys, const float* __restrict__ x1, const float* __restrict__ x2,
+    int k, int n2, long long nkeys, const int* __restrict__ order, int xcd_per,
+    const float* __restrict__ x1, const float* __restrict__ x2,
     const float* __restrict__ p1, const float* __restrict__ p2, const float* __restrict__ wpos,
     const float* __restrict__ bpos, const float* __restrict__ w1, const float* __restrict__ out,
     const unsigned char* __restrict__ amax, const float* __restrict__ dout,
@@ -715,7 +716,7 @@ __global__ __launch_bounds__(256) void cv_pull_kernel(
   constexpr int RPP = D < 64 ? 64 / D : 1;  // pairs per step
   constexpr int CPL = D > 64 ? D / 64 : 1;  // channels per lane: c = lane % D + 64 j
   constexpr int DL = D < 64 ? D : 64;       // lanes per pair
-  constexpr int U = D > 128 ? 2 : 4;        // steps whose loads are in flight together
+  constexpr int U = UU;                     // steps whose loads are in flight together
   constexpr bool W1_LDS = D <= 64;          // D >= 128: W1 rows from L2 (~1 row per pair)
   __shared__ float w1s[W1_LDS ? D * D : 1];
   if constexpr (W1_LDS) {
@@ -724,8 +725,15 @@ __global__ __launch_bounds__(256) void cv_pull_kernel(
   }
   const int wave = threadIdx.x >> 6, lane = lane_id();
   const int c0 = lane % DL, sub = lane / DL;
-  const long long key = (long long)blockIdx.x * kWaves + wave;
+  // xcd_per > 0: workgroup w runs on XCD w % 8; give each XCD a contiguous range of blocks
+  const long long blk = xcd_per > 0 ? (long long)(blockIdx.x % 8) * xcd_per + blockIdx.x / 8
+                                    : (long long)blockIdx.x;
+  long long key = blk * kWaves + wave;
   if (key >= nkeys) return;
+  if (order) {  // keys in the given per-cloud order (Morton: neighbouring waves share queries)
+    const long long b = key / n2;
+    key = b * n2 + order[key];
+  }
   float w0[CPL], wy[CPL], wz[CPL], bp[CPL], pj[CPL], acc[CPL];
 #pragma unroll
   for (int j = 0; j < CPL; ++j) {
@@ -821,23 +829,42 @@ __global__ __launch_bounds__(256) void cv_pull_kernel(
   }
 }
 
-hipError_t pull_sum(int d, int k, int n2, long long nkeys, const float* x1, const float* x2,
-                    const float* p1, const float* p2, const float* wpos, const float* bpos,
-                    const float* w1, const float* out, const unsigned char* amax,
-                    const float* dout, const int* offsets, const int* perm, float* dp2,
-                    float* dx2, hipStream_t st) {
+// A/B knobs of the pull kernel: KDPC_CV_PULL_U (steps in flight: 4 default, 8), KDPC_CV_PULL_XCD=1
+// (contiguous block ranges per XCD)
+inline int pull_u() {
+  static const int u = [] {
+    const char* v = getenv("KDPC_CV_PULL_U");
+    return v && atoi(v) == 8 ? 8 : 4;
+  }();
+  return u;
+}
+inline bool pull_xcd() {
+  static const bool x = getenv("KDPC_CV_PULL_XCD") && getenv("KDPC_CV_PULL_XCD")[0] == '1';
+  return x;
+}
+
+hipError_t pull_sum(int d, int k, int n2, long long nkeys, const int* order, const float* x1,
+                    const float* x2, const float* p1, const float* p2, const float* wpos,
+                    const float* bpos, const float* w1, const float* out,
+                    const unsigned char* amax, const float* dout, const int* offsets,
+                    const int* perm, float* dp2, float* dx2, hipStream_t st) {
   if (nkeys <= 0) return hipSuccess;
-  const dim3 grid((unsigned)divupll(nkeys, kWaves));
-#define KDPC_CV_PULL(DD)                                                                    \
-  if (d == DD) {                                                                            \
-    hipLaunchKernelGGL((cv_pull_kernel<DD>), grid, dim3(256), 0, st, k, n2, nkeys, x1, x2, p1, \
-                       p2, wpos, bpos, w1, out, amax, dout, offsets, perm, dp2, dx2);          \
-    return hipGetLastError();                                                               \
+  const long long blocks = divupll(nkeys, kWaves);
+  const int per = pull_xcd() ? (int)divupll(blocks, 8) : 0;
+  const dim3 grid((unsigned)(per > 0 ? 8ll * per : blocks));
+#define KDPC_CV_PULL(DD, UU)                                                                   \
+  if (d == DD && (DD > 64 || pull_u() == UU)) {                                               \
+    hipLaunchKernelGGL((cv_pull_kernel<DD, UU>), grid, dim3(256), 0, st, k, n2, nkeys, order,   \
+                       per, x1, x2, p1, p2, wpos, bpos, w1, out, amax, dout, offsets, perm, dp2, \
+                       dx2);                                                                   \
+    return hipGetLastError();                                                                 \
   }
-  KDPC_CV_PULL(32)
-  KDPC_CV_PULL(64)
-  KDPC_CV_PULL(128)
-  KDPC_CV_PULL(256)
+  KDPC_CV_PULL(32, 4)
+  KDPC_CV_PULL(32, 8)
+  KDPC_CV_PULL(64, 4)
+  KDPC_CV_PULL(64, 8)
+  KDPC_CV_PULL(128, 4)
+  KDPC_CV_PULL(256, 2)
 #undef KDPC_CV_PULL
   return hipErrorInvalidValue;
 }
@@ -970,7 +997,8 @@ KDPC_API int kdpc_cost_volume_bwd_csr(int b, int n1, int n2, int k, int din, int
 }
 
 // Backward with the per-point sums in pull form (cv_pull_kernel): offsets (B*N2+1) / perm
-// (B*N1*K) of the CSR of idx over the N2 points (kdpc_csr_build).  No per-neighbour rows are
+// (B*N1*K) of the CSR of idx over the N2 points (kdpc_csr_build); order (B*N2, nullable): the
+// order the reference points are walked in per cloud (kdpc_morton_order of x2).  No per-neighbour rows are
 // written; D_IN == D_OUT in {32, 64} only (kdpc_cost_volume_bwd_pull_supported).  Outputs as
 // kdpc_cost_volume_bwd_csr (dp2 / dx2 within rounding of it); workspace as
 // kdpc_cost_volume_bwd_workspace_bytes.
@@ -984,8 +1012,8 @@ KDPC_API int kdpc_cost_volume_bwd_pull(int b, int n1, int n2, int k, int din, in
                                        const float* p1, const float* p2, const float* wpos,
                                        const float* bpos, const float* w1, const float* out,
                                        const unsigned char* amax, const float* dout_grad,
-                                       const int* offsets, const int* perm, float* dp1,
-                                       float* dp2, float* dx1, float* dx2, void* workspace,
+                                       const int* offsets, const int* perm, const int* order,
+                                       float* dp1, float* dp2, float* dx1, float* dx2, void* workspace,
                                        size_t workspace_bytes, float* dparams, void* stream) {
   KDPC_CHECK_ARG(b > 0 && n1 > 0 && n2 > 0 && b <= 65535 &&
                  kdpc_cost_volume_bwd_pull_supported(din, dout, k));
@@ -999,6 +1027,6 @@ KDPC_API int kdpc_cost_volume_bwd_pull(int b, int n1, int n2, int k, int din, in
                               amax, dout_grad, dp1, nullptr, dx1, nullptr, nullptr, nullptr,
                               (float*)workspace, dparams, st);
   if (e != hipSuccess) return (int)e;
-  return (int)pull_sum(din, k, n2, (long long)b * n2, x1, x2, p1, p2, wpos, bpos, w1, out, amax,
-                       dout_grad, offsets, perm, dp2, dx2, st);
+  return (int)pull_sum(din, k, n2, (long long)b * n2, order, x1, x2, p1, p2, wpos, bpos, w1, out,
+                       amax, dout_grad, offsets, perm, dp2, dx2, st);
 }

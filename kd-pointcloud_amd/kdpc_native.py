@@ -64,7 +64,7 @@ _SIGNATURES = {
     "kdpc_cost_volume_bwd_csr_workspace_bytes": [_c_int] * 5,
     "kdpc_cost_volume_bwd_csr": [_c_int] * 6 + [_vp] * 18 + [_c_size, _vp, _vp],
     "kdpc_cost_volume_bwd_pull_supported": [_c_int] * 3,
-    "kdpc_cost_volume_bwd_pull": [_c_int] * 6 + [_vp] * 18 + [_c_size, _vp, _vp],
+    "kdpc_cost_volume_bwd_pull": [_c_int] * 6 + [_vp] * 19 + [_c_size, _vp, _vp],
     "kdpc_pointconv_supported": [_c_int] * 3,
     "kdpc_pointconv_fwd_workspace_bytes": [_c_int] * 5,
     "kdpc_pointconv_fwd": [_c_int] * 6 + [_vp] * 9 + [_c_size, _vp],
@@ -643,6 +643,9 @@ def cost_volume_bwd_csr(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout):
                      4.0 * B * N1 * K * din * dout))
 
 
+_PULL_MORTON = os.environ.get("KDPC_CV_PULL_MORTON") == "1"
+
+
 @functools.lru_cache(maxsize=None)
 def cost_volume_bwd_pull_supported(din, dout, k):
     return bool(load_library().kdpc_cost_volume_bwd_pull_supported(din, dout, k))
@@ -660,8 +663,11 @@ def cost_volume_bwd_pull(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout):
     # reads x1, idx, p1, the K gathered p2 rows, out, gout, amax (backward kernel); offsets,
     # perm, p2, x2 and the per-pair query rows p1 / out / gout / amax / x1 (pull kernel, cache-
     # resident per cloud; counted once); writes dp1, dx1, dp2, dx2
+    # KDPC_CV_PULL_MORTON=1 (A/B): reference points walked in Morton order of x2
+    order = (_op("kdpc_morton_order", "morton_order", x2.contiguous())
+             if _PULL_MORTON and N2 <= 8192 else None)
     return _op("kdpc_cost_volume_bwd_pull", "cost_volume_bwd_pull", x1, x2, idx, p1, p2,
-               wpos, bpos, w1, out, amax, gout, csr.offsets, csr.perm,
+               wpos, bpos, w1, out, amax, gout, csr.offsets, csr.perm, order,
                work=(4 * B * N1 * (3 + 2 * K + din + K * din + 2 * dout + din + 3)
                      + B * N1 * dout + 4 * B * N2 * (2 * din + 7) + 4,
                      4.0 * B * N1 * K * din * dout))

@@ -535,10 +535,13 @@ class PointConvD(_PointConvBase):
 # KDPC_CV_BWD_PLAIN=1: the D <= 64 backward writes its per-neighbour rows in (query,
 # neighbour) order and sums them through the CSR's perm (A/B runs; bit-identical)
 _CV_BWD_PLAIN = os.environ.get("KDPC_CV_BWD_PLAIN") == "1"
-# KDPC_CV_BWD_PULL=0: the ranked path (rows at their CSR slots, summed per point) instead of
-# the pull form (kdpc_cost_volume_bwd_pull: no per-neighbour rows in HBM) for Din == Dout
-_CV_BWD_PULL = os.environ.get("KDPC_CV_BWD_PULL", "1") != "0"
-# KDPC_CV_BWD_PULL_WIDE=1: the pull form for the wide levels too (D in {128, 256}; A/B)
+# KDPC_CV_BWD_PULL=1: the pull form (kdpc_cost_volume_bwd_pull: no per-neighbour rows in HBM,
+# each reference point recomputes its rows) instead of the ranked path for Din == Dout <= 64;
+# KDPC_CV_BWD_PULL_WIDE=1 also for D in {128, 256}.  Off by default: measured slower (round 4,
+# profiles/round04/pull: cross0 641 vs 623 us, step 15.94 vs 15.71 ms; the backward kernel
+# alone is 368 us without any row stores, and the pull's per-pair query gathers cost more
+# than the rows' round trip)
+_CV_BWD_PULL = os.environ.get("KDPC_CV_BWD_PULL", "0") == "1"
 _CV_BWD_PULL_WIDE = os.environ.get("KDPC_CV_BWD_PULL_WIDE", "0") == "1"
 
 

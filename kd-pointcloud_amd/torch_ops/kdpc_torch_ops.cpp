@@ -434,7 +434,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> cost_volume_bwd_csr(
 
 std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> cost_volume_bwd_pull(
     Tensor x1, Tensor x2, Tensor idx, Tensor p1, Tensor p2, Tensor wpos, Tensor bpos, Tensor w1,
-    Tensor out, Tensor amax, Tensor gout, Tensor offsets, Tensor perm) {
+    Tensor out, Tensor amax, Tensor gout, Tensor offsets, Tensor perm,
+    c10::optional<Tensor> order) {
   for (auto* t : {&x1, &x2, &p1, &p2, &wpos, &bpos, &w1, &out, &gout})
     dev(*t, kF, "cost volume input");
   dev(idx, kI, "idx"), dev(amax, at::kByte, "amax"), dev(offsets, kI, "offsets");
@@ -456,7 +457,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> cost_volume_bwd_pull(
   Tensor ws = workspace(nb, x1);
   check(kdpc_cost_volume_bwd_pull(b, n1, n2, k, din, dout, F(x1), F(x2), I(idx), F(p1), F(p2),
                                   F(wpos), F(bpos), F(w1), F(out), amax.data_ptr<uint8_t>(),
-                                  F(gout), I(offsets), I(perm), F(dp1), F(dp2), F(dx1), F(dx2),
+                                  F(gout), I(offsets), I(perm),
+                                  order.has_value() ? I(*order) : nullptr, F(dp1), F(dp2), F(dx1), F(dx2),
                                   ws.data_ptr(), nb, F(dparams), stream_of(x1)),
         "cost_volume_bwd_pull");
   return {dp1, dp2, dx1, dx2, dparams};
@@ -1082,7 +1084,7 @@ TORCH_LIBRARY(kdpc, m) {
         "Tensor offsets, Tensor rank) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("cost_volume_bwd_pull(Tensor x1, Tensor x2, Tensor idx, Tensor p1, Tensor p2, "
         "Tensor wpos, Tensor bpos, Tensor w1, Tensor out, Tensor amax, Tensor gout, "
-        "Tensor offsets, Tensor perm) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
+        "Tensor offsets, Tensor perm, Tensor? order=None) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("cost_volume_wide_h0(Tensor x1, Tensor x2, Tensor idx, Tensor p1, Tensor p2, "
         "Tensor wpos, Tensor bpos) -> Tensor");
   m.def("cost_volume_wide_max(Tensor z1, int b, int n1, int k, int dout) -> (Tensor, Tensor)");
