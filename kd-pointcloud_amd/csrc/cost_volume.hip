@@ -513,8 +513,21 @@ inline int bwd_wpe_env() {
   return w;
 }
 
+// KDPC_CV_BWD_QPW (A/B runs): a fixed query count per wave instead of one resident round (in
+// the step the kernel shares the CUs with the parameter-gradient streams' kernels); the
+// per-query arithmetic does not depend on which wave runs the query, the slab count does
+inline int bwd_qpw_env() {
+  static const int q = [] {
+    const char* v = getenv("KDPC_CV_BWD_QPW");
+    const int x = v ? atoi(v) : 0;
+    return x >= 2 && x <= 1024 ? x : 0;
+  }();
+  return q;
+}
+
 template <int DI, int DO, int W>
 inline int bwd_qpw(int b, int n1) {
+  if (bwd_qpw_env()) return bwd_qpw_env();
   return std::max(2, (int)divupll((long long)b * n1, bwd_waves_resident<DI, DO, W>()));
 }
 
