@@ -219,7 +219,12 @@ void cost_volume_bwd_kernel(
   constexpr int TILE = kRows * LD;
   constexpr int PER_WAVE = TILE + 4 * kRows + 2 * D_OUT;  // h0/dz0, directions, (g', argmax)
   constexpr int SHARED = 4 * D_IN;                         // Wpos rows (x, y, z, 0)
-  constexpr int BODY = SHARED + kWaves * PER_WAVE;
+  // LEAN (the 3 / 4 waves-per-SIMD builds): W1's B fragments read from LDS at each MFMA
+  // instead of held in registers, and no cross-query prefetch (a query's loads are issued at
+  // the top of its iteration; the other resident waves cover their latency)
+  constexpr bool LEAN = WPE >= 3;
+  constexpr int W1_AT = SHARED + kWaves * PER_WAVE;
+  constexpr int BODY = W1_AT + (LEAN ? D_OUT * D_IN : 0);
   constexpr int LDS_FLOATS = BODY > SLAB ? BODY : SLAB;
   static_assert(TILE % 4 == 0 && PER_WAVE % 4 == 0, "16-byte aligned LDS tables");
   __shared__ __attribute__((aligned(16))) float lds_all[LDS_FLOATS];
@@ -235,14 +240,19 @@ void cost_volume_bwd_kernel(
   float2* gdam = reinterpret_cast<float2*>(T + TILE + 4 * kRows);
   for (int e = threadIdx.x; e < D_IN; e += blockDim.x)
     wposT[e] = make_float4(wpos[e * 3 + 0], wpos[e * 3 + 1], wpos[e * 3 + 2], 0.f);
+  float* w1s = lds_all + W1_AT;
+  if constexpr (LEAN)
+    for (int e = threadIdx.x; e < D_OUT * D_IN; e += blockDim.x) w1s[e] = w1[e];
   __syncthreads();
 
   // B fragments of W1 for dh0 = M W1 (inner index d): lane supplies W1[2s + half][32t + l32]
-  float bwt[TI][D_OUT / 2];
+  float bwt[TI][LEAN ? 1 : D_OUT / 2];
+  if constexpr (!LEAN) {
 #pragma unroll
-  for (int t = 0; t < TI; ++t)
+    for (int t = 0; t < TI; ++t)
 #pragma unroll
-    for (int s2 = 0; s2 < D_OUT / 2; ++s2) bwt[t][s2] = w1[(2 * s2 + half) * D_IN + 32 * t + l32];
+      for (int s2 = 0; s2 < D_OUT / 2; ++s2) bwt[t][s2] = w1[(2 * s2 + half) * D_IN + 32 * t + l32];
+  }
   const float w0 = wpos[c * 3 + 0], wy = wpos[c * 3 + 1], wz = wpos[c * 3 + 2], bp = bpos[c];
 
   const float* x1b = x1 + (long long)b * n1 * 3;
@@ -308,10 +318,16 @@ void cost_volume_bwd_kernel(
     amv = __builtin_amdgcn_raw_buffer_load_b8(amr, (int)oo, 0, 0);
   };
   load_idx(q0);
-  issue(q0);
-  load_idx(q0 + 1);
+  if constexpr (!LEAN) {
+    issue(q0);
+    load_idx(q0 + 1);
+  }
 
   for (int n = q0; n < q1; ++n) {
+    if constexpr (LEAN) {
+      issue(n);
+      load_idx(n + 1);
+    }
     // lane r: the slot of row r (used by the row passes, after this query's MFMAs)
     const int rkv = (int)__builtin_amdgcn_raw_buffer_load_b32(
         rkr, (int)(lane < k ? ((unsigned)n * (unsigned)k + lane) * 4u : kOOB), 0, 0);
@@ -330,8 +346,10 @@ void cost_volume_bwd_kernel(
       if (i % 4 == 3) __builtin_amdgcn_sched_barrier(0);
     }
     // ---- the next query's loads, in flight during this query's compute
-    issue(n + 1);
-    load_idx(n + 2);
+    if constexpr (!LEAN) {
+      issue(n + 1);
+      load_idx(n + 2);
+    }
     __builtin_amdgcn_sched_barrier(0);
 
     // ---- dh0 = M W1 on the matrix cores, M[r][d] = g'[d] [am[d] == r]: the MFMA's f32
@@ -346,7 +364,9 @@ void cost_volume_bwd_kernel(
       const float a = __float_as_int(ga.y) == l32 ? ga.x : 0.f;
 #pragma unroll
       for (int t = 0; t < TI; ++t)
-        dacc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bwt[t][s2], dacc[t], 0, 0, 0);
+        dacc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+            a, LEAN ? w1s[(2 * s2 + half) * D_IN + 32 * t + l32] : bwt[t][LEAN ? 0 : s2],
+            dacc[t], 0, 0, 0);
     }
     // ---- dW1[d, c] += g'[d] h0[am[d], c] (reads h0 before dz0 overwrites it)
 #pragma unroll
@@ -499,19 +519,21 @@ int bwd_waves_resident() {
   return w;
 }
 
-// waves per SIMD the kernel is compiled for: 2 for D_IN = 32 (183 VGPRs), 1 for D_IN = 64;
-// KDPC_CV_BWD_WPE=3|4 picks a higher-occupancy build of the D = 32 kernel (A/B runs: the
-// compiler then spills to reach 168 / 128 VGPRs)
-template <int DI>
-constexpr int bwd_wpe_default() { return DI == 32 ? 2 : 1; }
+// waves per SIMD the kernel is compiled for: D_IN = D_OUT = 32 -> 3, the LEAN build (168 VGPRs, no
+// spill: W1 fragments from LDS, no cross-query prefetch; round 4, tools/gpu_s2h.sh: cross0
+// 621 -> 574 us with the CSR sums, bit-identical), (32, 64) -> 2, D_IN = 64 -> 1.  KDPC_CV_BWD_WPE=2 picks
+// the prefetching 2-wave build (206 VGPRs), =4 a LEAN 4-wave build (spills; slower).
+template <int DI, int DO>
+constexpr int bwd_wpe_default() { return DI == 32 ? (DO == 32 ? 3 : 2) : 1; }
 
 inline int bwd_wpe_env() {
   static const int w = [] {
     const char* v = getenv("KDPC_CV_BWD_WPE");
-    return v && (v[0] == '3' || v[0] == '4') ? v[0] - '0' : 0;
+    return v && (v[0] == '2' || v[0] == '3' || v[0] == '4') ? v[0] - '0' : 0;
   }();
   return w;
 }
+inline int cv32_wpe() { return bwd_wpe_env() ? bwd_wpe_env() : bwd_wpe_default<32, 32>(); }
 
 // KDPC_CV_BWD_QPW (A/B runs): a fixed query count per wave instead of one resident round (in
 // the step the kernel shares the CUs with the parameter-gradient streams' kernels); the
@@ -533,9 +555,9 @@ inline int bwd_qpw(int b, int n1) {
 
 inline int bwd_qpw_of(int b, int n1, int din, int dout) {
   if (din == 32 && dout == 32) {
-    if (bwd_wpe_env() == 3) return bwd_qpw<32, 32, 3>(b, n1);
-    if (bwd_wpe_env() == 4) return bwd_qpw<32, 32, 4>(b, n1);
-    return bwd_qpw<32, 32, 2>(b, n1);
+    if (cv32_wpe() == 2) return bwd_qpw<32, 32, 2>(b, n1);
+    if (cv32_wpe() == 4) return bwd_qpw<32, 32, 4>(b, n1);
+    return bwd_qpw<32, 32, 3>(b, n1);
   }
   if (din == 32 && dout == 64) return bwd_qpw<32, 64, 2>(b, n1);
   if (din == 64 && dout == 32) return bwd_qpw<64, 32, 1>(b, n1);
@@ -589,10 +611,10 @@ hipError_t bwd_launch(int b, int n1, int n2, int k, const float* x1, const float
 #define KDPC_CV_BWD_ARGS b, n1, n2, k, x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, dout, dp1, \
                          dp2_rows, dx1, ddir_rows, rank, rows, slab, dparams, st
   if constexpr (DI == 32 && DO == 32) {
-    if (bwd_wpe_env() == 3) return bwd_launch_w<32, 32, 3>(KDPC_CV_BWD_ARGS);
-    if (bwd_wpe_env() == 4) return bwd_launch_w<32, 32, 4>(KDPC_CV_BWD_ARGS);
+    if (cv32_wpe() == 2) return bwd_launch_w<32, 32, 2>(KDPC_CV_BWD_ARGS);
+    if (cv32_wpe() == 4) return bwd_launch_w<32, 32, 4>(KDPC_CV_BWD_ARGS);
   }
-  return bwd_launch_w<DI, DO, bwd_wpe_default<DI>()>(KDPC_CV_BWD_ARGS);
+  return bwd_launch_w<DI, DO, bwd_wpe_default<DI, DO>()>(KDPC_CV_BWD_ARGS);
 #undef KDPC_CV_BWD_ARGS
 }
 
