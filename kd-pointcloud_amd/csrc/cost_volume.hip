@@ -53,8 +53,12 @@ constexpr unsigned kOOB = 0x80000000u;  // out-of-range byte offset: loads read 
 // Forward: one wave per query, queries walked in a software pipeline (as the backward
 // below): query n+1's P2 rows / directions / P1 row and query n+2's neighbour indices are in
 // flight while query n's MLP runs on the matrix cores.  Rows r >= k build h0 = 0.
-template <int D_IN, int D_OUT>
-__global__ __launch_bounds__(256) void cost_volume_fwd_kernel(
+// LEAN (D_IN = 64 A/B, KDPC_CV_FWD_LEAN): W1's B fragments read from a padded LDS copy at each
+// MFMA instead of D_IN * D_OUT / 64 registers, and no cross-query prefetch, so more waves fit
+// per SIMD; the same MFMAs on the same values (bit-identical outputs)
+template <int D_IN, int D_OUT, bool LEAN = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAN ? 3 : 1)))
+void cost_volume_fwd_kernel(
     int n1, int n2, int k, int queries_per_wave, const float* __restrict__ x1,
     const float* __restrict__ x2, const int* __restrict__ idx, const float* __restrict__ p1,
     const float* __restrict__ p2, const float* __restrict__ wpos, const float* __restrict__ bpos,
@@ -66,6 +70,8 @@ __global__ __launch_bounds__(256) void cost_volume_fwd_kernel(
   constexpr int RT = kRows / RPP;
   __shared__ float lds[kWaves][kRows * LD];
   __shared__ float4 dir_lds[kWaves][kRows];  // the query's neighbour directions (lane r)
+  constexpr int LDW = D_IN + 1;              // padded W1 rows: the 32 rows a read names differ in bank
+  __shared__ float w1s[LEAN ? D_OUT * LDW : 1];
   const int b = blockIdx.y;
   const int wave = threadIdx.x >> 6;
   const int lane = lane_id();
@@ -82,12 +88,18 @@ __global__ __launch_bounds__(256) void cost_volume_fwd_kernel(
   const int q0 = (blockIdx.x * kWaves + wave) * queries_per_wave;
   const int q1 = min(n1, q0 + queries_per_wave);
   // B fragments of W1 (lane l: W1[t*32 + (l&31)][2s + (l>>5)]), reused for every query
-  float bw[TILES][D_IN / 2];
+  float bw[TILES][LEAN ? 1 : D_IN / 2];
+  if constexpr (LEAN) {
+    for (int e = threadIdx.x; e < D_OUT * D_IN; e += blockDim.x)
+      w1s[(e / D_IN) * LDW + e % D_IN] = w1[e];
+    __syncthreads();
+  } else {
 #pragma unroll
-  for (int t = 0; t < TILES; ++t)
+    for (int t = 0; t < TILES; ++t)
 #pragma unroll
-    for (int s = 0; s < D_IN / 2; ++s)
-      bw[t][s] = w1[(t * 32 + (lane & 31)) * D_IN + 2 * s + (lane >> 5)];
+      for (int s = 0; s < D_IN / 2; ++s)
+        bw[t][s] = w1[(t * 32 + (lane & 31)) * D_IN + 2 * s + (lane >> 5)];
+  }
   float bias[TILES];
 #pragma unroll
   for (int t = 0; t < TILES; ++t) bias[t] = b1[t * 32 + (lane & 31)];
@@ -120,10 +132,16 @@ __global__ __launch_bounds__(256) void cost_volume_fwd_kernel(
   };
   if (q0 < q1) {
     load_idx(q0);
-    issue(q0);
-    load_idx(q0 + 1);
+    if constexpr (!LEAN) {
+      issue(q0);
+      load_idx(q0 + 1);
+    }
   }
   for (int n = q0; n < q1; ++n) {
+    if constexpr (LEAN) {
+      issue(n);
+      if (n + 1 < q1) load_idx(n + 1);
+    }
     // ---- h0 of query n into LDS (layout L) from the prefetched registers
     const float qx = x1b[n * 3 + 0], qy = x1b[n * 3 + 1], qz = x1b[n * 3 + 2];
     // lane r's direction to its neighbour, broadcast to the row passes through LDS (one
@@ -141,7 +159,7 @@ __global__ __launch_bounds__(256) void cost_volume_fwd_kernel(
       if (i % 4 == 3) __builtin_amdgcn_sched_barrier(0);
     }
     // ---- the next query's loads, in flight during this query's MFMAs
-    if (n + 1 < q1) {
+    if (!LEAN && n + 1 < q1) {
       issue(n + 1);
       if (n + 2 < q1) load_idx(n + 2);
     }
@@ -155,7 +173,9 @@ __global__ __launch_bounds__(256) void cost_volume_fwd_kernel(
       const float a = lds_h[(lane & 31) * LD + 2 * s + (lane >> 5)];
 #pragma unroll
       for (int t = 0; t < TILES; ++t)
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bw[t][s], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+            a, LEAN ? w1s[(t * 32 + (lane & 31)) * LDW + 2 * s + (lane >> 5)] : bw[t][LEAN ? 0 : s],
+            acc[t], 0, 0, 0);
     }
     const int h = lane >> 5;
 #pragma unroll
@@ -566,6 +586,11 @@ inline int bwd_qpw_of(int b, int n1, int din, int dout) {
 
 inline int slab_len(int din, int dout) { return dout * din + dout + 4 * din; }
 
+inline bool fwd_lean() {
+  static const bool l = getenv("KDPC_CV_FWD_LEAN") && getenv("KDPC_CV_FWD_LEAN")[0] == '1';
+  return l;
+}
+
 template <int DI, int DO>
 hipError_t fwd_launch(int b, int n1, int n2, int k, const float* x1, const float* x2,
                       const int* idx, const float* p1, const float* p2, const float* wpos,
@@ -573,6 +598,13 @@ hipError_t fwd_launch(int b, int n1, int n2, int k, const float* x1, const float
                       unsigned char* amax, hipStream_t st) {
   const int qpw = fwd_qpw();
   dim3 grid(divup(n1, kWaves * qpw), b);
+  if constexpr (DI == 64) {
+    if (fwd_lean()) {
+      hipLaunchKernelGGL((cost_volume_fwd_kernel<DI, DO, true>), grid, dim3(256), 0, st, n1, n2,
+                         k, qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, b1, out, amax);
+      return hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL((cost_volume_fwd_kernel<DI, DO>), grid, dim3(256), 0, st, n1, n2, k,
                      qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, b1, out, amax);
   return hipGetLastError();

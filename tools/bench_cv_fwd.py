@@ -42,7 +42,7 @@ def main():
         torch.cuda.synchronize()
         print(name, "qpw", os.environ.get("KDPC_CV_FWD_QPW", "8"), "us",
               round(s.elapsed_time(e) / 20 * 1e3, 1),
-              "checksum", float(out0[0].double().sum()), flush=True)
+              "checksum", float(out0[0].double().sum()), int(out0[1].long().sum()), flush=True)
 
 
 if __name__ == "__main__":
