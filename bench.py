@@ -74,11 +74,12 @@ ROOFLINE = {
     "kdpc_cost_volume_bwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF, ["cost_volume_bwd_kernel"]),
     # the model's backward: rows in CSR order + contiguous per-point sums (+ the slab colsum)
     "kdpc_cost_volume_bwd_csr": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF,
-                                 ["cost_volume_bwd_kernel", "cv_rows_sum_kernel<32>",
-                                  "cv_rows_sum_kernel<64>"]),
+                                 ["cost_volume_bwd_kernel", "cv_rows_sum_lds_kernel<32>",
+                                  "cv_rows_sum_lds_kernel<64>"]),
     "kdpc_cost_volume_bwd_csr_wide": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF,
                                       ["cvw_fused_bwd_kernel", "cvw_transpose_kernel",
-                                       "cv_rows_sum_kernel<128>", "cv_rows_sum_kernel<256>"]),
+                                       "cv_rows_sum_lds_kernel<128>",
+                                       "cv_rows_sum_lds_kernel<256>"]),
     "kdpc_idw_blend_fwd": ("hbm", "GB/s", HBM_PEAK_GBS, ["idw_fwd_kernel"]),
 }
 # the step's dominant entry point (rocprofv3 step profile, profiles/)
@@ -487,8 +488,6 @@ def main(argv=None):
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    if os.environ.get("KDPC_BLAS"):
-        torch.backends.cuda.preferred_blas_library(os.environ["KDPC_BLAS"])
     sections = set(args.sections.split(","))
     head_mode = args.mode
     head_batch = args.batch

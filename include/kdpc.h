@@ -199,12 +199,18 @@ int kdpc_cost_volume_fwd(int b, int n1, int n2, int k, int din, int dout, const 
 /* Backward: dout_grad (B,N1,Dout) -> dp1 (B,N1,Din), dp2_rows (B,N1,K,Din), dx1 (B,N1,3),
  * ddir_rows (B,N1,K,3), dparams = [dW1 (Dout*Din) | db1 (Dout) | dWpos^T (3*Din) | dbpos (Din)].
  * dp2_rows/ddir_rows are per-neighbour rows: sum them per reference point with
- * kdpc_group_rows_grad_csr over the CSR of idx.  workspace: see *_workspace_bytes. */
+ * kdpc_group_rows_grad_csr over the CSR of idx.  workspace: see *_workspace_bytes.
+ * The two LeakyReLUs' derivatives are the backward's only discrete inputs besides amax: the
+ * second one's is read from the sign of `out`; slope0 (B,N1,K,Din) u8, nullable (null in
+ * training) overrides the first one's per (query, neighbour, channel): 1 -> 1, 2 -> 0.1,
+ * 0 -> the sign of the recomputed pre-activation.  The parity tests replay a float64
+ * reference run's decisions at near-ties through slope0 and `out`. */
 size_t kdpc_cost_volume_bwd_workspace_bytes(int b, int n1, int din, int dout);
 int kdpc_cost_volume_bwd(int b, int n1, int n2, int k, int din, int dout, const float *x1,
                          const float *x2, const int *idx, const float *p1, const float *p2,
                          const float *wpos, const float *bpos, const float *w1, const float *out,
-                         const unsigned char *amax, const float *dout_grad, float *dp1,
+                         const unsigned char *amax, const unsigned char *slope0,
+                         const float *dout_grad, float *dp1,
                          float *dp2_rows, float *dx1, float *ddir_rows, void *workspace,
                          size_t workspace_bytes, float *dparams, void *stream);
 
@@ -218,29 +224,10 @@ int kdpc_cost_volume_bwd_csr(int b, int n1, int n2, int k, int din, int dout, co
                              const float *x2, const int *idx, const float *p1, const float *p2,
                              const float *wpos, const float *bpos, const float *w1,
                              const float *out, const unsigned char *amax,
-                             const float *dout_grad, const int *offsets, const int *rank,
-                             float *dp1, float *dp2, float *dx1, float *dx2, void *workspace,
-                             size_t workspace_bytes, float *dparams, void *stream);
-
-/* Backward with the per-reference-point sums in pull form: offsets (B*N2+1) / perm (B*N1*K)
- * of the CSR of idx over the N2 points (kdpc_csr_build).  No per-neighbour rows are written:
- * one wave per reference point recomputes the dz0 rows of its CSR segment (the forward's
- * arithmetic for h0, so every LeakyReLU branch is the forward's).  Din == Dout in
- * {32, 64, 128, 256}, K <= 32 (kdpc_cost_volume_bwd_pull_supported).  Outputs as
- * kdpc_cost_volume_bwd_csr (dp1, dx1, dparams bit-identical; dp2 / dx2 within rounding);
- * order (B*N2, nullable): per-cloud order the reference points are walked in (e.g.
- * kdpc_morton_order of x2; results do not depend on it).
- * workspace: kdpc_cost_volume_bwd_workspace_bytes.  Replaces the same backward as
- * kdpc_cost_volume_bwd (reference pointconv_util.py:1826-1850 autograd). */
-int kdpc_cost_volume_bwd_pull_supported(int din, int dout, int k);
-int kdpc_cost_volume_bwd_pull(int b, int n1, int n2, int k, int din, int dout, const float *x1,
-                              const float *x2, const int *idx, const float *p1, const float *p2,
-                              const float *wpos, const float *bpos, const float *w1,
-                              const float *out, const unsigned char *amax,
-                              const float *dout_grad, const int *offsets, const int *perm,
-                              const int *order, float *dp1, float *dp2, float *dx1, float *dx2,
-                              void *workspace,
-                              size_t workspace_bytes, float *dparams, void *stream);
+                             const unsigned char *slope0, const float *dout_grad,
+                             const int *offsets, const int *rank, float *dp1, float *dp2,
+                             float *dx1, float *dx2, void *workspace, size_t workspace_bytes,
+                             float *dparams, void *stream);
 
 /* ---- unfused wide cost volume (same layers, the widths kdpc_cost_volume_fwd does not take,
  *      Din in {64,128,256,512}): the Din -> Dout MLP is the caller's BLAS GEMM between these

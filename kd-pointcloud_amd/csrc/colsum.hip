@@ -20,18 +20,10 @@ using kdpc::divupll;
 constexpr int kCols = 64;        // columns per workgroup
 constexpr int kGroups = 4;       // row groups per workgroup (256 threads)
 constexpr int kOneLevel = 256;   // rows summed in a single launch
-// level-1 workgroups aimed for: 512 (round-4 whole-step A/B, tools/gpu_r4aa.sh, six runs
-// each: 16.04 vs 16.15 ms mean at 1024; 2048 in between).  KDPC_COLSUM_WG overrides for A/B
-// runs: the slab partition, hence the summation grouping, follows it.
-constexpr int kLevel1WGDefault = 512;
-inline int level1_wg() {
-  static const int w = [] {
-    const char* v = getenv("KDPC_COLSUM_WG");
-    const int x = v ? atoi(v) : 0;
-    return x >= 64 && x <= 16384 ? x : kLevel1WGDefault;
-  }();
-  return w;
-}
+// level-1 workgroups aimed for: 512 (round-4 whole-step A/B, six runs each: 16.04 vs 16.15 ms
+// mean at 1024; 2048 in between)
+constexpr int kLevel1WG = 512;
+inline int level1_wg() { return kLevel1WG; }
 
 // out[blockIdx.y][c] = sum of rows [blockIdx.y*rpw, +rpw) of column c: row group g sums the
 // g-th contiguous quarter ascending, the quarters are added in order

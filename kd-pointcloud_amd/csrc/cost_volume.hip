@@ -53,11 +53,8 @@ constexpr unsigned kOOB = 0x80000000u;  // out-of-range byte offset: loads read 
 // Forward: one wave per query, queries walked in a software pipeline (as the backward
 // below): query n+1's P2 rows / directions / P1 row and query n+2's neighbour indices are in
 // flight while query n's MLP runs on the matrix cores.  Rows r >= k build h0 = 0.
-// LEAN (D_IN = 64 A/B, KDPC_CV_FWD_LEAN): W1's B fragments read from a padded LDS copy at each
-// MFMA instead of D_IN * D_OUT / 64 registers, and no cross-query prefetch, so more waves fit
-// per SIMD; the same MFMAs on the same values (bit-identical outputs)
-template <int D_IN, int D_OUT, bool LEAN = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEAN ? 3 : 1)))
+template <int D_IN, int D_OUT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
 void cost_volume_fwd_kernel(
     int n1, int n2, int k, int queries_per_wave, const float* __restrict__ x1,
     const float* __restrict__ x2, const int* __restrict__ idx, const float* __restrict__ p1,
@@ -70,8 +67,6 @@ void cost_volume_fwd_kernel(
   constexpr int RT = kRows / RPP;
   __shared__ float lds[kWaves][kRows * LD];
   __shared__ float4 dir_lds[kWaves][kRows];  // the query's neighbour directions (lane r)
-  constexpr int LDW = D_IN + 1;              // padded W1 rows: the 32 rows a read names differ in bank
-  __shared__ float w1s[LEAN ? D_OUT * LDW : 1];
   const int b = blockIdx.y;
   const int wave = threadIdx.x >> 6;
   const int lane = lane_id();
@@ -88,18 +83,12 @@ void cost_volume_fwd_kernel(
   const int q0 = (blockIdx.x * kWaves + wave) * queries_per_wave;
   const int q1 = min(n1, q0 + queries_per_wave);
   // B fragments of W1 (lane l: W1[t*32 + (l&31)][2s + (l>>5)]), reused for every query
-  float bw[TILES][LEAN ? 1 : D_IN / 2];
-  if constexpr (LEAN) {
-    for (int e = threadIdx.x; e < D_OUT * D_IN; e += blockDim.x)
-      w1s[(e / D_IN) * LDW + e % D_IN] = w1[e];
-    __syncthreads();
-  } else {
+  float bw[TILES][D_IN / 2];
 #pragma unroll
-    for (int t = 0; t < TILES; ++t)
+  for (int t = 0; t < TILES; ++t)
 #pragma unroll
-      for (int s = 0; s < D_IN / 2; ++s)
-        bw[t][s] = w1[(t * 32 + (lane & 31)) * D_IN + 2 * s + (lane >> 5)];
-  }
+    for (int s = 0; s < D_IN / 2; ++s)
+      bw[t][s] = w1[(t * 32 + (lane & 31)) * D_IN + 2 * s + (lane >> 5)];
   float bias[TILES];
 #pragma unroll
   for (int t = 0; t < TILES; ++t) bias[t] = b1[t * 32 + (lane & 31)];
@@ -132,16 +121,10 @@ void cost_volume_fwd_kernel(
   };
   if (q0 < q1) {
     load_idx(q0);
-    if constexpr (!LEAN) {
-      issue(q0);
-      load_idx(q0 + 1);
-    }
+    issue(q0);
+    load_idx(q0 + 1);
   }
   for (int n = q0; n < q1; ++n) {
-    if constexpr (LEAN) {
-      issue(n);
-      if (n + 1 < q1) load_idx(n + 1);
-    }
     // ---- h0 of query n into LDS (layout L) from the prefetched registers
     const float qx = x1b[n * 3 + 0], qy = x1b[n * 3 + 1], qz = x1b[n * 3 + 2];
     // lane r's direction to its neighbour, broadcast to the row passes through LDS (one
@@ -159,7 +142,7 @@ void cost_volume_fwd_kernel(
       if (i % 4 == 3) __builtin_amdgcn_sched_barrier(0);
     }
     // ---- the next query's loads, in flight during this query's MFMAs
-    if (!LEAN && n + 1 < q1) {
+    if (n + 1 < q1) {
       issue(n + 1);
       if (n + 2 < q1) load_idx(n + 2);
     }
@@ -173,9 +156,7 @@ void cost_volume_fwd_kernel(
       const float a = lds_h[(lane & 31) * LD + 2 * s + (lane >> 5)];
 #pragma unroll
       for (int t = 0; t < TILES; ++t)
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(
-            a, LEAN ? w1s[(t * 32 + (lane & 31)) * LDW + 2 * s + (lane >> 5)] : bw[t][LEAN ? 0 : s],
-            acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bw[t][s], acc[t], 0, 0, 0);
     }
     const int h = lane >> 5;
 #pragma unroll
@@ -217,15 +198,22 @@ void cost_volume_fwd_kernel(
 // MFMA accumulator: lane (half, l32), tile t: column 32t + l32, rows (e&3) + 8(e>>2) + 4 half.
 // Row-per-lane (direction gradients): lane l32 = neighbour row, the two halves split the
 // channels.  D_IN = 32: the halves of L split the rows and the dW1 rows, nothing idles.
+//
+// OVR (test seam, never the training path): slope0 (B,N1,K,D_IN) u8 overrides the first
+// LeakyReLU's derivative per (query, neighbour, channel): 1 -> slope 1, 2 -> slope 0.1, 0 -> the
+// sign of the recomputed h0.  The gradient parity tests replay a float64 reference run's
+// decisions at near-ties through it (tests/test_gpu_model.py::_CvReplay); the second LeakyReLU
+// reads its decision from the sign of `out` only, so those are replayed through `out`.
 
-template <int D_IN, int D_OUT, int WPE>
+template <int D_IN, int D_OUT, int WPE, bool OVR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 void cost_volume_bwd_kernel(
     int n1, int n2, int k, int queries_per_wave, const float* __restrict__ x1,
     const float* __restrict__ x2, const int* __restrict__ idx, const float* __restrict__ p1,
     const float* __restrict__ p2, const float* __restrict__ wpos, const float* __restrict__ bpos,
     const float* __restrict__ w1, const float* __restrict__ out,
-    const unsigned char* __restrict__ amax, const float* __restrict__ dout,
+    const unsigned char* __restrict__ amax, const unsigned char* __restrict__ slope0,
+    const float* __restrict__ dout,
     float* __restrict__ dp1, float* __restrict__ dp2_rows, float* __restrict__ dx1,
     float* __restrict__ ddir_rows, const int* __restrict__ rank, float* __restrict__ rows,
     float* __restrict__ slab) {
@@ -284,6 +272,8 @@ void cost_volume_bwd_kernel(
   const __amdgpu_buffer_rsrc_t outr = rsrc_of(out + ob0, (long long)n1 * D_OUT * 4);
   const __amdgpu_buffer_rsrc_t dor = rsrc_of(dout + ob0, (long long)n1 * D_OUT * 4);
   const __amdgpu_buffer_rsrc_t amr = rsrc_of(amax + ob0, (long long)n1 * D_OUT);
+  const __amdgpu_buffer_rsrc_t s0r =
+      rsrc_of(OVR ? slope0 + (long long)b * n1 * k * D_IN : amax, OVR ? (long long)n1 * k * D_IN : 0);
   // ranked rows (rank != null): row (n, r) goes to slot rank[n, r] of the CSR of idx, so the
   // per-point sums read each segment contiguously (cv_rows_sum_kernel)
   const bool ranked = rank != nullptr;
@@ -402,9 +392,16 @@ void cost_volume_bwd_kernel(
     for (int t = 0; t < TI; ++t)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int a = ((e & 3) + 8 * (e >> 2) + 4 * half) * LD + 32 * t + l32;
+        const int row = (e & 3) + 8 * (e >> 2) + 4 * half;
+        const int a = row * LD + 32 * t + l32;
         const float hv = T[a];
-        T[a] = dacc[t][e] * (hv > 0.f ? 1.f : kSlope);
+        float sl = hv > 0.f ? 1.f : kSlope;
+        if constexpr (OVR) {  // rows >= k read past the query's block or 0: dacc is 0 there
+          const unsigned o = __builtin_amdgcn_raw_buffer_load_b8(
+              s0r, (int)((((unsigned)n * (unsigned)k + row) * D_IN + 32 * t + l32)), 0, 0);
+          sl = o == 1u ? 1.f : (o == 2u ? kSlope : sl);
+        }
+        T[a] = dacc[t][e] * sl;
         if (e % 8 == 7) __builtin_amdgcn_sched_barrier(0);
       }
     __builtin_amdgcn_sched_barrier(0);
@@ -507,27 +504,19 @@ void cost_volume_bwd_kernel(
   for (int e = threadIdx.x; e < SLAB; e += blockDim.x) sb[e] = rw[e];
 }
 
-// forward queries per wave: 16 (A/B, tools/gpu_r4t.sh: cross0 191.6 -> 185.3 us, cross1
-// 146.9 -> 136.9 us against 8; 32+ leaves SIMDs idle at the tail).  KDPC_CV_FWD_QPW overrides
-// for A/B runs: the per-query arithmetic does not depend on which wave runs the query.
-inline int fwd_qpw() {
-  static const int q = [] {
-    const char* v = getenv("KDPC_CV_FWD_QPW");
-    const int x = v ? atoi(v) : 0;
-    return x >= 2 && x <= 256 ? x : 16;
-  }();
-  return q;
-}
-// backward queries per wave: enough waves for ~8 per SIMD over the launch (the workgroups'
-// partial slabs grow with the wave count; the pipeline amortises its prologue over the rest)
+// forward queries per wave: 16 (round 4 A/B: cross0 191.6 -> 185.3 us, cross1 146.9 -> 136.9 us
+// against 8; 32+ leaves SIMDs idle at the tail)
+constexpr int kFwdQpw = 16;
+
 // backward queries per wave: as many waves as the chip holds at the kernel's occupancy, in
-// ONE round (16 per wave at 8192 waves left the D=32 kernel -- 5 waves per SIMD by its
-// registers -- a 60 %-full second round); at least 2 queries per wave for the pipeline
+// ONE round (16 per wave at 8192 waves left the D=32 kernel a 60 %-full second round); at
+// least 2 queries per wave for the pipeline
 template <int DI, int DO, int W>
 int bwd_waves_resident() {
   static const int w = [] {
     int blocks = 0, dev = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, cost_volume_bwd_kernel<DI, DO, W>,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks,
+                                                     cost_volume_bwd_kernel<DI, DO, W, false>,
                                                      256, 0) != hipSuccess || blocks < 1)
       blocks = 1;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -539,115 +528,58 @@ int bwd_waves_resident() {
   return w;
 }
 
-// waves per SIMD the kernel is compiled for: D_IN = D_OUT = 32 -> 3, the LEAN build (168 VGPRs, no
-// spill: W1 fragments from LDS, no cross-query prefetch; round 4, tools/gpu_s2h.sh: cross0
-// 621 -> 574 us with the CSR sums, bit-identical), (32, 64) -> 2, D_IN = 64 -> 1.  KDPC_CV_BWD_WPE=2 picks
-// the prefetching 2-wave build (206 VGPRs), =4 a LEAN 4-wave build (spills; slower).
+// waves per SIMD the backward is compiled for: D_IN = D_OUT = 32 -> 3 (the LEAN build, 168
+// VGPRs, no spill: W1 fragments from LDS, no cross-query prefetch; round 4: cross0 621 -> 574
+// us with the CSR sums against the prefetching 2-wave build), (32, 64) -> 2, D_IN = 64 -> 1
 template <int DI, int DO>
-constexpr int bwd_wpe_default() { return DI == 32 ? (DO == 32 ? 3 : 2) : 1; }
+constexpr int bwd_wpe() { return DI == 32 ? (DO == 32 ? 3 : 2) : 1; }
 
-inline int bwd_wpe_env() {
-  static const int w = [] {
-    const char* v = getenv("KDPC_CV_BWD_WPE");
-    return v && (v[0] == '2' || v[0] == '3' || v[0] == '4') ? v[0] - '0' : 0;
-  }();
-  return w;
-}
-inline int cv32_wpe() { return bwd_wpe_env() ? bwd_wpe_env() : bwd_wpe_default<32, 32>(); }
-
-// KDPC_CV_BWD_QPW (A/B runs): a fixed query count per wave instead of one resident round (in
-// the step the kernel shares the CUs with the parameter-gradient streams' kernels); the
-// per-query arithmetic does not depend on which wave runs the query, the slab count does
-inline int bwd_qpw_env() {
-  static const int q = [] {
-    const char* v = getenv("KDPC_CV_BWD_QPW");
-    const int x = v ? atoi(v) : 0;
-    return x >= 2 && x <= 1024 ? x : 0;
-  }();
-  return q;
-}
-
-template <int DI, int DO, int W>
+template <int DI, int DO>
 inline int bwd_qpw(int b, int n1) {
-  if (bwd_qpw_env()) return bwd_qpw_env();
-  return std::max(2, (int)divupll((long long)b * n1, bwd_waves_resident<DI, DO, W>()));
+  return std::max(2, (int)divupll((long long)b * n1, bwd_waves_resident<DI, DO, bwd_wpe<DI, DO>()>()));
 }
 
 inline int bwd_qpw_of(int b, int n1, int din, int dout) {
-  if (din == 32 && dout == 32) {
-    if (cv32_wpe() == 2) return bwd_qpw<32, 32, 2>(b, n1);
-    if (cv32_wpe() == 4) return bwd_qpw<32, 32, 4>(b, n1);
-    return bwd_qpw<32, 32, 3>(b, n1);
-  }
-  if (din == 32 && dout == 64) return bwd_qpw<32, 64, 2>(b, n1);
-  if (din == 64 && dout == 32) return bwd_qpw<64, 32, 1>(b, n1);
-  return bwd_qpw<64, 64, 1>(b, n1);
+  if (din == 32) return dout == 32 ? bwd_qpw<32, 32>(b, n1) : bwd_qpw<32, 64>(b, n1);
+  return dout == 32 ? bwd_qpw<64, 32>(b, n1) : bwd_qpw<64, 64>(b, n1);
 }
 
 inline int slab_len(int din, int dout) { return dout * din + dout + 4 * din; }
-
-inline bool fwd_lean() {
-  static const bool l = getenv("KDPC_CV_FWD_LEAN") && getenv("KDPC_CV_FWD_LEAN")[0] == '1';
-  return l;
-}
 
 template <int DI, int DO>
 hipError_t fwd_launch(int b, int n1, int n2, int k, const float* x1, const float* x2,
                       const int* idx, const float* p1, const float* p2, const float* wpos,
                       const float* bpos, const float* w1, const float* b1, float* out,
                       unsigned char* amax, hipStream_t st) {
-  const int qpw = fwd_qpw();
-  dim3 grid(divup(n1, kWaves * qpw), b);
-  if constexpr (DI == 64) {
-    if (fwd_lean()) {
-      hipLaunchKernelGGL((cost_volume_fwd_kernel<DI, DO, true>), grid, dim3(256), 0, st, n1, n2,
-                         k, qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, b1, out, amax);
-      return hipGetLastError();
-    }
-  }
+  dim3 grid(divup(n1, kWaves * kFwdQpw), b);
   hipLaunchKernelGGL((cost_volume_fwd_kernel<DI, DO>), grid, dim3(256), 0, st, n1, n2, k,
-                     qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, b1, out, amax);
+                     kFwdQpw, x1, x2, idx, p1, p2, wpos, bpos, w1, b1, out, amax);
   return hipGetLastError();
-}
-
-template <int DI, int DO, int W>
-hipError_t bwd_launch_w(int b, int n1, int n2, int k, const float* x1, const float* x2,
-                        const int* idx, const float* p1, const float* p2, const float* wpos,
-                        const float* bpos, const float* w1, const float* out,
-                        const unsigned char* amax, const float* dout, float* dp1,
-                        float* dp2_rows, float* dx1, float* ddir_rows, const int* rank,
-                        float* rows, float* slab, float* dparams, hipStream_t st) {
-  const int qpw = bwd_qpw<DI, DO, W>(b, n1);
-  dim3 grid(divup(n1, kWaves * qpw), b);
-  // diagnostic (tools/bench_cv_bwd.py): KDPC_CV_BWD_DIAG_NOROWS=1 drops the per-neighbour row
-  // stores of the plain entry, timing the kernel's arithmetic without its scatter
-  static const bool norows = getenv("KDPC_CV_BWD_DIAG_NOROWS") != nullptr;
-  if (norows && rank == nullptr) dp2_rows = ddir_rows = nullptr;
-  hipLaunchKernelGGL((cost_volume_bwd_kernel<DI, DO, W>), grid, dim3(256), 0, st, n1, n2, k,
-                     qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, dout, dp1,
-                     dp2_rows, dx1, ddir_rows, rank, rows, slab);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  const int len = slab_len(DI, DO);
-  const int nslab = (int)(grid.x * grid.y);
-  return colsum(nslab, len, slab, dparams, slab + (size_t)nslab * len, st);
 }
 
 template <int DI, int DO>
 hipError_t bwd_launch(int b, int n1, int n2, int k, const float* x1, const float* x2,
                       const int* idx, const float* p1, const float* p2, const float* wpos,
                       const float* bpos, const float* w1, const float* out,
-                      const unsigned char* amax, const float* dout, float* dp1, float* dp2_rows,
-                      float* dx1, float* ddir_rows, const int* rank, float* rows, float* slab,
-                      float* dparams, hipStream_t st) {
-#define KDPC_CV_BWD_ARGS b, n1, n2, k, x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, dout, dp1, \
-                         dp2_rows, dx1, ddir_rows, rank, rows, slab, dparams, st
-  if constexpr (DI == 32 && DO == 32) {
-    if (cv32_wpe() == 2) return bwd_launch_w<32, 32, 2>(KDPC_CV_BWD_ARGS);
-    if (cv32_wpe() == 4) return bwd_launch_w<32, 32, 4>(KDPC_CV_BWD_ARGS);
-  }
-  return bwd_launch_w<DI, DO, bwd_wpe_default<DI, DO>()>(KDPC_CV_BWD_ARGS);
-#undef KDPC_CV_BWD_ARGS
+                      const unsigned char* amax, const unsigned char* s0, const float* dout,
+                      float* dp1, float* dp2_rows, float* dx1, float* ddir_rows, const int* rank,
+                      float* rows, float* slab, float* dparams, hipStream_t st) {
+  constexpr int W = bwd_wpe<DI, DO>();
+  const int qpw = bwd_qpw<DI, DO>(b, n1);
+  dim3 grid(divup(n1, kWaves * qpw), b);
+  if (s0)
+    hipLaunchKernelGGL((cost_volume_bwd_kernel<DI, DO, W, true>), grid, dim3(256), 0, st, n1, n2,
+                       k, qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, s0, dout, dp1,
+                       dp2_rows, dx1, ddir_rows, rank, rows, slab);
+  else
+    hipLaunchKernelGGL((cost_volume_bwd_kernel<DI, DO, W, false>), grid, dim3(256), 0, st, n1, n2,
+                       k, qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, s0, dout, dp1,
+                       dp2_rows, dx1, ddir_rows, rank, rows, slab);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int len = slab_len(DI, DO);
+  const int nslab = (int)(grid.x * grid.y);
+  return colsum(nslab, len, slab, dparams, slab + (size_t)nslab * len, st);
 }
 
 // Per-point sums of the ranked rows: key e = b*N2 + j owns the contiguous slots
@@ -756,186 +688,6 @@ hipError_t rows_sum(int din, long long nkeys, const float* rows, const float* di
   }
 }
 
-// Pull form of the per-point sums (D_IN == D_OUT in {32, 64, 128, 256}, K <= 32; round 4).  The ranked
-// path writes one dz0 row per (query, neighbour) pair at its CSR slot and sums the rows per
-// point: B*N1*K*(D+4)*4 bytes out to HBM and back (604 MB each way at cross0, B=16 clouds of
-// 8192, K=32).  Here the backward kernel writes no rows, and one wave per reference point j
-// walks its CSR segment (perm: the positions (n, k) naming j, ascending) and recomputes each
-// pair's row from the query's inputs, which stay cache-resident (one cloud's P1 / out / dout
-// rows at a time, ~3.5 MB at D=32):
-//   h0  = LeakyReLU((P2[j] + P1[n]) + (Wpos (x2[j] - x1[n]) + bpos))   the forward's exact
-//         arithmetic, so every LeakyReLU branch is the forward's
-//   dh0 = sum over d ascending with am[n, d] == k of g'[n, d] W1[d, :],
-//         g' = dout * LeakyReLU'(out)        (one term per output channel routed to row k)
-//   dz0 = dh0 * LeakyReLU'(h0);   dP2[j] = the segment's sum;   dx2[j] = Wpos^T dP2[j]
-// D = 32 runs two pairs per step (the wave's halves take alternate pairs; the two partial sums
-// are added at the end); D >= 128 gives each lane D/64 channels and reads W1 rows from L2.  Fixed order throughout: deterministic.  Rounding differs from the
-// ranked path's (per-pair d(dir) sums; MFMA vs fma-chain dh0 when two channels route to one row).
-template <int D, int UU>
-__global__ __launch_bounds__(256) void cv_pull_kernel(
-    int k, int n2, long long nkeys, const int* __restrict__ order, int xcd_per,
-    const float* __restrict__ x1, const float* __restrict__ x2,
-    const float* __restrict__ p1, const float* __restrict__ p2, const float* __restrict__ wpos,
-    const float* __restrict__ bpos, const float* __restrict__ w1, const float* __restrict__ out,
-    const unsigned char* __restrict__ amax, const float* __restrict__ dout,
-    const int* __restrict__ offsets, const int* __restrict__ perm, float* __restrict__ dp2,
-    float* __restrict__ dx2) {
-  constexpr int RPP = D < 64 ? 64 / D : 1;  // pairs per step
-  constexpr int CPL = D > 64 ? D / 64 : 1;  // channels per lane: c = lane % D + 64 j
-  constexpr int DL = D < 64 ? D : 64;       // lanes per pair
-  constexpr int U = UU;                     // steps whose loads are in flight together
-  constexpr bool W1_LDS = D <= 64;          // D >= 128: W1 rows from L2 (~1 row per pair)
-  __shared__ float w1s[W1_LDS ? D * D : 1];
-  if constexpr (W1_LDS) {
-    for (int e = threadIdx.x; e < D * D; e += blockDim.x) w1s[e] = w1[e];
-    __syncthreads();
-  }
-  const int wave = threadIdx.x >> 6, lane = lane_id();
-  const int c0 = lane % DL, sub = lane / DL;
-  // xcd_per > 0: workgroup w runs on XCD w % 8; give each XCD a contiguous range of blocks
-  const long long blk = xcd_per > 0 ? (long long)(blockIdx.x % 8) * xcd_per + blockIdx.x / 8
-                                    : (long long)blockIdx.x;
-  long long key = blk * kWaves + wave;
-  if (key >= nkeys) return;
-  if (order) {  // keys in the given per-cloud order (Morton: neighbouring waves share queries)
-    const long long b = key / n2;
-    key = b * n2 + order[key];
-  }
-  float w0[CPL], wy[CPL], wz[CPL], bp[CPL], pj[CPL], acc[CPL];
-#pragma unroll
-  for (int j = 0; j < CPL; ++j) {
-    const int c = c0 + 64 * j;
-    w0[j] = wpos[c * 3 + 0];
-    wy[j] = wpos[c * 3 + 1];
-    wz[j] = wpos[c * 3 + 2];
-    bp[j] = bpos[c];
-    pj[j] = p2[key * D + c];
-    acc[j] = 0.f;
-  }
-  const float xj0 = x2[key * 3 + 0], xj1 = x2[key * 3 + 1], xj2 = x2[key * 3 + 2];
-  const int s0 = offsets[key], s1 = offsets[key + 1];
-  for (int cs = s0; cs < s1; cs += 64) {  // chunks of 64 pairs: lane l holds pair cs + l
-    const int cn = min(64, s1 - cs);
-    const int pl = lane < cn ? perm[cs + lane] : 0;
-    for (int i0 = 0; i0 < cn; i0 += RPP * U) {
-      float p1v[U][CPL], ov[U][CPL], gv[U][CPL], q0[U], q1[U], q2[U];
-      int am[U][CPL], kk[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = i0 + RPP * u + sub;
-        const int gp = __shfl(pl, i < cn ? i : 0, kWave);
-        const int ng = gp / k;  // b*N1 + n
-        kk[u] = gp - ng * k;
-#pragma unroll
-        for (int j = 0; j < CPL; ++j) {
-          const long long ro = (long long)ng * D + c0 + 64 * j;
-          p1v[u][j] = p1[ro];
-          ov[u][j] = out[ro];
-          gv[u][j] = dout[ro];
-          am[u][j] = amax[ro];
-        }
-        q0[u] = x1[ng * 3 + 0];
-        q1[u] = x1[ng * 3 + 1];
-        q2[u] = x1[ng * 3 + 2];
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = i0 + RPP * u + sub;
-        const float dx = xj0 - q0[u], dy = xj1 - q1[u], dzz = xj2 - q2[u];
-        float dh[CPL];
-#pragma unroll
-        for (int j = 0; j < CPL; ++j) dh[j] = 0.f;
-        // output channels d = 64 j' + bit routed to this row, ascending d; the routing mask is
-        // uniform over the lanes of one pair, so they run each step together
-#pragma unroll
-        for (int jo = 0; jo < CPL; ++jo) {
-          const float gd = gv[u][jo] * (ov[u][jo] > 0.f ? 1.f : kSlope);
-          const unsigned long long m = __ballot(am[u][jo] == kk[u]);
-          unsigned long long hm = DL == 64 ? m : ((m >> (DL * sub)) & ((1ull << DL) - 1ull));
-          while (hm) {
-            const int bit = __builtin_ctzll(hm);
-            hm &= hm - 1;
-            const float g = __shfl(gd, sub * DL + bit, kWave);
-            const int d = 64 * jo + bit;
-#pragma unroll
-            for (int j = 0; j < CPL; ++j)
-              dh[j] = __builtin_fmaf(g, W1_LDS ? w1s[d * D + c0 + 64 * j] : w1[d * D + c0 + 64 * j], dh[j]);
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < CPL; ++j) {
-          const float pos = __fadd_rn(__builtin_fmaf(wz[j], dzz, __builtin_fmaf(wy[j], dy, __fmul_rn(w0[j], dx))), bp[j]);
-          const float h = lrelu(__fadd_rn(__fadd_rn(pj[j], p1v[u][j]), pos));
-          const float dz = dh[j] * (h > 0.f ? 1.f : kSlope);
-          if (i < cn) acc[j] = __fadd_rn(acc[j], dz);
-        }
-      }
-    }
-  }
-  if (RPP == 2) acc[0] = __fadd_rn(acc[0], __shfl_xor(acc[0], 32, kWave));
-  float g0 = 0.f, g1 = 0.f, g2 = 0.f;
-#pragma unroll
-  for (int j = 0; j < CPL; ++j) {
-    g0 = __builtin_fmaf(w0[j], acc[j], g0);
-    g1 = __builtin_fmaf(wy[j], acc[j], g1);
-    g2 = __builtin_fmaf(wz[j], acc[j], g2);
-  }
-#pragma unroll
-  for (int o = DL / 2; o >= 1; o >>= 1) {
-    g0 = __fadd_rn(g0, __shfl_xor(g0, o, kWave));
-    g1 = __fadd_rn(g1, __shfl_xor(g1, o, kWave));
-    g2 = __fadd_rn(g2, __shfl_xor(g2, o, kWave));
-  }
-  if (sub == 0)
-#pragma unroll
-    for (int j = 0; j < CPL; ++j) dp2[key * D + c0 + 64 * j] = acc[j];
-  if (lane == 0) {
-    dx2[key * 3 + 0] = g0;
-    dx2[key * 3 + 1] = g1;
-    dx2[key * 3 + 2] = g2;
-  }
-}
-
-// A/B knobs of the pull kernel: KDPC_CV_PULL_U (steps in flight: 4 default, 8), KDPC_CV_PULL_XCD=1
-// (contiguous block ranges per XCD)
-inline int pull_u() {
-  static const int u = [] {
-    const char* v = getenv("KDPC_CV_PULL_U");
-    return v && atoi(v) == 8 ? 8 : 4;
-  }();
-  return u;
-}
-inline bool pull_xcd() {
-  static const bool x = getenv("KDPC_CV_PULL_XCD") && getenv("KDPC_CV_PULL_XCD")[0] == '1';
-  return x;
-}
-
-hipError_t pull_sum(int d, int k, int n2, long long nkeys, const int* order, const float* x1,
-                    const float* x2, const float* p1, const float* p2, const float* wpos,
-                    const float* bpos, const float* w1, const float* out,
-                    const unsigned char* amax, const float* dout, const int* offsets,
-                    const int* perm, float* dp2, float* dx2, hipStream_t st) {
-  if (nkeys <= 0) return hipSuccess;
-  const long long blocks = divupll(nkeys, kWaves);
-  const int per = pull_xcd() ? (int)divupll(blocks, 8) : 0;
-  const dim3 grid((unsigned)(per > 0 ? 8ll * per : blocks));
-#define KDPC_CV_PULL(DD, UU)                                                                   \
-  if (d == DD && (DD > 64 || pull_u() == UU)) {                                               \
-    hipLaunchKernelGGL((cv_pull_kernel<DD, UU>), grid, dim3(256), 0, st, k, n2, nkeys, order,   \
-                       per, x1, x2, p1, p2, wpos, bpos, w1, out, amax, dout, offsets, perm, dp2, \
-                       dx2);                                                                   \
-    return hipGetLastError();                                                                 \
-  }
-  KDPC_CV_PULL(32, 4)
-  KDPC_CV_PULL(32, 8)
-  KDPC_CV_PULL(64, 4)
-  KDPC_CV_PULL(64, 8)
-  KDPC_CV_PULL(128, 4)
-  KDPC_CV_PULL(256, 2)
-#undef KDPC_CV_PULL
-  return hipErrorInvalidValue;
-}
-
 bool narrow(int din, int dout, int k) {
   return (din == 32 || din == 64) && (dout == 32 || dout == 64) && k >= 1 && k <= 32;
 }
@@ -947,16 +699,17 @@ bool supported(int din, int dout, int k) {
 hipError_t bwd_dispatch(int b, int n1, int n2, int k, int din, int dout, const float* x1,
                         const float* x2, const int* idx, const float* p1, const float* p2,
                         const float* wpos, const float* bpos, const float* w1, const float* out,
-                        const unsigned char* amax, const float* dout_grad, float* dp1,
-                        float* dp2_rows, float* dx1, float* ddir_rows, const int* rank,
-                        float* rows, float* slab, float* dparams, hipStream_t st) {
+                        const unsigned char* amax, const unsigned char* s0,
+                        const float* dout_grad, float* dp1, float* dp2_rows, float* dx1,
+                        float* ddir_rows, const int* rank, float* rows, float* slab,
+                        float* dparams, hipStream_t st) {
   if (!narrow(din, dout, k))
     return cost_volume_wide_fused_bwd(b, n1, n2, k, din, x1, x2, idx, p1, p2, wpos, bpos, w1, out,
-                                      amax, dout_grad, dp1, dp2_rows, dx1, ddir_rows, rank, rows,
-                                      slab, dparams, st);
+                                      amax, s0, dout_grad, dp1, dp2_rows, dx1, ddir_rows, rank,
+                                      rows, slab, dparams, st);
 #define KDPC_CV_BWD(DI, DO)                                                                    \
   if (din == DI && dout == DO)                                                                 \
-    return bwd_launch<DI, DO>(b, n1, n2, k, x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax,      \
+    return bwd_launch<DI, DO>(b, n1, n2, k, x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, s0,  \
                               dout_grad, dp1, dp2_rows, dx1, ddir_rows, rank, rows, slab,        \
                               dparams, st);
   KDPC_CV_BWD(32, 32)
@@ -1015,7 +768,8 @@ KDPC_API int kdpc_cost_volume_bwd(int b, int n1, int n2, int k, int din, int dou
                                   const float* x1, const float* x2, const int* idx,
                                   const float* p1, const float* p2, const float* wpos,
                                   const float* bpos, const float* w1, const float* out,
-                                  const unsigned char* amax, const float* dout_grad, float* dp1,
+                                  const unsigned char* amax, const unsigned char* slope0,
+                                  const float* dout_grad, float* dp1,
                                   float* dp2_rows, float* dx1, float* ddir_rows, void* workspace,
                                   size_t workspace_bytes, float* dparams, void* stream) {
   KDPC_CHECK_ARG(b > 0 && n1 > 0 && n2 > 0 && supported(din, dout, k) && b <= 65535);
@@ -1025,8 +779,8 @@ KDPC_API int kdpc_cost_volume_bwd(int b, int n1, int n2, int k, int din, int dou
   hipStream_t st = (hipStream_t)stream;
   float* slab = (float*)workspace;
   return (int)bwd_dispatch(b, n1, n2, k, din, dout, x1, x2, idx, p1, p2, wpos, bpos, w1, out,
-                           amax, dout_grad, dp1, dp2_rows, dx1, ddir_rows, nullptr, nullptr, slab,
-                           dparams, st);
+                           amax, slope0, dout_grad, dp1, dp2_rows, dx1, ddir_rows, nullptr, nullptr,
+                           slab, dparams, st);
 }
 
 // Backward with the per-point sums done here, through the CSR of idx over the N2 points
@@ -1043,7 +797,8 @@ KDPC_API int kdpc_cost_volume_bwd_csr(int b, int n1, int n2, int k, int din, int
                                       const float* x1, const float* x2, const int* idx,
                                       const float* p1, const float* p2, const float* wpos,
                                       const float* bpos, const float* w1, const float* out,
-                                      const unsigned char* amax, const float* dout_grad,
+                                      const unsigned char* amax, const unsigned char* slope0,
+                                      const float* dout_grad,
                                       const int* offsets, const int* rank, float* dp1, float* dp2,
                                       float* dx1, float* dx2, void* workspace,
                                       size_t workspace_bytes, float* dparams, void* stream) {
@@ -1056,44 +811,9 @@ KDPC_API int kdpc_cost_volume_bwd_csr(int b, int n1, int n2, int k, int din, int
   float* slab = (float*)workspace;
   float* rows = (float*)((char*)workspace + slab_bytes);
   hipError_t e = bwd_dispatch(b, n1, n2, k, din, dout, x1, x2, idx, p1, p2, wpos, bpos, w1, out,
-                              amax, dout_grad, dp1, nullptr, dx1, nullptr, rank, rows, slab,
+                              amax, slope0, dout_grad, dp1, nullptr, dx1, nullptr, rank, rows, slab,
                               dparams, st);
   if (e != hipSuccess) return (int)e;
   return (int)rows_sum(din, (long long)b * n2, rows, rows + (size_t)b * n1 * k * din, offsets, dp2,
                        dx2, st);
-}
-
-// Backward with the per-point sums in pull form (cv_pull_kernel): offsets (B*N2+1) / perm
-// (B*N1*K) of the CSR of idx over the N2 points (kdpc_csr_build); order (B*N2, nullable): the
-// order the reference points are walked in per cloud (kdpc_morton_order of x2).  No per-neighbour rows are
-// written; D_IN == D_OUT in {32, 64} only (kdpc_cost_volume_bwd_pull_supported).  Outputs as
-// kdpc_cost_volume_bwd_csr (dp2 / dx2 within rounding of it); workspace as
-// kdpc_cost_volume_bwd_workspace_bytes.
-KDPC_API int kdpc_cost_volume_bwd_pull_supported(int din, int dout, int k) {
-  return din == dout && (din == 32 || din == 64 || din == 128 || din == 256) && k >= 1 &&
-         k <= 32 && supported(din, dout, k);
-}
-
-KDPC_API int kdpc_cost_volume_bwd_pull(int b, int n1, int n2, int k, int din, int dout,
-                                       const float* x1, const float* x2, const int* idx,
-                                       const float* p1, const float* p2, const float* wpos,
-                                       const float* bpos, const float* w1, const float* out,
-                                       const unsigned char* amax, const float* dout_grad,
-                                       const int* offsets, const int* perm, const int* order,
-                                       float* dp1, float* dp2, float* dx1, float* dx2, void* workspace,
-                                       size_t workspace_bytes, float* dparams, void* stream) {
-  KDPC_CHECK_ARG(b > 0 && n1 > 0 && n2 > 0 && b <= 65535 &&
-                 kdpc_cost_volume_bwd_pull_supported(din, dout, k));
-  KDPC_CHECK_ARG((long long)b * n1 * k < (1ll << 31));
-  KDPC_CHECK_ARG(x1 && x2 && idx && p1 && p2 && wpos && bpos && w1 && out && amax && dout_grad &&
-                 offsets && perm && dp1 && dp2 && dx1 && dx2 && workspace && dparams);
-  KDPC_CHECK_ARG(workspace_bytes >= kdpc_cost_volume_bwd_workspace_bytes(b, n1, din, dout));
-  hipStream_t st = (hipStream_t)stream;
-  // rank == rows == null and no plain row buffers: the backward writes dp1 / dx1 / slabs only
-  hipError_t e = bwd_dispatch(b, n1, n2, k, din, dout, x1, x2, idx, p1, p2, wpos, bpos, w1, out,
-                              amax, dout_grad, dp1, nullptr, dx1, nullptr, nullptr, nullptr,
-                              (float*)workspace, dparams, st);
-  if (e != hipSuccess) return (int)e;
-  return (int)pull_sum(din, k, n2, (long long)b * n2, order, x1, x2, p1, p2, wpos, bpos, w1, out,
-                       amax, dout_grad, offsets, perm, dp2, dx2, st);
 }

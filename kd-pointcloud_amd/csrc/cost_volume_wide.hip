@@ -421,14 +421,17 @@ struct WideBwd {
 };
 
 // PART: 0 = everything (D = 128), 1 = all but dW1 / db1, 2 = dW1 / db1 only (the D = 256
-// pair: the dW1 accumulators and the rest do not fit one wave's 256 registers together)
-template <int D, int PART>
+// pair: the dW1 accumulators and the rest do not fit one wave's 256 registers together).
+// OVR: slope0 (B*N1, K, D) u8 overrides the first LeakyReLU's derivative (test seam; see
+// cost_volume_bwd_kernel in cost_volume.hip)
+template <int D, int PART, bool OVR>
 __global__ __launch_bounds__(2 * D) void cvw_fused_bwd_kernel(
     int b, int n1, int n2, int k, int qpw, const float* __restrict__ x1,
     const float* __restrict__ x2, const int* __restrict__ idx, const float* __restrict__ p1,
     const float* __restrict__ p2, const float* __restrict__ wpos, const float* __restrict__ bpos,
     const float* __restrict__ w1, const float* __restrict__ w1t, const float* __restrict__ out,
-    const unsigned char* __restrict__ amax, const float* __restrict__ dout,
+    const unsigned char* __restrict__ amax, const unsigned char* __restrict__ slope0,
+    const float* __restrict__ dout,
     float* __restrict__ dp1, float* __restrict__ dp2_rows, float* __restrict__ dx1,
     float* __restrict__ ddir_rows, const int* __restrict__ rank, float* __restrict__ rows,
     float* __restrict__ slab) {
@@ -462,6 +465,7 @@ __global__ __launch_bounds__(2 * D) void cvw_fused_bwd_kernel(
   const __amdgpu_buffer_rsrc_t outr = rsrc_of(out, (long long)s.nq * D * 4);
   const __amdgpu_buffer_rsrc_t dor = rsrc_of(dout, (long long)s.nq * D * 4);
   const __amdgpu_buffer_rsrc_t amr = rsrc_of(amax, (long long)s.nq * D);
+  const __amdgpu_buffer_rsrc_t s0r = rsrc_of(OVR ? slope0 : amax, OVR ? (long long)s.nq * k * D : 0);
   // ranked rows: row (q, r) -> slot rank[q*k + r]; a query's slots are loaded as it starts
   // and used by its column / direction passes after the MFMAs
   const bool ranked = rank != nullptr;
@@ -586,9 +590,16 @@ __global__ __launch_bounds__(2 * D) void cvw_fused_bwd_kernel(
     // ---- dz0 = dh0 * LeakyReLU'(h0), in place (accumulator layout)
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      const int a = ((e & 3) + 8 * (e >> 2) + 4 * half) * G::LD + 32 * w + l32;
+      const int row = (e & 3) + 8 * (e >> 2) + 4 * half;
+      const int a = row * G::LD + 32 * w + l32;
       const float hv = H[a];
-      H[a] = dacc[e] * (hv > 0.f ? 1.f : kSlope);
+      float sl = hv > 0.f ? 1.f : kSlope;
+      if constexpr (OVR) {  // rows >= k: dacc is 0 there
+        const unsigned o = __builtin_amdgcn_raw_buffer_load_b8(
+            s0r, (int)(((unsigned)q * (unsigned)k + row) * D + 32 * w + l32), 0, 0);
+        sl = o == 1u ? 1.f : (o == 2u ? kSlope : sl);
+      }
+      H[a] = dacc[e] * sl;
     }
     __syncthreads();
     // ---- column pass: dP2 rows out, dP1 partials, dWpos / dbpos
@@ -737,24 +748,12 @@ __global__ __launch_bounds__(256) void cvw_transpose_kernel(int d, const float* 
   if (e < d * d) w1t[e] = w1[(e % d) * d + e / d];
 }
 
-// queries per workgroup (KDPC_CVW_WGS overrides the workgroup target for A/B runs: the
-// per-query arithmetic does not depend on it, the backward's parameter-gradient slab count
-// does, so dW1 / dWpos regroup their sums -- bit-identical only at equal settings)
-inline int cvw_target_wgs() {
-  static const int w = [] {
-    const char* v = getenv("KDPC_CVW_WGS");
-    const int x = v ? atoi(v) : 0;
-    return x >= 64 && x <= 8192 ? x : 0;
-  }();
-  return w;
-}
-
-// A/B at the model's calls (B=16 pair batch, K=32; tools/gpu_r4u.sh): forward D=128 512
-// workgroups (108.5 us; 256: 140), D=256 256 (173.6 vs 180.7 at 512); backward 256 for both
-// (cross2 251 vs 256 us, cross3 394 vs 428 us)
+// queries per workgroup: A/B at the model's calls (round 4, B=16 pair batch, K=32): forward
+// D=128 512 workgroups (108.5 us; 256: 140), D=256 256 (173.6 vs 180.7 at 512); backward 256
+// for both (cross2 251 vs 256 us, cross3 394 vs 428 us).  The backward's parameter-gradient
+// slab count follows it, so the dW1 / dWpos sums are grouped by it.
 inline int fused_qpw(long long nq, int d, bool bwd) {
-  const int env = cvw_target_wgs();
-  const int target = env ? env : (bwd || d == 256 ? 256 : 512);
+  const int target = bwd || d == 256 ? 256 : 512;
   return (int)std::max<long long>(2, divupll(nq, target));
 }
 
@@ -794,9 +793,9 @@ hipError_t cost_volume_wide_fused_bwd(int b, int n1, int n2, int k, int d, const
                                       const float* x2, const int* idx, const float* p1,
                                       const float* p2, const float* wpos, const float* bpos,
                                       const float* w1, const float* out,
-                                      const unsigned char* amax, const float* dout, float* dp1,
-                                      float* dp2_rows, float* dx1, float* ddir_rows,
-                                      const int* rank, float* rows, float* ws,
+                                      const unsigned char* amax, const unsigned char* slope0,
+                                      const float* dout, float* dp1, float* dp2_rows, float* dx1,
+                                      float* ddir_rows, const int* rank, float* rows, float* ws,
                                       float* dparams, hipStream_t st) {
   const long long nq = (long long)b * n1;
   const int qpw = fused_qpw(nq, d, true);
@@ -805,24 +804,29 @@ hipError_t cost_volume_wide_fused_bwd(int b, int n1, int n2, int k, int d, const
   float* slab = ws;
   float* scratch = ws + (long long)nwg * len;
   float* w1t = scratch + colsum_scratch_floats(nwg, len);
+#define KDPC_CVW_BWD(DD, PART, OV, GRID)                                                          \
+  hipLaunchKernelGGL((cvw_fused_bwd_kernel<DD, PART, OV>), GRID, dim3(2 * DD), 0, st, b, n1, n2, k, \
+                     qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, w1t, out, amax, slope0, dout, dp1,    \
+                     dp2_rows, dx1, ddir_rows, rank, rows, slab)
   if (d == 128) {
-    hipLaunchKernelGGL((cvw_fused_bwd_kernel<128, 0>), dim3(nwg), dim3(256), 0, st, b, n1, n2, k,
-                       qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, w1t, out, amax, dout, dp1,
-                       dp2_rows, dx1, ddir_rows, rank, rows, slab);
+    if (slope0)
+      KDPC_CVW_BWD(128, 0, true, dim3(nwg));
+    else
+      KDPC_CVW_BWD(128, 0, false, dim3(nwg));
   } else {
     hipLaunchKernelGGL(cvw_transpose_kernel, dim3(divup(d * d, 256)), dim3(256), 0, st, d, w1,
                        w1t);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((cvw_fused_bwd_kernel<256, 1>), dim3(nwg), dim3(512), 0, st, b, n1, n2, k,
-                       qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, w1t, out, amax, dout, dp1,
-                       dp2_rows, dx1, ddir_rows, rank, rows, slab);
+    if (slope0)
+      KDPC_CVW_BWD(256, 1, true, dim3(nwg));
+    else
+      KDPC_CVW_BWD(256, 1, false, dim3(nwg));
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL((cvw_fused_bwd_kernel<256, 2>), dim3(nwg, WideBwd<256>::OSPLIT), dim3(512),
-                       0, st, b, n1, n2, k,
-                       qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, w1t, out, amax, dout, dp1,
-                       dp2_rows, dx1, ddir_rows, rank, rows, slab);
+    // dW1 / db1 read g', argmax and h0 only: no slope0 there
+    KDPC_CVW_BWD(256, 2, false, dim3(nwg, WideBwd<256>::OSPLIT));
   }
+#undef KDPC_CVW_BWD
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return colsum(nwg, len, slab, dparams, scratch, st);

@@ -90,9 +90,9 @@ hipError_t cost_volume_wide_fused_bwd(int b, int n1, int n2, int k, int d, const
                                       const float* x2, const int* idx, const float* p1,
                                       const float* p2, const float* wpos, const float* bpos,
                                       const float* w1, const float* out,
-                                      const unsigned char* amax, const float* dout, float* dp1,
-                                      float* dp2_rows, float* dx1, float* ddir_rows,
-                                      const int* rank, float* rows, float* ws,
+                                      const unsigned char* amax, const unsigned char* slope0,
+                                      const float* dout, float* dp1, float* dp2_rows, float* dx1,
+                                      float* ddir_rows, const int* rank, float* rows, float* ws,
                                       float* dparams, hipStream_t st);
 
 }  // namespace kdpc

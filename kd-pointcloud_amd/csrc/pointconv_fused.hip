@@ -1338,33 +1338,17 @@ inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 inline int km_of(int k) { return k <= 9 ? 9 : 16; }
 
-// every gathered table must be addressable by a 31-bit byte offset (buffer loads)
-// CUs the weight half may fill when it runs on its own stream (kdpc_pointconv_bwd_weight):
-// its workgroups hold 90-158 KB of LDS each, one per CU for the whole kernel, so a launch
-// sized for all 256 CUs shuts the main stream's kernels out until it finishes (round-4
-// trace: a 17 us BatchNorm reduction waited 458 us behind the level-0 weight kernel).
-// KDPC_PC_WGT_CUS overrides (A/B runs).
-inline int side_weight_cus() {
-  static const int w = [] {
-    const char* v = getenv("KDPC_PC_WGT_CUS");
-    const int x = v ? atoi(v) : 0;
-    return x >= 8 && x <= 4 * kCUs ? x : kCUs;  // > 256: several rounds of workgroups
-  }();
-  return w;
-}
+// CUs the weight half fills when it runs on its own stream (kdpc_pointconv_bwd_weight): all of
+// them.  Its workgroups hold 90-158 KB of LDS each, one per CU, so it shuts the main stream's
+// kernels out until it ends, but capping its grid measured slower (round 4 A/B: 256 CUs
+// 16.26 ms per train step, 192 16.77, 128 17.36, 64 20.8): the side work is the long pole.
+inline int side_weight_cus() { return kCUs; }
 
-// workgroups the backward data kernel's channel splits aim for (KDPC_PC_BWD_TARGET_WG
-// overrides for A/B runs; backward-only: the dwt split partials regroup).  A/B round 4
-// (tools/gpu_r4w.sh, tiled data half): 512 beats 256 / 1024 / 2048 at flow2 (112 vs 125-135
-// us) and ties at flow0 / flow1.
-inline int bwd_target_wg() {
-  static const int w = [] {
-    const char* v = getenv("KDPC_PC_BWD_TARGET_WG");
-    const int x = v ? atoi(v) : 0;
-    return x >= 64 && x <= 8192 ? x : kTargetWG;
-  }();
-  return w;
-}
+// workgroups the backward data kernel's channel splits aim for (round-4 A/B, tiled data half:
+// 512 beats 256 / 1024 / 2048 at flow2, 112 vs 125-135 us, and ties at flow0 / flow1)
+inline int bwd_target_wg() { return kTargetWG; }
+
+// every gathered table must be addressable by a 31-bit byte offset (buffer loads)
 
 inline bool fits_buffers(long long b, long long n, long long s, int d) {
   const long long lim = 1ll << 31;
@@ -1454,20 +1438,13 @@ hipError_t fwd_launch(const Geo& g, const Plan& p, const float* wt, const float*
 }
 
 // Data kernel choice.  The pipelined kernel (chunk ch+1's MFMAs interleaved with chunk ch's
-// pair work) is the default for K <= 9: with every wave carrying the same pair work (one whole
-// pair + one left-over item) it is faster there (flow0, B=8, N=8192: 534 vs 584 us per
-// launch, round 2); for K = 16 (two whole pairs per thread) the two are within 2 % and the
-// unpipelined kernel stays.  KDPC_PC_BWD_PIPE=0 / =1 forces either (A/B runs; bit-identical
-// outputs).  Round-1 note: the pipelined kernel without the balanced pair mapping made every
+// pair work) for K <= 9: with every wave carrying the same pair work (one whole pair + one
+// left-over item) it is faster there (flow0, B=8, N=8192: 534 vs 584 us per launch, round 2);
+// for K = 16 (two whole pairs per thread) the two are within 2 % and the unpipelined kernel
+// stays.  Round-1 note: the pipelined kernel without the balanced pair mapping made every
 // wave run two pairs and did not pay (1199 vs 1191 us).
 template <int KM>
-inline bool bwd_pipe_enabled() {
-  static const int force = [] {
-    const char* v = getenv("KDPC_PC_BWD_PIPE");
-    return v && (v[0] == '0' || v[0] == '1') ? v[0] - '0' : -1;
-  }();
-  return force >= 0 ? force == 1 : KM <= 9;
-}
+constexpr bool bwd_pipe_enabled() { return KM <= 9; }
 
 // Data half of the backward: dxyz, dfeats, dcenter, dwt (workspace: dG rows | dwt slabs | -
 // | swizzled wl).

@@ -13,15 +13,10 @@ from torch.autograd import Function
 
 import wgrad
 
-import os
-
 # split-K geometry of the weight gradients: >= 1024 rows per chunk, <= 128 chunks (round-4
-# A/B on the whole step, tools/gpu_r4y.sh: 2048/64 16.35-16.41 ms, 1024/128 16.10-16.17,
-# 1024/256 16.15-16.31, 512/128 16.9, 4096/32 16.6-16.7).  KDPC_SPLITK="rows,chunks"
-# overrides for A/B runs.
-_MIN_ROWS_PER_CHUNK, _MAX_CHUNKS = (
-    tuple(int(v) for v in os.environ["KDPC_SPLITK"].split(",")) if os.environ.get("KDPC_SPLITK")
-    else (1024, 128))
+# A/B on the whole step: 2048/64 16.35-16.41 ms, 1024/128 16.10-16.17, 1024/256 16.15-16.31,
+# 512/128 16.9, 4096/32 16.6-16.7)
+_MIN_ROWS_PER_CHUNK, _MAX_CHUNKS = 1024, 128
 
 
 def _colsum(g2):

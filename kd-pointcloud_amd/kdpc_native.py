@@ -60,11 +60,9 @@ _SIGNATURES = {
     "kdpc_pointconv_contract_fwd": [_c_int] * 5 + [_vp] * 7,
     "kdpc_pointconv_contract_bwd": [_c_int] * 5 + [_vp] * 10,
     "kdpc_cost_volume_bwd_workspace_bytes": [_c_int] * 4,
-    "kdpc_cost_volume_bwd": [_c_int] * 6 + [_vp] * 16 + [_c_size, _vp, _vp],
+    "kdpc_cost_volume_bwd": [_c_int] * 6 + [_vp] * 17 + [_c_size, _vp, _vp],
     "kdpc_cost_volume_bwd_csr_workspace_bytes": [_c_int] * 5,
-    "kdpc_cost_volume_bwd_csr": [_c_int] * 6 + [_vp] * 18 + [_c_size, _vp, _vp],
-    "kdpc_cost_volume_bwd_pull_supported": [_c_int] * 3,
-    "kdpc_cost_volume_bwd_pull": [_c_int] * 6 + [_vp] * 19 + [_c_size, _vp, _vp],
+    "kdpc_cost_volume_bwd_csr": [_c_int] * 6 + [_vp] * 19 + [_c_size, _vp, _vp],
     "kdpc_pointconv_supported": [_c_int] * 3,
     "kdpc_pointconv_fwd_workspace_bytes": [_c_int] * 5,
     "kdpc_pointconv_fwd": [_c_int] * 6 + [_vp] * 9 + [_c_size, _vp],
@@ -462,14 +460,14 @@ def csr_rank_of(idx, n):
 # The PointConv backward with the dG rows summed per (32-row tile, destination) inside the
 # data kernel (csrc/tile_plan.hip, pointconv_fused.hip): rows of a tile in Morton order of
 # their centers, so their 32K neighbours name few distinct points (self-kNN K=9: ~69 of 288
-# at N=8192).  Used for K <= 9 (the estimators' layers); KDPC_PC_TILED=0 keeps the per-pair
-# rows for A/B runs.
-TILED_PC = os.environ.get("KDPC_PC_TILED", "1") != "0"
-# the PointConv bias gradient from the weight kernel's MFMAs (KDPC_PC_BIAS_IN_WEIGHT=0: the
-# fixed-order column sum of dy instead, for A/B)
-BIAS_IN_WEIGHT = os.environ.get("KDPC_PC_BIAS_IN_WEIGHT", "1") != "0"
-# the forward through the same row tiles (bit-identical; KDPC_PC_TILED_FWD=0 for A/B)
-TILED_FWD = TILED_PC and os.environ.get("KDPC_PC_TILED_FWD", "1") != "0"
+# at N=8192).  Used for K <= 9 (the estimators' layers).  The three switches below are test
+# seams (the tests compare each path with its untiled / unfused counterpart), not settings.
+TILED_PC = True
+# the PointConv bias gradient from the weight kernel's MFMAs (False: the fixed-order column
+# sum of dy)
+BIAS_IN_WEIGHT = True
+# the forward through the same row tiles (bit-identical)
+TILED_FWD = True
 TILED_MAX_K = 9
 
 
@@ -497,6 +495,7 @@ def tile_plan_of(idx, center, n):
             nt = b * ((idx.shape[1] + 31) // 32)
             tp = TilePlan()
             tp.trow, tp.tpair, tp.tsoff = pp.trow[:nt], pp.tpair[:nt], pp.tsoff[:nt]
+            # tdst is (B, tiles per element * 32K): the prefix's partial-row slots
             tp.offsets, tp.tdst = pp.offsets[:b * n + 1], pp.tdst[:b]
             tp.n = n
             idx._kdpc_tplan = tp
@@ -506,11 +505,25 @@ def tile_plan_of(idx, center, n):
     trow, tpair, tsoff, tkey = _op("kdpc_pc_tile_plan", "pc_tile_plan", idx, order, n)
     offsets, perm = _op("kdpc_csr_build", "csr_build", tkey, n)
     tdst = _op("kdpc_csr_rank", "csr_rank", tkey, offsets, perm, n)
-    return attach_tile_plan(idx, n, trow, tpair, tsoff, offsets, tdst.view(tkey.shape))
+    return attach_tile_plan(idx, n, trow, tpair, tsoff, offsets, tdst)
+
+
+def tile_rows_of(idx, center, n):
+    """The row order of the tiled forward only (trow: the Morton-ordered rows of every 32-row
+    tile): a forward without gradients needs nothing else of the plan, so the CSR of the
+    partial rows is not built for it.  A full plan cached on idx is used as it is."""
+    if torch.is_grad_enabled():
+        return tile_plan_of(idx, center, n).trow
+    tp = getattr(idx, "_kdpc_tplan", None)
+    if tp is not None and tp.n == n:
+        return tp.trow
+    order = _op("kdpc_morton_order", "morton_order", _gpu(center, "center").contiguous())
+    return _op("kdpc_pc_tile_plan", "pc_tile_plan", _gpu(idx, "idx"), order, n)[0]
 
 
 def attach_tile_plan(idx, n, trow, tpair, tsoff, offsets, tdst):
-    """Cache a tile plan built elsewhere (PointConvBidirection.precompute_plan) on idx."""
+    """Cache a tile plan built elsewhere (PointConvBidirection.precompute_plan) on idx.
+    tdst is kept as (B, tiles per element * 32K), the layout a batch prefix slices."""
     B, S, K = idx.shape
     nt = B * ((S + 31) // 32)
     if trow.shape != (nt, 32) or tpair.shape != (nt, 32 * K) or \
@@ -518,7 +531,8 @@ def attach_tile_plan(idx, n, trow, tpair, tsoff, offsets, tdst):
             tdst.numel() != nt * 32 * K:
         raise ValueError("attach_tile_plan: plan sizes do not match the index tensor")
     tp = TilePlan()
-    tp.trow, tp.tpair, tp.tsoff, tp.offsets, tp.tdst, tp.n = trow, tpair, tsoff, offsets, tdst, n
+    tp.trow, tp.tpair, tp.tsoff, tp.offsets, tp.n = trow, tpair, tsoff, offsets, n
+    tp.tdst = tdst.reshape(B, -1)
     try:
         idx._kdpc_tplan = tp
     except AttributeError:
@@ -530,14 +544,14 @@ def tile_plan_tensors(tp):
     return [tp.trow, tp.tpair, tp.tsoff, tp.offsets, tp.tdst]
 
 
-def pointconv_fwd_tiled(xyz, center, feats, idx, wt, wl, bias, tp):
-    """pointconv_fwd with the rows of each tile from the tile plan tp (bit-identical)."""
+def pointconv_fwd_tiled(xyz, center, feats, idx, wt, wl, bias, trow):
+    """pointconv_fwd with the rows of each tile from a tile plan's trow (bit-identical)."""
     B, N, _ = _gpu(xyz, "xyz").shape
     S, K = idx.shape[1], idx.shape[2]
     O, C = wl.shape[0], 3 + feats.shape[2]
     R = B * S
     return _op("kdpc_pointconv_fwd", "pointconv_fwd_tiled", xyz, center, feats, idx, wt, wl,
-               bias, tp.trow, work=(4 * R * (K + K * C + 16 * K + O) + 4 * O * 16 * C,
+               bias, trow, work=(4 * R * (K + K * C + 16 * K + O) + 4 * O * 16 * C,
                                     2.0 * R * K * C * 16 + 2.0 * R * 16 * C * O))
 
 
@@ -580,24 +594,18 @@ def three_interpolate_grad(grad_out, idx, weight, m):
 
 
 # ------------------------------------------------------------------ fused cost volume
-# The wide cost-volume levels (Din = Dout in {128, 256}) run the one-kernel MFMA path of
-# cost_volume_wide.hip (cvw_fused_*): gather + position transform + LeakyReLU + the Din x Dout
-# MLP + max/argmax in one forward kernel, its backward in one more; no h0 / z1 in HBM.
-# Whole-step A/B (round 4): 16.96 / 17.12 ms -> 16.63 / 16.60 ms per train step against the
-# BLAS-GEMM wide path (cvw_h0 -> hipBLASLt -> cvw_max), which KDPC_CV_WIDE_FUSED=0 keeps for
-# A/B runs.  Its fp32 rounding differs from the GEMM's; the gradient parity test replays the
-# float64 reference's LeakyReLU decisions at near-ties (tests/test_gpu_model.py::_CvReplay)
-# as it replays the max routing.
-WIDE_FUSED = os.environ.get("KDPC_CV_WIDE_FUSED", "1") != "0"
+# Every model width runs a one-kernel-each-way path: Din, Dout in {32, 64} (cost_volume.hip)
+# and Din = Dout in {128, 256} (the fused MFMA kernels of cost_volume_wide.hip: gather +
+# position transform + LeakyReLU + the Din x Dout MLP + max/argmax in one forward kernel, no
+# h0 / z1 in HBM; round 4 whole-step A/B 16.96 / 17.12 -> 16.63 / 16.60 ms against the
+# BLAS-GEMM formulation, which stays for the other widths: cost_volume_wide_*).
 
 
 def cost_volume_supported(din, dout, k):
-    """Shapes the model layers run through kdpc_cost_volume_fwd/_bwd: Din, Dout in {32, 64}
-    (cost_volume.hip), plus Din = Dout in {128, 256} (the fused wide kernels of
-    cost_volume_wide.hip) when WIDE_FUSED; K <= 32.  (The C entry points accept the wide
-    shapes either way.)"""
+    """Shapes kdpc_cost_volume_fwd/_bwd take: Din, Dout in {32, 64} (cost_volume.hip), plus
+    Din = Dout in {128, 256} (the fused wide kernels of cost_volume_wide.hip); K <= 32."""
     narrow = din in (32, 64) and dout in (32, 64)
-    wide = WIDE_FUSED and din == dout and din in (128, 256)
+    wide = din == dout and din in (128, 256)
     return (narrow or wide) and 1 <= k <= 32
 
 
@@ -613,22 +621,25 @@ def cost_volume_fwd(x1, x2, idx, p1, p2, wpos, bpos, w1, b1):
                          2.0 * B * N1 * K * din * dout))
 
 
-def cost_volume_bwd(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout):
-    """-> dp1 (B,N1,Din), dp2_rows (B,N1,K,Din), dx1 (B,N1,3), ddir_rows (B,N1,K,3), dparams."""
+def cost_volume_bwd(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout, slope0=None):
+    """-> dp1 (B,N1,Din), dp2_rows (B,N1,K,Din), dx1 (B,N1,3), ddir_rows (B,N1,K,3), dparams.
+    slope0: optional (B,N1,K,Din) u8 override of the first LeakyReLU's derivative (test seam,
+    include/kdpc.h)."""
     B, N1, _ = _gpu(x1, "x1").shape
     K = idx.shape[2]
     din, dout = p1.shape[2], w1.shape[0]
     # reads x1, idx, p1, the K gathered p2 rows, out, gout, amax; writes dp1, dp2_rows,
     # dx1, ddir_rows.  flops: dh0 = M W1 and dW1 = h0^T M over the K x Din x Dout tile
     return _op("kdpc_cost_volume_bwd", "cost_volume_bwd", x1, x2, idx, p1, p2,
-               wpos, bpos, w1, out, amax, gout,
+               wpos, bpos, w1, out, amax, gout, slope0,
                work=(4 * B * N1 * (3 + K + din + K * din + 2 * dout + din + K * din + 3 + 3 * K)
                      + B * N1 * dout, 4.0 * B * N1 * K * din * dout))
 
 
-def cost_volume_bwd_csr(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout):
+def cost_volume_bwd_csr(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout, slope0=None):
     """-> dp1 (B,N1,Din), dp2 (B,N2,Din), dx1 (B,N1,3), dx2 (B,N2,3), dparams: the backward
-    with the per-point sums through the (cached) CSR of idx done inside the entry point."""
+    with the per-point sums through the (cached) CSR of idx done inside the entry point.
+    slope0 as cost_volume_bwd."""
     B, N1, _ = _gpu(x1, "x1").shape
     N2, K = x2.shape[1], idx.shape[2]
     din, dout = p1.shape[2], w1.shape[0]
@@ -637,39 +648,9 @@ def cost_volume_bwd_csr(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout):
     # dx1 and the per-point dp2 / dx2 (the CSR-ordered rows in between are not counted)
     entry = "kdpc_cost_volume_bwd_csr_wide" if din >= 128 else "kdpc_cost_volume_bwd_csr"
     return _op(entry, "cost_volume_bwd_csr", x1, x2, idx, p1, p2,
-               wpos, bpos, w1, out, amax, gout, csr.offsets, csr.rank,
+               wpos, bpos, w1, out, amax, gout, csr.offsets, csr.rank, slope0,
                work=(4 * B * N1 * (3 + 2 * K + din + K * din + 2 * dout + din + 3)
                      + B * N1 * dout + 4 * B * N2 * (din + 4) + 4,
-                     4.0 * B * N1 * K * din * dout))
-
-
-_PULL_MORTON = os.environ.get("KDPC_CV_PULL_MORTON") == "1"
-
-
-@functools.lru_cache(maxsize=None)
-def cost_volume_bwd_pull_supported(din, dout, k):
-    return bool(load_library().kdpc_cost_volume_bwd_pull_supported(din, dout, k))
-
-
-def cost_volume_bwd_pull(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout):
-    """-> dp1 (B,N1,Din), dp2 (B,N2,Din), dx1 (B,N1,3), dx2 (B,N2,3), dparams: the backward
-    with the per-point sums in pull form (csrc/cost_volume.hip cv_pull_kernel: one wave per
-    reference point recomputes the dz0 rows of its CSR segment; no per-neighbour rows in HBM).
-    Din == Dout in {32, 64, 128, 256} (cost_volume_bwd_pull_supported)."""
-    B, N1, _ = _gpu(x1, "x1").shape
-    N2, K = x2.shape[1], idx.shape[2]
-    din, dout = p1.shape[2], w1.shape[0]
-    csr = csr_of(idx, N2)
-    # reads x1, idx, p1, the K gathered p2 rows, out, gout, amax (backward kernel); offsets,
-    # perm, p2, x2 and the per-pair query rows p1 / out / gout / amax / x1 (pull kernel, cache-
-    # resident per cloud; counted once); writes dp1, dx1, dp2, dx2
-    # KDPC_CV_PULL_MORTON=1 (A/B): reference points walked in Morton order of x2
-    order = (_op("kdpc_morton_order", "morton_order", x2.contiguous())
-             if _PULL_MORTON and N2 <= 8192 else None)
-    return _op("kdpc_cost_volume_bwd_pull", "cost_volume_bwd_pull", x1, x2, idx, p1, p2,
-               wpos, bpos, w1, out, amax, gout, csr.offsets, csr.perm, order,
-               work=(4 * B * N1 * (3 + 2 * K + din + K * din + 2 * dout + din + 3)
-                     + B * N1 * dout + 4 * B * N2 * (2 * din + 7) + 4,
                      4.0 * B * N1 * K * din * dout))
 
 

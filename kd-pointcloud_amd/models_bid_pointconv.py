@@ -17,20 +17,19 @@ import torch
 import torch.nn as nn
 
 from pointconv_util import (PointConvD, PointWarping, UpsampleFlow, CrossLayerLight as CrossLayer,
-                            SceneFlowEstimatorResidual, Conv1d, cost_volume_bwd_uses_rank)
+                            SceneFlowEstimatorResidual, Conv1d)
 from pointconv_util import index_points_gather as index_points, index_points_group, square_distance  # noqa: F401
 from loss_functions import multiScaleLoss  # noqa: F401  (the reference defines it here too)
 import kdpc_native
 import wgrad
 from pointnet2 import pointnet2_utils
 
-# KDPC_COORD_FORK=0 runs the decoder's flow-dependent searches in line (A/B runs)
+# KDPC_COORD_FORK=0 runs the decoder's flow-dependent searches in line (stream switch)
 COORD_FORK = os.environ.get("KDPC_COORD_FORK", "1") != "0"
 _coord_streams = {}  # (device index, forking stream handle) -> side stream
-# KDPC_COORD_OWN_STREAM=1 gives the fork a stream of its own instead of wgrad's (A/B runs)
-SHARED_SIDE_STREAM = os.environ.get("KDPC_COORD_OWN_STREAM") != "1"
-# KDPC_COORD_FORK_CSR=0 leaves the CSRs to the backward (A/B runs)
-FORK_CSR = os.environ.get("KDPC_COORD_FORK_CSR", "1") != "0"
+# the fork shares the parameter-gradient stream (idle during the forward); False gives it a
+# stream of its own (test seam: tests/test_gpu_graph.py captures both)
+SHARED_SIDE_STREAM = True
 
 
 class _CoordFork:
@@ -84,16 +83,11 @@ class _CoordFork:
             return None
         idx, n, warp_idx, d = pending
         self.cur.wait_stream(self.side)
-        if torch.is_grad_enabled() and FORK_CSR:
+        if torch.is_grad_enabled():
             keep = []
             with torch.cuda.stream(self.side):
-                # the pull-form backward (D <= 64) reads offsets / perm only
-                if cost_volume_bwd_uses_rank(d, idx.shape[-1]):
-                    c = kdpc_native.csr_rank_of(idx, n)
-                    keep += [c.offsets, c.perm, c.rank]
-                else:
-                    c = kdpc_native.csr_of(idx, n)
-                    keep += [c.offsets, c.perm]
+                c = kdpc_native.csr_rank_of(idx, n)  # what the cost volume's backward reads
+                keep += [c.offsets, c.perm, c.rank]
                 if warp_idx is not None:
                     warp_idx.record_stream(self.side)
                     c = kdpc_native.csr_of(warp_idx, n)

@@ -378,8 +378,8 @@ class _PointConvLayer(torch.autograd.Function):
         if _nat.TILED_FWD and _nat.tiled_supported(idx, center) and \
                 idx.shape[-1] == _nat.TILED_MAX_K:
             # the backward's Morton-ordered row tiles: the same rows, spatially close gathers
-            tp = _nat.tile_plan_of(idx, center, xyz.shape[1])
-            return _nat.pointconv_fwd_tiled(xyz, center, feats, idx, wt, wl, bias, tp)
+            trow = _nat.tile_rows_of(idx, center, xyz.shape[1])
+            return _nat.pointconv_fwd_tiled(xyz, center, feats, idx, wt, wl, bias, trow)
         return _nat.pointconv_fwd(xyz, center, feats, idx, wt, wl, bias)
 
     @staticmethod
@@ -532,64 +532,27 @@ class PointConvD(_PointConvBase):
         return new_xyz, new_points, fps_idx
 
 
-# KDPC_CV_BWD_PLAIN=1: the D <= 64 backward writes its per-neighbour rows in (query,
-# neighbour) order and sums them through the CSR's perm (A/B runs; bit-identical)
-_CV_BWD_PLAIN = os.environ.get("KDPC_CV_BWD_PLAIN") == "1"
-# KDPC_CV_BWD_PULL=1: the pull form (kdpc_cost_volume_bwd_pull: no per-neighbour rows in HBM,
-# each reference point recomputes its rows) instead of the ranked path for Din == Dout <= 64;
-# KDPC_CV_BWD_PULL_WIDE=1 also for D in {128, 256}.  Off by default: measured slower (round 4,
-# profiles/round04/pull: cross0 641 vs 623 us, step 15.94 vs 15.71 ms; the backward kernel
-# alone is 368 us without any row stores, and the pull's per-pair query gathers cost more
-# than the rows' round trip)
-_CV_BWD_PULL = os.environ.get("KDPC_CV_BWD_PULL", "0") == "1"
-_CV_BWD_PULL_WIDE = os.environ.get("KDPC_CV_BWD_PULL_WIDE", "0") == "1"
-
-
-def _cv_bwd_pull(din, dout, k):
-    if not _CV_BWD_PULL or (din > 64 and not _CV_BWD_PULL_WIDE):
-        return False
-    return _nat.cost_volume_bwd_pull_supported(din, dout, k)
-
-
-def cost_volume_bwd_uses_rank(d, k):
-    """Whether the backward of a (d -> d, K = k) cost volume reads the CSR's rank (the ranked
-    path) or only offsets / perm (the pull form)."""
-    return not (not _CV_BWD_PLAIN and _cv_bwd_pull(d, d, k))
-
-
 class _CostVolume(torch.autograd.Function):
-    """Fused cost volume (csrc/cost_volume.hip): x1 (B,N1,3), x2 (B,N2,3), idx (B,N1,K),
-    p1 (B,N1,D), p2 (B,N2,D) channel-last -> (B,N1,Dout) channel-last."""
+    """Fused cost volume (csrc/cost_volume.hip, cost_volume_wide.hip): x1 (B,N1,3),
+    x2 (B,N2,3), idx (B,N1,K), p1 (B,N1,D), p2 (B,N2,D) channel-last -> (B,N1,Dout)
+    channel-last.  The backward writes its per-neighbour rows at their slots of the (cached)
+    CSR of idx and sums them per reference point inside the entry point."""
 
     @staticmethod
-    def forward(ctx, x1, x2, idx, p1, p2, wpos, bpos, w1, b1, amax_override=None):
+    def forward(ctx, x1, x2, idx, p1, p2, wpos, bpos, w1, b1, decisions=None):
         out, amax = _nat.cost_volume_fwd(x1, x2, idx, p1, p2, wpos, bpos, w1, b1)
-        if amax_override is not None:
-            amax = amax_override(amax)
-        ctx.save_for_backward(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax)
+        out_b, slope0 = out, None
+        if decisions is not None:
+            amax, out_b, slope0 = decisions(amax, out, idx.shape[2], p1.shape[2])
+        ctx.save_for_backward(x1, x2, idx, p1, p2, wpos, bpos, w1, out_b, amax, slope0)
         return out
 
     @staticmethod
     def backward(ctx, gout):
-        x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax = ctx.saved_tensors
-        B, N1, K = idx.shape
-        N2 = x2.shape[1]
+        x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, slope0 = ctx.saved_tensors
         din, dout = p1.shape[2], w1.shape[0]
-        if _CV_BWD_PLAIN and din <= 64:
-            # A/B: rows in (query, neighbour) order, summed per point through perm
-            dp1, rows, dx1, drows, dpar = _nat.cost_volume_bwd(
-                x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout.contiguous())
-            csr = _nat.csr_of(idx, N2)
-            dp2 = _nat.group_rows_grad(rows.view(B, N1 * K, din), csr, B, N2, din)
-            dx2 = _nat.group_rows_grad(drows.view(B, N1 * K, 3), csr, B, N2, 3)
-        elif _cv_bwd_pull(din, dout, K):
-            # each reference point recomputes the dz0 rows naming it (no rows through HBM)
-            dp1, dp2, dx1, dx2, dpar = _nat.cost_volume_bwd_pull(
-                x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout.contiguous())
-        else:
-            # per-neighbour rows straight into the CSR order of idx, summed per point inside
-            dp1, dp2, dx1, dx2, dpar = _nat.cost_volume_bwd_csr(
-                x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout.contiguous())
+        dp1, dp2, dx1, dx2, dpar = _nat.cost_volume_bwd_csr(
+            x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout.contiguous(), slope0)
         o = dout * din
         dw1 = dpar[:o].view(dout, din)
         db1 = dpar[o:o + dout]
@@ -599,18 +562,20 @@ class _CostVolume(torch.autograd.Function):
 
 
 class _CostVolumeWide(torch.autograd.Function):
-    """Wide cost volume (csrc/cost_volume_wide.hip): the Din -> Dout MLP is one BLAS GEMM,
-    the gather / position transform / activations / max around it are fused kernels.
-    Same arguments and result as _CostVolume."""
+    """The widths the fused kernels do not take (Din in {64, 128, 256, 512} with another
+    Dout, csrc/cost_volume_wide.hip): the Din -> Dout MLP is one BLAS GEMM, the gather /
+    position transform / activations / max around it are fused kernels.  Same arguments and
+    result as _CostVolume."""
 
     @staticmethod
-    def forward(ctx, x1, x2, idx, p1, p2, wpos, bpos, w1, b1, amax_override=None):
+    def forward(ctx, x1, x2, idx, p1, p2, wpos, bpos, w1, b1, decisions=None):
         B, N1, K = idx.shape
         h0 = _nat.cost_volume_wide_h0(x1, x2, idx, p1, p2, wpos, bpos)
         z1 = torch.addmm(b1, h0.view(-1, h0.shape[-1]), w1.t())
         out, amax = _nat.cost_volume_wide_max(z1, B, N1, K, w1.shape[0])
-        if amax_override is not None:
-            amax = amax_override(amax)
+        if decisions is not None:
+            amax, out_b, slope0 = decisions(amax, out, K, p1.shape[2])
+            assert slope0 is None and out_b is out, "no decision replay on the unfused path"
         ctx.save_for_backward(x1, x2, idx, wpos, w1, h0, out, amax, bpos, b1)
         return out
 
@@ -642,32 +607,21 @@ class _CostVolumeWide(torch.autograd.Function):
 
 
 _FUSED_COST_VOLUME = True  # test seam: False forces the unfused torch formulation
-_amax_override = None
+_cv_decisions = None
 
 
-def set_amax_override(fn):
-    """Test seam: `fn(amax) -> amax` replaces the max-over-K routing (which neighbour each
-    (point, channel) maximum came from, (B,N1,Dout) uint8) that the fused cost volume's
-    backward uses, for every call made with gradients enabled -- the parity tests replay
-    the float64 reference's routing with it, as set_knn_override replays its neighbours.
-    None restores the computed routing.  Returns the previous override."""
-    global _amax_override
-    prev, _amax_override = _amax_override, fn
-    return prev
-
-
-_cv_override = None
-
-
-def set_cv_override(fn):
-    """Test seam: `fn(x1, x2, idx, p1, p2, wpos, bpos, w1, b1) -> out | None` is offered
-    every fused cost-volume call made with gradients enabled, before the kernel runs; a
-    tensor it returns replaces the call's result (None: the kernels run).  The gradient
-    parity test uses it to replay the float64 reference's LeakyReLU decisions for a call
-    whose pre-activations include a near-tie this build's fp32 evaluation cannot place on
-    the reference's side (tests/test_gpu_model.py::_CvReplay).  Returns the previous one."""
-    global _cv_override
-    prev, _cv_override = _cv_override, fn
+def set_cv_decisions(fn):
+    """Test seam: `fn(amax, out, K, Din) -> (amax, out_for_backward, slope0)` is offered the
+    result of every fused cost-volume forward made with gradients enabled and returns the
+    discrete decisions its backward is to use: the max routing amax (which neighbour each
+    (point, channel) maximum came from, (B,N1,Dout) u8), a tensor whose sign gives the second
+    LeakyReLU's derivative (the output itself by default), and slope0 (B,N1,K,Din) u8 or None,
+    the first LeakyReLU's derivative per (point, neighbour, channel) (include/kdpc.h).  The
+    parity tests replay a float64 reference run's decisions with it, as set_knn_override
+    replays its neighbours (tests/test_gpu_model.py::_CvReplay).  None restores the computed
+    ones.  Returns the previous function."""
+    global _cv_decisions
+    prev, _cv_decisions = _cv_decisions, fn
     return prev
 
 
@@ -709,15 +663,10 @@ def _cost_volume_cl(nsample, x1, x2, p1, p2, pos, mlp, act, knn_idx=None):
     fn = _fusable(nsample, pos, mlp, act, din)
     if fn:
         conv = mlp[0].composed_module[0]
-        ovr = _amax_override if torch.is_grad_enabled() else None
-        args = (x1, x2, _as_idx32(knn_idx).contiguous(), p1.contiguous(), p2.contiguous(),
-                pos.weight.view(din, 3), pos.bias, conv.weight.view(conv.out_channels, din),
-                conv.bias)
-        if _cv_override is not None and torch.is_grad_enabled():
-            out = _cv_override(*args)
-            if out is not None:
-                return out
-        return fn.apply(*args, ovr)
+        dec = _cv_decisions if torch.is_grad_enabled() else None
+        return fn.apply(x1, x2, _as_idx32(knn_idx).contiguous(), p1.contiguous(), p2.contiguous(),
+                        pos.weight.view(din, 3), pos.bias, conv.weight.view(conv.out_channels, din),
+                        conv.bias, dec)
     direction = index_points_group(x2, knn_idx) - x1.view(B, N1, 1, C)
     grouped_points2 = index_points_group(p2, knn_idx)
     h = act((grouped_points2 + p1.unsqueeze(2)) + _linear_1x1(pos, direction))

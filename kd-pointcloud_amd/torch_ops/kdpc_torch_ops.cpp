@@ -381,15 +381,26 @@ TT cost_volume_fwd(Tensor x1, Tensor x2, Tensor idx, Tensor p1, Tensor p2, Tenso
   return {out, amax};
 }
 
+// slope0 (B,N1,K,Din) u8, optional: the first LeakyReLU's derivative per (query, neighbour,
+// channel) for replaying a reference run's decisions (include/kdpc.h); None in training
+static const uint8_t* slope0_of(const c10::optional<Tensor>& s0, int64_t b, int64_t n1,
+                                int64_t k, int64_t din) {
+  if (!s0.has_value()) return nullptr;
+  dev(*s0, at::kByte, "slope0");
+  TORCH_CHECK(s0->numel() == b * n1 * k * din, "kdpc: slope0 must be (B, N1, K, Din)");
+  return s0->data_ptr<uint8_t>();
+}
+
 std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> cost_volume_bwd(
     Tensor x1, Tensor x2, Tensor idx, Tensor p1, Tensor p2, Tensor wpos, Tensor bpos, Tensor w1,
-    Tensor out, Tensor amax, Tensor gout) {
+    Tensor out, Tensor amax, Tensor gout, c10::optional<Tensor> slope0) {
   for (auto* t : {&x1, &x2, &p1, &p2, &wpos, &bpos, &w1, &out, &gout})
     dev(*t, kF, "cost volume input");
   dev(idx, kI, "idx"), dev(amax, at::kByte, "amax");
   GUARD(x1);
   const int64_t b = x1.size(0), n1 = x1.size(1), n2 = x2.size(1), k = idx.size(2);
   const int64_t din = p1.size(2), dout = w1.size(0);
+  const uint8_t* s0 = slope0_of(slope0, b, n1, k, din);
   Tensor dp1 = empty_f({b, n1, din}, x1);
   Tensor dp2_rows = empty_f({b, n1, k, din}, x1);
   Tensor dx1 = empty_f({b, n1, 3}, x1);
@@ -398,15 +409,16 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> cost_volume_bwd(
   const size_t nb = kdpc_cost_volume_bwd_workspace_bytes(b, n1, din, dout);
   Tensor ws = workspace(nb, x1);
   check(kdpc_cost_volume_bwd(b, n1, n2, k, din, dout, F(x1), F(x2), I(idx), F(p1), F(p2),
-                             F(wpos), F(bpos), F(w1), F(out), amax.data_ptr<uint8_t>(), F(gout),
-                             F(dp1), F(dp2_rows), F(dx1), F(ddir_rows), ws.data_ptr(), nb,
+                             F(wpos), F(bpos), F(w1), F(out), amax.data_ptr<uint8_t>(), s0,
+                             F(gout), F(dp1), F(dp2_rows), F(dx1), F(ddir_rows), ws.data_ptr(), nb,
                              F(dparams), stream_of(x1)), "cost_volume_bwd");
   return {dp1, dp2_rows, dx1, ddir_rows, dparams};
 }
 
 std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> cost_volume_bwd_csr(
     Tensor x1, Tensor x2, Tensor idx, Tensor p1, Tensor p2, Tensor wpos, Tensor bpos, Tensor w1,
-    Tensor out, Tensor amax, Tensor gout, Tensor offsets, Tensor rank) {
+    Tensor out, Tensor amax, Tensor gout, Tensor offsets, Tensor rank,
+    c10::optional<Tensor> slope0) {
   for (auto* t : {&x1, &x2, &p1, &p2, &wpos, &bpos, &w1, &out, &gout})
     dev(*t, kF, "cost volume input");
   dev(idx, kI, "idx"), dev(amax, at::kByte, "amax"), dev(offsets, kI, "offsets");
@@ -414,6 +426,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> cost_volume_bwd_csr(
   GUARD(x1);
   const int64_t b = x1.size(0), n1 = x1.size(1), n2 = x2.size(1), k = idx.size(2);
   const int64_t din = p1.size(2), dout = w1.size(0);
+  const uint8_t* s0 = slope0_of(slope0, b, n1, k, din);
   TORCH_CHECK(offsets.numel() >= b * n2 + 1 && rank.numel() >= b * n1 * k,
               "kdpc: cost_volume_bwd_csr: offsets / rank do not match idx");
   Tensor dp1 = empty_f({b, n1, din}, x1);
@@ -425,42 +438,10 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> cost_volume_bwd_csr(
   TORCH_CHECK(nb > 0, "kdpc: cost_volume_bwd_csr: unsupported shape");
   Tensor ws = workspace(nb, x1);
   check(kdpc_cost_volume_bwd_csr(b, n1, n2, k, din, dout, F(x1), F(x2), I(idx), F(p1), F(p2),
-                                 F(wpos), F(bpos), F(w1), F(out), amax.data_ptr<uint8_t>(),
+                                 F(wpos), F(bpos), F(w1), F(out), amax.data_ptr<uint8_t>(), s0,
                                  F(gout), I(offsets), I(rank), F(dp1), F(dp2), F(dx1), F(dx2),
                                  ws.data_ptr(), nb, F(dparams), stream_of(x1)),
         "cost_volume_bwd_csr");
-  return {dp1, dp2, dx1, dx2, dparams};
-}
-
-std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> cost_volume_bwd_pull(
-    Tensor x1, Tensor x2, Tensor idx, Tensor p1, Tensor p2, Tensor wpos, Tensor bpos, Tensor w1,
-    Tensor out, Tensor amax, Tensor gout, Tensor offsets, Tensor perm,
-    c10::optional<Tensor> order) {
-  for (auto* t : {&x1, &x2, &p1, &p2, &wpos, &bpos, &w1, &out, &gout})
-    dev(*t, kF, "cost volume input");
-  dev(idx, kI, "idx"), dev(amax, at::kByte, "amax"), dev(offsets, kI, "offsets");
-  dev(perm, kI, "perm");
-  GUARD(x1);
-  const int64_t b = x1.size(0), n1 = x1.size(1), n2 = x2.size(1), k = idx.size(2);
-  const int64_t din = p1.size(2), dout = w1.size(0);
-  TORCH_CHECK(kdpc_cost_volume_bwd_pull_supported(din, dout, k),
-              "kdpc: cost_volume_bwd_pull: unsupported shape");
-  TORCH_CHECK(offsets.numel() >= b * n2 + 1 && perm.numel() >= b * n1 * k,
-              "kdpc: cost_volume_bwd_pull: offsets / perm do not match idx");
-  Tensor dp1 = empty_f({b, n1, din}, x1);
-  Tensor dp2 = empty_f({b, n2, din}, x1);
-  Tensor dx1 = empty_f({b, n1, 3}, x1);
-  Tensor dx2 = empty_f({b, n2, 3}, x1);
-  Tensor dparams = empty_f({dout * din + dout + 4 * din}, x1);
-  const size_t nb = kdpc_cost_volume_bwd_workspace_bytes(b, n1, din, dout);
-  TORCH_CHECK(nb > 0, "kdpc: cost_volume_bwd_pull: unsupported shape");
-  Tensor ws = workspace(nb, x1);
-  check(kdpc_cost_volume_bwd_pull(b, n1, n2, k, din, dout, F(x1), F(x2), I(idx), F(p1), F(p2),
-                                  F(wpos), F(bpos), F(w1), F(out), amax.data_ptr<uint8_t>(),
-                                  F(gout), I(offsets), I(perm),
-                                  order.has_value() ? I(*order) : nullptr, F(dp1), F(dp2), F(dx1), F(dx2),
-                                  ws.data_ptr(), nb, F(dparams), stream_of(x1)),
-        "cost_volume_bwd_pull");
   return {dp1, dp2, dx1, dx2, dparams};
 }
 
@@ -1077,14 +1058,12 @@ TORCH_LIBRARY(kdpc, m) {
   m.def("cost_volume_fwd(Tensor x1, Tensor x2, Tensor idx, Tensor p1, Tensor p2, Tensor wpos, "
         "Tensor bpos, Tensor w1, Tensor b1) -> (Tensor, Tensor)");
   m.def("cost_volume_bwd(Tensor x1, Tensor x2, Tensor idx, Tensor p1, Tensor p2, Tensor wpos, "
-        "Tensor bpos, Tensor w1, Tensor out, Tensor amax, Tensor gout) "
+        "Tensor bpos, Tensor w1, Tensor out, Tensor amax, Tensor gout, Tensor? slope0=None) "
         "-> (Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("cost_volume_bwd_csr(Tensor x1, Tensor x2, Tensor idx, Tensor p1, Tensor p2, "
         "Tensor wpos, Tensor bpos, Tensor w1, Tensor out, Tensor amax, Tensor gout, "
-        "Tensor offsets, Tensor rank) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
-  m.def("cost_volume_bwd_pull(Tensor x1, Tensor x2, Tensor idx, Tensor p1, Tensor p2, "
-        "Tensor wpos, Tensor bpos, Tensor w1, Tensor out, Tensor amax, Tensor gout, "
-        "Tensor offsets, Tensor perm, Tensor? order=None) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
+        "Tensor offsets, Tensor rank, Tensor? slope0=None) "
+        "-> (Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("cost_volume_wide_h0(Tensor x1, Tensor x2, Tensor idx, Tensor p1, Tensor p2, "
         "Tensor wpos, Tensor bpos) -> Tensor");
   m.def("cost_volume_wide_max(Tensor z1, int b, int n1, int k, int dout) -> (Tensor, Tensor)");
@@ -1172,7 +1151,6 @@ TORCH_LIBRARY_IMPL(kdpc, CUDA, m) {
   m.impl("cost_volume_fwd", cost_volume_fwd);
   m.impl("cost_volume_bwd", cost_volume_bwd);
   m.impl("cost_volume_bwd_csr", cost_volume_bwd_csr);
-  m.impl("cost_volume_bwd_pull", cost_volume_bwd_pull);
   m.impl("cost_volume_wide_h0", cost_volume_wide_h0);
   m.impl("cost_volume_wide_max", cost_volume_wide_max);
   m.impl("cost_volume_wide_max_bwd", cost_volume_wide_max_bwd);

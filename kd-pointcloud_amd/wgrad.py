@@ -21,6 +21,12 @@ Ordering (eager and inside a captured HIP graph alike):
     waits for the side-stream event recorded after the launch that produced those
     parameters' gradients (not for everything queued on the side stream so far), or join()
     for all of it;
+  * every input of a side-stream launch stays referenced here until that join: autograd's
+    InputBuffer adds a second gradient contribution IN PLACE into a gradient tensor it holds
+    the only reference to, and AddBackward hands one gradient tensor to both of its inputs, so
+    an incoming gradient that run() passed to the side stream could otherwise be modified on
+    the backward's stream before the side stream has read it (record_stream only keeps the
+    memory from being reused; a held reference keeps the in-place path off);
   * autograd's AccumulateGrad runs on the backward's stream right after the layer's backward
     returns.  With `.grad` None it only takes the new tensor (no kernel reads it), but onto
     an existing `.grad` (accumulation over micro-batches, zero_grad(set_to_none=False)) it
@@ -49,6 +55,7 @@ _side = {}      # device index -> the first side stream (the decoder coordinate 
 _pool = {}      # device index -> [side streams]
 _turn = {}      # device index -> next pool entry
 _pending = {}   # (main, side) raw stream handles -> (main, side) joins queued in this backward
+_held = {}      # same key -> the side-stream launches' inputs, released at the join
 _suspended = weakref.WeakSet()  # objects (DDP wrappers) for whose lifetime run() is in line
 # id(leaf parameter) -> (weak reference to it, side-stream event recorded after the launch
 # that produced its gradient).  The events stay referenced until overwritten (a HIP event destroyed while a
@@ -119,6 +126,7 @@ def run(fn, inputs, params=()):
     # its callbacks leaves nothing stale behind: the next pass queues its own)
     key = (main.cuda_stream, side.cuda_stream)
     _pending[key] = (main, side)
+    _held.setdefault(key, []).append([t for t in inputs if t is not None])
     torch.autograd.Variable._execution_engine.queue_callback(lambda k=key: _join_pending(k))
     return out
 
@@ -155,6 +163,7 @@ def _join_pending(key):
     pair = _pending.pop(key, None)
     if pair is not None:
         pair[0].wait_stream(pair[1])
+    _held.pop(key, None)
 
 
 def join(device=None):

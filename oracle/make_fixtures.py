@@ -228,6 +228,8 @@ def make_flow_layers(R):
         "fe32": (lambda: R.pcu.FlowEmbeddingLayer(32, 64, [32, 32]), 51),
         "fe64": (lambda: R.pcu.FlowEmbeddingLayer(32, 64, [64, 64]), 52),
         "fe128": (lambda: R.pcu.FlowEmbeddingLayer(16, 64, [128, 128]), 53),
+        # D = 256: the width of the models' level-3 cost volume (cvw_fused_bwd_kernel<256, *>)
+        "fe256": (lambda: R.pcu.FlowEmbeddingLayer(16, 64, [256, 256]), 55),
         "pcf": (lambda: R.pcu.PointConvFlow(16, 64 + 64 + 3, [64, 64]), 54),
     }
     knn = R.pcu.knn_point

@@ -144,6 +144,48 @@ def test_parameter_gradient_stream_is_bit_identical():
         assert torch.equal(g0[n], g1[n]), n
 
 
+def test_parameter_gradient_stream_survives_in_place_gradient_accumulation():
+    """A residual add around a dense layer: AddBackward hands the SAME gradient tensor to the
+    layer's backward (whose weight gradient reads it on the side stream) and to the input
+    buffer of the residual branch, which then adds the layer's input gradient into it -- in
+    place whenever that buffer holds the only reference.  wgrad.run keeps the
+    side-stream inputs referenced until the end-of-backward join, so the weight / bias
+    gradients equal the in-line ones bit for bit.  The side stream is kept busy first (a long
+    GEMM chain) so that an unprotected read would come after the in-place add."""
+    import dense
+    import wgrad
+    torch.manual_seed(3)
+    x0 = torch.randn(65536, 64, device=DEV)
+    w1 = torch.randn(64, 64, device=DEV) * 0.1
+    w2 = torch.randn(64, 64, device=DEV) * 0.1
+    b2 = torch.randn(64, device=DEV) * 0.1
+    big = torch.randn(2048, 2048, device=DEV)
+    res = []
+    prev = wgrad.enabled
+    try:
+        for on in (False, True):
+            wgrad.enabled = on
+            a = w1.clone().requires_grad_(True)
+            w = w2.clone().requires_grad_(True)
+            b = b2.clone().requires_grad_(True)
+            h = dense.linear(x0, a)
+            out = dense.linear(h, w, b) + h
+            if on:  # queue work ahead on every side stream
+                for sd in wgrad.side_streams(torch.device(DEV)):
+                    sd.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(sd):
+                        y = big
+                        for _ in range(20):
+                            y = y @ big * 1e-3
+            (out * out).sum().backward()
+            torch.cuda.synchronize()
+            res.append([t.grad.clone() for t in (a, w, b)])
+    finally:
+        wgrad.enabled = prev
+    for n, g0, g1 in zip(("w1", "w2", "b2"), *res):
+        assert torch.equal(g0, g1), n
+
+
 def test_parameter_gradient_stream_accumulates_onto_existing_grads():
     """Two backward() calls without zero_grad (gradient accumulation): the second pass's
     AccumulateGrad adds onto the first pass's .grad on the backward's stream, so wgrad.run

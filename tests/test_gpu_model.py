@@ -70,9 +70,10 @@ def test_layers_match_reference(golden):
     _close(flo, g["est_out_flow"], rtol=2e-5, name="estimator flow")
 
 
-@pytest.mark.parametrize("name", ["fe32", "fe64", "fe128", "pcf"])
+@pytest.mark.parametrize("name", ["fe32", "fe64", "fe128", "fe256", "pcf"])
 def test_flow_layers_match_reference(golden, name):
-    """FlowEmbeddingLayer (D 32 / 64: fused cost volume; 128: the wide path) and
+    """FlowEmbeddingLayer (D 32 / 64: cost_volume.hip; 128 / 256: the fused wide kernels of
+    cost_volume_wide.hip, D = 256 being the models' level-3 width) and
     PointConvFlow vs the reference at B=2, N=512: the output at 1e-5 of its scale, every input
     and parameter gradient of sum(out * weight) at 1e-4 of its scale (the reference's CPU GEMMs
     and the max-over-K routing accumulate in other orders)."""
@@ -82,8 +83,9 @@ def test_flow_layers_match_reference(golden, name):
     make = {"fe32": lambda: P.FlowEmbeddingLayer(32, 64, [32, 32]),
             "fe64": lambda: P.FlowEmbeddingLayer(32, 64, [64, 64]),
             "fe128": lambda: P.FlowEmbeddingLayer(16, 64, [128, 128]),
+            "fe256": lambda: P.FlowEmbeddingLayer(16, 64, [256, 256]),
             "pcf": lambda: P.PointConvFlow(16, 64 + 64 + 3, [64, 64])}[name]
-    seed = {"fe32": 51, "fe64": 52, "fe128": 53, "pcf": 54}[name]
+    seed = {"fe32": 51, "fe64": 52, "fe128": 53, "fe256": 55, "pcf": 54}[name]
     layer = load_synthetic(make(), seed=seed).to(DEV)
     x1 = _t(g["x1"].transpose(0, 2, 1)).permute(0, 2, 1)
     x2 = _t(g["x2"].transpose(0, 2, 1)).permute(0, 2, 1)
@@ -258,113 +260,62 @@ class _AmaxReplay:
 
 
 class _CvReplay(_AmaxReplay):
-    """_AmaxReplay plus the float64 reference's LeakyReLU decisions at near-ties.
+    """The float64 reference run's discrete cost-volume decisions, replayed into the HIP
+    kernels (pointconv_util.set_cv_decisions): its max routing (_AmaxReplay) and its
+    LeakyReLU decisions at near-ties.
 
     At LeakyReLU's kink (pre-activation 0) the derivative jumps from 0.1 to 1: like the max
     routing, a discrete choice.  The float64 fixture lists, per cost-volume call, every
     first-activation pre-activation z0 and every maximum over K of the second activation's
     pre-activation z1 that lies within 1e-4 of the call's scale of 0, with its float64 sign
-    (oracle/make_f64_fixture.py).  For each call this replay evaluates the build's own
-    pre-activations at those positions -- in float64 from the build's fp32 inputs (the
-    gathered rows, the weights) -- and when one of them is on the other side of 0 from the
-    float64 run, or closer to 0 than this build's fp32 rounding can resolve, the call is
-    computed by an unfused torch formulation that takes the float64 side at every listed
-    position (and the float64 max routing); every other call runs the HIP kernels with the
-    replayed routing.  `replayed` lists the calls that needed it."""
-
-    Z0_BAND = 1e-6   # x the call's scale: fp32 evaluation error of z0 is ~4 ulp of its terms
-    Z1_BAND = 1e-5   # z1 sums Din products
+    (oracle/make_f64_fixture.py); every other pre-activation is far enough from 0 that fp32
+    rounding cannot move it across.  The listed z0 decisions reach the backward kernels
+    through slope0 (B,N1,K,Din) u8 (1: slope 1, 2: slope 0.1), the listed z1 decisions through
+    the tensor whose sign the backward reads the second derivative from (the output, with
+    +-1 at the listed positions).  Every call runs the fused HIP kernels (no call is computed
+    any other way; the BLAS-GEMM path of the other widths refuses a slope0); `calls` counts
+    them, `replayed` the listed z0 / z1 decisions imposed."""
 
     def __init__(self, g64):
         super().__init__(g64)
         n = len(self.recs)
-        self.z0 = [(g64[f"z0tie{j}_nkd"], g64[f"z0tie{j}_sign"], float(g64[f"z0tie{j}_scale"]))
-                   for j in range(n)]
-        self.z1 = [(g64[f"z1tie{j}_nd"], g64[f"z1tie{j}_sign"], float(g64[f"z1tie{j}_scale"]))
-                   for j in range(n)]
-        self.replayed = []
+        self.z0 = [(g64[f"z0tie{j}_nkd"], g64[f"z0tie{j}_sign"]) for j in range(n)]
+        self.z1 = [(g64[f"z1tie{j}_nd"], g64[f"z1tie{j}_sign"]) for j in range(n)]
+        self.calls = 0
+        self.replayed = [0, 0]  # listed z0 / z1 decisions imposed
 
-    @staticmethod
-    def _z0_at(b, n, k, d, x1, x2, idx, p1, p2, wpos, bpos):
-        """float64 z0 = (P2[j] + P1[n]) + (Wpos dir + bpos) at (n, k, d) of batch b."""
-        j = idx[b, n, k]
-        dr = x2[b, j] - x1[b, n]                                   # (m, 3)
-        return (p2[b, j, d] + p1[b, n, d]) + ((wpos[d] * dr).sum(-1) + bpos[d])
-
-    def _uncertain(self, jc, b, a):
-        x1, x2, idx, p1, p2, wpos, bpos, w1, b1 = a
-        nkd, sg, scale = self.z0[jc]
-        if len(nkd):
-            n, k, d = (torch.from_numpy(c.astype(np.int64)).to(DEV) for c in nkd.T)
-            z = self._z0_at(b, n, k, d, x1, x2, idx, p1, p2, wpos, bpos)
-            s = torch.from_numpy(sg.astype(np.float64)).to(DEV)
-            if bool(((torch.sign(z) != s) | (z.abs() < self.Z0_BAND * scale)).any()):
-                return True
-        nd, sg1, scale1 = self.z1[jc]
-        if len(nd):
-            am = torch.from_numpy(self.recs[jc].astype(np.int64)).to(DEV)   # (1, N1, Dout)
-            n, d = (torch.from_numpy(c.astype(np.int64)).to(DEV) for c in nd.T)
-            k = am[0, n, d]
-            K, din = idx.shape[2], p1.shape[2]
-            # every input channel of the routed neighbour row: z0 -> h0 (own sign) -> z1
-            nn_ = n[:, None].expand(-1, din)
-            kk = k[:, None].expand(-1, din)
-            cc = torch.arange(din, device=DEV)[None, :].expand(len(n), -1)
-            z0 = self._z0_at(b, nn_, kk, cc, x1, x2, idx, p1, p2, wpos, bpos)
-            h0 = torch.where(z0 > 0, z0, 0.1 * z0)
-            z1 = (h0 * w1[d]).sum(-1) + b1[d]
-            s = torch.from_numpy(sg1.astype(np.float64)).to(DEV)
-            if bool(((torch.sign(z1) != s) | (z1.abs() < self.Z1_BAND * scale1)).any()):
-                return True
-        return False
-
-    def cv(self, x1, x2, idx, p1, p2, wpos, bpos, w1, b1):
-        bp = x1.shape[0]
-        a64 = [t.detach().double() for t in (x1, x2, p1, p2, wpos, bpos, w1, b1)]
-        a = (a64[0], a64[1], idx.long(), *a64[2:])
-        js = list(range(self.pos, self.pos + bp))
-        if not any(self._uncertain(jc, b, a) for b, jc in enumerate(js)):
-            return None  # the kernels run; __call__ serves their routing
-        self.replayed.append(tuple(js))
-        self.pos += bp
-        return self._torch_cv(js, x1, x2, idx, p1, p2, wpos, bpos, w1, b1)
-
-    def _torch_cv(self, js, x1, x2, idx, p1, p2, wpos, bpos, w1, b1):
-        B, N1, K = idx.shape
-        il = idx.long()
-        bi = torch.arange(B, device=DEV)[:, None, None]
-        dirs = x2[bi, il] - x1[:, :, None, :]
-        z0 = (p2[bi, il] + p1[:, :, None, :]) + (dirs @ wpos.t() + bpos)
-        f0 = torch.where(z0 > 0, 1.0, 0.1).detach()
-        am = torch.from_numpy(np.concatenate([self.recs[j] for j in js], 0).astype(np.int64)).to(DEV)
+    def __call__(self, amax, out, k, din):
+        js = list(range(self.pos, self.pos + amax.shape[0]))
+        am = super().__call__(amax)
+        B, N1, _ = amax.shape
+        s0 = torch.zeros((B, N1, k, din), dtype=torch.uint8, device=amax.device)
+        out_b = out.clone()
         for b, jc in enumerate(js):
-            nkd, sg, _ = self.z0[jc]
+            nkd, sg = self.z0[jc]
             if len(nkd):
-                n, k, d = (torch.from_numpy(c.astype(np.int64)).to(DEV) for c in nkd.T)
-                f0[b, n, k, d] = torch.from_numpy(np.where(sg > 0, 1.0, 0.1)).float().to(DEV)
-        z1 = (z0 * f0) @ w1.t() + b1
-        z1r = z1.gather(2, am[:, :, None, :]).squeeze(2)      # float64 routing: (B, N1, Dout)
-        f1 = torch.where(z1r > 0, 1.0, 0.1).detach()
-        for b, jc in enumerate(js):
-            nd, sg1, _ = self.z1[jc]
+                n_, k_, d_ = (torch.from_numpy(c.astype(np.int64)).to(DEV) for c in nkd.T)
+                s0[b, n_, k_, d_] = torch.from_numpy(np.where(sg > 0, 1, 2).astype(np.uint8)).to(DEV)
+                self.replayed[0] += len(nkd)
+            nd, sg1 = self.z1[jc]
             if len(nd):
-                n, d = (torch.from_numpy(c.astype(np.int64)).to(DEV) for c in nd.T)
-                f1[b, n, d] = torch.from_numpy(np.where(sg1 > 0, 1.0, 0.1)).float().to(DEV)
-        return z1r * f1
+                n_, d_ = (torch.from_numpy(c.astype(np.int64)).to(DEV) for c in nd.T)
+                out_b[b, n_, d_] = torch.from_numpy(np.where(sg1 > 0, 1.0, -1.0)).float().to(DEV)
+                self.replayed[1] += len(nd)
+        self.calls += 1
+        return am, out_b, s0
 
 
-def _run_models(g, override=None, amax_override=None):
+def _run_models(g, override=None, decisions=None):
     """Teacher (eval) + student (train) forward, multiScaleLoss, KD loss and its backward on
     the fixture's pair (B=1), with knn_point optionally routed through `override` and the
-    student's cost-volume max routing through `amax_override`."""
+    student's cost-volume decisions through `decisions` (set_cv_decisions)."""
     import loss_functions as L
     import pointconv_util as P
     from models_bid_lighttoken_res import PointConvBidirection as Student
     from models_bid_pointconv import PointConvBidirection as Teacher
     pos1, pos2, flow = _t(g["pos1"]), _t(g["pos2"]), _t(g["flow"])
     prev = P.set_knn_override(override) if override is not None else None
-    prev_a = P.set_amax_override(amax_override)
-    prev_c = P.set_cv_override(getattr(amax_override, "cv", None))
+    prev_d = P.set_cv_decisions(decisions)
     try:
         teacher = load_synthetic(Teacher(), seed=1).to(DEV).eval()
         student = load_synthetic(Student(), seed=2).to(DEV).train()
@@ -379,8 +330,7 @@ def _run_models(g, override=None, amax_override=None):
     finally:
         if override is not None:
             P.set_knn_override(prev)
-        P.set_amax_override(prev_a)
-        P.set_cv_override(prev_c)
+        P.set_cv_decisions(prev_d)
     epe_s = torch.norm(flows[0].permute(0, 2, 1) - flow, dim=2).mean()
     epe_t = torch.norm(t_out[0][0].permute(0, 2, 1) - flow, dim=2).mean()
     return dict(t=t_out, s=s_out, msl=msl, kd=kd, epe_s=epe_s, epe_t=epe_t, student=student)
@@ -475,15 +425,17 @@ def test_model_matches_reference_with_reference_neighbours(golden, n):
     routing = _CvReplay(g64)
     r2 = _run_models(g, _KnnReplay(g), routing)
     assert routing.pos == len(routing.recs)  # every max of the student was replayed
+    assert routing.calls == 8, routing.calls  # 4 levels x (both directions + refinement)
     # N=2048: 1e-5 per parameter (measured round 2: 9e-7).  N=8192: the level-0 cost-volume
     # chain's gradient sums cancel heavily (the fp32 reference itself is off from float64 by
     # up to 1.1e-4 there): the build's worst may not exceed twice the reference's worst
     tol = 1e-5 if n == 2048 else max(1e-5, 2 * max(ref32.values()))
     worst = _check_grads_vs_f64(r2["student"], g, g64, tol)
-    print(f"N={n}: gradient error vs float64 with its max routing and LeakyReLU near-ties "
-          f"{worst:.2e} (bound {tol:.2e}; calls replayed in torch for a near-tie: "
-          f"{routing.replayed}); with the build's own routing ({routing.changed} max choices "
-          f"differ: {routing.per_call}) {max(own.values()):.2e}; fp32 reference "
+    print(f"N={n}: gradient error vs float64, HIP cost-volume kernels on all {routing.calls} "
+          f"calls with the float64 max routing and LeakyReLU near-tie decisions replayed "
+          f"({routing.replayed[0]} z0 / {routing.replayed[1]} z1) {worst:.2e} (bound {tol:.2e}); "
+          f"with the build's own routing ({routing.changed} max choices differ: "
+          f"{routing.per_call}) {max(own.values()):.2e}; fp32 reference "
           f"{max(ref32.values()):.2e}")
 
 
@@ -714,14 +666,16 @@ def test_kd_step_matches_reference(golden):
     before = {n: p.detach().clone() for n, p in student.named_parameters()}
     prev = P.set_knn_override(_KnnReplay(g))
     routing = _CvReplay(g64)
-    prev_a, prev_c = P.set_amax_override(routing), P.set_cv_override(routing.cv)
+    prev_d = P.set_cv_decisions(routing)
     try:
         loss = KDTrainStep(teacher, student, opt)(_t(g["pos1"]), _t(g["pos2"]), _t(g["flow"]))
     finally:
         P.set_knn_override(prev)
-        P.set_amax_override(prev_a)
-        P.set_cv_override(prev_c)
+        P.set_cv_decisions(prev_d)
     assert routing.pos == len(routing.recs)  # every max of the student was replayed
+    assert routing.calls == 8, routing.calls  # every call on the HIP kernels
+    print(f"KD step: gradients vs float64 with the HIP cost volume on all {routing.calls} calls "
+          f"({routing.replayed[0]} z0 / {routing.replayed[1]} z1 decisions replayed)")
     _close(loss, g["kd"], name="KD loss")
 
     class _View:  # the recorded gradients, shaped like the module for _check_grads_vs_f64

@@ -141,7 +141,6 @@ TORCH_OPS = {
     "three_interpolate_grad_csr": "kdpc_three_interpolate_grad_csr",
     "cost_volume_fwd": "kdpc_cost_volume_fwd", "cost_volume_bwd": "kdpc_cost_volume_bwd",
     "cost_volume_bwd_csr": "kdpc_cost_volume_bwd_csr", "csr_rank": "kdpc_csr_rank",
-    "cost_volume_bwd_pull": "kdpc_cost_volume_bwd_pull",
     "cost_volume_wide_h0": "kdpc_cost_volume_wide_h0",
     "cost_volume_wide_max": "kdpc_cost_volume_wide_max",
     "cost_volume_wide_max_bwd": "kdpc_cost_volume_wide_max_bwd",

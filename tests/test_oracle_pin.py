@@ -53,7 +53,7 @@ def test_layer_oracle_matches_reference(golden):
     _close(M.PointWarping()(x1, x2, flow), g["warp_out"])
 
 
-@pytest.mark.parametrize("name", ["fe32", "fe64", "fe128", "pcf"])
+@pytest.mark.parametrize("name", ["fe32", "fe64", "fe128", "fe256", "pcf"])
 def test_flow_layer_oracle_matches_reference(golden, name):
     """FlowEmbeddingLayer / PointConvFlow restatements vs the reference (B=2, N=512): output
     and every input / parameter gradient of sum(out * weight)."""
@@ -62,8 +62,9 @@ def test_flow_layer_oracle_matches_reference(golden, name):
     make = {"fe32": lambda: M.FlowEmbeddingLayer(32, 64, [32, 32]),
             "fe64": lambda: M.FlowEmbeddingLayer(32, 64, [64, 64]),
             "fe128": lambda: M.FlowEmbeddingLayer(16, 64, [128, 128]),
+            "fe256": lambda: M.FlowEmbeddingLayer(16, 64, [256, 256]),
             "pcf": lambda: M.PointConvFlow(16, 64 + 64 + 3, [64, 64])}[name]
-    seed = {"fe32": 51, "fe64": 52, "fe128": 53, "pcf": 54}[name]
+    seed = {"fe32": 51, "fe64": 52, "fe128": 53, "fe256": 55, "pcf": 54}[name]
     layer = load_synthetic(make(), seed=seed)
     x1 = torch.from_numpy(g["x1"].transpose(0, 2, 1).copy()).permute(0, 2, 1)
     x2 = torch.from_numpy(g["x2"].transpose(0, 2, 1).copy()).permute(0, 2, 1)

@@ -73,34 +73,6 @@ def main():
         t_ranked = timeit(ranked, a.iters)
         res = {"plain_bwd_plus_sums_us": round(t_plain, 1), "plain_bwd_us": round(t_bwd, 1),
                "ranked_us": round(t_ranked, 1), "bit_identical": same}
-        if K.cost_volume_bwd_pull_supported(di, do, Kn):
-            def pull():
-                return K.cost_volume_bwd_pull(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout)
-            q = pull()
-            res["pull_us"] = round(timeit(pull, a.iters), 1)
-            res["pull_max_rel_dp2"] = ((q[1] - r2[1]).abs().max() / r2[1].abs().max()).item()
-        # batch chunks (A/B): each chunk's rows written and summed while they may still sit
-        # in the memory-side cache (a chunk of 4 clouds at cross0: 134 MB of rows)
-        for nch in (2, 4, 8):
-            if B % nch:
-                continue
-            cb = B // nch
-            sl = [slice(i * cb, (i + 1) * cb) for i in range(nch)]
-            args = [[t[s_].contiguous() for t in (x1, x2, idx, p1, p2)] + [wpos, bpos, w1] +
-                    [out[s_].contiguous(), amax[s_].contiguous(), gout[s_].contiguous()] for s_ in sl]
-            csrs = [K.csr_rank_of(a[2], N2) for a in args]
-
-            def plain_chunks():
-                for a, c in zip(args, csrs):
-                    dp1, rows, dx1, drows, dpar = K.cost_volume_bwd(*a)
-                    K.group_rows_grad(rows.view(cb, N1 * Kn, di), c, cb, N2, di)
-                    K.group_rows_grad(drows.view(cb, N1 * Kn, 3), c, cb, N2, 3)
-
-            def ranked_chunks():
-                for a in args:
-                    K.cost_volume_bwd_csr(*a)
-            res[f"plain_chunks{nch}_us"] = round(timeit(plain_chunks, a.iters), 1)
-            res[f"ranked_chunks{nch}_us"] = round(timeit(ranked_chunks, a.iters), 1)
         print(name, res, flush=True)
 
 

@@ -1,8 +1,7 @@
 """Wide cost volume (D in {128, 256}, one-kernel MFMA path) at the model's cross2 / cross3
 calls (B=16 pair batch, K=32): forward and backward (with the CSR sums) per call, HIP events.
-Run once per KDPC_CVW_WGS value (read once per process).
 
-    KDPC_CVW_WGS=1024 python tools/bench_cv_wide.py
+    python tools/bench_cv_wide.py
 """
 import os
 import sys
@@ -48,7 +47,7 @@ def main():
         t_f = timeit(lambda: K.cost_volume_fwd(x1, x2, idx, p1, p2, wpos, bpos, w1, b1))
         t_b = timeit(lambda: K.cost_volume_bwd_csr(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax,
                                                    gout))
-        print(name, "wgs", os.environ.get("KDPC_CVW_WGS", "512"), {"fwd_us": round(t_f, 1),
+        print(name, {"fwd_us": round(t_f, 1),
               "bwd_csr_us": round(t_b, 1), "checksum": float(out.double().sum())}, flush=True)
 
 

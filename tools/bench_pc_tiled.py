@@ -61,7 +61,7 @@ def main():
                                                    weight=False), a.iters)
         bias = torch.randn(o, generator=g).to(DEV)
         f_u = timeit(lambda: K.pointconv_fwd(xyz, xyz, feats, idx, wt, wl, bias), a.iters)
-        f_t = timeit(lambda: K.pointconv_fwd_tiled(xyz, xyz, feats, idx, wt, wl, bias, tp),
+        f_t = timeit(lambda: K.pointconv_fwd_tiled(xyz, xyz, feats, idx, wt, wl, bias, tp.trow),
                      a.iters)
         print(name, {"fwd_untiled_us": round(f_u, 1), "fwd_tiled_us": round(f_t, 1)},
               flush=True)
