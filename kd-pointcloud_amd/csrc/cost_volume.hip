@@ -199,6 +199,14 @@ void cost_volume_fwd_kernel(
 // Row-per-lane (direction gradients): lane l32 = neighbour row, the two halves split the
 // channels.  D_IN = 32: the halves of L split the rows and the dW1 rows, nothing idles.
 //
+// D_IN = 64 runs two waves per query (round 5), each on one 32-channel half of the rows: h0,
+// dh0 = M W1[:, half], dz0, the dP1 / dP2 / dWpos / dbpos / dW1 columns of the half are
+// independent of the other half; only d(dir_r) = Wpos^T dz0[r] sums over both, so the second
+// wave hands its partial to the first through LDS (one barrier per query; the two waves of a
+// query are consecutive waves of the workgroup and walk the same queries in lockstep).  With
+// the per-wave state of a 32-channel kernel it runs at 2 waves per SIMD instead of 1 (one
+// wave holding all 64 channels needed 465 registers).
+//
 // OVR (test seam, never the training path): slope0 (B,N1,K,D_IN) u8 overrides the first
 // LeakyReLU's derivative per (query, neighbour, channel): 1 -> slope 1, 2 -> slope 0.1, 0 -> the
 // sign of the recomputed h0.  The gradient parity tests replay a float64 reference run's
@@ -217,12 +225,14 @@ void cost_volume_bwd_kernel(
     float* __restrict__ dp1, float* __restrict__ dp2_rows, float* __restrict__ dx1,
     float* __restrict__ ddir_rows, const int* __restrict__ rank, float* __restrict__ rows,
     float* __restrict__ slab) {
-  constexpr int LD = D_IN + 1;            // odd row stride: row-per-lane reads hit 32 banks
-  constexpr int RPP = 64 / D_IN;          // layout-L rows per pass
+  constexpr int CS = D_IN == 64 ? 2 : 1;  // waves per query (channel halves)
+  constexpr int DL = D_IN / CS;           // channels of one wave
+  constexpr int LD = DL + 1;              // odd row stride: row-per-lane reads hit 32 banks
+  constexpr int RPP = 64 / DL;            // layout-L rows per pass
   constexpr int RT = kRows / RPP;         // layout-L passes
-  constexpr int TI = D_IN / 32;           // 32-column tiles of dh0
+  constexpr int TI = DL / 32;             // 32-column tiles of dh0
   constexpr int DPL = RPP == 2 ? D_OUT / 2 : D_OUT;  // dW1 rows per lane
-  constexpr int CPH = D_IN / 2;           // channels per half in the row-per-lane pass
+  constexpr int CPH = DL / 2;             // channels per half in the row-per-lane pass
   constexpr int SLAB = D_OUT * D_IN + D_OUT + 4 * D_IN;
   constexpr int TILE = kRows * LD;
   constexpr int PER_WAVE = TILE + 4 * kRows + 2 * D_OUT;  // h0/dz0, directions, (g', argmax)
@@ -230,9 +240,14 @@ void cost_volume_bwd_kernel(
   // LEAN (the 3 / 4 waves-per-SIMD builds): W1's B fragments read from LDS at each MFMA
   // instead of held in registers, and no cross-query prefetch (a query's loads are issued at
   // the top of its iteration; the other resident waves cover their latency)
-  constexpr bool LEAN = WPE >= 3;
+  // (the two-waves-per-query D_IN = 64 build is LEAN too: prefetching, it spilled at 2 waves)
+  constexpr bool LEAN = WPE >= 3 || CS > 1;
+  constexpr bool W1L = LEAN;
   constexpr int W1_AT = SHARED + kWaves * PER_WAVE;
-  constexpr int BODY = W1_AT + (LEAN ? D_OUT * D_IN : 0);
+  constexpr int XCH_AT = W1_AT + (W1L ? D_OUT * D_IN : 0);
+  // CS = 2: the second wave's d(dir) partials, [iteration parity][query stream][row] float4
+  constexpr int XCH = CS > 1 ? 2 * (kWaves / CS) * kRows * 4 : 0;
+  constexpr int BODY = XCH_AT + XCH;
   constexpr int LDS_FLOATS = BODY > SLAB ? BODY : SLAB;
   static_assert(TILE % 4 == 0 && PER_WAVE % 4 == 0, "16-byte aligned LDS tables");
   __shared__ __attribute__((aligned(16))) float lds_all[LDS_FLOATS];
@@ -240,7 +255,10 @@ void cost_volume_bwd_kernel(
   const int wave = threadIdx.x >> 6;
   const int lane = lane_id();
   const int half = lane >> 5, l32 = lane & 31;
-  const int c = lane % D_IN, sub = lane / D_IN;
+  const int c = lane % DL, sub = lane / DL;
+  const int hc = CS > 1 ? (wave & 1) : 0;      // channel half of this wave
+  const int qw = CS > 1 ? (wave >> 1) : wave;  // query stream of this wave in the workgroup
+  const int cg = hc * DL + c;                  // layout-L channel of the row
   const int dl = lane % D_OUT;
   float4* wposT = reinterpret_cast<float4*>(lds_all);
   float* T = lds_all + SHARED + wave * PER_WAVE;
@@ -249,19 +267,20 @@ void cost_volume_bwd_kernel(
   for (int e = threadIdx.x; e < D_IN; e += blockDim.x)
     wposT[e] = make_float4(wpos[e * 3 + 0], wpos[e * 3 + 1], wpos[e * 3 + 2], 0.f);
   float* w1s = lds_all + W1_AT;
-  if constexpr (LEAN)
+  if constexpr (W1L)
     for (int e = threadIdx.x; e < D_OUT * D_IN; e += blockDim.x) w1s[e] = w1[e];
   __syncthreads();
 
   // B fragments of W1 for dh0 = M W1 (inner index d): lane supplies W1[2s + half][32t + l32]
-  float bwt[TI][LEAN ? 1 : D_OUT / 2];
-  if constexpr (!LEAN) {
+  float bwt[TI][W1L ? 1 : D_OUT / 2];
+  if constexpr (!W1L) {
 #pragma unroll
     for (int t = 0; t < TI; ++t)
 #pragma unroll
-      for (int s2 = 0; s2 < D_OUT / 2; ++s2) bwt[t][s2] = w1[(2 * s2 + half) * D_IN + 32 * t + l32];
+      for (int s2 = 0; s2 < D_OUT / 2; ++s2)
+        bwt[t][s2] = w1[(2 * s2 + half) * D_IN + hc * DL + 32 * t + l32];
   }
-  const float w0 = wpos[c * 3 + 0], wy = wpos[c * 3 + 1], wz = wpos[c * 3 + 2], bp = bpos[c];
+  const float w0 = wpos[cg * 3 + 0], wy = wpos[cg * 3 + 1], wz = wpos[cg * 3 + 2], bp = bpos[cg];
 
   const float* x1b = x1 + (long long)b * n1 * 3;
   const __amdgpu_buffer_rsrc_t x2r = rsrc_of(x2 + (long long)b * n2 * 3, (long long)n2 * 12);
@@ -283,14 +302,14 @@ void cost_volume_bwd_kernel(
   const __amdgpu_buffer_rsrc_t rkr = rsrc_of(ranked ? rank + (long long)b * n1 * k : idx,
                                              ranked ? (long long)n1 * k * 4 : 0);
 
-  // parameter-gradient accumulators: gw1[i] = dW1[d0 + i][c]; gwp / gbp per (c, row parity)
+  // parameter-gradient accumulators: gw1[i] = dW1[d0 + i][cg]; gwp / gbp per (cg, row parity)
   const int d0 = RPP == 2 ? sub * (D_OUT / 2) : 0;
   float gw1[DPL];
 #pragma unroll
   for (int i = 0; i < DPL; ++i) gw1[i] = 0.f;
   float gb1 = 0.f, gwp0 = 0.f, gwp1 = 0.f, gwp2 = 0.f, gbp = 0.f;
 
-  const int q0 = (blockIdx.x * kWaves + wave) * queries_per_wave;
+  const int q0 = (blockIdx.x * (kWaves / CS) + qw) * queries_per_wave;
   const int q1 = min(n1, q0 + queries_per_wave);
   // prefetched state of the next query
   int jn = 0;                 // lane r: its neighbour index (query n + 1 during query n)
@@ -319,9 +338,9 @@ void cost_volume_bwd_kernel(
         const int ja = __builtin_amdgcn_readlane(jn, 2 * i), jb = __builtin_amdgcn_readlane(jn, 2 * i + 1);
         j = sub ? jb : ja;
       }
-      pv[i] = bload(p2r, ((unsigned)j * D_IN + c) * 4u);
+      pv[i] = bload(p2r, ((unsigned)j * D_IN + cg) * 4u);
     }
-    p1v = bload(p1r, ((unsigned)n * D_IN + c) * 4u);
+    p1v = bload(p1r, ((unsigned)n * D_IN + cg) * 4u);
     const unsigned oo = (unsigned)n * D_OUT + dl;
     outv = bload(outr, oo * 4u);
     doutv = bload(dor, oo * 4u);
@@ -333,13 +352,21 @@ void cost_volume_bwd_kernel(
     load_idx(q0 + 1);
   }
 
-  for (int n = q0; n < q1; ++n) {
+  // CS = 2: every wave of the workgroup walks queries_per_wave iterations (the exchange
+  // barrier), idle past its stream's end
+  const int nit = CS > 1 ? queries_per_wave : q1 - q0;
+  for (int it = 0; it < nit; ++it) {
+    const int n = q0 + it;
+    const bool act = CS == 1 || n < q1;  // wave-uniform
+    float g0 = 0.f, g1 = 0.f, g2 = 0.f;  // d(dir) of the wave's lane-row (direction pass)
+    int rkv = -1;
+    if (act) {
     if constexpr (LEAN) {
       issue(n);
       load_idx(n + 1);
     }
     // lane r: the slot of row r (used by the row passes, after this query's MFMAs)
-    const int rkv = (int)__builtin_amdgcn_raw_buffer_load_b32(
+    rkv = (int)__builtin_amdgcn_raw_buffer_load_b32(
         rkr, (int)(lane < k ? ((unsigned)n * (unsigned)k + lane) * 4u : kOOB), 0, 0);
     // ---- h0 of query n into T (layout L), directions into dirT, (g', argmax) into gdam
     const float qx = x1b[n * 3 + 0], qy = x1b[n * 3 + 1], qz = x1b[n * 3 + 2];
@@ -375,7 +402,7 @@ void cost_volume_bwd_kernel(
 #pragma unroll
       for (int t = 0; t < TI; ++t)
         dacc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(
-            a, LEAN ? w1s[(2 * s2 + half) * D_IN + 32 * t + l32] : bwt[t][LEAN ? 0 : s2],
+            a, W1L ? w1s[(2 * s2 + half) * D_IN + hc * DL + 32 * t + l32] : bwt[t][W1L ? 0 : s2],
             dacc[t], 0, 0, 0);
     }
     // ---- dW1[d, c] += g'[d] h0[am[d], c] (reads h0 before dz0 overwrites it)
@@ -385,7 +412,7 @@ void cost_volume_bwd_kernel(
       gw1[i] = __builtin_fmaf(ga.x, T[__float_as_int(ga.y) * LD + c], gw1[i]);
       if (i % 8 == 7) __builtin_amdgcn_sched_barrier(0);  // bound the hoisted LDS reads
     }
-    if (lane < D_OUT) gb1 += gd_l;
+    if (lane < D_OUT && hc == 0) gb1 += gd_l;
     __builtin_amdgcn_sched_barrier(0);
     // ---- dz0 = dh0 * LeakyReLU'(h0), in place (accumulator layout)
 #pragma unroll
@@ -398,7 +425,7 @@ void cost_volume_bwd_kernel(
         float sl = hv > 0.f ? 1.f : kSlope;
         if constexpr (OVR) {  // rows >= k read past the query's block or 0: dacc is 0 there
           const unsigned o = __builtin_amdgcn_raw_buffer_load_b8(
-              s0r, (int)((((unsigned)n * (unsigned)k + row) * D_IN + 32 * t + l32)), 0, 0);
+              s0r, (int)((((unsigned)n * (unsigned)k + row) * D_IN + hc * DL + 32 * t + l32)), 0, 0);
           sl = o == 1u ? 1.f : (o == 2u ? kSlope : sl);
         }
         T[a] = dacc[t][e] * sl;
@@ -407,7 +434,7 @@ void cost_volume_bwd_kernel(
     __builtin_amdgcn_sched_barrier(0);
     // ---- row pass (layout L): dP2 rows out; dP1, dWpos, dbpos channel sums
     float dp1_acc = 0.f;
-    float* dp2n = dp2_rows + (((long long)b * n1 + n) * k) * D_IN + c;
+    float* dp2n = dp2_rows + (((long long)b * n1 + n) * k) * D_IN + cg;
 #pragma unroll 4
     for (int r0 = 0; r0 < k; r0 += RPP) {  // rows >= k are zero
       const int r = r0 + sub;
@@ -417,7 +444,7 @@ void cost_volume_bwd_kernel(
       if (ranked) {
         const int sa = __builtin_amdgcn_readlane(rkv, r0);
         const int slot = RPP == 2 ? (sub ? __builtin_amdgcn_readlane(rkv, r0 + 1) : sa) : sa;
-        if (slot >= 0) rows[(long long)slot * D_IN + c] = v;
+        if (slot >= 0) rows[(long long)slot * D_IN + cg] = v;
       } else if (dp2_rows) {
         dp2n[r * D_IN] = v;
       }
@@ -428,14 +455,13 @@ void cost_volume_bwd_kernel(
       gbp = __fadd_rn(gbp, v);
     }
     if (RPP == 2) dp1_acc = __fadd_rn(dp1_acc, __shfl_xor(dp1_acc, 32, kWave));
-    if (sub == 0) dp1[((long long)b * n1 + n) * D_IN + c] = dp1_acc;
+    if (sub == 0) dp1[((long long)b * n1 + n) * D_IN + cg] = dp1_acc;
     // ---- d(dir_r) = Wpos^T dz0[r] (lane l32 = row, halves split the channels)
-    float g0 = 0.f, g1 = 0.f, g2 = 0.f;
 #pragma unroll
     for (int i = 0; i < CPH; ++i) {
       const int cc = half * CPH + i;
       const float v = T[l32 * LD + cc];
-      const float4 wp = wposT[cc];
+      const float4 wp = wposT[hc * DL + cc];
       g0 = __builtin_fmaf(wp.x, v, g0);
       g1 = __builtin_fmaf(wp.y, v, g1);
       g2 = __builtin_fmaf(wp.z, v, g2);
@@ -444,6 +470,22 @@ void cost_volume_bwd_kernel(
     g0 = __fadd_rn(g0, __shfl_xor(g0, 32, kWave));
     g1 = __fadd_rn(g1, __shfl_xor(g1, 32, kWave));
     g2 = __fadd_rn(g2, __shfl_xor(g2, 32, kWave));
+    }  // act
+    if constexpr (CS > 1) {  // the second channel half's d(dir) partials -> the first wave
+      float4* xch = reinterpret_cast<float4*>(lds_all + XCH_AT) +
+                    ((it & 1) * (kWaves / CS) + qw) * kRows;
+      if (act && hc == 1 && lane < kRows) xch[lane] = make_float4(g0, g1, g2, 0.f);
+      // LDS writes done, then the barrier; no vmcnt drain (the next query's loads and this
+      // query's row stores stay in flight).  Parity-double-buffered: no second barrier.
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (act && hc == 0) {
+        const float4 o = xch[l32];
+        g0 = __fadd_rn(g0, o.x);
+        g1 = __fadd_rn(g1, o.y);
+        g2 = __fadd_rn(g2, o.z);
+      }
+    }
+    if (act && hc == 0) {
     const bool row = lane < k;  // lanes >= 32 never (k <= 32)
     if (row && ranked) {
       if (rkv >= 0)
@@ -468,6 +510,7 @@ void cost_volume_bwd_kernel(
       o[1] = -s1;
       o[2] = -s2;
     }
+    }  // act && hc == 0
   }
   // ---- workgroup partials: waves add their accumulators into one LDS slab in wave order
   if (RPP == 2) {  // fold the row-parity halves of the channel sums
@@ -480,21 +523,22 @@ void cost_volume_bwd_kernel(
   float* rw = lds_all;
   for (int w = 0; w < kWaves; ++w) {
     if (wave == w) {
+      const bool first = qw == 0;  // the first wave of this channel half's columns
 #pragma unroll
       for (int i = 0; i < DPL; ++i) {
-        float* e = rw + (d0 + i) * D_IN + c;
-        *e = w ? __fadd_rn(*e, gw1[i]) : gw1[i];
+        float* e = rw + (d0 + i) * D_IN + cg;
+        *e = first ? gw1[i] : __fadd_rn(*e, gw1[i]);
       }
-      if (lane < D_OUT) {
+      if (lane < D_OUT && hc == 0) {
         float* e = rw + D_OUT * D_IN + lane;
-        *e = w ? __fadd_rn(*e, gb1) : gb1;
+        *e = first ? gb1 : __fadd_rn(*e, gb1);
       }
       if (sub == 0) {
         const float v4[4] = {gwp0, gwp1, gwp2, gbp};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          float* e = rw + D_OUT * D_IN + D_OUT + q * D_IN + c;
-          *e = w ? __fadd_rn(*e, v4[q]) : v4[q];
+          float* e = rw + D_OUT * D_IN + D_OUT + q * D_IN + cg;
+          *e = first ? v4[q] : __fadd_rn(*e, v4[q]);
         }
       }
     }
@@ -530,13 +574,17 @@ int bwd_waves_resident() {
 
 // waves per SIMD the backward is compiled for: D_IN = D_OUT = 32 -> 3 (the LEAN build, 168
 // VGPRs, no spill: W1 fragments from LDS, no cross-query prefetch; round 4: cross0 621 -> 574
-// us with the CSR sums against the prefetching 2-wave build), (32, 64) -> 2, D_IN = 64 -> 1
+// us with the CSR sums against the prefetching 2-wave build), (32, 64) -> 2, D_IN = 64 -> 2
+// (two waves per query, one per channel half; round 5: was one wave per query at 1 per SIMD)
 template <int DI, int DO>
-constexpr int bwd_wpe() { return DI == 32 ? (DO == 32 ? 3 : 2) : 1; }
+constexpr int bwd_wpe() { return DI == 32 && DO == 32 ? 3 : 2; }
+template <int DI>
+constexpr int bwd_cs() { return DI == 64 ? 2 : 1; }  // waves per query
 
 template <int DI, int DO>
 inline int bwd_qpw(int b, int n1) {
-  return std::max(2, (int)divupll((long long)b * n1, bwd_waves_resident<DI, DO, bwd_wpe<DI, DO>()>()));
+  const long long streams = bwd_waves_resident<DI, DO, bwd_wpe<DI, DO>()>() / bwd_cs<DI>();
+  return std::max(2, (int)divupll((long long)b * n1, streams));
 }
 
 inline int bwd_qpw_of(int b, int n1, int din, int dout) {
@@ -566,7 +614,7 @@ hipError_t bwd_launch(int b, int n1, int n2, int k, const float* x1, const float
                       float* rows, float* slab, float* dparams, hipStream_t st) {
   constexpr int W = bwd_wpe<DI, DO>();
   const int qpw = bwd_qpw<DI, DO>(b, n1);
-  dim3 grid(divup(n1, kWaves * qpw), b);
+  dim3 grid(divup(n1, (kWaves / bwd_cs<DI>()) * qpw), b);
   if (s0)
     hipLaunchKernelGGL((cost_volume_bwd_kernel<DI, DO, W, true>), grid, dim3(256), 0, st, n1, n2,
                        k, qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, s0, dout, dp1,
@@ -754,7 +802,8 @@ KDPC_API size_t kdpc_cost_volume_bwd_workspace_bytes(int b, int n1, int din, int
   if (b <= 0 || n1 <= 0 || !supported(din, dout, 1)) return 0;
   if (!narrow(din, dout, 1))
     return cost_volume_wide_fused_bwd_workspace_floats(b, n1, din) * sizeof(float);
-  const long long nslabs = (long long)divup(n1, kWaves * bwd_qpw_of(b, n1, din, dout)) * b;
+  const long long nslabs =
+      (long long)divup(n1, (kWaves / (din == 64 ? 2 : 1)) * bwd_qpw_of(b, n1, din, dout)) * b;
   const int len = slab_len(din, dout);
   return (size_t)(nslabs * len + colsum_scratch_floats((int)nslabs, len)) * sizeof(float);
 }
