@@ -35,6 +35,7 @@ using namespace kdpc;
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr float kSlope = 0.1f;
 constexpr int kRows = 32;        // MFMA M-tile = neighbour rows of one query
@@ -56,7 +57,7 @@ constexpr unsigned kOOB = 0x80000000u;  // out-of-range byte offset: loads read 
 template <int D_IN, int D_OUT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
 void cost_volume_fwd_kernel(
-    int n1, int n2, int k, int queries_per_wave, const float* __restrict__ x1,
+    int nb, int gx, int n1, int n2, int k, int queries_per_wave, const float* __restrict__ x1,
     const float* __restrict__ x2, const int* __restrict__ idx, const float* __restrict__ p1,
     const float* __restrict__ p2, const float* __restrict__ wpos, const float* __restrict__ bpos,
     const float* __restrict__ w1, const float* __restrict__ b1, float* __restrict__ out,
@@ -67,7 +68,11 @@ void cost_volume_fwd_kernel(
   constexpr int RT = kRows / RPP;
   __shared__ float lds[kWaves][kRows * LD];
   __shared__ float4 dir_lds[kWaves][kRows];  // the query's neighbour directions (lane r)
-  const int b = blockIdx.y;
+  // XCD-aware virtual blocks (as cost_volume_bwd_kernel): each XCD gathers from ~B/8 clouds
+  const int nblk = nb * gx, per = (nblk + 7) >> 3;
+  const int pblk = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  if (pblk >= nblk) return;
+  const int b = pblk / gx, bx = pblk - b * gx;
   const int wave = threadIdx.x >> 6;
   const int lane = lane_id();
   const int c = lane % D_IN, sub = lane / D_IN;
@@ -80,7 +85,7 @@ void cost_volume_fwd_kernel(
   const __amdgpu_buffer_rsrc_t p2r = rsrc_of(p2 + (long long)b * n2 * D_IN, (long long)n2 * D_IN * 4);
   float* outb = out + (long long)b * n1 * D_OUT;
   unsigned char* amb = amax + (long long)b * n1 * D_OUT;
-  const int q0 = (blockIdx.x * kWaves + wave) * queries_per_wave;
+  const int q0 = (bx * kWaves + wave) * queries_per_wave;
   const int q1 = min(n1, q0 + queries_per_wave);
   // B fragments of W1 (lane l: W1[t*32 + (l&31)][2s + (l>>5)]), reused for every query
   float bw[TILES][D_IN / 2];
@@ -188,98 +193,94 @@ void cost_volume_fwd_kernel(
 }
 
 // ------------------------------------------------------------------------------ backward
-// One wave per query, queries walked in a software pipeline: the next query's loads (its
-// neighbour indices one query further ahead, then its P2 rows, directions, P1 row, output,
-// output gradient and argmax) are issued as soon as the current query's h0 is built, so
-// they land under the current query's MFMAs and channel loops.  One LDS tile per wave
-// holds h0 and is overwritten in place by dz0 (h0 is last read by the dW1 update).
+// Per query n (K <= 32 neighbour rows): the max routes each output channel's gradient to one
+// neighbour row (amax), so dz1 has one nonzero per column; dh0 = dz1 W1; dz0 = dh0 *
+// LeakyReLU'(h0); dP1[n] = sum_k dz0, the dP2 / d(dir) rows per (n, k) (summed per reference
+// point through the kNN index's CSR: deterministic, no float atomics), dx1[n] = -sum_k d(dir),
+// and the parameter partials dW1, db1, dWpos, dbpos (per-workgroup slabs, summed in a fixed
+// order by colsum).
 //
-// Lane layouts.  L (gathers, row passes): lane = (sub, c), c = lane % D_IN, rows RPP*i + sub.
-// MFMA accumulator: lane (half, l32), tile t: column 32t + l32, rows (e&3) + 8(e>>2) + 4 half.
-// Row-per-lane (direction gradients): lane l32 = neighbour row, the two halves split the
-// channels.  D_IN = 32: the halves of L split the rows and the dW1 rows, nothing idles.
-//
-// D_IN = 64 runs two waves per query (round 5), each on one 32-channel half of the rows: h0,
-// dh0 = M W1[:, half], dz0, the dP1 / dP2 / dWpos / dbpos / dW1 columns of the half are
-// independent of the other half; only d(dir_r) = Wpos^T dz0[r] sums over both, so the second
-// wave hands its partial to the first through LDS (one barrier per query; the two waves of a
-// query are consecutive waves of the workgroup and walk the same queries in lockstep).  With
-// the per-wave state of a 32-channel kernel it runs at 2 waves per SIMD instead of 1 (one
-// wave holding all 64 channels needed 465 registers).
+// Dataflow (round 5; the round-1..4 kernel moved h0 / dz0 through LDS three times per query
+// and spent ~770 VALU / 170 LDS / 320 scalar instructions per query at D = 32).  A wave owns
+// one query and 32 channels; D_IN = 64 runs two waves per query, each on one 32-channel half
+// of the rows (h0, dh0 = M W1[:, half], dz0 and the dP1 / dP2 / dWpos / dbpos / dW1 columns of
+// a half are independent of the other half; only d(dir_r) = Wpos^T dz0[r] sums over both, so
+// the second wave hands its partial to the first through LDS: one barrier per query, the two
+// waves walk the same queries in lockstep) -- 2 waves per SIMD where one wave holding all 64
+// channels needed 465 registers (1 per SIMD).  Lane (h, c), c = l32, holds
+// column c of the 32 neighbour rows R_h(e) = (e & 3) + 8 (e >> 2) + 4 h, e < 16 -- the rows of
+// the accumulator element e -- so every per-element step runs in registers:
+//   h0[e]  gathered and built straight into that layout (16 registers),
+//   dh0    = M W1 on the matrix cores (accumulator layout, as before),
+//   dW1   += M^T h0 on the matrix cores: step s pairs rows R_0(s) / R_1(s), A = the one-hot
+//            routing of output o = l32 (g'[o] where am[o] is the step's row), B = h0[s] of the
+//            lane -- the same fma chain as the VALU update it replaces, no LDS,
+//   dz0[e] = dh0[e] * LeakyReLU'(h0[e]), then the row pass (dP2 rows at their CSR slots, dP1,
+//            dWpos) over the lane's 16 registers.
+// Only the direction gradient d(dir_r) = Wpos^T dz0[r] sums across lanes: dz0 goes through one
+// LDS tile into the row-per-lane layout.
 //
 // OVR (test seam, never the training path): slope0 (B,N1,K,D_IN) u8 overrides the first
 // LeakyReLU's derivative per (query, neighbour, channel): 1 -> slope 1, 2 -> slope 0.1, 0 -> the
 // sign of the recomputed h0.  The gradient parity tests replay a float64 reference run's
 // decisions at near-ties through it (tests/test_gpu_model.py::_CvReplay); the second LeakyReLU
 // reads its decision from the sign of `out` only, so those are replayed through `out`.
-
-template <int D_IN, int D_OUT, int WPE, bool OVR>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
+template <int D_IN, int D_OUT, bool OVR>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 void cost_volume_bwd_kernel(
-    int n1, int n2, int k, int queries_per_wave, const float* __restrict__ x1,
+    int nb, int gx, int n1, int n2, int k, int queries_per_wave, const float* __restrict__ x1,
     const float* __restrict__ x2, const int* __restrict__ idx, const float* __restrict__ p1,
     const float* __restrict__ p2, const float* __restrict__ wpos, const float* __restrict__ bpos,
     const float* __restrict__ w1, const float* __restrict__ out,
     const unsigned char* __restrict__ amax, const unsigned char* __restrict__ slope0,
-    const float* __restrict__ dout,
-    float* __restrict__ dp1, float* __restrict__ dp2_rows, float* __restrict__ dx1,
-    float* __restrict__ ddir_rows, const int* __restrict__ rank, float* __restrict__ rows,
+    const float* __restrict__ dout, float* __restrict__ dp1, float* __restrict__ dx1,
+    const int* __restrict__ rank, float* __restrict__ rows_out, float* __restrict__ dirs_out,
     float* __restrict__ slab) {
-  constexpr int CS = D_IN == 64 ? 2 : 1;  // waves per query (channel halves)
-  constexpr int DL = D_IN / CS;           // channels of one wave
-  constexpr int LD = DL + 1;              // odd row stride: row-per-lane reads hit 32 banks
-  constexpr int RPP = 64 / DL;            // layout-L rows per pass
-  constexpr int RT = kRows / RPP;         // layout-L passes
-  constexpr int TI = DL / 32;             // 32-column tiles of dh0
-  constexpr int DPL = RPP == 2 ? D_OUT / 2 : D_OUT;  // dW1 rows per lane
-  constexpr int CPH = DL / 2;             // channels per half in the row-per-lane pass
+  // rank != null (ranked): row (n, r) -> rows_out[rank[n, r]] (the CSR slots of idx over all
+  // batch elements), d(dir) -> dirs_out as float4 rows; rank == null (plain): rows_out[(b, n, r)]
+  // and dirs_out[(b, n, r)] as 3 floats; rows_out == null: no rows
+  constexpr int CS = D_IN / 32;           // waves per query (channel halves)
+  constexpr int OT = D_OUT / 32;          // 32-row blocks of dW1
+  constexpr int LD = 33;                  // dz0 tile stride: row-per-lane reads hit 32 banks
   constexpr int SLAB = D_OUT * D_IN + D_OUT + 4 * D_IN;
   constexpr int TILE = kRows * LD;
-  constexpr int PER_WAVE = TILE + 4 * kRows + 2 * D_OUT;  // h0/dz0, directions, (g', argmax)
+  constexpr int PER_WAVE = TILE + 4 * kRows + 2 * D_OUT;  // dz0, directions, (g', argmax)
   constexpr int SHARED = 4 * D_IN;                         // Wpos rows (x, y, z, 0)
-  // LEAN (the 3 / 4 waves-per-SIMD builds): W1's B fragments read from LDS at each MFMA
-  // instead of held in registers, and no cross-query prefetch (a query's loads are issued at
-  // the top of its iteration; the other resident waves cover their latency)
-  // (the two-waves-per-query D_IN = 64 build is LEAN too: prefetching, it spilled at 2 waves)
-  constexpr bool LEAN = WPE >= 3 || CS > 1;
-  constexpr bool W1L = LEAN;
-  constexpr int W1_AT = SHARED + kWaves * PER_WAVE;
-  constexpr int XCH_AT = W1_AT + (W1L ? D_OUT * D_IN : 0);
-  // CS = 2: the second wave's d(dir) partials, [iteration parity][query stream][row] float4
+  // dW1 on the VALU through the h0 tile (D_OUT = 32) or as M^T h0 on the matrix cores
+  // (D_OUT = 64: the VALU update's 32 accumulators and hoisted reads spilled at 2 waves/SIMD)
+  constexpr bool DW1_MFMA = D_OUT > 32;
+  constexpr int XCH_AT = SHARED + kWaves * PER_WAVE;
   constexpr int XCH = CS > 1 ? 2 * (kWaves / CS) * kRows * 4 : 0;
   constexpr int BODY = XCH_AT + XCH;
   constexpr int LDS_FLOATS = BODY > SLAB ? BODY : SLAB;
   static_assert(TILE % 4 == 0 && PER_WAVE % 4 == 0, "16-byte aligned LDS tables");
   __shared__ __attribute__((aligned(16))) float lds_all[LDS_FLOATS];
-  const int b = blockIdx.y;
+  // XCD-aware placement: the dispatcher deals workgroup L to XCD L % 8, so virtual block
+  // p = (L % 8) * per + L / 8 gives every XCD a contiguous run of (cloud, query chunk) blocks,
+  // i.e. ~B/8 whole clouds: their P2 tables (1-2 MB each) stay in that XCD's 4 MB L2 instead of
+  // every XCD gathering from every cloud.  Speed only: p alone decides the work and the slab.
+  const int nblk = nb * gx, per = (nblk + 7) >> 3;
+  const int pblk = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  if (pblk >= nblk) return;  // whole workgroup, before any barrier
+  const int b = pblk / gx, bx = pblk - b * gx;
   const int wave = threadIdx.x >> 6;
   const int lane = lane_id();
   const int half = lane >> 5, l32 = lane & 31;
-  const int c = lane % DL, sub = lane / DL;
   const int hc = CS > 1 ? (wave & 1) : 0;      // channel half of this wave
   const int qw = CS > 1 ? (wave >> 1) : wave;  // query stream of this wave in the workgroup
-  const int cg = hc * DL + c;                  // layout-L channel of the row
-  const int dl = lane % D_OUT;
+  const int cg = hc * 32 + l32;                // the lane's channel
   float4* wposT = reinterpret_cast<float4*>(lds_all);
   float* T = lds_all + SHARED + wave * PER_WAVE;
   float4* dirT = reinterpret_cast<float4*>(T + TILE);
   float2* gdam = reinterpret_cast<float2*>(T + TILE + 4 * kRows);
   for (int e = threadIdx.x; e < D_IN; e += blockDim.x)
     wposT[e] = make_float4(wpos[e * 3 + 0], wpos[e * 3 + 1], wpos[e * 3 + 2], 0.f);
-  float* w1s = lds_all + W1_AT;
-  if constexpr (W1L)
-    for (int e = threadIdx.x; e < D_OUT * D_IN; e += blockDim.x) w1s[e] = w1[e];
   __syncthreads();
 
-  // B fragments of W1 for dh0 = M W1 (inner index d): lane supplies W1[2s + half][32t + l32]
-  float bwt[TI][W1L ? 1 : D_OUT / 2];
-  if constexpr (!W1L) {
+  // B fragments of W1 for dh0 = M W1 (inner index o): lane supplies W1[2s + half][cg]
+  float bw[D_OUT / 2];
 #pragma unroll
-    for (int t = 0; t < TI; ++t)
-#pragma unroll
-      for (int s2 = 0; s2 < D_OUT / 2; ++s2)
-        bwt[t][s2] = w1[(2 * s2 + half) * D_IN + hc * DL + 32 * t + l32];
-  }
+  for (int s2 = 0; s2 < D_OUT / 2; ++s2) bw[s2] = w1[(2 * s2 + half) * D_IN + cg];
   const float w0 = wpos[cg * 3 + 0], wy = wpos[cg * 3 + 1], wz = wpos[cg * 3 + 2], bp = bpos[cg];
 
   const float* x1b = x1 + (long long)b * n1 * 3;
@@ -293,190 +294,202 @@ void cost_volume_bwd_kernel(
   const __amdgpu_buffer_rsrc_t amr = rsrc_of(amax + ob0, (long long)n1 * D_OUT);
   const __amdgpu_buffer_rsrc_t s0r =
       rsrc_of(OVR ? slope0 + (long long)b * n1 * k * D_IN : amax, OVR ? (long long)n1 * k * D_IN : 0);
-  // ranked rows (rank != null): row (n, r) goes to slot rank[n, r] of the CSR of idx, so the
-  // per-point sums read each segment contiguously (cv_rows_sum_kernel)
   const bool ranked = rank != nullptr;
-  // ranked rows: dP2 rows (P, D_IN) -- whole 128 / 256-byte lines -- then the d(dir) rows
-  // (P, 4) (round 3 interleaved them as (P, D_IN + 4): every 144-byte row straddled lines)
-  float* dirs = ranked ? rows + (long long)gridDim.y * n1 * k * D_IN : nullptr;
   const __amdgpu_buffer_rsrc_t rkr = rsrc_of(ranked ? rank + (long long)b * n1 * k : idx,
                                              ranked ? (long long)n1 * k * 4 : 0);
+  // per-neighbour rows through buffer stores over the whole batch (< 2^31 bytes, checked by
+  // the entry points), branch-free: a dropped row gets an out-of-range offset
+  const long long nrow_all = (long long)nb * n1 * k;
+  const __amdgpu_buffer_rsrc_t rowr = rsrc_of(rows_out, rows_out ? nrow_all * D_IN * 4 : 0);
+  const __amdgpu_buffer_rsrc_t dirr = rsrc_of(dirs_out, dirs_out ? nrow_all * (ranked ? 16 : 12) : 0);
+  const int nbase = b * n1;  // plain rows: (b, n, r) = ((nbase + n) k + r)
 
-  // parameter-gradient accumulators: gw1[i] = dW1[d0 + i][cg]; gwp / gbp per (cg, row parity)
-  const int d0 = RPP == 2 ? sub * (D_OUT / 2) : 0;
-  float gw1[DPL];
+  // parameter-gradient accumulators: dW1 -- VALU: gw1[i] = dW1[2 i + half][cg]; MFMA: block t,
+  // element e = dW1[32 t + R_h(e)][cg] -- and dWpos / dbpos of the lane's channel (half 0 and 1
+  // fold at the end)
+  float gw1[DW1_MFMA ? 1 : D_OUT / 2];
+  f32x16 gw[DW1_MFMA ? OT : 1];
+  if constexpr (DW1_MFMA) {
 #pragma unroll
-  for (int i = 0; i < DPL; ++i) gw1[i] = 0.f;
-  float gb1 = 0.f, gwp0 = 0.f, gwp1 = 0.f, gwp2 = 0.f, gbp = 0.f;
+    for (int t = 0; t < OT; ++t) gw[t] = f32x16{0};
+  } else {
+#pragma unroll
+    for (int i = 0; i < D_OUT / 2; ++i) gw1[i] = 0.f;
+  }
+  float gb1[OT];  // db1[32 t + l32]: sum of g' (the same add chain as the previous kernel)
+#pragma unroll
+  for (int t = 0; t < OT; ++t) gb1[t] = 0.f;
+  float gwp0 = 0.f, gwp1 = 0.f, gwp2 = 0.f, gbp = 0.f;
 
-  const int q0 = (blockIdx.x * (kWaves / CS) + qw) * queries_per_wave;
+  const int q0 = (bx * (kWaves / CS) + qw) * queries_per_wave;
   const int q1 = min(n1, q0 + queries_per_wave);
-  // prefetched state of the next query
-  int jn = 0;                 // lane r: its neighbour index (query n + 1 during query n)
-  float pv[RT];               // layout L: P2[j_r][c]
-  float xv0, xv1, xv2;        // lane r: x2[j_r]
-  float p1v, outv, doutv;
-  unsigned amv;
-  // No per-row masks on the load offsets (they would be hoisted out of the query loop as
-  // per-row registers): past-the-end offsets read 0 through the buffers' bounds, and the
-  // neighbour slots r >= k read some valid row (the next query's indices, or row 0) whose
-  // h0 row only ever meets zeros (no argmax points there; its dz0 row is dh0 = 0).
-  auto load_idx = [&](int n) {
-    jn = (int)__builtin_amdgcn_raw_buffer_load_b32(ixr, (int)(((unsigned)n * (unsigned)k + lane) * 4u), 0, 0);
-  };
+  // Software pipeline: query n+1's loads are issued right after query n's h0 is built, before
+  // its MFMAs and its row stores, so they land under this query's work and -- vmcnt retiring
+  // in issue order -- never wait behind this query's stores.  Query n+2's indices one further.
+  int jn = (int)__builtin_amdgcn_raw_buffer_load_b32(ixr, (int)(((unsigned)q0 * (unsigned)k + lane) * 4u), 0, 0);
+  float pv[16], xv0, xv1, xv2, p1v, ovq[OT], dvq[OT];
+  int amq[OT], rkn;
   auto issue = [&](int n) {  // loads of query n (jn = its indices)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int j = __shfl(jn, (e & 3) + 8 * (e >> 2) + 4 * half, kWave);
+      pv[e] = bload(p2r, ((unsigned)j * D_IN + cg) * 4u);
+    }
     const unsigned xo = (unsigned)jn * 12u;
     xv0 = bload(x2r, xo);
     xv1 = bload(x2r, xo + 4u);
     xv2 = bload(x2r, xo + 8u);
-#pragma unroll
-    for (int i = 0; i < RT; ++i) {
-      int j;
-      if (RPP == 1) {
-        j = __builtin_amdgcn_readlane(jn, i);
-      } else {
-        const int ja = __builtin_amdgcn_readlane(jn, 2 * i), jb = __builtin_amdgcn_readlane(jn, 2 * i + 1);
-        j = sub ? jb : ja;
-      }
-      pv[i] = bload(p2r, ((unsigned)j * D_IN + cg) * 4u);
-    }
     p1v = bload(p1r, ((unsigned)n * D_IN + cg) * 4u);
-    const unsigned oo = (unsigned)n * D_OUT + dl;
-    outv = bload(outr, oo * 4u);
-    doutv = bload(dor, oo * 4u);
-    amv = __builtin_amdgcn_raw_buffer_load_b8(amr, (int)oo, 0, 0);
+#pragma unroll
+    for (int t = 0; t < OT; ++t) {  // output o = 32 t + l32 (both halves)
+      const unsigned oo = (unsigned)n * D_OUT + 32 * t + l32;
+      ovq[t] = bload(outr, oo * 4u);
+      dvq[t] = bload(dor, oo * 4u);
+      amq[t] = (int)__builtin_amdgcn_raw_buffer_load_b8(amr, (int)oo, 0, 0);
+    }
+    rkn = (int)__builtin_amdgcn_raw_buffer_load_b32(
+        rkr, (int)(lane < k ? ((unsigned)n * (unsigned)k + lane) * 4u : kOOB), 0, 0);
   };
-  load_idx(q0);
-  if constexpr (!LEAN) {
-    issue(q0);
-    load_idx(q0 + 1);
-  }
-
-  // CS = 2: every wave of the workgroup walks queries_per_wave iterations (the exchange
-  // barrier), idle past its stream's end
+  auto load_idx = [&](int n) {
+    jn = (int)__builtin_amdgcn_raw_buffer_load_b32(ixr, (int)(((unsigned)n * (unsigned)k + lane) * 4u), 0, 0);
+  };
+  issue(q0);
+  load_idx(q0 + 1);
   const int nit = CS > 1 ? queries_per_wave : q1 - q0;
   for (int it = 0; it < nit; ++it) {
     const int n = q0 + it;
     const bool act = CS == 1 || n < q1;  // wave-uniform
-    float g0 = 0.f, g1 = 0.f, g2 = 0.f;  // d(dir) of the wave's lane-row (direction pass)
+    float g0 = 0.f, g1 = 0.f, g2 = 0.f;  // d(dir) of the lane's row (direction pass)
     int rkv = -1;
     if (act) {
-    if constexpr (LEAN) {
-      issue(n);
-      load_idx(n + 1);
-    }
-    // lane r: the slot of row r (used by the row passes, after this query's MFMAs)
-    rkv = (int)__builtin_amdgcn_raw_buffer_load_b32(
-        rkr, (int)(lane < k ? ((unsigned)n * (unsigned)k + lane) * 4u : kOOB), 0, 0);
-    // ---- h0 of query n into T (layout L), directions into dirT, (g', argmax) into gdam
-    const float qx = x1b[n * 3 + 0], qy = x1b[n * 3 + 1], qz = x1b[n * 3 + 2];
-    if (lane < kRows) dirT[lane] = make_float4(xv0 - qx, xv1 - qy, xv2 - qz, 0.f);
-    if (lane < D_OUT)
-      gdam[lane] = make_float2(doutv * (outv > 0.f ? 1.f : kSlope), __int_as_float((int)amv));
-    const float gd_l = doutv * (outv > 0.f ? 1.f : kSlope);
+      rkv = rkn;
+      float gq[OT];
+      int amc[OT];
 #pragma unroll
-    for (int i = 0; i < RT; ++i) {
-      const int r = RPP * i + sub;
-      const float4 dr = dirT[r];
-      const float pos = __fadd_rn(__builtin_fmaf(wz, dr.z, __builtin_fmaf(wy, dr.y, __fmul_rn(w0, dr.x))), bp);
-      T[r * LD + c] = lrelu(__fadd_rn(__fadd_rn(pv[i], p1v), pos));
-      if (i % 4 == 3) __builtin_amdgcn_sched_barrier(0);
-    }
-    // ---- the next query's loads, in flight during this query's compute
-    if constexpr (!LEAN) {
-      issue(n + 1);
-      load_idx(n + 2);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-
-    // ---- dh0 = M W1 on the matrix cores, M[r][d] = g'[d] [am[d] == r]: the MFMA's f32
-    // accumulation is the fma chain over ascending d, i.e. the same sums as scattering
-    // g'[d] W1[d, :] into row am[d] in ascending d
-    f32x16 dacc[TI];
+      for (int t = 0; t < OT; ++t) {
+        gq[t] = dvq[t] * (ovq[t] > 0.f ? 1.f : kSlope);
+        amc[t] = amq[t];
+      }
+      // ---- directions (lane r) and (g', argmax) per output into the wave's LDS tables
+      const float qx = x1b[n * 3 + 0], qy = x1b[n * 3 + 1], qz = x1b[n * 3 + 2];
+      if (lane < kRows) dirT[lane] = make_float4(xv0 - qx, xv1 - qy, xv2 - qz, 0.f);
 #pragma unroll
-    for (int t = 0; t < TI; ++t) dacc[t] = f32x16{0};
-#pragma unroll
-    for (int s2 = 0; s2 < D_OUT / 2; ++s2) {
-      const float2 ga = gdam[2 * s2 + half];
-      const float a = __float_as_int(ga.y) == l32 ? ga.x : 0.f;
-#pragma unroll
-      for (int t = 0; t < TI; ++t)
-        dacc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(
-            a, W1L ? w1s[(2 * s2 + half) * D_IN + hc * DL + 32 * t + l32] : bwt[t][W1L ? 0 : s2],
-            dacc[t], 0, 0, 0);
-    }
-    // ---- dW1[d, c] += g'[d] h0[am[d], c] (reads h0 before dz0 overwrites it)
-#pragma unroll
-    for (int i = 0; i < DPL; ++i) {
-      const float2 ga = gdam[d0 + i];
-      gw1[i] = __builtin_fmaf(ga.x, T[__float_as_int(ga.y) * LD + c], gw1[i]);
-      if (i % 8 == 7) __builtin_amdgcn_sched_barrier(0);  // bound the hoisted LDS reads
-    }
-    if (lane < D_OUT && hc == 0) gb1 += gd_l;
-    __builtin_amdgcn_sched_barrier(0);
-    // ---- dz0 = dh0 * LeakyReLU'(h0), in place (accumulator layout)
-#pragma unroll
-    for (int t = 0; t < TI; ++t)
+      for (int t = 0; t < OT; ++t)
+        if (half == 0) gdam[32 * t + l32] = make_float2(gq[t], __int_as_float(amc[t]));
+      __builtin_amdgcn_wave_barrier();
+      // ---- h0 in the accumulator layout (the forward's arithmetic; rows >= k are 0)
+      float h0[16];
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int row = (e & 3) + 8 * (e >> 2) + 4 * half;
-        const int a = row * LD + 32 * t + l32;
-        const float hv = T[a];
-        float sl = hv > 0.f ? 1.f : kSlope;
-        if constexpr (OVR) {  // rows >= k read past the query's block or 0: dacc is 0 there
+        const int r = (e & 3) + 8 * (e >> 2) + 4 * half;
+        const float4 dr = dirT[r];
+        const float pos = __fadd_rn(__builtin_fmaf(wz, dr.z, __builtin_fmaf(wy, dr.y, __fmul_rn(w0, dr.x))), bp);
+        const float h = lrelu(__fadd_rn(__fadd_rn(pv[e], p1v), pos));
+        h0[e] = r < k ? h : 0.f;
+        if constexpr (!DW1_MFMA) T[r * LD + l32] = h0[e];  // the tile the dW1 update reads
+        if (e % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // bound the hoisted LDS reads
+      }
+      // the row pass re-reads the directions from LDS: without this compiler barrier they
+      // stay live in 64 registers across the MFMAs
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- the next query's loads, in flight during this query's MFMAs and stores
+      issue(n + 1);
+      load_idx(n + 2);
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- dh0 = M W1 (matrix cores), M[r][o] = g'[o] [am[o] == r]: the fma chain over
+      // ascending o, the sums of scattering g'[o] W1[o, :] into row am[o]
+      f32x16 dacc = f32x16{0};
+#pragma unroll
+      for (int s2 = 0; s2 < D_OUT / 2; ++s2) {
+        const float2 ga = gdam[2 * s2 + half];
+        const float a = __float_as_int(ga.y) == l32 ? ga.x : 0.f;
+        dacc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bw[s2], dacc, 0, 0, 0);
+        if (s2 % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // bound the hoisted LDS reads
+      }
+      // ---- dW1[o, c] += g'[o] h0[am[o], c] for o = 2 i + half (VALU, beside the MFMA chain:
+      // the one-hot product on the matrix cores cost 16 more 64-cycle MFMAs per query); the
+      // same fma chain per (o, c) as the previous kernel's update
+      if constexpr (DW1_MFMA) {
+        // dW1 += M^T h0: step s = rows R_0(s) (half 0) / R_1(s) (half 1), A = the one-hot routing
+        // of output o = 32 t + l32, B = the lane's h0[s]
+#pragma unroll
+        for (int t = 0; t < OT; ++t) {
+          const int amh = amc[t] - 4 * half;
+#pragma unroll
+          for (int s = 0; s < 16; ++s) {
+            const float a = amh == (s & 3) + 8 * (s >> 2) ? gq[t] : 0.f;
+            gw[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, h0[s], gw[t], 0, 0, 0);
+            if (s % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < D_OUT / 2; ++i) {
+          const float2 ga = gdam[2 * i + half];
+          gw1[i] = __builtin_fmaf(ga.x, T[__float_as_int(ga.y) * LD + l32], gw1[i]);
+          if (i % 8 == 7) __builtin_amdgcn_sched_barrier(0);  // bound the hoisted LDS reads
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < OT; ++t) gb1[t] += gq[t];
+      __builtin_amdgcn_wave_barrier();  // the h0 tile is read before dz0 overwrites it
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- dz0 = dh0 * LeakyReLU'(h0) (registers)
+      float dz[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        float sl = h0[e] > 0.f ? 1.f : kSlope;
+        if constexpr (OVR) {
+          const int r = (e & 3) + 8 * (e >> 2) + 4 * half;
           const unsigned o = __builtin_amdgcn_raw_buffer_load_b8(
-              s0r, (int)((((unsigned)n * (unsigned)k + row) * D_IN + hc * DL + 32 * t + l32)), 0, 0);
+              s0r, (int)((((unsigned)n * (unsigned)k + r) * D_IN + cg)), 0, 0);
           sl = o == 1u ? 1.f : (o == 2u ? kSlope : sl);
         }
-        T[a] = dacc[t][e] * sl;
-        if (e % 8 == 7) __builtin_amdgcn_sched_barrier(0);
+        dz[e] = dacc[e] * sl;
       }
-    __builtin_amdgcn_sched_barrier(0);
-    // ---- row pass (layout L): dP2 rows out; dP1, dWpos, dbpos channel sums
-    float dp1_acc = 0.f;
-    float* dp2n = dp2_rows + (((long long)b * n1 + n) * k) * D_IN + cg;
-#pragma unroll 4
-    for (int r0 = 0; r0 < k; r0 += RPP) {  // rows >= k are zero
-      const int r = r0 + sub;
-      if (RPP == 2 && r >= k) break;
-      const float v = T[r * LD + c];
-      const float4 dr = dirT[r];
-      if (ranked) {
-        const int sa = __builtin_amdgcn_readlane(rkv, r0);
-        const int slot = RPP == 2 ? (sub ? __builtin_amdgcn_readlane(rkv, r0 + 1) : sa) : sa;
-        if (slot >= 0) rows[(long long)slot * D_IN + cg] = v;
-      } else if (dp2_rows) {
-        dp2n[r * D_IN] = v;
-      }
-      dp1_acc = __fadd_rn(dp1_acc, v);
-      gwp0 = __builtin_fmaf(v, dr.x, gwp0);
-      gwp1 = __builtin_fmaf(v, dr.y, gwp1);
-      gwp2 = __builtin_fmaf(v, dr.z, gwp2);
-      gbp = __fadd_rn(gbp, v);
-    }
-    if (RPP == 2) dp1_acc = __fadd_rn(dp1_acc, __shfl_xor(dp1_acc, 32, kWave));
-    if (sub == 0) dp1[((long long)b * n1 + n) * D_IN + cg] = dp1_acc;
-    // ---- d(dir_r) = Wpos^T dz0[r] (lane l32 = row, halves split the channels)
+      // ---- row pass: dP2 rows out, dP1, dWpos
+      float dp1_acc = 0.f;
 #pragma unroll
-    for (int i = 0; i < CPH; ++i) {
-      const int cc = half * CPH + i;
-      const float v = T[l32 * LD + cc];
-      const float4 wp = wposT[hc * DL + cc];
-      g0 = __builtin_fmaf(wp.x, v, g0);
-      g1 = __builtin_fmaf(wp.y, v, g1);
-      g2 = __builtin_fmaf(wp.z, v, g2);
-      if (i % 4 == 3) __builtin_amdgcn_sched_barrier(0);
-    }
-    g0 = __fadd_rn(g0, __shfl_xor(g0, 32, kWave));
-    g1 = __fadd_rn(g1, __shfl_xor(g1, 32, kWave));
-    g2 = __fadd_rn(g2, __shfl_xor(g2, 32, kWave));
+      for (int e = 0; e < 16; ++e) {
+        const int r = (e & 3) + 8 * (e >> 2) + 4 * half;
+        const float v = dz[e];
+        const float4 dr = dirT[r];
+        const int slot = ranked ? __shfl(rkv, r, kWave) : (nbase + n) * k + r;
+        const unsigned off = (r < k && slot >= 0) ? ((unsigned)slot * D_IN + cg) * 4u : kOOB;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rowr, (int)off, 0, 0);
+        dp1_acc = __fadd_rn(dp1_acc, v);
+        gwp0 = __builtin_fmaf(v, dr.x, gwp0);
+        gwp1 = __builtin_fmaf(v, dr.y, gwp1);
+        gwp2 = __builtin_fmaf(v, dr.z, gwp2);
+        if (e % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+      }
+      dp1_acc = __fadd_rn(dp1_acc, __shfl_xor(dp1_acc, 32, kWave));
+      if (half == 0) dp1[((long long)b * n1 + n) * D_IN + cg] = dp1_acc;
+      gbp = __fadd_rn(gbp, dp1_acc);
+      // ---- d(dir_r) = Wpos^T dz0[r]: dz0 through the LDS tile into row-per-lane
+#pragma unroll
+      for (int e = 0; e < 16; ++e) T[((e & 3) + 8 * (e >> 2) + 4 * half) * LD + l32] = dz[e];
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int cc = half * 16 + i;
+        const float v = T[l32 * LD + cc];
+        const float4 wp = wposT[hc * 32 + cc];
+        g0 = __builtin_fmaf(wp.x, v, g0);
+        g1 = __builtin_fmaf(wp.y, v, g1);
+        g2 = __builtin_fmaf(wp.z, v, g2);
+        if (i % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+      }
+      g0 = __fadd_rn(g0, __shfl_xor(g0, 32, kWave));
+      g1 = __fadd_rn(g1, __shfl_xor(g1, 32, kWave));
+      g2 = __fadd_rn(g2, __shfl_xor(g2, 32, kWave));
+      __builtin_amdgcn_wave_barrier();  // the tile is rewritten by the next query
     }  // act
     if constexpr (CS > 1) {  // the second channel half's d(dir) partials -> the first wave
       float4* xch = reinterpret_cast<float4*>(lds_all + XCH_AT) +
                     ((it & 1) * (kWaves / CS) + qw) * kRows;
       if (act && hc == 1 && lane < kRows) xch[lane] = make_float4(g0, g1, g2, 0.f);
-      // LDS writes done, then the barrier; no vmcnt drain (the next query's loads and this
-      // query's row stores stay in flight).  Parity-double-buffered: no second barrier.
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if (act && hc == 0) {
         const float4 o = xch[l32];
@@ -486,65 +499,74 @@ void cost_volume_bwd_kernel(
       }
     }
     if (act && hc == 0) {
-    const bool row = lane < k;  // lanes >= 32 never (k <= 32)
-    if (row && ranked) {
-      if (rkv >= 0)
-        *reinterpret_cast<float4*>(dirs + (long long)rkv * 4) = make_float4(g0, g1, g2, 0.f);
-    } else if (row && ddir_rows) {
-      float* dd = ddir_rows + (((long long)b * n1 + n) * k + lane) * 3;
-      dd[0] = g0;
-      dd[1] = g1;
-      dd[2] = g2;
-    }
-    // ---- dx1[n] = -sum_r d(dir_r) (butterfly over the 32 row lanes)
-    float s0 = row ? g0 : 0.f, s1 = row ? g1 : 0.f, s2 = row ? g2 : 0.f;
+      const bool row = lane < k;  // lanes >= 32 never (k <= 32)
+      if (ranked) {
+        const unsigned off = (row && rkv >= 0) ? (unsigned)rkv * 16u : kOOB;
+        __builtin_amdgcn_raw_buffer_store_b128(f32x4{g0, g1, g2, 0.f}, dirr, (int)off, 0, 0);
+      } else {
+        const unsigned off = row ? ((unsigned)((nbase + n) * k + lane)) * 12u : kOOB;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(g0), dirr, (int)off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(g1), dirr, (int)(off == kOOB ? kOOB : off + 4u), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(g2), dirr, (int)(off == kOOB ? kOOB : off + 8u), 0, 0);
+      }
+      float s0 = row ? g0 : 0.f, s1 = row ? g1 : 0.f, s2 = row ? g2 : 0.f;
 #pragma unroll
-    for (int m = 16; m >= 1; m >>= 1) {
-      s0 = __fadd_rn(s0, __shfl_xor(s0, m, kWave));
-      s1 = __fadd_rn(s1, __shfl_xor(s1, m, kWave));
-      s2 = __fadd_rn(s2, __shfl_xor(s2, m, kWave));
+      for (int m = 16; m >= 1; m >>= 1) {
+        s0 = __fadd_rn(s0, __shfl_xor(s0, m, kWave));
+        s1 = __fadd_rn(s1, __shfl_xor(s1, m, kWave));
+        s2 = __fadd_rn(s2, __shfl_xor(s2, m, kWave));
+      }
+      if (lane == 0) {
+        float* o = dx1 + ((long long)b * n1 + n) * 3;
+        o[0] = -s0;
+        o[1] = -s1;
+        o[2] = -s2;
+      }
     }
-    if (lane == 0) {
-      float* o = dx1 + ((long long)b * n1 + n) * 3;
-      o[0] = -s0;
-      o[1] = -s1;
-      o[2] = -s2;
-    }
-    }  // act && hc == 0
   }
   // ---- workgroup partials: waves add their accumulators into one LDS slab in wave order
-  if (RPP == 2) {  // fold the row-parity halves of the channel sums
-    gwp0 = __fadd_rn(gwp0, __shfl_xor(gwp0, 32, kWave));
-    gwp1 = __fadd_rn(gwp1, __shfl_xor(gwp1, 32, kWave));
-    gwp2 = __fadd_rn(gwp2, __shfl_xor(gwp2, 32, kWave));
-    gbp = __fadd_rn(gbp, __shfl_xor(gbp, 32, kWave));
-  }
+  gwp0 = __fadd_rn(gwp0, __shfl_xor(gwp0, 32, kWave));
+  gwp1 = __fadd_rn(gwp1, __shfl_xor(gwp1, 32, kWave));
+  gwp2 = __fadd_rn(gwp2, __shfl_xor(gwp2, 32, kWave));
   __syncthreads();  // every wave is done with its tiles (the buffer is reused)
   float* rw = lds_all;
   for (int w = 0; w < kWaves; ++w) {
     if (wave == w) {
       const bool first = qw == 0;  // the first wave of this channel half's columns
+      if constexpr (DW1_MFMA) {
 #pragma unroll
-      for (int i = 0; i < DPL; ++i) {
-        float* e = rw + (d0 + i) * D_IN + cg;
-        *e = first ? gw1[i] : __fadd_rn(*e, gw1[i]);
+        for (int t = 0; t < OT; ++t)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            float* p = rw + (32 * t + (e & 3) + 8 * (e >> 2) + 4 * half) * D_IN + cg;
+            *p = first ? gw[t][e] : __fadd_rn(*p, gw[t][e]);
+          }
+      } else {
+#pragma unroll
+        for (int i = 0; i < D_OUT / 2; ++i) {
+          float* p = rw + (2 * i + half) * D_IN + cg;
+          *p = first ? gw1[i] : __fadd_rn(*p, gw1[i]);
+        }
       }
-      if (lane < D_OUT && hc == 0) {
-        float* e = rw + D_OUT * D_IN + lane;
-        *e = first ? gb1 : __fadd_rn(*e, gb1);
+      if (hc == 0 && half == 0) {
+#pragma unroll
+        for (int t = 0; t < OT; ++t) {
+          float* p = rw + D_OUT * D_IN + 32 * t + l32;
+          *p = first ? gb1[t] : __fadd_rn(*p, gb1[t]);
+        }
       }
-      if (sub == 0) {
+      if (half == 0) {
         const float v4[4] = {gwp0, gwp1, gwp2, gbp};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          float* e = rw + D_OUT * D_IN + D_OUT + q * D_IN + cg;
-          *e = first ? v4[q] : __fadd_rn(*e, v4[q]);
+          float* p = rw + D_OUT * D_IN + D_OUT + q * D_IN + cg;
+          *p = first ? v4[q] : __fadd_rn(*p, v4[q]);
         }
       }
     }
     __syncthreads();
   }
-  float* sb = slab + ((long long)blockIdx.y * gridDim.x + blockIdx.x) * SLAB;
+  float* sb = slab + (long long)pblk * SLAB;
   for (int e = threadIdx.x; e < SLAB; e += blockDim.x) sb[e] = rw[e];
 }
 
@@ -552,15 +574,14 @@ void cost_volume_bwd_kernel(
 // against 8; 32+ leaves SIMDs idle at the tail)
 constexpr int kFwdQpw = 16;
 
-// backward queries per wave: as many waves as the chip holds at the kernel's occupancy, in
-// ONE round (16 per wave at 8192 waves left the D=32 kernel a 60 %-full second round); at
-// least 2 queries per wave for the pipeline
-template <int DI, int DO, int W>
+// backward queries per wave: as many waves as the chip holds at the kernel's occupancy (2 per
+// SIMD: 225-256 VGPRs), in ONE round; at least 2 queries per wave for the pipeline
+template <int DI, int DO>
 int bwd_waves_resident() {
   static const int w = [] {
     int blocks = 0, dev = 0, cus = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks,
-                                                     cost_volume_bwd_kernel<DI, DO, W, false>,
+                                                     cost_volume_bwd_kernel<DI, DO, false>,
                                                      256, 0) != hipSuccess || blocks < 1)
       blocks = 1;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -572,18 +593,12 @@ int bwd_waves_resident() {
   return w;
 }
 
-// waves per SIMD the backward is compiled for: D_IN = D_OUT = 32 -> 3 (the LEAN build, 168
-// VGPRs, no spill: W1 fragments from LDS, no cross-query prefetch; round 4: cross0 621 -> 574
-// us with the CSR sums against the prefetching 2-wave build), (32, 64) -> 2, D_IN = 64 -> 2
-// (two waves per query, one per channel half; round 5: was one wave per query at 1 per SIMD)
-template <int DI, int DO>
-constexpr int bwd_wpe() { return DI == 32 && DO == 32 ? 3 : 2; }
 template <int DI>
 constexpr int bwd_cs() { return DI == 64 ? 2 : 1; }  // waves per query
 
 template <int DI, int DO>
 inline int bwd_qpw(int b, int n1) {
-  const long long streams = bwd_waves_resident<DI, DO, bwd_wpe<DI, DO>()>() / bwd_cs<DI>();
+  const long long streams = bwd_waves_resident<DI, DO>() / bwd_cs<DI>();
   return std::max(2, (int)divupll((long long)b * n1, streams));
 }
 
@@ -599,8 +614,9 @@ hipError_t fwd_launch(int b, int n1, int n2, int k, const float* x1, const float
                       const int* idx, const float* p1, const float* p2, const float* wpos,
                       const float* bpos, const float* w1, const float* b1, float* out,
                       unsigned char* amax, hipStream_t st) {
-  dim3 grid(divup(n1, kWaves * kFwdQpw), b);
-  hipLaunchKernelGGL((cost_volume_fwd_kernel<DI, DO>), grid, dim3(256), 0, st, n1, n2, k,
+  const int gx = divup(n1, kWaves * kFwdQpw);
+  dim3 grid(8 * divup(gx * b, 8));
+  hipLaunchKernelGGL((cost_volume_fwd_kernel<DI, DO>), grid, dim3(256), 0, st, b, gx, n1, n2, k,
                      kFwdQpw, x1, x2, idx, p1, p2, wpos, bpos, w1, b1, out, amax);
   return hipGetLastError();
 }
@@ -612,21 +628,24 @@ hipError_t bwd_launch(int b, int n1, int n2, int k, const float* x1, const float
                       const unsigned char* amax, const unsigned char* s0, const float* dout,
                       float* dp1, float* dp2_rows, float* dx1, float* ddir_rows, const int* rank,
                       float* rows, float* slab, float* dparams, hipStream_t st) {
-  constexpr int W = bwd_wpe<DI, DO>();
   const int qpw = bwd_qpw<DI, DO>(b, n1);
-  dim3 grid(divup(n1, (kWaves / bwd_cs<DI>()) * qpw), b);
+  const int gx = divup(n1, (kWaves / bwd_cs<DI>()) * qpw);
+  dim3 grid(8 * divup(gx * b, 8));  // XCD-aware virtual blocks (cost_volume_bwd_kernel)
+  // ranked: rows then their d(dir) float4 rows in one workspace (cv_rows_sum_lds_kernel)
+  float* rows_out = rank ? rows : dp2_rows;
+  float* dirs_out = rank ? rows + (long long)b * n1 * k * DI : ddir_rows;
   if (s0)
-    hipLaunchKernelGGL((cost_volume_bwd_kernel<DI, DO, W, true>), grid, dim3(256), 0, st, n1, n2,
-                       k, qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, s0, dout, dp1,
-                       dp2_rows, dx1, ddir_rows, rank, rows, slab);
+    hipLaunchKernelGGL((cost_volume_bwd_kernel<DI, DO, true>), grid, dim3(256), 0, st, b, gx, n1,
+                       n2, k, qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, s0, dout, dp1,
+                       dx1, rank, rows_out, dirs_out, slab);
   else
-    hipLaunchKernelGGL((cost_volume_bwd_kernel<DI, DO, W, false>), grid, dim3(256), 0, st, n1, n2,
-                       k, qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, s0, dout, dp1,
-                       dp2_rows, dx1, ddir_rows, rank, rows, slab);
+    hipLaunchKernelGGL((cost_volume_bwd_kernel<DI, DO, false>), grid, dim3(256), 0, st, b, gx,
+                       n1, n2, k, qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, s0, dout, dp1,
+                       dx1, rank, rows_out, dirs_out, slab);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int len = slab_len(DI, DO);
-  const int nslab = (int)(grid.x * grid.y);
+  const int nslab = gx * b;
   return colsum(nslab, len, slab, dparams, slab + (size_t)nslab * len, st);
 }
 
@@ -744,6 +763,12 @@ bool supported(int din, int dout, int k) {
   return narrow(din, dout, k) || cost_volume_wide_fused_supported(din, dout, k);
 }
 
+// the D <= 64 backward writes its per-neighbour rows through buffer resources over the whole
+// batch: byte offsets must fit 31 bits
+bool rows_fit(int b, int n1, int k, int din, int dout) {
+  return !narrow(din, dout, k) || (long long)b * n1 * k * din * 4 < (1ll << 31);
+}
+
 hipError_t bwd_dispatch(int b, int n1, int n2, int k, int din, int dout, const float* x1,
                         const float* x2, const int* idx, const float* p1, const float* p2,
                         const float* wpos, const float* bpos, const float* w1, const float* out,
@@ -821,7 +846,8 @@ KDPC_API int kdpc_cost_volume_bwd(int b, int n1, int n2, int k, int din, int dou
                                   const float* dout_grad, float* dp1,
                                   float* dp2_rows, float* dx1, float* ddir_rows, void* workspace,
                                   size_t workspace_bytes, float* dparams, void* stream) {
-  KDPC_CHECK_ARG(b > 0 && n1 > 0 && n2 > 0 && supported(din, dout, k) && b <= 65535);
+  KDPC_CHECK_ARG(b > 0 && n1 > 0 && n2 > 0 && supported(din, dout, k) && b <= 65535 &&
+                 rows_fit(b, n1, k, din, dout));
   KDPC_CHECK_ARG(x1 && x2 && idx && p1 && p2 && wpos && bpos && w1 && out && amax && dout_grad &&
                  dp1 && dp2_rows && dx1 && ddir_rows && workspace && dparams);
   KDPC_CHECK_ARG(workspace_bytes >= kdpc_cost_volume_bwd_workspace_bytes(b, n1, din, dout));
@@ -851,7 +877,8 @@ KDPC_API int kdpc_cost_volume_bwd_csr(int b, int n1, int n2, int k, int din, int
                                       const int* offsets, const int* rank, float* dp1, float* dp2,
                                       float* dx1, float* dx2, void* workspace,
                                       size_t workspace_bytes, float* dparams, void* stream) {
-  KDPC_CHECK_ARG(b > 0 && n1 > 0 && n2 > 0 && supported(din, dout, k) && b <= 65535);
+  KDPC_CHECK_ARG(b > 0 && n1 > 0 && n2 > 0 && supported(din, dout, k) && b <= 65535 &&
+                 rows_fit(b, n1, k, din, dout));
   KDPC_CHECK_ARG(x1 && x2 && idx && p1 && p2 && wpos && bpos && w1 && out && amax && dout_grad &&
                  offsets && rank && dp1 && dp2 && dx1 && dx2 && workspace && dparams);
   KDPC_CHECK_ARG(workspace_bytes >= kdpc_cost_volume_bwd_csr_workspace_bytes(b, n1, k, din, dout));
