@@ -1078,17 +1078,27 @@ __global__ __launch_bounds__(256) void pc_csr_sum_kernel(long long npts, long lo
 // after the barrier, so no load latency sits between barriers).  The phases are independent
 // within one basic block, so the MFMAs' 64-cycle shadows carry the build (the unpipelined
 // kernel serialised them behind barriers: ~27 % MFMA busy, profiles/round02).
+//
+// O <= 128 runs 256-thread workgroups on 32-row tiles with ONE dy^T buffer (dy of tile t+1 is
+// staged after tile t's MFMAs): 62-71 KB of LDS, so two workgroups share a CU and one's
+// barriers / build phases overlap the other's MFMAs.  O = 256 (acc registers for 8 output
+// tiles per wave do not fit) keeps one 512-thread workgroup per CU with two dy^T buffers.
+constexpr int wgt_threads(int o) { return o <= 128 ? 256 : 512; }
+
 template <int O, int KM>
-constexpr int wgt_tile_rows() { return O == 256 || (O == 128 && KM > 9) ? 32 : 64; }
+constexpr int wgt_tile_rows() {
+  return wgt_threads(O) == 256 ? 32 : (O == 256 || (O == 128 && KM > 9) ? 32 : 64);
+}
 
 template <int O, int KM, bool EX>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+__global__ __launch_bounds__(wgt_threads(O)) __attribute__((amdgpu_waves_per_eu(2)))
 void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __restrict__ dy,
                           float* __restrict__ dwl, int rows_per_split, int nsplit, int xcd_map,
                           float* __restrict__ dbias) {
   constexpr int TR = wgt_tile_rows<O, KM>();
   constexpr int TS = TR + 4;               // row stride of the transposed tiles
-  constexpr int NT = 512;                  // threads: 2 waves per SIMD
+  constexpr int NT = wgt_threads(O);       // threads
+  constexpr bool SDY = NT == 256;          // single dy^T buffer (dy fetched one tile ahead)
   constexpr int RS = NT / 16;              // rows per build pass (16 threads per row)
   constexpr int RP = TR / RS;              // build passes (rows rb, rb + RS, ...)
   constexpr int MT = O / 32;
@@ -1100,7 +1110,7 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
   static_assert(DV >= 1 && TR * O % (NT * 4) == 0, "dy tile must split into float4 slots");
   static_assert(MT >= 2, "O >= 64");
   __shared__ __attribute__((aligned(16))) float gl[TR * KM * kCC];
-  __shared__ __attribute__((aligned(16))) float dyt[2][O * TS];
+  __shared__ __attribute__((aligned(16))) float dyt[SDY ? 1 : 2][O * TS];
   __shared__ __attribute__((aligned(16))) float at[2][kNC * TS];
 
   // XCD fill: workgroups are dealt to the 8 XCDs round-robin by id, so block L runs on XCD
@@ -1174,7 +1184,7 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
       nbi[i] = base + (int)__builtin_amdgcn_raw_buffer_load_b32(idx_rs, (int)off, 0, 0);
     }
   };
-  auto fetch = [&](int tile) {
+  auto fetch_g = [&](int tile) {
     const int row0 = rbeg + tile * TR;
 #pragma unroll
     for (int p2 = 0; p2 < RP; ++p2) {
@@ -1219,8 +1229,11 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
       gr[i] = make_float4(a0 + (x[0] - cc[0]), a1 + (x[1] - cc[1]), a2 + (x[2] - cc[2]), a3);
     }
     fetch_idx(tile + 1);
-    // dy slot q = t + 512 i: row q % TR (consecutive lanes: consecutive rows, so the
-    // transposed LDS writes below hit consecutive banks), columns 4 (q / TR) .. +3
+  };
+  // dy slot q = t + NT i: row q % TR (consecutive lanes: consecutive rows, so the
+  // transposed LDS writes below hit consecutive banks), columns 4 (q / TR) .. +3
+  auto fetch_dy = [&](int tile) {
+    const int row0 = rbeg + tile * TR;
 #pragma unroll
     for (int i = 0; i < DV; ++i) {
       const int q = t + NT * i;
@@ -1230,13 +1243,19 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
           float4, __builtin_amdgcn_raw_buffer_load_b128(dy_rs, (int)off, 0, 0));
     }
   };
-  // registers -> LDS: gathered G into gl, dy transposed into dyt[buf], weights into wc
-  auto stage = [&](int buf) {
+  // registers -> LDS: gathered G into gl, weights into wc; dy transposed into dyt[buf]
+  auto stage_g = [&]() {
 #pragma unroll
     for (int i = 0; i < GS; ++i) {
       const int rk = (t >> 1) + (NT / 2) * i;
       if (rk < tk) *reinterpret_cast<float4*>(gl + rk * kCC + 4 * h4) = gr[i];
     }
+#pragma unroll
+    for (int p2 = 0; p2 < RP; ++p2)
+#pragma unroll
+      for (int k = 0; k < KM; ++k) wc[p2][k] = wr[p2][k];
+  };
+  auto stage_dy = [&](int buf) {
     float* dt = dyt[buf];
 #pragma unroll
     for (int i = 0; i < DV; ++i) {
@@ -1247,10 +1266,6 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
       dt[(o + 2) * TS + r] = dr[i].z;
       dt[(o + 3) * TS + r] = dr[i].w;
     }
-#pragma unroll
-    for (int p2 = 0; p2 < RP; ++p2)
-#pragma unroll
-      for (int k = 0; k < KM; ++k) wc[p2][k] = wr[p2][k];
   };
   // A block of the tile staged in gl / wc -> at[buf] (transposed: column-major rows)
   // bias gradient for free (dbias != null): the first padding channel's w = 0 column of A
@@ -1274,22 +1289,28 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
 #pragma unroll
   for (int i = 0; i < MPW; ++i) acc[i] = zero16();
   if (ntiles <= 0) return;
-  // prologue: tile 0 staged and built, tile 1 staged
+  // prologue: tile 0 staged and built, tile 1's G / weights (and dy with two buffers) staged
   fetch_idx(0);
-  fetch(0);
-  stage(0);
+  fetch_g(0);
+  fetch_dy(0);
+  stage_g();
+  stage_dy(0);
   __syncthreads();
   build(0);
-  fetch(1);
+  fetch_g(1);
+  if (!SDY) fetch_dy(1);
   __syncthreads();
-  stage(1);
+  stage_g();
+  if (!SDY) stage_dy(1);
   __syncthreads();
   for (int tile = 0; tile < ntiles; ++tile) {
     const int cur = tile & 1;
-    // tile+2's loads are issued first and land under this tile's MFMAs; tile's MFMAs || tile+1's
-    // build (independent: at[cur] / dyt[cur] vs gl, wc -> at[!cur])
-    fetch(tile + 2);
-    const float* dt = dyt[cur];
+    // tile+2's loads (tile+1's dy with one buffer) are issued first and land under this
+    // tile's MFMAs; tile's MFMAs || tile+1's build (independent: at[cur] / dyt vs gl, wc ->
+    // at[!cur])
+    fetch_g(tile + 2);
+    fetch_dy(SDY ? tile + 1 : tile + 2);
+    const float* dt = dyt[SDY ? 0 : cur];
     const float* ab = at[cur];
 #pragma unroll
     for (int gb = 0; gb < TR / 8; ++gb) {
@@ -1302,8 +1323,9 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
       }
     }
     build(cur ^ 1);
-    __syncthreads();  // at[cur] / dyt[cur] / gl consumed; at[cur ^ 1] complete
-    stage(cur);  // tile + 2
+    __syncthreads();  // at[cur] / dyt / gl consumed; at[cur ^ 1] complete
+    stage_g();        // tile + 2
+    stage_dy(SDY ? 0 : cur);  // tile + 1 (one buffer) or tile + 2
     __syncthreads();
   }
   const long long col = (long long)c0 * kW + nt * 32 + l32;
@@ -1380,7 +1402,9 @@ bool plan_of(int b, int s, int k, int d, int o, Plan* p, int wcus = kCUs) {
   // busiest CU) x (tiles per split); pick the split count minimising that.  Multiples of 8
   // keep the XCD mapping (a split's chunks share its dy / wt rows in one L2) unless >6%
   // slower.  (round 1, unpipelined: 2-3 co-resident workgroups per CU ran slower than one.)
-  const int trw = km_of(k) <= 9 ? (o == 256 ? 32 : 64) : (o == 64 ? 64 : 32);
+  // (O <= 128: 256-thread workgroups, two per CU -- wgt_threads)
+  const int trw = wgt_threads(o) == 256 ? 32 : (km_of(k) <= 9 ? (o == 256 ? 32 : 64) : 32);
+  wcus *= wgt_threads(o) == 256 ? 2 : 1;
   const int t32 = std::max(1, divup(p->r, trw));
   const int cap = std::max(1, std::min(t32, wcus / p->nch));
   auto cost = [&](int rs) {
@@ -1498,10 +1522,10 @@ hipError_t bwd_weight_launch(const Geo& g, const Plan& p, const float* wt, const
   float* bias_slab = reinterpret_cast<float*>(ws + p.dwl_slab);
   float* bdst = dbias == nullptr ? nullptr : (p.rs > 1 ? bias_slab : dbias);
   if (g.k == KM)
-    hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM, true>), dim3(p.wgs), dim3(512), 0, st, g, wt,
+    hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM, true>), dim3(p.wgs), dim3(wgt_threads(O)), 0, st, g, wt,
                        dy, wdst, p.rps, p.rs, p.xcd, bdst);
   else
-    hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM, false>), dim3(p.wgs), dim3(512), 0, st, g, wt,
+    hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM, false>), dim3(p.wgs), dim3(wgt_threads(O)), 0, st, g, wt,
                        dy, wdst, p.rps, p.rs, p.xcd, bdst);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || p.rs == 1) return e;

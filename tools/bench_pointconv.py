@@ -1,5 +1,6 @@
 """Fused PointConv layer at the model's shapes (batch 8 pairs, N=8192): forward and backward
-time per call with HIP events, and the f32 MFMA rate they reach.
+time per call with HIP events (and the weight half alone, as the side stream runs it), and
+the f32 MFMA rate they reach.
 
     python tools/bench_pointconv.py [--json out.json]
 """
@@ -80,7 +81,11 @@ def main():
         fwd = timeit(lambda: K.pointconv_fwd(xyz, center, feats, idx, wt, wl, bias), args.iters)
         bwd = timeit(lambda: K.pointconv_bwd(xyz, center, feats, idx, wt, wl, dy, csr,
                                              need_xyz=False), args.iters)
+        wgt = timeit(lambda: K.pointconv_bwd_weight(xyz, center, feats, idx, wt, dy, O),
+                     args.iters)
         if args.dump:
+            dump[f"{name}/dwl"] = K.pointconv_bwd_weight(xyz, center, feats, idx, wt, dy,
+                                                         O).cpu().numpy()
             outs = K.pointconv_bwd(xyz, center, feats, idx, wt, wl, dy, csr, need_xyz=True)
             for i, o in enumerate(outs):
                 if torch.is_tensor(o):
@@ -88,7 +93,8 @@ def main():
         R = B * S
         gemm = 2.0 * R * 16 * C * O
         build = 2.0 * R * Kn * C * 16
-        res[name] = {"fwd_us": round(fwd, 1), "bwd_us": round(bwd, 1),
+        res[name] = {"fwd_us": round(fwd, 1), "bwd_us": round(bwd, 1), "weight_us": round(wgt, 1),
+                     "weight_TFLOPs": round((gemm + build) / (wgt * 1e-6) / 1e12, 1),
                      "fwd_TFLOPs": round((gemm + build) / (fwd * 1e-6) / 1e12, 1),
                      "bwd_TFLOPs": round((2 * gemm + 3 * build) / (bwd * 1e-6) / 1e12, 1)}
         print(name, res[name], flush=True)
