@@ -584,7 +584,7 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
 // (partial row g.tdst).  The forward arithmetic per pair is unchanged.
 template <int O, int KM, bool TP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
-void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* __restrict__ wsw,
+void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const bf16x8* __restrict__ wsw,
                              const float* __restrict__ dy, float* __restrict__ dgr,
                              float* __restrict__ dwt, float* __restrict__ dcenter,
                              int chunks_per_split) {
@@ -596,15 +596,23 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
   constexpr int XP = TR * KM - PP * NT;
   constexpr bool XI = XP > 0;
   static_assert(PP >= 1 && (!XI || XP * kCC == NT), "left-over pairs must fill one item/thread");
-  constexpr int NOG = O / 8;
-  // B blocks in flight: the first PF of the next chunk are issued before its gathers, the
-  // rest inside the step, PF steps ahead of their MFMAs (behind the gathers in vmcnt order)
-  constexpr int PF = NOG < 8 ? NOG : 8;
+  // dA = dy wl on the bf16 matrix cores (mfma_x6): NKS 16-deep K-steps per chunk, 6 MFMAs each
+  constexpr int NKS = O / 16;
+  // B planes in flight: the first PF K-steps of the next chunk are issued before its gathers,
+  // the rest inside the step, PF steps ahead of their MFMAs (behind the gathers in vmcnt order)
+  constexpr int PF = NKS < 2 ? NKS : 2;
   constexpr int NIT = PP * kCC + (XI ? 1 : 0);  // VALU items per chunk per thread
-  constexpr int STEPS = NOG > NIT ? NOG : NIT;
-  __shared__ __attribute__((aligned(16))) float dyl[(O / 4) * kBlk];
+  constexpr int STEPS = NKS > NIT ? NKS : NIT;
+  // dy of the tile as three bf16 planes (A operands), rows of O/8 16-byte chunks, chunk c of
+  // row r at c ^ (r & SW) (the 32 lanes of a half read one chunk column of 32 rows)
+  constexpr int DCH = O / 8;
+  constexpr int SW = (DCH < 16 ? DCH : 16) - 1;
+  __shared__ __attribute__((aligned(16))) bf16x8 dyp[3][32 * DCH];
   __shared__ __attribute__((aligned(16))) float dal[2][32 * kDaS];
-  __shared__ float dcl[TR * KM * 3];  // every pair slot (invalid ones write zeros)
+  // dcenter partials of every pair slot (chunk 0's first three channels): held in registers
+  // through the chunk loop, then written over dal (free after the last step) and summed
+  float* dcl = dal[0];
+  static_assert(TR * KM * 3 <= 2 * 32 * kDaS, "dcenter partials fit over dA");
   // TP: the chunk's per-pair dG values (double-buffered by chunk parity) and the tile's
   // pairs in (destination, pair) order
   constexpr int TRK = TR * KM;
@@ -627,10 +635,24 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
   const long long rk_total = (long long)g.r * g.k;
   const Srcs src = srcs_of(g);
 
-  for (int e = t; e < 32 * O; e += NT) {
-    const int r = e / O, o = e % O;
+  for (int e = t; e < 32 * DCH; e += NT) {
+    const int r = e / DCH, c = e % DCH;
     const int row = grow(r);
-    dyl[(o >> 2) * kBlk + r * 4 + (o & 3)] = row >= 0 ? dy[(long long)row * O + o] : 0.f;
+    float v[8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float4 x = row >= 0 ? reinterpret_cast<const float4*>(dy + (long long)row * O)[2 * c + h]
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[4 * h + 0] = x.x;
+      v[4 * h + 1] = x.y;
+      v[4 * h + 2] = x.z;
+      v[4 * h + 3] = x.w;
+    }
+    const Planes pl = split8(v);
+    const int cix = r * DCH + (c ^ (r & SW));
+    dyp[0][cix] = pl.h;
+    dyp[1][cix] = pl.m;
+    dyp[2][cix] = pl.l;
   }
   float wp[PP][kW], dw[PP][kW];
   int pr[PP], pk[PP], pn[PP], ps[PP], prc[PP], prow[PP];
@@ -700,7 +722,18 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
     return bload(src.feats, fo) + (bload(src.xyz, xo) - bload(src.center, co));
   };
 
-  auto brow = [&](int ch) { return wsw + (long long)((ch * 4 + wv) * NOG) * 64 + lane; };
+  // this wave's B planes of chunk ch: K-step ks, plane p at [(3 ks + p) * 64]
+  auto brow = [&](int ch) { return wsw + (long long)((ch * 4 + wv) * NKS * 3) * 64 + lane; };
+  // one K-step of dA: A planes from dyp (row l32, 16-byte chunk 2 ks + half), B planes in b
+  auto kstep = [&](int ks, const Planes& b, f32x16 acc) {
+    const int cix = l32 * DCH + ((2 * ks + half) ^ (l32 & SW));
+    return mfma_x6(dyp[0][cix], dyp[1][cix], dyp[2][cix], b.h, b.m, b.l, acc);
+  };
+  auto bload = [&](const bf16x8* wr, int ks, Planes& b) {
+    b.h = wr[(3 * ks + 0) * 64];
+    b.m = wr[(3 * ks + 1) * 64];
+    b.l = wr[(3 * ks + 2) * 64];
+  };
   auto gather = [&](int ch, float (&dst)[PP][kCC]) {
     const bool c0 = ch == 0;
     const unsigned lo_ch = c0 ? 0u : (unsigned)(ch * kCC - 3) * 4u;
@@ -736,30 +769,29 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
       dal[buf][((e & 3) + 8 * (e >> 2) + 4 * half) * kDaS + wv * 32 + l32] = acc[e];
   };
 
-  float4 bq[PF];
+  Planes bq[PF];
   float gv[PP][kCC], gn[PP][kCC];
   if (ch0 < ch1) {
-    const float4* wr0 = brow(ch0);
+    const bf16x8* wr0 = brow(ch0);
 #pragma unroll
-    for (int p2 = 0; p2 < PF; ++p2) bq[p2] = wr0[p2 * 64];
+    for (int p2 = 0; p2 < PF; ++p2) bload(wr0, p2, bq[p2]);
     gather(ch0, gv);
     if constexpr (XI) xg = gather_x(ch0);
   }
-  __syncthreads();  // dyl
+  __syncthreads();  // dyp
   if (ch0 < ch1) {  // prologue: chunk ch0's dA
-    const float4* wrow = brow(ch0);
+    const bf16x8* wrow = brow(ch0);
     f32x16 acc = zero16();
 #pragma unroll
-    for (int og = 0; og < NOG; ++og) {
-      const float4 av = *reinterpret_cast<const float4*>(dyl + (2 * og + half) * kBlk + l32 * 4);
-      acc = mfma4(av, bq[og % PF], acc);
-      if (og + PF < NOG) bq[og % PF] = wrow[(og + PF) * 64];
+    for (int ks = 0; ks < NKS; ++ks) {
+      acc = kstep(ks, bq[ks % PF], acc);
+      if (ks + PF < NKS) bload(wrow, ks + PF, bq[ks % PF]);
     }
     store_da(acc, 0);
     if (ch0 + 1 < ch1) {
-      const float4* wr1 = brow(ch0 + 1);
+      const bf16x8* wr1 = brow(ch0 + 1);
 #pragma unroll
-      for (int p2 = 0; p2 < PF; ++p2) bq[p2] = wr1[p2 * 64];
+      for (int p2 = 0; p2 < PF; ++p2) bload(wr1, p2, bq[p2]);
     }
   }
   __syncthreads();
@@ -843,17 +875,15 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
       *reinterpret_cast<float4*>(rb + tpl[b0] * kCC + h4) = v;
     }
   };
-  constexpr int SI = NOG - PF > 0 ? NOG - PF - 1 : 0;  // step issuing the last B load
-  auto step = [&](auto mf, const float* dab, const float4* wr1, f32x16& acc,
+  constexpr int SI = NKS - PF > 0 ? NKS - PF - 1 : 0;  // step issuing the last B load
+  auto step = [&](auto mf, const float* dab, const bf16x8* wr1, f32x16& acc,
                   float (&sv)[PP][kCC], int prev) {
 #pragma unroll
     for (int i = 0; i < STEPS; ++i) {
       if constexpr (decltype(mf)::value) {
-        if (i < NOG) {
-          const float4 av =
-              *reinterpret_cast<const float4*>(dyl + (2 * i + half) * kBlk + l32 * 4);
-          acc = mfma4(av, bq[i % PF], acc);
-          if (i + PF < NOG) bq[i % PF] = wr1[(i + PF) * 64];
+        if (i < NKS) {
+          acc = kstep(i, bq[i % PF], acc);
+          if (i + PF < NKS) bload(wr1, i + PF, bq[i % PF]);
         }
       }
       if (XI && i == NIT - 1) {  // the left-over item
@@ -898,6 +928,7 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
       __builtin_amdgcn_sched_barrier(0);
     }
   };
+  float dcr[PP][3], dcx = 0.f;  // chunk 0's dcenter partials (dcl after the loop)
   for (int ch = ch0; ch < ch1; ++ch) {
     const int buf = (ch - ch0) & 1;
     const bool more = ch + 1 < ch1;  // uniform
@@ -920,7 +951,7 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
     for (int q = 0; q < PP; ++q) {
       if (c0 == 0) {
 #pragma unroll
-        for (int cl = 0; cl < 3; ++cl) dcl[(t + NT * q) * 3 + cl] = sv[q][cl];
+        for (int cl = 0; cl < 3; ++cl) dcr[q][cl] = sv[q][cl];
       }
       if constexpr (TP) {
         float4* rp = reinterpret_cast<float4*>(red[buf] + (t + NT * q) * kCC);
@@ -934,14 +965,14 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
     if constexpr (XI) {
       xsh = xs;
       if constexpr (TP) red[buf][xp * kCC + xc] = xs;
-      if (xn >= 0 && c0 == 0 && xc < 3) dcl[xp * 3 + xc] = xs;
+      if (c0 == 0) dcx = xs;
     }
     if (more) {
       store_da(acc, buf ^ 1);
       if (ch + 2 < ch1) {
-        const float4* wr2 = brow(ch + 2);
+        const bf16x8* wr2 = brow(ch + 2);
 #pragma unroll
-        for (int p2 = 0; p2 < PF; ++p2) bq[p2] = wr2[p2 * 64];
+        for (int p2 = 0; p2 < PF; ++p2) bload(wr2, p2, bq[p2]);
       }
     }
     __syncthreads();
@@ -955,13 +986,23 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const float4* 
     if constexpr (TP) reduce(red[(ch1 - 1 - ch0) & 1]);
     store_dg(ch1 - 1);
   }
-  if (ch0 == 0 && t < TR * 3) {
-    const int r = t / 3, i = t - (t / 3) * 3;
-    const int row = grow(r);
-    if (row >= 0) {
-      float s = 0.f;
-      for (int k = 0; k < g.k; ++k) s = __fadd_rn(s, dcl[(r * g.k + k) * 3 + i]);  // slot p
-      dcenter[(long long)row * 3 + i] = -s;
+  if (ch0 == 0) {  // uniform: the loop's last barrier has retired every dA read
+#pragma unroll
+    for (int q = 0; q < PP; ++q)
+#pragma unroll
+      for (int cl = 0; cl < 3; ++cl) dcl[(t + NT * q) * 3 + cl] = dcr[q][cl];
+    if constexpr (XI) {
+      if (xn >= 0 && xc < 3) dcl[xp * 3 + xc] = dcx;
+    }
+    __syncthreads();
+    if (t < TR * 3) {
+      const int r = t / 3, i = t - (t / 3) * 3;
+      const int row = grow(r);
+      if (row >= 0) {
+        float s = 0.f;
+        for (int k = 0; k < g.k; ++k) s = __fadd_rn(s, dcl[(r * g.k + k) * 3 + i]);  // slot p
+        dcenter[(long long)row * 3 + i] = -s;
+      }
     }
   }
   float* dwt_dst = dwt + (long long)split * rk_total * kW;
@@ -1015,6 +1056,34 @@ __global__ __launch_bounds__(256) void pc_swizzle_bwd_kernel(int o, int c16, int
       v.w = wl[(long long)(o0 + 3) * c16 + col];
     }
     wsw[e] = v;
+  }
+}
+
+// wl (O, 16C) -> the pipelined data kernel's B operand planes (split-bf16 MFMA, mfma_x6):
+// bf16x8 (ch, wave, ks, plane, lane) = plane {h, m, l} of wl[16 ks + 8 (lane >> 5) + 0..7]
+// [ch * 128 + 32 wave + (lane & 31)], zero past column 16C.  One thread per (ch, wave, ks,
+// lane); a wave reads 32 consecutive columns of 8 rows.
+__global__ __launch_bounds__(256) void pc_swizzle_bwd3_kernel(int o, int c16, int nch,
+                                                              const float* __restrict__ wl,
+                                                              bf16x8* __restrict__ wsw) {
+  const int nks = o / 16;
+  const long long total = (long long)nch * 4 * nks * 64;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int lane = (int)(e & 63);
+    const long long q = e >> 6;
+    const int ks = (int)(q % nks);
+    const long long cw = q / nks;  // ch * 4 + wave
+    const int col = (int)(cw * 32) + (lane & 31);
+    const int o0 = 16 * ks + 8 * (lane >> 5);
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = col < c16 ? wl[(long long)(o0 + j) * c16 + col] : 0.f;
+    const Planes p = split8(v);
+    bf16x8* dst = wsw + (q * 3) * 64 + lane;
+    dst[0] = p.h;
+    dst[64] = p.m;
+    dst[128] = p.l;
   }
 }
 
@@ -1429,7 +1498,8 @@ bool plan_of(int b, int s, int k, int d, int o, Plan* p, int wcus = kCUs) {
   p->dgr = align256((size_t)b * divup(s, 32) * 32 * k * p->c8 * 4);
   p->dwt_slab = p->bks > 1 ? align256((size_t)p->bks * p->r * k * kW * 4) : 0;
   p->dwl_slab = p->rs > 1 ? align256((size_t)p->rs * o * c16 * 4) : 0;
-  p->wlt = align256((size_t)p->nch * kNC * o * 4);  // swizzled B, padded to whole chunks
+  // swizzled B, padded to whole chunks: f32 (4 B) or three bf16 planes (6 B) per element
+  p->wlt = align256((size_t)p->nch * kNC * o * 6);
   return true;
 }
 
@@ -1478,27 +1548,36 @@ hipError_t bwd_data_launch(const Geo& g, const Plan& p, int b, const float* wt, 
                            float* dcenter, float* dwt, char* ws, hipStream_t st) {
   float* dgr = reinterpret_cast<float*>(ws);
   float* dwt_slab = reinterpret_cast<float*>(ws + p.dgr);
-  float4* wsw = reinterpret_cast<float4*>(ws + p.dgr + p.dwt_slab + p.dwl_slab);
+  char* wsb = ws + p.dgr + p.dwt_slab + p.dwl_slab;  // swizzled wl (p.wlt bytes)
   const int c16 = g.c * kW;
-  const long long nsw = (long long)g.nch * 4 * (O / 8) * 64;
-  hipLaunchKernelGGL(pc_swizzle_bwd_kernel, dim3((unsigned)divupll(nsw, 256)), dim3(256), 0, st,
-                     O, c16, g.nch, wl, wsw);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
   // the pipelined kernels store dG through a buffer resource (31-bit byte offsets)
   const bool dg31 = (long long)p.r * g.k * p.c8 * 4 < (1ll << 31);
   const long long rk = (long long)p.r * g.k;
-  if (g.trow)  // tiled plan (checked by the entry point: dG partial rows fit 31 bits)
-    hipLaunchKernelGGL((pc_bwd_data_pipe_kernel<O, KM, true>),
-                       dim3((unsigned)((long long)b * divup(g.s, 32)), p.bks), dim3(256), 0, st,
-                       g, wt, wsw, dy, dgr, p.bks > 1 ? dwt_slab : dwt, dcenter, p.bcps);
-  else if (bwd_pipe_enabled<KM>() && dg31)
-    hipLaunchKernelGGL((pc_bwd_data_pipe_kernel<O, KM, false>), dim3(divup(p.r, 32), p.bks), dim3(256),
-                       0, st, g, wt, wsw, dy, dgr, p.bks > 1 ? dwt_slab : dwt, dcenter, p.bcps);
-  else
+  hipError_t e;
+  if (g.trow || (bwd_pipe_enabled<KM>() && dg31)) {  // split-bf16 B planes
+    bf16x8* wsw = reinterpret_cast<bf16x8*>(wsb);
+    const long long nsw = (long long)g.nch * 4 * (O / 16) * 64;
+    hipLaunchKernelGGL(pc_swizzle_bwd3_kernel, dim3((unsigned)divupll(nsw, 256)), dim3(256), 0,
+                       st, O, c16, g.nch, wl, wsw);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (g.trow)  // tiled plan (checked by the entry point: dG partial rows fit 31 bits)
+      hipLaunchKernelGGL((pc_bwd_data_pipe_kernel<O, KM, true>),
+                         dim3((unsigned)((long long)b * divup(g.s, 32)), p.bks), dim3(256), 0, st,
+                         g, wt, wsw, dy, dgr, p.bks > 1 ? dwt_slab : dwt, dcenter, p.bcps);
+    else
+      hipLaunchKernelGGL((pc_bwd_data_pipe_kernel<O, KM, false>), dim3(divup(p.r, 32), p.bks),
+                         dim3(256), 0, st, g, wt, wsw, dy, dgr, p.bks > 1 ? dwt_slab : dwt,
+                         dcenter, p.bcps);
+  } else {
+    float4* wsw = reinterpret_cast<float4*>(wsb);
+    const long long nsw = (long long)g.nch * 4 * (O / 8) * 64;
+    hipLaunchKernelGGL(pc_swizzle_bwd_kernel, dim3((unsigned)divupll(nsw, 256)), dim3(256), 0,
+                       st, O, c16, g.nch, wl, wsw);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL((pc_bwd_data_kernel<O, KM>), dim3(divup(p.r, bwd_tile_rows<KM>()), p.bks),
                        dim3(bwd_threads<KM>()), 0, st,
                        g, wt, wsw, dy, dgr, p.bks > 1 ? dwt_slab : dwt, dcenter, p.bcps);
+  }
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (p.bks > 1 && (e = slab_sum(p.bks, rk * kW, dwt_slab, nullptr, 1, dwt, st)) != hipSuccess)

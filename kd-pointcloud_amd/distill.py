@@ -16,7 +16,6 @@ train_bid_pointconv.py) MI355X-first:
 The step is model-agnostic (any module returning the reference's 8-tuple), which lets the
 multi-process path be tested on CPU with gloo.
 """
-import os
 
 import torch
 import torch.distributed as dist
@@ -65,8 +64,8 @@ def _core(model):
     return model.module if isinstance(model, torch.nn.parallel.DistributedDataParallel) else model
 
 
-# KDPC_KD_TEACHER_STREAM=0 runs the frozen teacher's forward in line (A/B runs)
-TEACHER_STREAM = os.environ.get("KDPC_KD_TEACHER_STREAM", "1") != "0"
+# False runs the frozen teacher's forward in line (the tests' reference)
+TEACHER_STREAM = True
 _teacher_streams = {}
 
 
@@ -97,8 +96,8 @@ class _TeacherFork:
         return self.out
 
 
-# KDPC_KD_COORD_FORK=1: the KD student forks its decoder searches too (A/B runs)
-KD_COORD_FORK = os.environ.get("KDPC_KD_COORD_FORK", "0") == "1"
+# True: the KD student forks its decoder searches too (measured slower; tests)
+KD_COORD_FORK = False
 
 
 class _kd_student_streams:
@@ -107,7 +106,7 @@ class _kd_student_streams:
     (models_bid_pointconv._CoordFork) measured slower, with its own stream (13.17-13.66 vs
     14.27-14.30 ms/step at configs[3]'s slice, profiles/round03/ab/bab_fkkd_*) and on the
     parameter-gradient stream alike (13.56-13.66 vs 14.30-14.32, bab_fskd_*), so the student
-    searches in line inside the KD step (KDPC_KD_COORD_FORK=1 keeps the fork).  Scoped to
+    searches in line inside the KD step (KD_COORD_FORK = True keeps the fork).  Scoped to
     the step's own forward: the same module trained by a FlowTrainStep keeps its fork."""
 
     def __init__(self, student):

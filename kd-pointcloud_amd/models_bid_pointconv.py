@@ -11,7 +11,6 @@ output.  MI355X-first restructuring of the forward, with identical per-sample ar
   * only the pc1-side layers (cost volume refinement, scene-flow estimators whose train-mode
     BatchNorm sees pc1 only, warping) run at batch B.
 """
-import os
 
 import torch
 import torch.nn as nn
@@ -24,8 +23,8 @@ import kdpc_native
 import wgrad
 from pointnet2 import pointnet2_utils
 
-# KDPC_COORD_FORK=0 runs the decoder's flow-dependent searches in line (stream switch)
-COORD_FORK = os.environ.get("KDPC_COORD_FORK", "1") != "0"
+# False runs the decoder's flow-dependent searches in line (the tests' reference)
+COORD_FORK = True
 _coord_streams = {}  # (device index, forking stream handle) -> side stream
 # the fork shares the parameter-gradient stream (idle during the forward); False gives it a
 # stream of its own (test seam: tests/test_gpu_graph.py captures both)

@@ -517,7 +517,8 @@ def _tiled_inputs(b, n, s, k, d, o, knn, seed):
 def test_pointconv_bwd_tiled(b, n, s, k, d, o, knn, morton):
     """The tiled backward (dG summed per (row tile, destination) in the data kernel, then per
     point through the partial rows' CSR): dwt, dcenter and dwl bit-equal to the untiled entry
-    points (same per-pair arithmetic), dxyz / dfeats within 1e-5 of the tensor scale of an
+    points (same per-pair arithmetic; K = 16: within 1e-5, see below), dxyz / dfeats within
+    1e-5 of the tensor scale of an
     fp64 evaluation, and run-to-run bit-identical.  Morton-ordered and identity row tiles,
     kNN and random (repeating) neighbours, S not a multiple of 32, K up to 16."""
     import kdpc_native as K
@@ -541,14 +542,21 @@ def test_pointconv_bwd_tiled(b, n, s, k, d, o, knn, morton):
         assert torch.equal(a, c), ("run-to-run", name)
     for name, a, c in zip(["dxyz", "dfeats", "dcenter", "dwt"], got, data):
         assert torch.equal(a, c), ("data half", name)
-    for name, i in (("dcenter", 2), ("dwl", 4)):
-        assert torch.equal(got[i], ref[i]), name
+    assert torch.equal(got[4], ref[4]), "dwl"
+    # K <= 9: the untiled entry runs the same pipelined data kernel (dA on split-bf16 MFMAs)
+    # -> bit-identical dcenter; K = 16 untiled runs the f32-MFMA data kernel (same f32-level
+    # accuracy, other rounding)
+    same = k <= 9
+    if same:
+        assert torch.equal(got[2], ref[2]), "dcenter"
+    else:
+        _scale_close(got[2], ref[2], rtol=1e-5, name="dcenter")
     # dwt of a pair is summed over its channels by one thread, or -- for the tile's 32K-256
     # left-over pairs -- by 8 lanes and a butterfly: a row's tile position picks the order,
     # so Morton-ordered tiles round some pairs differently (the untiled kernel does the same
     # under any row permutation); identity-ordered tiles are bit-identical
-    if morton:
-        _scale_close(got[3], ref[3], rtol=1e-6, name="dwt")
+    if morton or not same:
+        _scale_close(got[3], ref[3], rtol=1e-6 if same else 1e-5, name="dwt")
     else:
         assert torch.equal(got[3], ref[3]), "dwt"
     X, F = xyz.double().requires_grad_(True), feats.double().requires_grad_(True)
