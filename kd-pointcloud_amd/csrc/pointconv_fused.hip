@@ -1416,6 +1416,275 @@ void pc_bwd_weight_kernel(Geo g, const float* __restrict__ wt, const float* __re
     }
 }
 
+// Split-bf16 weight kernel (O <= 128; mfma_x6): the same (chunk, split) workgroups and row
+// tiles as pc_bwd_weight_kernel, with the MFMA operands as bf16 planes in LDS: dy^T planes
+// (o, 8-row group) and A planes (column, 8-row group), 16-byte chunks, the group index
+// XOR-swizzled by (index >> 2) & 3 so that the 32 lanes of an MFMA operand read hit 16
+// distinct chunk positions.  Each thread builds two adjacent rows of one WeightNet column for
+// the 8 channels of the chunk (one packed 32-bit plane word per channel) and splits two
+// adjacent rows of 8 dy columns.  One A buffer: per 32-row tile, [MFMAs of tile t] barrier
+// [build + split of tile t+1, dy of t+1 and G of t+2 to LDS] barrier -- 62-68 KB of LDS, two
+// workgroups per CU, whose phases overlap each other (a bf16 MFMA leaves 24 of its 32 cycles
+// of vector issue to other waves).  G is double-buffered (tile t+2's gathers land while tile
+// t+1 is built from the other buffer).
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void split_pair(float a, float b, unsigned& h, unsigned& m,
+                                           unsigned& l) {
+  __bf16 h0, m0, l0, h1, m1, l1;
+  split3(a, h0, m0, l0);
+  split3(b, h1, m1, l1);
+  h = __builtin_bit_cast(unsigned, bf16x2{h0, h1});
+  m = __builtin_bit_cast(unsigned, bf16x2{m0, m1});
+  l = __builtin_bit_cast(unsigned, bf16x2{l0, l1});
+}
+
+template <int O, int KM, bool EX>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+void pc_bwd_weight_x6_kernel(Geo g, const float* __restrict__ wt, const float* __restrict__ dy,
+                             float* __restrict__ dwl, int rows_per_split, int nsplit,
+                             int xcd_map, float* __restrict__ dbias) {
+  constexpr int TR = 32;                   // tile rows: two 16-deep K-steps
+  constexpr int NT = 256;
+  constexpr int NG = TR / 8;               // 8-row groups (16-byte plane chunks) per column
+  constexpr int MT = O / 32;               // output tiles per wave (o blocks)
+  constexpr int GS = (TR * KM + NT / 2 - 1) / (NT / 2);  // gather slots (float4) per thread
+  constexpr int DI = (TR / 2) * (O / 8);   // dy items: (row pair, 8 columns)
+  constexpr int DVI = (DI + NT - 1) / NT;  // dy items per thread
+  static_assert(O == 64 || O == 128, "x6 weight kernel: O in {64, 128}");
+  __shared__ __attribute__((aligned(16))) float gl[2][TR * KM * kCC];
+  __shared__ __attribute__((aligned(16))) bf16x8 dyp[3][O * NG];
+  __shared__ __attribute__((aligned(16))) bf16x8 atp[3][kNC * NG];
+  auto cidx = [](int x, int grp) { return x * NG + (grp ^ ((x >> 2) & (NG - 1))); };
+
+  const int L = blockIdx.x;
+  int ch, split;
+  if (xcd_map) {  // as pc_bwd_weight_kernel: a split's chunks share an XCD's L2
+    const int per_xcd = (int)gridDim.x >> 3;
+    const int pidx = (L & 7) * per_xcd + (L >> 3);
+    split = pidx / g.nch;
+    ch = pidx % g.nch;
+  } else {
+    ch = L % g.nch;
+    split = L / g.nch;
+  }
+  if (split >= nsplit) return;
+  const int c0 = ch * kCC;
+  const int kk = EX ? KM : g.k;
+  const int rbeg = split * rows_per_split;
+  const int rend = min(g.r, rbeg + rows_per_split);
+  const int ntiles = (rend - rbeg + TR - 1) / TR;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, half = lane >> 5, l32 = lane & 31;
+  const int w = t & (kW - 1), rp = t >> 4;  // build: WeightNet column w, rows 2 rp, 2 rp + 1
+  const long long c16 = (long long)g.c * kW;
+  const int tk = TR * kk;
+  const Srcs src = srcs_of(g);
+
+  const int h4 = t & 1;
+  float wr[2][KM], wc[2][KM];
+  float4 gr[GS];
+  float dr[DVI][2][8];
+  int nbi[GS];
+  constexpr int kNoNbr = 1 << 30;
+  const __amdgpu_buffer_rsrc_t idx_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<int*>(g.idx), (short)0, (int)((long long)g.r * g.k * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wt_rs = rsrc(wt, (long long)g.r * kk * kW);
+  const __amdgpu_buffer_rsrc_t dy_rs = rsrc(dy, (long long)g.r * O);
+  const float inv_s = 1.f / (float)g.s;
+  // neighbour indices one fetch ahead (as pc_bwd_weight_kernel)
+  auto fetch_idx = [&](int tile) {
+    const int row0 = rbeg + tile * TR;
+    const int b0 = row0 / g.s;
+    const int rr = row0 - b0 * g.s;
+#pragma unroll
+    for (int i = 0; i < GS; ++i) {
+      const int rk = (t >> 1) + (NT / 2) * i;
+      const int r = rk / kk;
+      const int rw = row0 + r;
+      const bool ok = rk < tk && rw < rend;
+      const int x = rr + r;
+      int q = (int)((float)x * inv_s);
+      q += ((q + 1) * g.s <= x ? 1 : 0) - (q * g.s > x ? 1 : 0);
+      const int base = ok ? (b0 + q) * g.n : kNoNbr;
+      const unsigned off = ok ? ((unsigned)rw * (unsigned)g.k + (unsigned)(rk - r * kk)) * 4u : kOOB;
+      nbi[i] = base + (int)__builtin_amdgcn_raw_buffer_load_b32(idx_rs, (int)off, 0, 0);
+    }
+  };
+  // WeightNet weights of rows 2 rp, 2 rp + 1 and the tile's gathered G (branch-free loads)
+  auto fetch_g = [&](int tile) {
+    const int row0 = rbeg + tile * TR;
+#pragma unroll
+    for (int p2 = 0; p2 < 2; ++p2) {
+      const int row = row0 + 2 * rp + p2;
+      const unsigned base = row < rend ? ((unsigned)row * (unsigned)kk * kW + w) * 4u : kOOB;
+#pragma unroll
+      for (int k = 0; k < KM; ++k) {
+        const unsigned off = k < kk ? base + (unsigned)(k * kW * 4) : kOOB;
+        wr[p2][k] = __builtin_bit_cast(
+            float, __builtin_amdgcn_raw_buffer_load_b32(wt_rs, (int)off, 0, 0));
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < GS; ++i) {
+      const int rk = (t >> 1) + (NT / 2) * i;
+      const int rw = row0 + rk / kk;
+      const int nb = nbi[i];
+      const bool live = (unsigned)nb < (unsigned)g.bn;
+      const bool xyz = c0 == 0 && h4 == 0;
+      const int vch = c0 == 0 ? (h4 ? 1 : 0) : c0 - 3 + 4 * h4;
+      const unsigned voff = live ? (unsigned)nb * (unsigned)g.d * 4u + (unsigned)vch * 4u : kOOB;
+      const unsigned xoff = (xyz && live) ? (unsigned)nb * 12u : kOOB;
+      const unsigned coff = (xyz && live) ? (unsigned)rw * 12u : kOOB;
+      const f32x4 v =
+          __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(src.feats, (int)voff, 0, 0));
+      const f32x4 x = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(src.xyz, (int)xoff, 0, 0));
+      const f32x4 cc = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(src.center, (int)coff, 0, 0));
+      const int cg = c0 + 4 * h4;
+      const float a0 = xyz ? 0.f : (cg < g.c ? v[0] : 0.f);
+      const float a1 = xyz ? 0.f : (cg + 1 < g.c ? v[1] : 0.f);
+      const float a2 = xyz ? 0.f : (cg + 2 < g.c ? v[2] : 0.f);
+      const float a3 = xyz ? (3 < g.c ? v[0] : 0.f) : (cg + 3 < g.c ? v[3] : 0.f);
+      gr[i] = make_float4(a0 + (x[0] - cc[0]), a1 + (x[1] - cc[1]), a2 + (x[2] - cc[2]), a3);
+    }
+    fetch_idx(tile + 1);
+  };
+  // dy item q = t + NT i: row pair q % (TR / 2) (consecutive threads: consecutive pairs, so
+  // the plane-word writes below fill consecutive banks), columns 8 (q / (TR / 2)) .. +7
+  auto fetch_dy = [&](int tile) {
+    const int row0 = rbeg + tile * TR;
+#pragma unroll
+    for (int i = 0; i < DVI; ++i) {
+      const int q = t + NT * i;
+      const int pr = q % (TR / 2), oc = q / (TR / 2);
+#pragma unroll
+      for (int p2 = 0; p2 < 2; ++p2) {
+        const int rw = row0 + 2 * pr + p2;
+        const unsigned off = (q < DI && rw < rend) ? ((unsigned)rw * O + 8u * (unsigned)oc) * 4u : kOOB;
+        const f32x4 lo = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(dy_rs, (int)off, 0, 0));
+        const f32x4 hi = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(dy_rs, (int)(off == kOOB ? kOOB : off + 16u), 0, 0));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          dr[i][p2][j] = lo[j];
+          dr[i][p2][4 + j] = hi[j];
+        }
+      }
+    }
+  };
+  auto stage_g = [&](float* gb) {
+#pragma unroll
+    for (int i = 0; i < GS; ++i) {
+      const int rk = (t >> 1) + (NT / 2) * i;
+      if (rk < tk) *reinterpret_cast<float4*>(gb + rk * kCC + 4 * h4) = gr[i];
+    }
+#pragma unroll
+    for (int p2 = 0; p2 < 2; ++p2)
+#pragma unroll
+      for (int k = 0; k < KM; ++k) wc[p2][k] = wr[p2][k];
+  };
+  auto stage_dy = [&]() {
+#pragma unroll
+    for (int i = 0; i < DVI; ++i) {
+      const int q = t + NT * i;
+      if (q < DI) {
+        const int pr = q % (TR / 2), oc = q / (TR / 2);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          unsigned h, m, l;
+          split_pair(dr[i][0][j], dr[i][1][j], h, m, l);
+          const int o = 8 * oc + j;
+          unsigned* base = reinterpret_cast<unsigned*>(dyp[0]);
+          const int word = cidx(o, pr >> 2) * 4 + (pr & 3);
+          base[word] = h;
+          reinterpret_cast<unsigned*>(dyp[1])[word] = m;
+          reinterpret_cast<unsigned*>(dyp[2])[word] = l;
+        }
+      }
+    }
+  };
+  // bias gradient for free (as pc_bwd_weight_kernel): the first padding column of the last
+  // chunk is set to 1 (planes 1, 0, 0: exact)
+  const int ones_col = (dbias != nullptr && ch == g.nch - 1 && g.c % kCC != 0)
+                           ? (g.c % kCC) * kW : -1;
+  auto build = [&](const float* gb) {
+    float a[2][kCC];
+    build_row<KM>(gb, 2 * rp, kk, wc[0], a[0]);
+    build_row<KM>(gb, 2 * rp + 1, kk, wc[1], a[1]);
+#pragma unroll
+    for (int c = 0; c < kCC; ++c) {
+      const int col = c * kW + w;
+      unsigned h, m, l;
+      split_pair(a[0][c], a[1][c], h, m, l);
+      if (col == ones_col) {  // 1.0 in both rows: planes (1, 0, 0)
+        h = 0x3F803F80u;
+        m = 0u;
+        l = 0u;
+      }
+      const int word = cidx(col, rp >> 2) * 4 + (rp & 3);
+      reinterpret_cast<unsigned*>(atp[0])[word] = h;
+      reinterpret_cast<unsigned*>(atp[1])[word] = m;
+      reinterpret_cast<unsigned*>(atp[2])[word] = l;
+    }
+  };
+
+  f32x16 acc[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) acc[i] = zero16();
+  if (ntiles <= 0) return;
+  // prologue: tile 0 built (A planes), dy of tile 0 split, G of tile 1 in gl[1]
+  fetch_idx(0);
+  fetch_g(0);
+  fetch_dy(0);
+  stage_g(gl[0]);
+  stage_dy();
+  fetch_g(1);
+  __syncthreads();
+  build(gl[0]);
+  stage_g(gl[1]);
+  __syncthreads();
+  const int col = wv * 32 + l32;  // this lane's A column (B operand) of the chunk
+  for (int tile = 0; tile < ntiles; ++tile) {
+    // loads of tile+2's G / weights and tile+1's dy land under this tile's MFMAs
+    fetch_g(tile + 2);
+    fetch_dy(tile + 1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int bi = cidx(col, 2 * ks + half);
+      const bf16x8 bh = atp[0][bi], bm = atp[1][bi], bl = atp[2][bi];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int ai = cidx(m * 32 + l32, 2 * ks + half);
+        acc[m] = mfma_x6(dyp[0][ai], dyp[1][ai], dyp[2][ai], bh, bm, bl, acc[m]);
+      }
+    }
+    __syncthreads();  // atp / dyp consumed
+    build(gl[(tile + 1) & 1]);  // tile + 1 (G staged one iteration ago, weights in wc)
+    stage_dy();                 // tile + 1
+    stage_g(gl[tile & 1]);      // tile + 2 (G of tile: built last iteration)
+    __syncthreads();
+  }
+  const long long cc16 = (long long)c0 * kW + col;
+  if (ones_col >= 0 && col == ones_col) {
+    float* bd = dbias + (long long)split * O;  // slab index when the rows are split
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) bd[i * 32 + (e & 3) + 8 * (e >> 2) + 4 * half] = acc[i][e];
+  }
+  if (cc16 >= c16) return;
+  float* dst = dwl + (long long)split * O * c16;  // slab index when the rows are split
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int o = i * 32 + (e & 3) + 8 * (e >> 2) + 4 * half;
+      dst[o * c16 + cc16] = acc[i][e];
+    }
+}
+
 // ------------------------------------------------------------------------------- host
 struct Plan {
   int r, c, nch, c8, tm, rt;  // tm: forward tile rows
@@ -1600,12 +1869,21 @@ hipError_t bwd_weight_launch(const Geo& g, const Plan& p, const float* wt, const
   // bias slab after the dwl slabs (kdpc_pointconv_bwd_weight_workspace_bytes)
   float* bias_slab = reinterpret_cast<float*>(ws + p.dwl_slab);
   float* bdst = dbias == nullptr ? nullptr : (p.rs > 1 ? bias_slab : dbias);
-  if (g.k == KM)
-    hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM, true>), dim3(p.wgs), dim3(wgt_threads(O)), 0, st, g, wt,
-                       dy, wdst, p.rps, p.rs, p.xcd, bdst);
-  else
-    hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM, false>), dim3(p.wgs), dim3(wgt_threads(O)), 0, st, g, wt,
-                       dy, wdst, p.rps, p.rs, p.xcd, bdst);
+  if constexpr (O <= 128) {  // split-bf16 MFMAs, 256 threads (wgt_threads)
+    if (g.k == KM)
+      hipLaunchKernelGGL((pc_bwd_weight_x6_kernel<O, KM, true>), dim3(p.wgs), dim3(256), 0, st, g,
+                         wt, dy, wdst, p.rps, p.rs, p.xcd, bdst);
+    else
+      hipLaunchKernelGGL((pc_bwd_weight_x6_kernel<O, KM, false>), dim3(p.wgs), dim3(256), 0, st, g,
+                         wt, dy, wdst, p.rps, p.rs, p.xcd, bdst);
+  } else {
+    if (g.k == KM)
+      hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM, true>), dim3(p.wgs), dim3(wgt_threads(O)), 0,
+                         st, g, wt, dy, wdst, p.rps, p.rs, p.xcd, bdst);
+    else
+      hipLaunchKernelGGL((pc_bwd_weight_kernel<O, KM, false>), dim3(p.wgs), dim3(wgt_threads(O)), 0,
+                         st, g, wt, dy, wdst, p.rps, p.rs, p.xcd, bdst);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || p.rs == 1) return e;
   if ((e = slab_sum(p.rs, (long long)O * g.c * kW, dwl_slab, nullptr, 1, dwl, st)) != hipSuccess)
