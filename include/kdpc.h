@@ -286,7 +286,8 @@ int kdpc_pointconv_supported(int k, int d, int o);
 /* y (B,S,O) = A wl^T + bias,  A[b,s, c*16+w] = sum_k G[b,s,k,c] wt[b,s,k,w],
  * G = cat(xyz[idx] - center, feats[idx]) (C = 3+D channels); A is never stored.
  * xyz (B,N,3), center (B,S,3), feats (B,N,D), idx (B,S,K) int32, wt (B,S,K,16),
- * wl (O, 16C) (nn.Linear weight), bias (O).  workspace: *_fwd_workspace_bytes (may be 0). */
+ * wl (O, 16C) (nn.Linear weight), bias (O).  workspace: *_fwd_workspace_bytes (> 0: wl split
+ * into the bf16 planes the kernel multiplies on the bf16 matrix cores, f32-accurate). */
 size_t kdpc_pointconv_fwd_workspace_bytes(int b, int s, int k, int d, int o);
 int kdpc_pointconv_fwd(int b, int n, int s, int k, int d, int o, const float *xyz,
                        const float *center, const float *feats, const int *idx, const float *wt,

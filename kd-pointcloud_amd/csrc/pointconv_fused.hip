@@ -44,9 +44,14 @@ namespace {
 // TP: the tile's rows come from the backward's tile plan (g.trow: Morton-ordered 32-row
 // tiles, two per 64-row forward tile), so a tile's neighbour gathers hit few distinct points;
 // every row's arithmetic is unchanged (bit-identical outputs).
+// The Linear runs on the bf16 matrix cores (mfma_x6, f32 accuracy): each builder thread's
+// 8 values of A (row r, WeightNet column w, the chunk's 8 channels) are one 16-byte chunk of
+// each bf16 plane, so the MFMA inner index of K-step ks / lane half h is (channel j, column
+// w = 2 ks + h) -- any inner order gives the same product -- and wl's B planes come
+// pre-split in that order (pc_swizzle_fwd3_kernel).
 template <int O, int KM, bool EX, bool TP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
-void pc_fwd_kernel(Geo g, const float* __restrict__ wt, const float* __restrict__ wl,
+void pc_fwd_kernel(Geo g, const float* __restrict__ wt, const bf16x8* __restrict__ wsf,
                    const float* __restrict__ bias, float* __restrict__ y,
                    float* __restrict__ slab, int chunks_per_split) {
   constexpr int MT = KM <= 9 ? 2 : 1;
@@ -54,13 +59,16 @@ void pc_fwd_kernel(Geo g, const float* __restrict__ wt, const float* __restrict_
   constexpr int NT = O / 32;
   constexpr bool SPLIT_M = (MT == 2 && NT < 4);   // O = 64: waves split the two row tiles
   constexpr int KG = (MT * NT < 4) ? 4 / (MT * NT) : 1;  // O = 64, 32 rows: waves split the
-                                                           // chunk's inner index in KG groups
+                                                           // chunk's K-steps in KG groups
   constexpr int MPW = (MT == 2 && !SPLIT_M) ? 2 : 1;
   constexpr int NPW = KG > 1 ? 1 : (MT * NT / 4) / MPW;
   constexpr int RPT = TM / 16;                    // builder rows per thread
   constexpr int GS = (TM * KM + 127) / 128;       // gather slots (float4) per thread
+  constexpr int NKS = 8 / KG;                     // 16-deep K-steps per wave and chunk
+  constexpr int PF = NKS < 2 ? NKS : 2;           // K-steps of B planes issued ahead
   __shared__ __attribute__((aligned(16))) float gl[TM * KM * kCC];
-  __shared__ __attribute__((aligned(16))) float al[MT][(kNC / 4) * kBlk];
+  // A planes: per 32-row tile, row r's chunk w at r * 16 + (w ^ (r & 15))
+  __shared__ __attribute__((aligned(16))) bf16x8 alp[MT][3][32 * kW];
 
   const int row0 = blockIdx.x * TM;
   // global row of tile row r, -1 for none
@@ -76,13 +84,10 @@ void pc_fwd_kernel(Geo g, const float* __restrict__ wt, const float* __restrict_
   const int ch0 = split * chunks_per_split;
   const int ch1 = min(g.nch, ch0 + chunks_per_split);
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, half = lane >> 5, l32 = lane & 31;
-  const int w = t & (kW - 1), rr = t >> 4, cs = t & (kCC - 1);
+  const int w = t & (kW - 1), rr = t >> 4;
   const int m0 = SPLIT_M ? (wv >> 1) : 0;
   const int n0 = SPLIT_M ? (wv & 1) : (KG > 1 ? wv % (4 / KG) : wv * NPW);
   const int kgrp = KG > 1 ? wv / (4 / KG) : 0;
-  constexpr int GB = 16 / KG;  // 8-column blocks per wave and chunk
-  constexpr int PF = NPW > 1 ? 4 : (KM <= 9 ? (GB < 6 ? GB : 6) : GB);  // B blocks issued ahead of the gathers
-  const long long c16 = (long long)g.c * kW;
   const int tk = TM * kk;
 
   float wr[RPT][KM];
@@ -119,36 +124,33 @@ void pc_fwd_kernel(Geo g, const float* __restrict__ wt, const float* __restrict_
 
   for (int ch = ch0; ch < ch1; ++ch) {
     const int c0 = ch * kCC;
-    __syncthreads();  // previous chunk's MFMAs are done with al; gl is free
+    __syncthreads();  // previous chunk's MFMAs are done with alp; gl is free
 #pragma unroll
     for (int i = 0; i < GS; ++i) {
       const int rk = (t >> 1) + 128 * i;
       if (rk < tk) *reinterpret_cast<float4*>(gl + rk * kCC + 4 * h4) = gr[i];
     }
     __syncthreads();
-    // The chunk's Linear-weight fragments (MFMA B operand, served from L2): the first PF
-    // of its GB blocks are issued now and land while the A block is built; each later
-    // one is issued PF blocks ahead of its MFMAs.
-    const float* wrow[NPW];
+    // The chunk's B planes (served from L2): the first PF K-steps are issued now and land
+    // while the A block is built; each later one PF K-steps ahead of its MFMAs.
+    const bf16x8* brow[NPW];
 #pragma unroll
-    for (int j = 0; j < NPW; ++j) wrow[j] = wl + ((long long)((n0 + j) * 32 + l32)) * c16;
-    const int gbeg = kgrp * GB;
-    // unconditional load (a clamped address) + select: no branch around the load, so the
-    // compiler can count outstanding loads exactly (a branchy load forces vmcnt(0))
-    auto bfrag = [&](int gb, int j) -> float4 {
-      const bool ok = c0 + (gb >> 1) < g.c;
-      const float4 v =
-          *reinterpret_cast<const float4*>(wrow[j] + (ok ? c0 * kW + 8 * gb + 4 * half : 0));
-      return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int j = 0; j < NPW; ++j)
+      brow[j] = wsf + ((long long)(ch * NT + n0 + j) * 8 * 3) * 64 + lane;
+    const int kbeg = kgrp * NKS;
+    auto bload = [&](int ks, int j, Planes& b) {
+      b.h = brow[j][(3 * ks + 0) * 64];
+      b.m = brow[j][(3 * ks + 1) * 64];
+      b.l = brow[j][(3 * ks + 2) * 64];
     };
-    float4 bq[PF][NPW];
+    Planes bq[PF][NPW];
 #pragma unroll
     for (int p2 = 0; p2 < PF; ++p2)
 #pragma unroll
-      for (int j = 0; j < NPW; ++j) bq[p2][j] = bfrag(gbeg + p2, j);
+      for (int j = 0; j < NPW; ++j) bload(kbeg + p2, j, bq[p2][j]);
     // next chunk's gather (feature channels only), in flight during build + MFMA.  Issued
-    // AFTER the B fragments: vmcnt retires loads in issue order, so an MFMA waiting on a
-    // B fragment issued after the gathers would wait for the gathers too.
+    // AFTER the B planes: vmcnt retires loads in issue order, so an MFMA waiting on a
+    // B plane issued after the gathers would wait for the gathers too.
     // (issued on the last chunk too -- the values are unused there -- so the loop body is
     // straight-line code and the compiler's load counting stays exact)
     {
@@ -168,39 +170,31 @@ void pc_fwd_kernel(Geo g, const float* __restrict__ wt, const float* __restrict_
       const int r = rr + 16 * q;
       float a[kCC];
       build_row<KM>(gl, r, kk, wr[q], a);
-      float* at = al[r >> 5] + (r & 31) * 4;
-#pragma unroll
-      for (int c = 0; c < kCC; ++c) {
-        const int col = c * kW + w;
-        at[(col >> 2) * kBlk + (col & 3)] = a[c];
-      }
+      const Planes pl = split8(a);
+      const int rt = r & 31, cix = rt * kW + (w ^ (rt & 15));
+      alp[r >> 5][0][cix] = pl.h;
+      alp[r >> 5][1][cix] = pl.m;
+      alp[r >> 5][2][cix] = pl.l;
       __builtin_amdgcn_sched_barrier(0);  // keep the rows' LDS reads from piling up
     }
     __syncthreads();
-    // GB blocks of 8 inner indices; the A fragments are read from LDS one block ahead
-    float4 avc[MPW], avn[MPW];
 #pragma unroll
-    for (int i = 0; i < MPW; ++i)
-      avc[i] = *reinterpret_cast<const float4*>(al[m0 + i] + (2 * gbeg + half) * kBlk + l32 * 4);
+    for (int s2 = 0; s2 < NKS; ++s2) {
+      const int ks = kbeg + s2;
+      const int cw = 2 * ks + half;  // WeightNet column of this K-step's lane half
 #pragma unroll
-    for (int gi = 0; gi < GB; ++gi) {
-      const int gb = gbeg + gi;
-      if (gi + 1 < GB) {
+      for (int i = 0; i < MPW; ++i) {
+        const int cix = l32 * kW + (cw ^ (l32 & 15));
+        const bf16x8 ah = alp[m0 + i][0][cix], am = alp[m0 + i][1][cix], al = alp[m0 + i][2][cix];
 #pragma unroll
-        for (int i = 0; i < MPW; ++i)
-          avn[i] = *reinterpret_cast<const float4*>(al[m0 + i] + (2 * gb + 2 + half) * kBlk +
-                                                    l32 * 4);
+        for (int j = 0; j < NPW; ++j)
+          acc[i][j] = mfma_x6(ah, am, al, bq[s2 % PF][j].h, bq[s2 % PF][j].m, bq[s2 % PF][j].l,
+                              acc[i][j]);
       }
+      if (s2 + PF < NKS) {
 #pragma unroll
-      for (int i = 0; i < MPW; ++i)
-#pragma unroll
-        for (int j = 0; j < NPW; ++j) acc[i][j] = mfma4(avc[i], bq[gi % PF][j], acc[i][j]);
-      if (gi + PF < GB) {
-#pragma unroll
-        for (int j = 0; j < NPW; ++j) bq[gi % PF][j] = bfrag(gb + PF, j);
+        for (int j = 0; j < NPW; ++j) bload(ks + PF, j, bq[s2 % PF][j]);
       }
-#pragma unroll
-      for (int i = 0; i < MPW; ++i) avc[i] = avn[i];
     }
   }
 
@@ -236,6 +230,36 @@ void pc_fwd_kernel(Geo g, const float* __restrict__ wt, const float* __restrict_
             y[(long long)row * O + n] = __fadd_rn(acc[i][j][e], bn);
         }
       }
+  }
+}
+
+// wl (O, 16C) -> the forward's B planes (mfma_x6): bf16x8 (ch, n tile nb, ks, plane, lane) =
+// plane {h, m, l} of wl[nb * 32 + (lane & 31)][ch * 128 + 16 j + 2 ks + (lane >> 5)], j = 0..7,
+// zero past column 16C.  One thread per (ch, nb, ks, lane).
+__global__ __launch_bounds__(256) void pc_swizzle_fwd3_kernel(int o, int c16, int nch,
+                                                              const float* __restrict__ wl,
+                                                              bf16x8* __restrict__ wsf) {
+  const long long total = (long long)nch * (o / 32) * 8 * 64;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int lane = (int)(e & 63);
+    const long long q = e >> 6;  // (ch * NT + nb) * 8 + ks
+    const int ks = (int)(q & 7);
+    const long long cn = q >> 3;
+    const int nt = o / 32;
+    const int nb = (int)(cn % nt), ch = (int)(cn / nt);
+    const float* src = wl + (long long)(nb * 32 + (lane & 31)) * c16;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = ch * 128 + 16 * j + 2 * ks + (lane >> 5);
+      v[j] = col < c16 ? src[col] : 0.f;
+    }
+    const Planes p = split8(v);
+    bf16x8* dst = wsf + (q * 3) * 64 + lane;
+    dst[0] = p.h;
+    dst[64] = p.m;
+    dst[128] = p.l;
   }
 }
 
@@ -1691,7 +1715,7 @@ struct Plan {
   int ks, cps;                 // fwd channel splits / chunks per split
   int bks, bcps;               // bwd-data channel splits (32-row tiles)
   int rs, rps, xcd, wgs;       // bwd-weight row splits, rows per split, XCD map, grid
-  size_t fwd_slab, dgr, dwt_slab, dwl_slab, wlt;  // bytes
+  size_t fwd_slab, fwd_wsf, dgr, dwt_slab, dwl_slab, wlt;  // bytes
 };
 
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -1762,6 +1786,8 @@ bool plan_of(int b, int s, int k, int d, int o, Plan* p, int wcus = kCUs) {
   p->wgs = divup(p->nch * p->rs, 8) * 8;  // XCD fill: a multiple of 8 workgroups
   const size_t c16 = (size_t)p->c * kW;
   p->fwd_slab = p->ks > 1 ? align256((size_t)p->ks * p->r * o * 4) : 0;
+  // the forward's B planes (pc_swizzle_fwd3_kernel): (nch, O/32, 8 K-steps, 3 planes) x 1 KB
+  p->fwd_wsf = align256((size_t)p->nch * (o / 32) * 8 * 3 * 64 * 16);
   // dG rows: one per pair, or (tiled) one per (32-row tile, destination): at most 32K per
   // tile, tiles per batch element
   p->dgr = align256((size_t)b * divup(s, 32) * 32 * k * p->c8 * 4);
@@ -1780,22 +1806,30 @@ hipError_t slab_sum(int nslabs, long long len, const float* slab, const float* b
   return hipGetLastError();
 }
 
+// workspace: [B planes of wl (p.fwd_wsf) | channel-split slabs (p.fwd_slab)]
 template <int O, int KM>
 hipError_t fwd_launch(const Geo& g, const Plan& p, const float* wt, const float* wl,
-                      const float* bias, float* y, float* slab, hipStream_t st) {
+                      const float* bias, float* y, char* ws, hipStream_t st) {
+  bf16x8* wsf = reinterpret_cast<bf16x8*>(ws);
+  float* slab = reinterpret_cast<float*>(ws + p.fwd_wsf);
   float* sl = p.ks > 1 ? slab : nullptr;
+  const long long nsw = (long long)g.nch * (O / 32) * 8 * 64;
+  hipLaunchKernelGGL(pc_swizzle_fwd3_kernel, dim3((unsigned)divupll(nsw, 256)), dim3(256), 0, st,
+                     O, g.c * kW, g.nch, wl, wsf);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
   if (g.trow) {  // tiled plan: exact-K only (the estimators' K = 9)
     const unsigned rt = (unsigned)divup(g.ntrow, p.tm);
     hipLaunchKernelGGL((pc_fwd_kernel<O, KM, true, true>), dim3(rt, p.ks), dim3(256), 0, st, g,
-                       wt, wl, bias, y, sl, p.cps);
+                       wt, wsf, bias, y, sl, p.cps);
   } else if (g.k == KM) {
     hipLaunchKernelGGL((pc_fwd_kernel<O, KM, true, false>), dim3(p.rt, p.ks), dim3(256), 0, st, g,
-                       wt, wl, bias, y, sl, p.cps);
+                       wt, wsf, bias, y, sl, p.cps);
   } else {
     hipLaunchKernelGGL((pc_fwd_kernel<O, KM, false, false>), dim3(p.rt, p.ks), dim3(256), 0, st,
-                       g, wt, wl, bias, y, sl, p.cps);
+                       g, wt, wsf, bias, y, sl, p.cps);
   }
-  hipError_t e = hipGetLastError();
+  e = hipGetLastError();
   if (e != hipSuccess || p.ks == 1) return e;
   return slab_sum(p.ks, (long long)p.r * O, slab, bias, O, y, st);
 }
@@ -1942,7 +1976,7 @@ KDPC_API int kdpc_pointconv_supported(int k, int d, int o) {
 
 KDPC_API size_t kdpc_pointconv_fwd_workspace_bytes(int b, int s, int k, int d, int o) {
   Plan p;
-  return plan_of(b, s, k, d, o, &p) ? p.fwd_slab : 0;
+  return plan_of(b, s, k, d, o, &p) ? p.fwd_wsf + p.fwd_slab : 0;
 }
 
 KDPC_API int kdpc_pointconv_fwd(int b, int n, int s, int k, int d, int o, const float* xyz,
@@ -1953,11 +1987,11 @@ KDPC_API int kdpc_pointconv_fwd(int b, int n, int s, int k, int d, int o, const 
   KDPC_CHECK_ARG(n > 0 && b <= 65535 && plan_of(b, s, k, d, o, &p) && fits_buffers(b, n, s, d));
   if (p.r == 0) return (int)hipSuccess;
   KDPC_CHECK_ARG(xyz && center && idx && wt && wl && bias && y && (d == 0 || feats));
-  KDPC_CHECK_ARG(workspace_bytes >= p.fwd_slab && (p.fwd_slab == 0 || workspace));
+  KDPC_CHECK_ARG(workspace && workspace_bytes >= p.fwd_wsf + p.fwd_slab);
   const Geo g = geo_of(b, n, s, k, d, p, xyz, center, feats, idx);
-  float* slab = reinterpret_cast<float*>(workspace);
+  char* ws = reinterpret_cast<char*>(workspace);
   hipStream_t st = (hipStream_t)stream;
-  return (int)KDPC_PC_DISPATCH(fwd_launch, g, p, wt, wl, bias, y, slab, st);
+  return (int)KDPC_PC_DISPATCH(fwd_launch, g, p, wt, wl, bias, y, ws, st);
 }
 
 KDPC_API size_t kdpc_pointconv_bwd_workspace_bytes(int b, int s, int k, int d, int o) {
@@ -2107,13 +2141,13 @@ KDPC_API int kdpc_pointconv_fwd_tiled(int b, int n, int s, int k, int d, int o, 
   KDPC_CHECK_ARG(k == km_of(k) && ntrow >= 0 && ntrow == b * divup(s, 32) * 32);
   if (p.r == 0) return (int)hipSuccess;
   KDPC_CHECK_ARG(xyz && center && idx && wt && wl && bias && y && trow && (d == 0 || feats));
-  KDPC_CHECK_ARG(workspace_bytes >= p.fwd_slab && (p.fwd_slab == 0 || workspace));
+  KDPC_CHECK_ARG(workspace && workspace_bytes >= p.fwd_wsf + p.fwd_slab);
   Geo g = geo_of(b, n, s, k, d, p, xyz, center, feats, idx);
   g.trow = trow;
   g.ntrow = ntrow;
-  float* slab = reinterpret_cast<float*>(workspace);
+  char* ws = reinterpret_cast<char*>(workspace);
   hipStream_t st = (hipStream_t)stream;
-  return (int)KDPC_PC_DISPATCH(fwd_launch, g, p, wt, wl, bias, y, slab, st);
+  return (int)KDPC_PC_DISPATCH(fwd_launch, g, p, wt, wl, bias, y, ws, st);
 }
 
 // Weight half plus the bias gradient (column sums of dy) from the same MFMAs: a padding
