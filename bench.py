@@ -39,6 +39,11 @@ import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK_TF = 157.3  # dense f32 MFMA peak (MI355X_MICROARCH.md, F32 row)
+# The PointConv kernels run their f32 GEMMs as six bf16 MFMAs per product (three-plane split,
+# f32-accurate): their own ceiling is the dense bf16 rate / 6 (2.52 PF: 32 cycles
+# per 32x32x16 MFMA per SIMD at 2.4 GHz), reported beside the f32 peak the roofline keeps.
+SPLIT_BF16_PEAK_TF = round(2 * 32 * 32 * 16 / 32 * 1024 * 2.4e9 / 1e12 / 6, 1)
+SPLIT_BF16_ENTRIES = ("kdpc_pointconv_bwd", "kdpc_pointconv_fwd")
 FP32_VALU_PEAK_TF = 157.3  # f32 vector peak (same table)
 
 # C entry point -> (bound, unit, peak, HIP kernels it launches).  An entry point is the unit
@@ -46,13 +51,14 @@ FP32_VALU_PEAK_TF = 157.3  # f32 vector peak (same table)
 # durations per entry launch to cross-check the live average.
 ROOFLINE = {
     "kdpc_pointconv_bwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF,
-                           # first name: one launch per entry call (tools count launches by it)
-                           ["pc_swizzle_bwd_kernel", "pc_bwd_data_kernel",
-                            "pc_bwd_data_pipe_kernel",
-                            "pc_csr_sum_kernel", "pc_bwd_weight_kernel",
-                            "pc_slab_sum_kernel"]),
+                           # first name: one launch per entry call (tools count launches by it;
+                           # the K <= 9 data path swizzles through pc_swizzle_bwd3_kernel)
+                           ["pc_csr_sum_kernel", "pc_swizzle_bwd_kernel",
+                            "pc_swizzle_bwd3_kernel", "pc_bwd_data_kernel",
+                            "pc_bwd_data_pipe_kernel", "pc_bwd_weight_kernel",
+                            "pc_bwd_weight_x6_kernel", "pc_slab_sum_kernel"]),
     "kdpc_pointconv_fwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF,
-                           ["pc_fwd_kernel", "pc_slab_sum_kernel"]),
+                           ["pc_fwd_kernel", "pc_swizzle_fwd3_kernel", "pc_slab_sum_kernel"]),
     "kdpc_group_rows": ("hbm", "GB/s", HBM_PEAK_GBS, ["group_rows_kernel"]),
     "kdpc_group_points": ("hbm", "GB/s", HBM_PEAK_GBS, ["group_points_lds_kernel",
                                                          "group_points_kernel",
@@ -162,6 +168,10 @@ def roofline_obj(entry, workload, ms, launches, nbytes, flops, bound=None, **ext
            "algorithmic_bytes_per_launch": round(nbytes / launches),
            "algorithmic_flops_per_launch": round(flops / launches),
            "traffic_source": os.path.relpath(PMC_FILE, ROOT)}
+    if entry in SPLIT_BF16_ENTRIES and bound == "mfma":
+        out["matrix_path"] = "f32 products as 6 bf16 MFMAs (three-plane split)"
+        out["peak_split_bf16"] = SPLIT_BF16_PEAK_TF
+        out["frac_split_bf16"] = round(achieved / SPLIT_BF16_PEAK_TF, 4)
     out.update(extra)
     return out
 
