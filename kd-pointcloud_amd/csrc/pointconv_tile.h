@@ -56,7 +56,7 @@ __device__ __forceinline__ f32x16 mfma4(float4 a, float4 b, f32x16 c) {
 // as the six plane products of order <= 2^-16 (al bh + am bm + ah bl + am bh + ah bm + ah bh,
 // exact products, f32 accumulation): 6 bf16 MFMAs (6 x 32 cycles per 32x32x16 block) for the
 // 8 f32 MFMAs (8 x 64 cycles) of the same block, at f32 accuracy (a 32x32x128 product: max
-// error 2.7-4.0e-7 of max|C| vs 2.6-4.5e-7 on the f32 MFMA, tools/scratch bf16probe).
+// error 2.7-4.0e-7 of max|C| vs 2.6-4.5e-7 on the f32 MFMA, tools/probe_bf16.hip).
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 struct Planes {
