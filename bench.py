@@ -51,10 +51,9 @@ FP32_VALU_PEAK_TF = 157.3  # f32 vector peak (same table)
 # durations per entry launch to cross-check the live average.
 ROOFLINE = {
     "kdpc_pointconv_bwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF,
-                           # first name: one launch per entry call (tools count launches by it;
-                           # the K <= 9 data path swizzles through pc_swizzle_bwd3_kernel)
-                           ["pc_csr_sum_kernel", "pc_swizzle_bwd_kernel",
-                            "pc_swizzle_bwd3_kernel", "pc_bwd_data_kernel",
+                           # first name: one launch per entry call (tools count launches by it)
+                           ["pc_csr_sum_kernel", "pc_swizzle_bwd3_kernel",
+                            "pc_bwd_data_kernel",
                             "pc_bwd_data_pipe_kernel", "pc_bwd_weight_kernel",
                             "pc_bwd_weight_x6_kernel", "pc_slab_sum_kernel"]),
     "kdpc_pointconv_fwd": ("mfma", "TFLOP/s", FP32_MFMA_PEAK_TF,

@@ -296,7 +296,7 @@ constexpr int bwd_threads() { return 256; }
 
 template <int O, int KM>
 __global__ __launch_bounds__(bwd_threads<KM>()) __attribute__((amdgpu_waves_per_eu(2)))
-void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __restrict__ wsw,
+void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const bf16x8* __restrict__ wsw,
                         const float* __restrict__ dy, float* __restrict__ dgr,
                         float* __restrict__ dwt, float* __restrict__ dcenter,
                         int chunks_per_split) {
@@ -310,7 +310,11 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
   constexpr int XP = TR * KM - PP * NT;
   constexpr bool XI = XP > 0;
   static_assert(PP >= 1 && (!XI || XP * kCC == NT), "left-over pairs must fill one item/thread");
-  __shared__ __attribute__((aligned(16))) float dyl[(O / 4) * kBlk];
+  // dy as three bf16 planes (dA on the bf16 matrix cores, mfma_x6; layout as
+  // pc_bwd_data_pipe_kernel's)
+  constexpr int DCH = O / 8;
+  constexpr int SW = (DCH < 16 ? DCH : 16) - 1;
+  __shared__ __attribute__((aligned(16))) bf16x8 dyp[3][32 * DCH];
   __shared__ __attribute__((aligned(16))) float dal[32 * kDaS];
   __shared__ float dcl[TR * KM * 3];
   const int row0 = blockIdx.x * TR;
@@ -322,11 +326,25 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
   const long long rk_total = (long long)g.r * g.k;
   const Srcs src = srcs_of(g);
 
-  for (int e = t; e < 32 * O; e += NT) {
-    const int r = e / O, o = e % O;
+  for (int e = t; e < 32 * DCH; e += NT) {
+    const int r = e / DCH, c = e % DCH;
     const int row = row0 + r;
-    dyl[(o >> 2) * kBlk + r * 4 + (o & 3)] =
-        (r < TR && row < g.r) ? dy[(long long)row * O + o] : 0.f;
+    float v[8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float4 x = (r < TR && row < g.r)
+                           ? reinterpret_cast<const float4*>(dy + (long long)row * O)[2 * c + h]
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[4 * h + 0] = x.x;
+      v[4 * h + 1] = x.y;
+      v[4 * h + 2] = x.z;
+      v[4 * h + 3] = x.w;
+    }
+    const Planes pl = split8(v);
+    const int cix = r * DCH + (c ^ (r & SW));
+    dyp[0][cix] = pl.h;
+    dyp[1][cix] = pl.m;
+    dyp[2][cix] = pl.l;
   }
   float wp[PP][kW], dw[PP][kW];
   int pr[PP], pk[PP], pn[PP], ps[PP];
@@ -391,16 +409,20 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
   // PF B blocks and the neighbour gathers of chunk ch+1 are issued right after chunk ch's
   // MFMAs -- before ch's dG stores -- so ch+1's first MFMAs wait only on those, and the
   // gathers land during ch's VALU phase (they are used in ch+1's VALU phase).
-  // B operand = the Linear weight columns of the chunk over the O outputs, pre-swizzled by
-  // pc_swizzle_bwd_kernel into the order the waves read them: one wave's fragment of one
-  // 8-output group is 1 KiB contiguous (a transposed (16C, O) copy, read a float4 per lane
-  // from 32 different rows, fetched 2x its bytes from L2); zero past the last column.
-  constexpr int NOG = O / 8;
-  constexpr int PF = NOG < 4 ? NOG : 4;  // (16 ahead measured slower: 949 vs 854 us)
+  // B operand = the Linear weight columns of the chunk over the O outputs as bf16 planes,
+  // pre-split by pc_swizzle_bwd3_kernel into the order the waves read them (one wave's
+  // plane of one K-step is 1 KiB contiguous); zero past the last column.
+  constexpr int NKS = O / 16;
+  constexpr int PF = NKS < 2 ? NKS : 2;
   auto brow = [&](int ch) {
-    return wsw + (long long)((ch * 4 + n0 / 32) * NOG) * 64 + lane;
+    return wsw + (long long)((ch * 4 + n0 / 32) * NKS * 3) * 64 + lane;
   };
-  float4 bq[PF];
+  auto bload = [&](const bf16x8* wr, int ks, Planes& b) {
+    b.h = wr[(3 * ks + 0) * 64];
+    b.m = wr[(3 * ks + 1) * 64];
+    b.l = wr[(3 * ks + 2) * 64];
+  };
+  Planes bq[PF];
   float gv[PP][kCC], gn[PP][kCC];
   // a pair's 8 channels of a chunk: two 16-byte buffer loads of its neighbour's feature row
   // (dword-aligned; past-the-row lanes masked, past-the-buffer reads 0), plus, for chunk 0,
@@ -437,9 +459,9 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
     }
   };
   if (ch0 < ch1) {
-    const float4* wr0 = brow(ch0);
+    const bf16x8* wr0 = brow(ch0);
 #pragma unroll
-    for (int p2 = 0; p2 < PF; ++p2) bq[p2] = wr0[p2 * 64];
+    for (int p2 = 0; p2 < PF; ++p2) bload(wr0, p2, bq[p2]);
     gather(ch0, gv);
     if constexpr (XI) xg = gather_x(ch0);
   }
@@ -460,21 +482,22 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
   };
   for (int ch = ch0; ch < ch1; ++ch) {
     const int c0 = ch * kCC;
-    const float4* wrow = brow(ch);
+    const bf16x8* wrow = brow(ch);
     f32x16 acc = zero16();
     if (mw) {  // wave-uniform
 #pragma unroll
-      for (int og = 0; og < NOG; ++og) {
-        const float4 av = *reinterpret_cast<const float4*>(dyl + (2 * og + half) * kBlk + l32 * 4);
-        acc = mfma4(av, bq[og % PF], acc);
-        if (og + PF < NOG) bq[og % PF] = wrow[(og + PF) * 64];
+      for (int ks = 0; ks < NKS; ++ks) {
+        const int cix = l32 * DCH + ((2 * ks + half) ^ (l32 & SW));
+        acc = mfma_x6(dyp[0][cix], dyp[1][cix], dyp[2][cix], bq[ks % PF].h, bq[ks % PF].m,
+                      bq[ks % PF].l, acc);
+        if (ks + PF < NKS) bload(wrow, ks + PF, bq[ks % PF]);
       }
     }
     if (ch > ch0) store_dg(ch - 1);
     if (ch + 1 < ch1) {
-      const float4* wr1 = brow(ch + 1);
+      const bf16x8* wr1 = brow(ch + 1);
 #pragma unroll
-      for (int p2 = 0; p2 < PF; ++p2) bq[p2] = wr1[p2 * 64];
+      for (int p2 = 0; p2 < PF; ++p2) bload(wr1, p2, bq[p2]);
       gather(ch + 1, gn);
       if constexpr (XI) xgn = gather_x(ch + 1);
     }
@@ -597,7 +620,7 @@ void pc_bwd_data_kernel(Geo g, const float* __restrict__ wt, const float4* __res
 // that dA): inside one workgroup the two never overlap, and the matrix cores idle through
 // the VALU phase unless the CU's other workgroup happens to be in its MFMA phase.  Here dA is
 // double-buffered in LDS and iteration ch issues chunk ch+1's MFMAs and chunk ch's VALU work
-// in one loop body (step i: one mfma4 of ch+1, then pair-channel item i of ch), so the VALU
+// in one loop body (step i: one K-step of ch+1 -- 6 bf16 MFMAs --, then pair-channel item i of ch), so the VALU
 // and LDS work fills the MFMAs' 64-cycle issue shadows of the same wave.  One barrier per
 // chunk.  Identical arithmetic to pc_bwd_data_kernel (same fma order in every sum), so the
 // two produce bit-identical dG / dwt / dcenter.
@@ -1056,34 +1079,7 @@ void pc_bwd_data_pipe_kernel(Geo g, const float* __restrict__ wt, const bf16x8* 
   }
 }
 
-// wl (O, 16C) -> the data kernel's B operand order: float4 (ch, wave, og, lane) =
-// wl[8 og + 4 (lane >> 5) + 0..3][ch * 128 + 32 wave + (lane & 31)], zero past column 16C.
-// One thread per float4; a wave reads 32 consecutive columns of 4 rows (coalesced).
-__global__ __launch_bounds__(256) void pc_swizzle_bwd_kernel(int o, int c16, int nch,
-                                                             const float* __restrict__ wl,
-                                                             float4* __restrict__ wsw) {
-  const int nog = o / 8;
-  const long long total = (long long)nch * 4 * nog * 64;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (long long)gridDim.x * blockDim.x) {
-    const int lane = (int)(e & 63);
-    const long long q = e >> 6;
-    const int og = (int)(q % nog);
-    const long long cw = q / nog;  // ch * 4 + wave
-    const int col = (int)(cw * 32) + (lane & 31);
-    const int o0 = 8 * og + 4 * (lane >> 5);
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (col < c16) {
-      v.x = wl[(long long)(o0 + 0) * c16 + col];
-      v.y = wl[(long long)(o0 + 1) * c16 + col];
-      v.z = wl[(long long)(o0 + 2) * c16 + col];
-      v.w = wl[(long long)(o0 + 3) * c16 + col];
-    }
-    wsw[e] = v;
-  }
-}
-
-// wl (O, 16C) -> the pipelined data kernel's B operand planes (split-bf16 MFMA, mfma_x6):
+// wl (O, 16C) -> the data kernels' B operand planes (split-bf16 MFMA, mfma_x6):
 // bf16x8 (ch, wave, ks, plane, lane) = plane {h, m, l} of wl[16 ks + 8 (lane >> 5) + 0..7]
 // [ch * 128 + 32 wave + (lane & 31)], zero past column 16C.  One thread per (ch, wave, ks,
 // lane); a wave reads 32 consecutive columns of 8 rows.
@@ -1793,7 +1789,7 @@ bool plan_of(int b, int s, int k, int d, int o, Plan* p, int wcus = kCUs) {
   p->dgr = align256((size_t)b * divup(s, 32) * 32 * k * p->c8 * 4);
   p->dwt_slab = p->bks > 1 ? align256((size_t)p->bks * p->r * k * kW * 4) : 0;
   p->dwl_slab = p->rs > 1 ? align256((size_t)p->rs * o * c16 * 4) : 0;
-  // swizzled B, padded to whole chunks: f32 (4 B) or three bf16 planes (6 B) per element
+  // swizzled B (three bf16 planes, 6 B per element), padded to whole chunks
   p->wlt = align256((size_t)p->nch * kNC * o * 6);
   return true;
 }
@@ -1856,31 +1852,25 @@ hipError_t bwd_data_launch(const Geo& g, const Plan& p, int b, const float* wt, 
   // the pipelined kernels store dG through a buffer resource (31-bit byte offsets)
   const bool dg31 = (long long)p.r * g.k * p.c8 * 4 < (1ll << 31);
   const long long rk = (long long)p.r * g.k;
-  hipError_t e;
-  if (g.trow || (bwd_pipe_enabled<KM>() && dg31)) {  // split-bf16 B planes
-    bf16x8* wsw = reinterpret_cast<bf16x8*>(wsb);
-    const long long nsw = (long long)g.nch * 4 * (O / 16) * 64;
-    hipLaunchKernelGGL(pc_swizzle_bwd3_kernel, dim3((unsigned)divupll(nsw, 256)), dim3(256), 0,
-                       st, O, c16, g.nch, wl, wsw);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (g.trow)  // tiled plan (checked by the entry point: dG partial rows fit 31 bits)
-      hipLaunchKernelGGL((pc_bwd_data_pipe_kernel<O, KM, true>),
-                         dim3((unsigned)((long long)b * divup(g.s, 32)), p.bks), dim3(256), 0, st,
-                         g, wt, wsw, dy, dgr, p.bks > 1 ? dwt_slab : dwt, dcenter, p.bcps);
-    else
-      hipLaunchKernelGGL((pc_bwd_data_pipe_kernel<O, KM, false>), dim3(divup(p.r, 32), p.bks),
-                         dim3(256), 0, st, g, wt, wsw, dy, dgr, p.bks > 1 ? dwt_slab : dwt,
-                         dcenter, p.bcps);
-  } else {
-    float4* wsw = reinterpret_cast<float4*>(wsb);
-    const long long nsw = (long long)g.nch * 4 * (O / 8) * 64;
-    hipLaunchKernelGGL(pc_swizzle_bwd_kernel, dim3((unsigned)divupll(nsw, 256)), dim3(256), 0,
-                       st, O, c16, g.nch, wl, wsw);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+  // wl as bf16 B planes (every data kernel multiplies dA = dy wl with mfma_x6)
+  bf16x8* wsw = reinterpret_cast<bf16x8*>(wsb);
+  const long long nsw = (long long)g.nch * 4 * (O / 16) * 64;
+  hipLaunchKernelGGL(pc_swizzle_bwd3_kernel, dim3((unsigned)divupll(nsw, 256)), dim3(256), 0, st,
+                     O, c16, g.nch, wl, wsw);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  if (g.trow)  // tiled plan (checked by the entry point: dG partial rows fit 31 bits)
+    hipLaunchKernelGGL((pc_bwd_data_pipe_kernel<O, KM, true>),
+                       dim3((unsigned)((long long)b * divup(g.s, 32)), p.bks), dim3(256), 0, st,
+                       g, wt, wsw, dy, dgr, p.bks > 1 ? dwt_slab : dwt, dcenter, p.bcps);
+  else if (bwd_pipe_enabled<KM>() && dg31)
+    hipLaunchKernelGGL((pc_bwd_data_pipe_kernel<O, KM, false>), dim3(divup(p.r, 32), p.bks),
+                       dim3(256), 0, st, g, wt, wsw, dy, dgr, p.bks > 1 ? dwt_slab : dwt, dcenter,
+                       p.bcps);
+  else
     hipLaunchKernelGGL((pc_bwd_data_kernel<O, KM>), dim3(divup(p.r, bwd_tile_rows<KM>()), p.bks),
                        dim3(bwd_threads<KM>()), 0, st,
                        g, wt, wsw, dy, dgr, p.bks > 1 ? dwt_slab : dwt, dcenter, p.bcps);
-  }
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (p.bks > 1 && (e = slab_sum(p.bks, rk * kW, dwt_slab, nullptr, 1, dwt, st)) != hipSuccess)
