@@ -17,8 +17,10 @@
 #include <algorithm>
 
 #include "kdpc_common.h"
+#include "split_bf16.h"
 
 using namespace kdpc;
+using namespace kdpc_x6;
 
 namespace {
 
@@ -295,6 +297,49 @@ __device__ __forceinline__ void wide_build(const WideLoads<D>& L, int k, int rg,
   }
 }
 
+// The same h0 rows as three bf16 planes (the forward's MFMA A operand, mfma_x6): row r's
+// 8-channel chunk g at r * (D / 8) + (g ^ (r & 15)) (the 32 lanes of an operand read hit 16
+// distinct chunk positions); this thread's 4 channels are half a chunk (8 bytes per plane).
+template <int D>
+__device__ __forceinline__ void wide_build_planes(const WideLoads<D>& L, int k, int rg, int c4,
+                                                  const float4* wposT, bf16x8 (*Hp)[32 * D / 8]) {
+  using G = WideGeo<D>;
+  float wp[4][3], bp[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float4 v = wposT[4 * c4 + e];
+    wp[e][0] = v.x;
+    wp[e][1] = v.y;
+    wp[e][2] = v.z;
+    bp[e] = v.w;
+  }
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int i = 0; i < G::RPT; ++i) {
+    const int r = rg + G::RG * i;
+    const float dx = L.x2[i][0] - L.x1[0], dy = L.x2[i][1] - L.x1[1], dz = L.x2[i][2] - L.x1[2];
+    const float g[4] = {L.p2[i].x, L.p2[i].y, L.p2[i].z, L.p2[i].w};
+    const float p[4] = {L.p1.x, L.p1.y, L.p1.z, L.p1.w};
+    bf16x4 hh, hm, hl;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float pos = __fadd_rn(
+          __builtin_fmaf(wp[e][2], dz, __builtin_fmaf(wp[e][1], dy, __fmul_rn(wp[e][0], dx))), bp[e]);
+      const float h = r < k ? lrelu(__fadd_rn(__fadd_rn(g[e], p[e]), pos)) : 0.f;
+      __bf16 a, b2, c2;
+      split3(h, a, b2, c2);
+      hh[e] = a;
+      hm[e] = b2;
+      hl[e] = c2;
+    }
+    const int cix = r * (D / 8) + ((c4 >> 1) ^ (r & 15));
+    const int sub = c4 & 1;  // which half of the chunk
+    reinterpret_cast<bf16x4*>(&Hp[0][cix])[sub] = hh;
+    reinterpret_cast<bf16x4*>(&Hp[1][cix])[sub] = hm;
+    reinterpret_cast<bf16x4*>(&Hp[2][cix])[sub] = hl;
+  }
+}
+
 // (Wpos row, bpos) per channel into an LDS table: wposT[c] = (wx, wy, wz, b)
 template <int D>
 __device__ __forceinline__ void wide_consts(const float* __restrict__ wpos,
@@ -330,7 +375,9 @@ __global__ __launch_bounds__(2 * D) void cvw_fused_fwd_kernel(
     const float* __restrict__ w1, const float* __restrict__ b1, float* __restrict__ out,
     unsigned char* __restrict__ amax) {
   using G = WideGeo<D>;
-  __shared__ __attribute__((aligned(16))) float Hs[2][32 * G::LD];
+  constexpr int NKS = D / 16;  // 16-deep K-steps of the D x D MLP (mfma_x6)
+  // h0 of a query as bf16 planes (wide_build_planes), double-buffered
+  __shared__ __attribute__((aligned(16))) bf16x8 Hp[2][3][32 * D / 8];
   __shared__ __attribute__((aligned(16))) float4 wposT[D];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, half = lane >> 5, l32 = lane & 31;
   const int c4 = t % G::C4, rg = t / G::C4;
@@ -339,11 +386,15 @@ __global__ __launch_bounds__(2 * D) void cvw_fused_fwd_kernel(
   const int q1 = min(s.nq, q0 + qpw);
   if (q0 >= q1) return;  // workgroup-uniform
   wide_consts<D>(wpos, bpos, wposT);
-  // B fragments: lane supplies W1[32w + l32][8blk + 4half + 0..3] for MFMA block blk
-  float4 bw[D / 8];
+  // B planes: lane supplies W1[32w + l32][16 ks + 8 half + 0..7] for K-step ks, split once
+  Planes bw[NKS];
 #pragma unroll
-  for (int blk = 0; blk < D / 8; ++blk)
-    bw[blk] = *reinterpret_cast<const float4*>(w1 + (long long)(32 * w + l32) * D + 8 * blk + 4 * half);
+  for (int ks = 0; ks < NKS; ++ks) {
+    const float4* src = reinterpret_cast<const float4*>(w1 + (long long)(32 * w + l32) * D + 16 * ks + 8 * half);
+    const float4 lo = src[0], hi = src[1];
+    const float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    bw[ks] = split8(v);
+  }
   const float bias = b1[32 * w + l32];
 
   int jn[G::RPT], jn2[G::RPT];
@@ -352,7 +403,7 @@ __global__ __launch_bounds__(2 * D) void cvw_fused_fwd_kernel(
   wide_load<D>(s, q0, jn, rg, c4, L);
   wide_load_idx<D>(s, q0 + 1, jn2, rg);
   __syncthreads();  // wposT
-  wide_build<D>(L, k, rg, c4, wposT, Hs[0], nullptr);
+  wide_build_planes<D>(L, k, rg, c4, wposT, Hp[0]);
   __syncthreads();
   for (int q = q0; q < q1; ++q) {
     const int p = (q - q0) & 1;
@@ -361,14 +412,13 @@ __global__ __launch_bounds__(2 * D) void cvw_fused_fwd_kernel(
     for (int i = 0; i < G::RPT; ++i) jn[i] = jn2[i];
     wide_load<D>(s, q + 1 < q1 ? q + 1 : s.nq, jn, rg, c4, L);
     wide_load_idx<D>(s, q + 2 < q1 ? q + 2 : s.nq, jn2, rg);
-    const float* H = Hs[p];
     f32x16 acc;
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[e] = 0.f;
 #pragma unroll
-    for (int blk = 0; blk < D / 8; ++blk) {
-      const float4 av = *reinterpret_cast<const float4*>(H + l32 * G::LD + 8 * blk + 4 * half);
-      acc = mfma4(av, bw[blk], acc);
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int cix = l32 * (D / 8) + ((2 * ks + half) ^ (l32 & 15));
+      acc = mfma_x6(Hp[p][0][cix], Hp[p][1][cix], Hp[p][2][cix], bw[ks].h, bw[ks].m, bw[ks].l, acc);
     }
     // max over the query's rows (< k) in LeakyReLU space, first maximal row
     float m = -INFINITY;
@@ -392,7 +442,7 @@ __global__ __launch_bounds__(2 * D) void cvw_fused_fwd_kernel(
       out[(long long)q * D + 32 * w + l32] = m;
       amax[(long long)q * D + 32 * w + l32] = (unsigned char)mr;
     }
-    if (q + 1 < q1) wide_build<D>(L, k, rg, c4, wposT, Hs[p ^ 1], nullptr);
+    if (q + 1 < q1) wide_build_planes<D>(L, k, rg, c4, wposT, Hp[p ^ 1]);
     __syncthreads();
   }
 }
