@@ -192,12 +192,6 @@ __device__ __forceinline__ float bld(__amdgpu_buffer_rsrc_t r, unsigned off) {
 __device__ __forceinline__ float4 bld4(__amdgpu_buffer_rsrc_t r, unsigned off) {
   return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
 }
-__device__ __forceinline__ f32x16 mfma4(float4 a, float4 b, f32x16 c) {
-  c = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, c, 0, 0, 0);
-  return __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, c, 0, 0, 0);
-}
 
 template <int D>
 struct WideGeo {
@@ -448,20 +442,18 @@ __global__ __launch_bounds__(2 * D) void cvw_fused_fwd_kernel(
 }
 
 // Backward.  Per query: h0 rebuilt (LDS tile), g'[o] = dout * LReLU'(out) and the argmax
-// rows am[o]; dh0 = M W1 on the matrix cores (M[r][o] = g'[o] [am[o] == r]: one nonzero per
-// column, and the MFMA's fma chain over ascending o equals scattering g'[o] W1[o,:] into
-// row am[o] in ascending o); dW1[o,:] += g'[o] h0[am[o],:] on the VALU (1/32 of a dense
+// rows am[o]; dh0 = M W1 on the bf16 matrix cores (mfma_x6; M[r][o] = g'[o] [am[o] == r]: one
+// nonzero per column); dW1[o,:] += g'[o] h0[am[o],:] on the VALU (1/32 of a dense
 // update); dz0 = dh0 * LReLU'(h0) in place; then per-row / per-channel passes write dP1,
 // the dP2 / d(dir) rows (summed per reference point by the caller through the CSR) and dx1,
 // and accumulate db1 / dWpos / dbpos.  Parameter gradients leave as one slab per workgroup
 // (summed in a fixed order by colsum: no float atomics).
-// B operand of dh0 (lane: W1[8blk + 4half + 0..3][32w + l32]): in registers for D = 128, read
-// per query from a transposed copy w1t (D x D, L2-resident) for D = 256 (the registers hold
-// the dW1 accumulators instead).
+// B operand of dh0: W1's bf16 planes in fragment order (cvw_w1_planes_kernel, L2-resident),
+// streamed per query two K-steps ahead.
 template <int D>
 struct WideBwd {
   static constexpr int OSPLIT = D <= 128 ? 1 : 2;  // dW1 o-halves (grid.y of the PART 2 kernel)
-  static constexpr bool BREG = D <= 128;
+  static constexpr int NKS = D / 16;  // 16-deep K-steps of dh0 = M W1 (mfma_x6)
   // the next query's gathers issued at the top of the iteration (held in registers across
   // the MFMA phase) for D = 128; at D = 256 the dW1 accumulators need those registers
   static constexpr bool PREFETCH = D <= 128;
@@ -475,11 +467,11 @@ struct WideBwd {
 // OVR: slope0 (B*N1, K, D) u8 overrides the first LeakyReLU's derivative (test seam; see
 // cost_volume_bwd_kernel in cost_volume.hip)
 template <int D, int PART, bool OVR>
-__global__ __launch_bounds__(2 * D) void cvw_fused_bwd_kernel(
+__global__ __launch_bounds__(2 * D) __attribute__((amdgpu_waves_per_eu(D == 128 ? 1 : 2))) void cvw_fused_bwd_kernel(
     int b, int n1, int n2, int k, int qpw, const float* __restrict__ x1,
     const float* __restrict__ x2, const int* __restrict__ idx, const float* __restrict__ p1,
     const float* __restrict__ p2, const float* __restrict__ wpos, const float* __restrict__ bpos,
-    const float* __restrict__ w1, const float* __restrict__ w1t, const float* __restrict__ out,
+    const float* __restrict__ w1, const bf16x8* __restrict__ w1p, const float* __restrict__ out,
     const unsigned char* __restrict__ amax, const unsigned char* __restrict__ slope0,
     const float* __restrict__ dout,
     float* __restrict__ dp1, float* __restrict__ dp2_rows, float* __restrict__ dx1,
@@ -494,6 +486,10 @@ __global__ __launch_bounds__(2 * D) void cvw_fused_bwd_kernel(
   __shared__ __attribute__((aligned(16))) float Hs[2][32 * G::LD];
   __shared__ __attribute__((aligned(16))) float4 dirs[2][32];
   __shared__ __attribute__((aligned(16))) float2 gam[2][D];   // (g', argmax row) per output
+  // the same per output as the bf16 planes of g' and the argmax row as u16: the A operand of
+  // dh0 = M W1 (M[r][o] = g'[o] [am[o] == r]) is 8 outputs' planes masked per 16-bit half
+  __shared__ __attribute__((aligned(16))) __bf16 gpl[2][3][D];
+  __shared__ __attribute__((aligned(16))) unsigned short gam16[2][D];
   __shared__ __attribute__((aligned(16))) float4 red[G::RG][G::C4];  // dP1 partials
   __shared__ __attribute__((aligned(16))) float4 red2[NG2][32];      // d(dir) partials
   __shared__ __attribute__((aligned(16))) float4 wposT[D];           // Wpos rows (x, y, z, 0)
@@ -521,17 +517,9 @@ __global__ __launch_bounds__(2 * D) void cvw_fused_bwd_kernel(
   const bool ranked = rank != nullptr;
   const __amdgpu_buffer_rsrc_t rkr = rsrc_of(ranked ? rank : idx, ranked ? (long long)s.nq * k * 4 : 0);
   wide_consts<D>(wpos, bpos, wposT);
-  float4 bt[W::BREG && MAIN ? D / 8 : 1];
-  if constexpr (W::BREG && MAIN) {
-#pragma unroll
-    for (int blk = 0; blk < D / 8; ++blk) {
-      const int o = 8 * blk + 4 * half;
-      const int c = 32 * w + l32;
-      bt[blk] = make_float4(w1[(long long)(o + 0) * D + c], w1[(long long)(o + 1) * D + c],
-                            w1[(long long)(o + 2) * D + c], w1[(long long)(o + 3) * D + c]);
-    }
-  }
-  const float* w1row = w1t + (long long)(32 * w + l32) * D + 4 * half;  // streamed B (D = 256)
+  // B planes of dh0 (cvw_w1_planes_kernel): this wave's column block, K-step ks, plane pl at
+  // [(3 ks + pl) * 64], streamed from L2 PF K-steps ahead
+  const bf16x8* w1row = w1p + (long long)(w * W::NKS * 3) * 64 + lane;
   // accumulators: dW1 rows o = og*OPT + i at channels 4 c4 .. +3 (og = rg), db1 (t < D),
   // dWpos / dbpos at (rg rows, channels 4 c4 .. +3)
   float4 gw[DW1 ? W::OPT : 1];
@@ -564,7 +552,16 @@ __global__ __launch_bounds__(2 * D) void cvw_fused_bwd_kernel(
         rkr, (int)(l32 < k ? ((unsigned)q * (unsigned)k + l32) * 4u : kOOB), 0, 0);
   };
   auto stage_out = [&](int p) {
-    if (t < D) gam[p][t] = make_float2(ov > 0.f ? dv : dv * kSlope, __int_as_float((int)av));
+    if (t < D) {
+      const float g = ov > 0.f ? dv : dv * kSlope;
+      gam[p][t] = make_float2(g, __int_as_float((int)av));
+      __bf16 gh, gm, gl;
+      split3(g, gh, gm, gl);
+      gpl[p][0][t] = gh;
+      gpl[p][1][t] = gm;
+      gpl[p][2][t] = gl;
+      gam16[p][t] = (unsigned short)av;
+    }
   };
 
   int jn[G::RPT], jn2[G::RPT];
@@ -591,34 +588,47 @@ __global__ __launch_bounds__(2 * D) void cvw_fused_bwd_kernel(
     if constexpr (W::PREFETCH) next_loads();  // in flight under this query's MFMAs
     float* H = Hs[p];
     const float2* ga = gam[p];
-    // ---- dh0 = M W1 (rows = neighbours, columns 32w .. +31 of Din)
+    // ---- dh0 = M W1 (rows = neighbours, columns 32w .. +31 of Din) on mfma_x6: K-step ks,
+    // lane half h: outputs o = 16 ks + 8 h + j; A[l32][o] = planes of g'[o] where am[o] == l32
+    // (a 16-bit mask per output from the packed u16 rows: (am ^ l32) - 1 < 0 <=> am == l32)
     f32x16 dacc;
     if constexpr (MAIN) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) dacc[e] = 0.f;
-    constexpr int PF = 4;  // streamed B blocks in flight (D = 256)
-    float4 bq[W::BREG ? 1 : PF];
-    if constexpr (!W::BREG) {
+    constexpr int PF = 2;  // K-steps of B planes in flight
+    Planes bq[PF];
+    auto bload = [&](int ks, Planes& bb) {
+      bb.h = w1row[(3 * ks + 0) * 64];
+      bb.m = w1row[(3 * ks + 1) * 64];
+      bb.l = w1row[(3 * ks + 2) * 64];
+    };
 #pragma unroll
-      for (int i = 0; i < PF; ++i) bq[i] = *reinterpret_cast<const float4*>(w1row + 8 * i);
-    }
+    for (int i = 0; i < PF; ++i) bload(i, bq[i]);
+    typedef short s16x2 __attribute__((ext_vector_type(2)));
+    const unsigned tgt = (unsigned)l32 * 0x00010001u;
+#pragma unroll 2
+    for (int ks = 0; ks < W::NKS; ++ks) {
+      const int o0 = 16 * ks + 8 * half;
+      const uint4 av4 = *reinterpret_cast<const uint4*>(&gam16[p][o0]);
+      const uint4 ph = *reinterpret_cast<const uint4*>(&gpl[p][0][o0]);
+      const uint4 pm = *reinterpret_cast<const uint4*>(&gpl[p][1][o0]);
+      const uint4 pl = *reinterpret_cast<const uint4*>(&gpl[p][2][o0]);
+      const unsigned aw[4] = {av4.x, av4.y, av4.z, av4.w};
+      unsigned mk[4];
 #pragma unroll
-    for (int blk = 0; blk < D / 8; ++blk) {
-      const float4 g01 = *reinterpret_cast<const float4*>(ga + 8 * blk + 4 * half);
-      const float4 g23 = *reinterpret_cast<const float4*>(ga + 8 * blk + 4 * half + 2);
-      float4 a;
-      a.x = __float_as_int(g01.y) == l32 ? g01.x : 0.f;
-      a.y = __float_as_int(g01.w) == l32 ? g01.z : 0.f;
-      a.z = __float_as_int(g23.y) == l32 ? g23.x : 0.f;
-      a.w = __float_as_int(g23.w) == l32 ? g23.z : 0.f;
-      if constexpr (W::BREG) {
-        dacc = mfma4(a, bt[blk], dacc);
-      } else {
-        dacc = mfma4(a, bq[blk % PF], dacc);
-        if (blk + PF < D / 8) bq[blk % PF] = *reinterpret_cast<const float4*>(w1row + 8 * (blk + PF));
+      for (int i = 0; i < 4; ++i) {
+        const s16x2 d = __builtin_bit_cast(s16x2, aw[i] ^ tgt) - (s16x2){1, 1};
+        mk[i] = __builtin_bit_cast(unsigned, d >> (s16x2){15, 15});
       }
-      // one block's LDS reads ahead at most (hoisting them all held 8 registers per block)
-      if (blk % 2 == 1) __builtin_amdgcn_sched_barrier(0);
+      const uint4 mh = make_uint4(ph.x & mk[0], ph.y & mk[1], ph.z & mk[2], ph.w & mk[3]);
+      const uint4 mm = make_uint4(pm.x & mk[0], pm.y & mk[1], pm.z & mk[2], pm.w & mk[3]);
+      const uint4 ml = make_uint4(pl.x & mk[0], pl.y & mk[1], pl.z & mk[2], pl.w & mk[3]);
+      dacc = mfma_x6(__builtin_bit_cast(bf16x8, mh), __builtin_bit_cast(bf16x8, mm),
+                     __builtin_bit_cast(bf16x8, ml), bq[ks % PF].h, bq[ks % PF].m, bq[ks % PF].l,
+                     dacc);
+      if (ks + PF < W::NKS) bload(ks + PF, bq[ks % PF]);
+      // one K-step's LDS reads ahead at most
+      __builtin_amdgcn_sched_barrier(0);
     }
     }  // MAIN
     // ---- dW1[o, 4c4..] += g'[o] h0[am[o], 4c4..] for this thread's o rows; db1
@@ -791,11 +801,22 @@ __global__ __launch_bounds__(2 * D) void cvw_fused_bwd_kernel(
   }
 }
 
-// w1 (D, D) -> w1t = w1^T (the streamed B operand of the D = 256 backward)
-__global__ __launch_bounds__(256) void cvw_transpose_kernel(int d, const float* __restrict__ w1,
-                                                            float* __restrict__ w1t) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e < d * d) w1t[e] = w1[(e % d) * d + e / d];
+// w1 (D, D) -> the backward's streamed B planes of dh0 = M W1 (mfma_x6): bf16x8 (wave w, ks,
+// plane, lane) = plane of W1[16 ks + 8 (lane >> 5) + 0..7][32 w + (lane & 31)]
+__global__ __launch_bounds__(256) void cvw_w1_planes_kernel(int d, const float* __restrict__ w1,
+                                                            bf16x8* __restrict__ w1p) {
+  const int e = blockIdx.x * 256 + threadIdx.x;  // (w, ks, lane)
+  const int nks = d / 16;
+  if (e >= (d / 32) * nks * 64) return;
+  const int lane = e & 63, q = e >> 6, ks = q % nks, w = q / nks;
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = w1[(16 * ks + 8 * (lane >> 5) + j) * d + 32 * w + (lane & 31)];
+  const Planes pl = split8(v);
+  bf16x8* dst = w1p + (long long)q * 3 * 64 + lane;
+  dst[0] = pl.h;
+  dst[64] = pl.m;
+  dst[128] = pl.l;
 }
 
 // queries per workgroup: A/B at the model's calls (round 4, B=16 pair batch, K=32): forward
@@ -836,7 +857,8 @@ size_t cost_volume_wide_fused_bwd_workspace_floats(int b, int n1, int d) {
   const long long nq = (long long)b * n1;
   const long long nwg = divupll(nq, fused_qpw(nq, d, true));
   const long long len = (long long)d * d + 5 * d;
-  return (size_t)(nwg * len + colsum_scratch_floats((int)nwg, len) + (long long)d * d);
+  // + the B planes of W1 (6 bytes per element)
+  return (size_t)(nwg * len + colsum_scratch_floats((int)nwg, len) + (long long)d * d * 3 / 2 + 4);
 }
 
 hipError_t cost_volume_wide_fused_bwd(int b, int n1, int n2, int k, int d, const float* x1,
@@ -853,21 +875,26 @@ hipError_t cost_volume_wide_fused_bwd(int b, int n1, int n2, int k, int d, const
   const long long len = (long long)d * d + 5 * d;
   float* slab = ws;
   float* scratch = ws + (long long)nwg * len;
-  float* w1t = scratch + colsum_scratch_floats(nwg, len);
+  // 16-byte aligned (the float count before it is a multiple of 4 only by luck: round up)
+  bf16x8* w1p = reinterpret_cast<bf16x8*>(
+      (reinterpret_cast<uintptr_t>(scratch + colsum_scratch_floats(nwg, len)) + 15) & ~(uintptr_t)15);
 #define KDPC_CVW_BWD(DD, PART, OV, GRID)                                                          \
   hipLaunchKernelGGL((cvw_fused_bwd_kernel<DD, PART, OV>), GRID, dim3(2 * DD), 0, st, b, n1, n2, k, \
-                     qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, w1t, out, amax, slope0, dout, dp1,    \
+                     qpw, x1, x2, idx, p1, p2, wpos, bpos, w1, w1p, out, amax, slope0, dout, dp1,    \
                      dp2_rows, dx1, ddir_rows, rank, rows, slab)
+  hipLaunchKernelGGL(cvw_w1_planes_kernel, dim3(divup((d / 32) * (d / 16) * 64, 256)), dim3(256),
+                     0, st, d, w1, w1p);
+  {
+    const hipError_t e0 = hipGetLastError();
+    if (e0 != hipSuccess) return e0;
+  }
   if (d == 128) {
     if (slope0)
       KDPC_CVW_BWD(128, 0, true, dim3(nwg));
     else
       KDPC_CVW_BWD(128, 0, false, dim3(nwg));
   } else {
-    hipLaunchKernelGGL(cvw_transpose_kernel, dim3(divup(d * d, 256)), dim3(256), 0, st, d, w1,
-                       w1t);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    hipError_t e;
     if (slope0)
       KDPC_CVW_BWD(256, 1, true, dim3(nwg));
     else
