@@ -29,8 +29,10 @@
 #include <algorithm>
 
 #include "kdpc_common.h"
+#include "split_bf16.h"
 
 using namespace kdpc;
+using namespace kdpc_x6;
 
 namespace {
 
@@ -244,7 +246,9 @@ void cost_volume_bwd_kernel(
   constexpr int LD = 33;                  // dz0 tile stride: row-per-lane reads hit 32 banks
   constexpr int SLAB = D_OUT * D_IN + D_OUT + 4 * D_IN;
   constexpr int TILE = kRows * LD;
-  constexpr int PER_WAVE = TILE + 4 * kRows + 2 * D_OUT;  // dz0, directions, (g', argmax)
+  // dz0, directions, (g', argmax), then g' as three bf16 planes + the argmax row as u16 (the A
+  // operand of dh0 = M W1 on mfma_x6: 8 outputs' planes masked per 16-bit half)
+  constexpr int PER_WAVE = TILE + 4 * kRows + 2 * D_OUT + 2 * D_OUT;
   constexpr int SHARED = 4 * D_IN;                         // Wpos rows (x, y, z, 0)
   // dW1 on the VALU through the h0 tile (D_OUT = 32) or as M^T h0 on the matrix cores
   // (D_OUT = 64: the VALU update's 32 accumulators and hoisted reads spilled at 2 waves/SIMD)
@@ -273,14 +277,22 @@ void cost_volume_bwd_kernel(
   float* T = lds_all + SHARED + wave * PER_WAVE;
   float4* dirT = reinterpret_cast<float4*>(T + TILE);
   float2* gdam = reinterpret_cast<float2*>(T + TILE + 4 * kRows);
+  __bf16* gpl = reinterpret_cast<__bf16*>(T + TILE + 4 * kRows + 2 * D_OUT);  // [3][D_OUT]
+  unsigned short* g16 = reinterpret_cast<unsigned short*>(gpl + 3 * D_OUT);
   for (int e = threadIdx.x; e < D_IN; e += blockDim.x)
     wposT[e] = make_float4(wpos[e * 3 + 0], wpos[e * 3 + 1], wpos[e * 3 + 2], 0.f);
   __syncthreads();
 
-  // B fragments of W1 for dh0 = M W1 (inner index o): lane supplies W1[2s + half][cg]
-  float bw[D_OUT / 2];
+  // B planes of W1 for dh0 = M W1 (inner index o): lane supplies W1[16 ks + 8 half + j][cg]
+  constexpr int NKS = D_OUT / 16;
+  Planes bwp[NKS];
 #pragma unroll
-  for (int s2 = 0; s2 < D_OUT / 2; ++s2) bw[s2] = w1[(2 * s2 + half) * D_IN + cg];
+  for (int ks = 0; ks < NKS; ++ks) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = w1[(16 * ks + 8 * half + j) * D_IN + cg];
+    bwp[ks] = split8(v);
+  }
   const float w0 = wpos[cg * 3 + 0], wy = wpos[cg * 3 + 1], wz = wpos[cg * 3 + 2], bp = bpos[cg];
 
   const float* x1b = x1 + (long long)b * n1 * 3;
@@ -375,7 +387,15 @@ void cost_volume_bwd_kernel(
       if (lane < kRows) dirT[lane] = make_float4(xv0 - qx, xv1 - qy, xv2 - qz, 0.f);
 #pragma unroll
       for (int t = 0; t < OT; ++t)
-        if (half == 0) gdam[32 * t + l32] = make_float2(gq[t], __int_as_float(amc[t]));
+        if (half == 0) {
+          gdam[32 * t + l32] = make_float2(gq[t], __int_as_float(amc[t]));
+          __bf16 gh, gm, gl;
+          split3(gq[t], gh, gm, gl);
+          gpl[32 * t + l32] = gh;
+          gpl[D_OUT + 32 * t + l32] = gm;
+          gpl[2 * D_OUT + 32 * t + l32] = gl;
+          g16[32 * t + l32] = (unsigned short)amc[t];
+        }
       __builtin_amdgcn_wave_barrier();
       // ---- h0 in the accumulator layout (the forward's arithmetic; rows >= k are 0)
       float h0[16];
@@ -397,31 +417,78 @@ void cost_volume_bwd_kernel(
       issue(n + 1);
       load_idx(n + 2);
       __builtin_amdgcn_sched_barrier(0);
-      // ---- dh0 = M W1 (matrix cores), M[r][o] = g'[o] [am[o] == r]: the fma chain over
-      // ascending o, the sums of scattering g'[o] W1[o, :] into row am[o]
+      // ---- dh0 = M W1 on the bf16 matrix cores (mfma_x6), M[r][o] = g'[o] [am[o] == r]: K-step
+      // ks, lane half h covers o = 16 ks + 8 h + j; the lane's A = the planes of g'[o] where
+      // am[o] == l32 (a 16-bit mask per output: (am ^ l32) - 1 < 0 <=> am == l32)
       f32x16 dacc = f32x16{0};
+      {
+        typedef short s16x2 __attribute__((ext_vector_type(2)));
+        const unsigned tgt = (unsigned)l32 * 0x00010001u;
 #pragma unroll
-      for (int s2 = 0; s2 < D_OUT / 2; ++s2) {
-        const float2 ga = gdam[2 * s2 + half];
-        const float a = __float_as_int(ga.y) == l32 ? ga.x : 0.f;
-        dacc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bw[s2], dacc, 0, 0, 0);
-        if (s2 % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // bound the hoisted LDS reads
+        for (int ks = 0; ks < NKS; ++ks) {
+          const int o0 = 16 * ks + 8 * half;
+          const uint4 av4 = *reinterpret_cast<const uint4*>(g16 + o0);
+          const uint4 ph = *reinterpret_cast<const uint4*>(gpl + o0);
+          const uint4 pm = *reinterpret_cast<const uint4*>(gpl + D_OUT + o0);
+          const uint4 pq = *reinterpret_cast<const uint4*>(gpl + 2 * D_OUT + o0);
+          const unsigned aw[4] = {av4.x, av4.y, av4.z, av4.w};
+          unsigned mk[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const s16x2 d = __builtin_bit_cast(s16x2, aw[i] ^ tgt) - (s16x2){1, 1};
+            mk[i] = __builtin_bit_cast(unsigned, d >> (s16x2){15, 15});
+          }
+          const uint4 mh = make_uint4(ph.x & mk[0], ph.y & mk[1], ph.z & mk[2], ph.w & mk[3]);
+          const uint4 mm = make_uint4(pm.x & mk[0], pm.y & mk[1], pm.z & mk[2], pm.w & mk[3]);
+          const uint4 ml = make_uint4(pq.x & mk[0], pq.y & mk[1], pq.z & mk[2], pq.w & mk[3]);
+          dacc = mfma_x6(__builtin_bit_cast(bf16x8, mh), __builtin_bit_cast(bf16x8, mm),
+                         __builtin_bit_cast(bf16x8, ml), bwp[ks].h, bwp[ks].m, bwp[ks].l, dacc);
+          __builtin_amdgcn_sched_barrier(0);  // bound the hoisted LDS reads
+        }
       }
       // ---- dW1[o, c] += g'[o] h0[am[o], c] for o = 2 i + half (VALU, beside the MFMA chain:
       // the one-hot product on the matrix cores cost 16 more 64-cycle MFMAs per query); the
       // same fma chain per (o, c) as the previous kernel's update
       if constexpr (DW1_MFMA) {
-        // dW1 += M^T h0: step s = rows R_0(s) (half 0) / R_1(s) (half 1), A = the one-hot routing
-        // of output o = 32 t + l32, B = the lane's h0[s]
+        // dW1 += M^T h0 on mfma_x6: K-step ks2, lane half h covers the lane's rows R_h(e),
+        // e = 8 ks2 + j; B = the planes of the lane's h0[e], A = the one-hot routing of output
+        // o = 32 t + l32: the planes of g'[o] at e(am[o]) = (am & 3) + 4 (am >> 3) when am[o]
+        // is a row of this half ((am >> 2) & 1 == h), zero elsewhere
+        Planes hp[2];
+#pragma unroll
+        for (int ks2 = 0; ks2 < 2; ++ks2) {
+          float v[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = h0[8 * ks2 + j];
+          hp[ks2] = split8(v);
+        }
 #pragma unroll
         for (int t = 0; t < OT; ++t) {
-          const int amh = amc[t] - 4 * half;
+          const int am = amc[t];
+          const bool mine = ((am >> 2) & 1) == half;
+          const int e = (am & 3) + 4 * (am >> 3);
+          __bf16 gh, gm, gl;
+          split3(gq[t], gh, gm, gl);
+          const unsigned sh = (e & 1) * 16;
+          const unsigned bh = (unsigned)__builtin_bit_cast(unsigned short, gh) << sh;
+          const unsigned bm = (unsigned)__builtin_bit_cast(unsigned short, gm) << sh;
+          const unsigned bl = (unsigned)__builtin_bit_cast(unsigned short, gl) << sh;
 #pragma unroll
-          for (int s = 0; s < 16; ++s) {
-            const float a = amh == (s & 3) + 8 * (s >> 2) ? gq[t] : 0.f;
-            gw[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, h0[s], gw[t], 0, 0, 0);
-            if (s % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+          for (int ks2 = 0; ks2 < 2; ++ks2) {
+            unsigned wh[4], wm[4], wl[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+              const bool sel = mine && (e >> 1) == 4 * ks2 + d;
+              wh[d] = sel ? bh : 0u;
+              wm[d] = sel ? bm : 0u;
+              wl[d] = sel ? bl : 0u;
+            }
+            gw[t] = mfma_x6(__builtin_bit_cast(bf16x8, make_uint4(wh[0], wh[1], wh[2], wh[3])),
+                            __builtin_bit_cast(bf16x8, make_uint4(wm[0], wm[1], wm[2], wm[3])),
+                            __builtin_bit_cast(bf16x8, make_uint4(wl[0], wl[1], wl[2], wl[3])),
+                            hp[ks2].h, hp[ks2].m, hp[ks2].l, gw[t]);
           }
+          __builtin_amdgcn_sched_barrier(0);
         }
       } else {
 #pragma unroll
