@@ -384,9 +384,11 @@ __global__ __launch_bounds__(2 * D) void cvw_fused_fwd_kernel(
   Planes bw[NKS];
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks) {
-    const float4* src = reinterpret_cast<const float4*>(w1 + (long long)(32 * w + l32) * D + 16 * ks + 8 * half);
-    const float4 lo = src[0], hi = src[1];
-    const float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    // scalar loads: w1 may be a view at any 4-byte offset (the flat parameter buffer)
+    const float* src = w1 + (long long)(32 * w + l32) * D + 16 * ks + 8 * half;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = src[j];
     bw[ks] = split8(v);
   }
   const float bias = b1[32 * w + l32];

@@ -479,12 +479,19 @@ class GraphedStep:
         if not torch.is_tensor(grp["lr"]):
             grp["lr"] = torch.tensor(float(grp["lr"]), device=dev)
         self._lr = grp["lr"]
-        n = sum(p.numel() for p in used)
-        P = torch.empty(n, device=dev, dtype=used[0].dtype)
-        M, V, G = torch.empty_like(P), torch.empty_like(P), torch.zeros_like(P)
+        # every parameter view starts 16-byte aligned (4 floats; the padding stays 0): kernels
+        # read weights with 16-byte vector loads, which a view at an arbitrary 4-byte offset
+        # would break (the round-5 cost-volume forward read wrong W1 rows / faulted that way)
+        al = lambda x: (x + 3) & ~3  # noqa: E731
+        n = 0
+        for p in used:
+            n = al(n) + p.numel()
+        P = torch.zeros(al(n), device=dev, dtype=used[0].dtype)
+        M, V, G = torch.zeros_like(P), torch.zeros_like(P), torch.zeros_like(P)
         self._gviews, self._used, self._offs, off = [], used, [], 0
         with torch.no_grad():
             for p in used:
+                off = al(off)
                 k, st = p.numel(), opt.state[p]
                 P[off:off + k].copy_(p.reshape(-1))
                 M[off:off + k].copy_(st["exp_avg"].reshape(-1))
