@@ -53,6 +53,30 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, long lo
 }
 constexpr unsigned kOOB = 0x80000000u;  // out-of-range byte offset: loads read 0, stores drop
 
+// lane l ^ 32's value (v_permlane32_swap: a VALU exchange of the two wave halves; a shuffle
+// through ds_bpermute waits out an LDS round trip)
+__device__ __forceinline__ unsigned xor32u(unsigned v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return lane_id() < 32 ? r[1] : r[0];
+}
+__device__ __forceinline__ float xor32(float v) { return __uint_as_float(xor32u(__float_as_uint(v))); }
+__device__ __forceinline__ int xor32(int v) { return (int)xor32u((unsigned)v); }
+
+// sum of lanes 0..31, valid in lane 0: pair, quad, 8- and 16-lane steps through DPP (VALU
+// operand modifiers, no LDS), then row 1 of the half through a readlane
+template <int CTRL>
+__device__ __forceinline__ float add_dpp(float v) {
+  return __fadd_rn(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf,
+                                                                 0xf, false)));
+}
+__device__ __forceinline__ float sum32_lane0(float v) {
+  v = add_dpp<0xB1>(v);   // quad_perm [1,0,3,2]: pairs
+  v = add_dpp<0x4E>(v);   // quad_perm [2,3,0,1]: quads
+  v = add_dpp<0x141>(v);  // row_half_mirror: 8 lanes
+  v = add_dpp<0x140>(v);  // row_mirror: 16 lanes
+  return __fadd_rn(v, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16)));
+}
+
 // Forward: one wave per query, queries walked in a software pipeline (as the backward
 // below): query n+1's P2 rows / directions / P1 row and query n+2's neighbour indices are in
 // flight while query n's MLP runs on the matrix cores.  Rows r >= k build h0 = 0.
@@ -80,7 +104,7 @@ void cost_volume_fwd_kernel(
   const int c = lane % D_IN, sub = lane / D_IN;
   float* lds_h = lds[wave];
   float4* dirT = dir_lds[wave];
-  const float* x1b = x1 + (long long)b * n1 * 3;
+  const __amdgpu_buffer_rsrc_t x1r = rsrc_of(x1 + (long long)b * n1 * 3, (long long)n1 * 12);
   const __amdgpu_buffer_rsrc_t x2r = rsrc_of(x2 + (long long)b * n2 * 3, (long long)n2 * 12);
   const __amdgpu_buffer_rsrc_t ixr = rsrc_of(idx + (long long)b * n1 * k, (long long)n1 * k * 4);
   const __amdgpu_buffer_rsrc_t p1r = rsrc_of(p1 + (long long)b * n1 * D_IN, (long long)n1 * D_IN * 4);
@@ -104,7 +128,7 @@ void cost_volume_fwd_kernel(
   // prefetched state (as the backward): lane r's neighbour index / x2 row, layout-L P2 values
   int jn = 0;
   float pv[RT];
-  float xv0, xv1, xv2, p1v;
+  float xv0, xv1, xv2, qv0, qv1, qv2, p1v;
   auto load_idx = [&](int n) {
     jn = (int)__builtin_amdgcn_raw_buffer_load_b32(ixr, (int)(((unsigned)n * (unsigned)k + lane) * 4u), 0, 0);
   };
@@ -113,6 +137,9 @@ void cost_volume_fwd_kernel(
     xv0 = bload(x2r, xo);
     xv1 = bload(x2r, xo + 4u);
     xv2 = bload(x2r, xo + 8u);
+    qv0 = bload(x1r, (unsigned)n * 12u);  // the query's own point, prefetched
+    qv1 = bload(x1r, (unsigned)n * 12u + 4u);
+    qv2 = bload(x1r, (unsigned)n * 12u + 8u);
 #pragma unroll
     for (int i = 0; i < RT; ++i) {
       int j;
@@ -133,11 +160,13 @@ void cost_volume_fwd_kernel(
   }
   for (int n = q0; n < q1; ++n) {
     // ---- h0 of query n into LDS (layout L) from the prefetched registers
-    const float qx = x1b[n * 3 + 0], qy = x1b[n * 3 + 1], qz = x1b[n * 3 + 2];
     // lane r's direction to its neighbour, broadcast to the row passes through LDS (one
     // 16-byte read per pass instead of 3-6 readlanes + selects; the same values)
-    if (lane < kRows) dirT[lane] = make_float4(xv0 - qx, xv1 - qy, xv2 - qz, 0.f);
+    if (lane < kRows) dirT[lane] = make_float4(xv0 - qv0, xv1 - qv1, xv2 - qv2, 0.f);
     __builtin_amdgcn_wave_barrier();
+    // all direction reads before the first h0 store (a store between them serialises the
+    // reads: the compiler cannot move a read of dirT above a store to the same LDS array)
+    float hv[RT];
 #pragma unroll
     for (int i = 0; i < RT; ++i) {
       const int r0 = RPP * i, r = r0 + sub;
@@ -145,9 +174,11 @@ void cost_volume_fwd_kernel(
       const float dx = dr.x, dy = dr.y, dz = dr.z;
       const float pos = __fadd_rn(__builtin_fmaf(wz, dz, __builtin_fmaf(wy, dy, __fmul_rn(w0, dx))), bp);
       const float h = lrelu(__fadd_rn(__fadd_rn(pv[i], p1v), pos));
-      lds_h[r * LD + c] = r < k ? h : 0.f;
+      hv[i] = r < k ? h : 0.f;
       if (i % 4 == 3) __builtin_amdgcn_sched_barrier(0);
     }
+#pragma unroll
+    for (int i = 0; i < RT; ++i) lds_h[(RPP * i + sub) * LD + c] = hv[i];
     // ---- the next query's loads, in flight during this query's MFMAs
     if (n + 1 < q1) {
       issue(n + 1);
@@ -179,8 +210,8 @@ void cost_volume_fwd_kernel(
           mr = row;
         }
       }
-      const float pm = __shfl_xor(m, 32, kWave);
-      const int pr = __shfl_xor(mr, 32, kWave);
+      const float pm = xor32(m);
+      const int pr = xor32(mr);
       if (pm > m || (pm == m && pr < mr)) {
         m = pm;
         mr = pr;
@@ -246,9 +277,11 @@ void cost_volume_bwd_kernel(
   constexpr int LD = 33;                  // dz0 tile stride: row-per-lane reads hit 32 banks
   constexpr int SLAB = D_OUT * D_IN + D_OUT + 4 * D_IN;
   constexpr int TILE = kRows * LD;
-  // dz0, directions, (g', argmax), then g' as three bf16 planes + the argmax row as u16 (the A
-  // operand of dh0 = M W1 on mfma_x6: 8 outputs' planes masked per 16-bit half)
-  constexpr int PER_WAVE = TILE + 4 * kRows + 2 * D_OUT + 2 * D_OUT;
+  // dz0 tile, then two buffers of the per-query tables (query n's are read while query n+1's
+  // are written): directions + slots, (g', argmax), g' as three bf16 planes + the argmax row
+  // as u16 (the A operand of dh0 = M W1 on mfma_x6: 8 outputs' planes masked per 16-bit half)
+  constexpr int TABLES = 4 * 2 * kRows + 2 * D_OUT + 2 * D_OUT;
+  constexpr int PER_WAVE = TILE + 2 * TABLES;
   constexpr int SHARED = 4 * D_IN;                         // Wpos rows (x, y, z, 0)
   // dW1 on the VALU through the h0 tile (D_OUT = 32) or as M^T h0 on the matrix cores
   // (D_OUT = 64: the VALU update's 32 accumulators and hoisted reads spilled at 2 waves/SIMD)
@@ -257,7 +290,7 @@ void cost_volume_bwd_kernel(
   constexpr int XCH = CS > 1 ? 2 * (kWaves / CS) * kRows * 4 : 0;
   constexpr int BODY = XCH_AT + XCH;
   constexpr int LDS_FLOATS = BODY > SLAB ? BODY : SLAB;
-  static_assert(TILE % 4 == 0 && PER_WAVE % 4 == 0, "16-byte aligned LDS tables");
+  static_assert(TILE % 4 == 0 && TABLES % 4 == 0, "16-byte aligned LDS tables");
   __shared__ __attribute__((aligned(16))) float lds_all[LDS_FLOATS];
   // XCD-aware placement: the dispatcher deals workgroup L to XCD L % 8, so virtual block
   // p = (L % 8) * per + L / 8 gives every XCD a contiguous run of (cloud, query chunk) blocks,
@@ -267,7 +300,7 @@ void cost_volume_bwd_kernel(
   const int pblk = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
   if (pblk >= nblk) return;  // whole workgroup, before any barrier
   const int b = pblk / gx, bx = pblk - b * gx;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: scalar query math
   const int lane = lane_id();
   const int half = lane >> 5, l32 = lane & 31;
   const int hc = CS > 1 ? (wave & 1) : 0;      // channel half of this wave
@@ -275,10 +308,13 @@ void cost_volume_bwd_kernel(
   const int cg = hc * 32 + l32;                // the lane's channel
   float4* wposT = reinterpret_cast<float4*>(lds_all);
   float* T = lds_all + SHARED + wave * PER_WAVE;
-  float4* dirT = reinterpret_cast<float4*>(T + TILE);
-  float2* gdam = reinterpret_cast<float2*>(T + TILE + 4 * kRows);
-  __bf16* gpl = reinterpret_cast<__bf16*>(T + TILE + 4 * kRows + 2 * D_OUT);  // [3][D_OUT]
-  unsigned short* g16 = reinterpret_cast<unsigned short*>(gpl + 3 * D_OUT);
+  // table buffer u: directions dirT(u), (g', argmax) gdam(u), planes gpl(u) [3][D_OUT], g16(u)
+  auto dirT = [&](int u) { return reinterpret_cast<float4*>(T + TILE + u * TABLES); };
+  auto gdam = [&](int u) { return reinterpret_cast<float2*>(T + TILE + u * TABLES + 8 * kRows); };
+  auto gpl = [&](int u) {
+    return reinterpret_cast<__bf16*>(T + TILE + u * TABLES + 8 * kRows + 2 * D_OUT);
+  };
+  auto g16 = [&](int u) { return reinterpret_cast<unsigned short*>(gpl(u) + 3 * D_OUT); };
   for (int e = threadIdx.x; e < D_IN; e += blockDim.x)
     wposT[e] = make_float4(wpos[e * 3 + 0], wpos[e * 3 + 1], wpos[e * 3 + 2], 0.f);
   __syncthreads();
@@ -340,18 +376,23 @@ void cost_volume_bwd_kernel(
   // in issue order -- never wait behind this query's stores.  Query n+2's indices one further.
   int jn = (int)__builtin_amdgcn_raw_buffer_load_b32(ixr, (int)(((unsigned)q0 * (unsigned)k + lane) * 4u), 0, 0);
   float pv[16], xv0, xv1, xv2, p1v, ovq[OT], dvq[OT];
+  // the query's own point, one query ahead in scalar registers (a load at its use waited out a
+  // whole memory round trip per query)
+  float qs0, qs1, qs2;
+  auto load_q = [&](int n) {
+    const int nq = min(n, n1 - 1);
+    qs0 = x1b[nq * 3 + 0];
+    qs1 = x1b[nq * 3 + 1];
+    qs2 = x1b[nq * 3 + 2];
+  };
   int amq[OT], rkn;
   auto issue = [&](int n) {  // loads of query n (jn = its indices)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int j = __shfl(jn, (e & 3) + 8 * (e >> 2) + 4 * half, kWave);
-      pv[e] = bload(p2r, ((unsigned)j * D_IN + cg) * 4u);
-    }
+    // what its tables need first (written while the P2 gathers are still in flight: vmcnt
+    // retires in issue order), then the gathers
     const unsigned xo = (unsigned)jn * 12u;
     xv0 = bload(x2r, xo);
     xv1 = bload(x2r, xo + 4u);
     xv2 = bload(x2r, xo + 8u);
-    p1v = bload(p1r, ((unsigned)n * D_IN + cg) * 4u);
 #pragma unroll
     for (int t = 0; t < OT; ++t) {  // output o = 32 t + l32 (both halves)
       const unsigned oo = (unsigned)n * D_OUT + 32 * t + l32;
@@ -361,60 +402,97 @@ void cost_volume_bwd_kernel(
     }
     rkn = (int)__builtin_amdgcn_raw_buffer_load_b32(
         rkr, (int)(lane < k ? ((unsigned)n * (unsigned)k + lane) * 4u : kOOB), 0, 0);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int j = __shfl(jn, (e & 3) + 8 * (e >> 2) + 4 * half, kWave);
+      pv[e] = bload(p2r, ((unsigned)j * D_IN + cg) * 4u);
+    }
+    p1v = bload(p1r, ((unsigned)n * D_IN + cg) * 4u);
   };
   auto load_idx = [&](int n) {
     jn = (int)__builtin_amdgcn_raw_buffer_load_b32(ixr, (int)(((unsigned)n * (unsigned)k + lane) * 4u), 0, 0);
   };
+  // query m's tables into buffer u from its prefetched loads (issue(m), load_q(m)): g' and the
+  // argmax rows (kept in registers for the dW1 / db1 updates), directions with the row's
+  // destination slot (-1: none; the row pass reads a row's slot with its direction -- a
+  // shuffle per row serialised 16 LDS round trips).  Written one query ahead, in the middle of
+  // query m-1, so the wait for their loads never waits behind query m-1's row stores.  Every
+  // lane stores (lanes >= 32: directions into the table's unused upper half; g' rows by both
+  // halves, the same values): a store under a lane condition let the compiler sink the loads
+  // it uses into that branch, next to the store, and wait for them there.
+  float gqn[OT];
+  int amn[OT], rkm = -1;
+  auto tables = [&](int m, int u) {
+#pragma unroll
+    for (int t = 0; t < OT; ++t) {
+      gqn[t] = dvq[t] * (ovq[t] > 0.f ? 1.f : kSlope);
+      amn[t] = amq[t];
+    }
+    rkm = rkn;
+    const int slot = lane < k ? (ranked ? rkm : (nbase + m) * k + lane) : -1;
+    dirT(u)[lane] = make_float4(xv0 - qs0, xv1 - qs1, xv2 - qs2, __int_as_float(slot));
+#pragma unroll
+    for (int t = 0; t < OT; ++t) {
+      gdam(u)[32 * t + l32] = make_float2(gqn[t], __int_as_float(amn[t]));
+      __bf16 gh, gm, gl;
+      split3(gqn[t], gh, gm, gl);
+      gpl(u)[32 * t + l32] = gh;
+      gpl(u)[D_OUT + 32 * t + l32] = gm;
+      gpl(u)[2 * D_OUT + 32 * t + l32] = gl;
+      g16(u)[32 * t + l32] = (unsigned short)amn[t];
+    }
+  };
+  // h0 of query m in the accumulator layout (the forward's arithmetic; rows >= k are 0) from
+  // its tables (buffer u) and its gathered P2 rows: built at the end of query m-1 (a wait at
+  // the loop head for loads of the previous iteration came out as vmcnt(0): behind every row
+  // store of that iteration)
+  float h0[16];
+  auto build_h0 = [&](int u) {
+    const float4* dT = dirT(u);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int r = (e & 3) + 8 * (e >> 2) + 4 * half;
+      const float4 dr = dT[r];
+      const float pos = __fadd_rn(__builtin_fmaf(wz, dr.z, __builtin_fmaf(wy, dr.y, __fmul_rn(w0, dr.x))), bp);
+      const float h = lrelu(__fadd_rn(__fadd_rn(pv[e], p1v), pos));
+      h0[e] = r < k ? h : 0.f;
+      if (e % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // bound the hoisted LDS reads
+    }
+  };
   issue(q0);
   load_idx(q0 + 1);
+  load_q(q0);
+  tables(q0, 0);
+  load_q(q0 + 1);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  build_h0(0);
   const int nit = CS > 1 ? queries_per_wave : q1 - q0;
   for (int it = 0; it < nit; ++it) {
     const int n = q0 + it;
+    const int cu = it & 1;               // this query's table buffer
     const bool act = CS == 1 || n < q1;  // wave-uniform
     float g0 = 0.f, g1 = 0.f, g2 = 0.f;  // d(dir) of the lane's row (direction pass)
-    int rkv = -1;
+    const int rkv = rkm;                 // this query's row slots (dirs store)
+    float gq[OT];
+    int amc[OT];
+#pragma unroll
+    for (int t = 0; t < OT; ++t) {
+      gq[t] = gqn[t];
+      amc[t] = amn[t];
+    }
     if (act) {
-      rkv = rkn;
-      float gq[OT];
-      int amc[OT];
-#pragma unroll
-      for (int t = 0; t < OT; ++t) {
-        gq[t] = dvq[t] * (ovq[t] > 0.f ? 1.f : kSlope);
-        amc[t] = amq[t];
-      }
-      // ---- directions (lane r) and (g', argmax) per output into the wave's LDS tables
-      const float qx = x1b[n * 3 + 0], qy = x1b[n * 3 + 1], qz = x1b[n * 3 + 2];
-      if (lane < kRows) dirT[lane] = make_float4(xv0 - qx, xv1 - qy, xv2 - qz, 0.f);
-#pragma unroll
-      for (int t = 0; t < OT; ++t)
-        if (half == 0) {
-          gdam[32 * t + l32] = make_float2(gq[t], __int_as_float(amc[t]));
-          __bf16 gh, gm, gl;
-          split3(gq[t], gh, gm, gl);
-          gpl[32 * t + l32] = gh;
-          gpl[D_OUT + 32 * t + l32] = gm;
-          gpl[2 * D_OUT + 32 * t + l32] = gl;
-          g16[32 * t + l32] = (unsigned short)amc[t];
-        }
+      const float4* dT = dirT(cu);
+      const __bf16* gp = gpl(cu);
+      const unsigned short* ga16 = g16(cu);
       // the tables are read back below through 16-byte (uint4) loads: a compiler memory barrier
-      // so those loads are not moved above these 2-byte stores (wave_barrier orders no memory)
+      // so those loads are not moved above their 2-byte stores (wave_barrier orders no memory)
       asm volatile("" ::: "memory");
       __builtin_amdgcn_wave_barrier();
-      // ---- h0 in the accumulator layout (the forward's arithmetic; rows >= k are 0)
-      float h0[16];
+      if constexpr (!DW1_MFMA) {  // the tile the dW1 update reads (h0 built by query n-1)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int r = (e & 3) + 8 * (e >> 2) + 4 * half;
-        const float4 dr = dirT[r];
-        const float pos = __fadd_rn(__builtin_fmaf(wz, dr.z, __builtin_fmaf(wy, dr.y, __fmul_rn(w0, dr.x))), bp);
-        const float h = lrelu(__fadd_rn(__fadd_rn(pv[e], p1v), pos));
-        h0[e] = r < k ? h : 0.f;
-        if constexpr (!DW1_MFMA) T[r * LD + l32] = h0[e];  // the tile the dW1 update reads
-        if (e % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // bound the hoisted LDS reads
+        for (int e = 0; e < 16; ++e) T[((e & 3) + 8 * (e >> 2) + 4 * half) * LD + l32] = h0[e];
       }
-      // the row pass re-reads the directions from LDS: without this compiler barrier they
-      // stay live in 64 registers across the MFMAs
-      asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       // ---- the next query's loads, in flight during this query's MFMAs and stores
       issue(n + 1);
@@ -430,10 +508,10 @@ void cost_volume_bwd_kernel(
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
           const int o0 = 16 * ks + 8 * half;
-          const uint4 av4 = *reinterpret_cast<const uint4*>(g16 + o0);
-          const uint4 ph = *reinterpret_cast<const uint4*>(gpl + o0);
-          const uint4 pm = *reinterpret_cast<const uint4*>(gpl + D_OUT + o0);
-          const uint4 pq = *reinterpret_cast<const uint4*>(gpl + 2 * D_OUT + o0);
+          const uint4 av4 = *reinterpret_cast<const uint4*>(ga16 + o0);
+          const uint4 ph = *reinterpret_cast<const uint4*>(gp + o0);
+          const uint4 pm = *reinterpret_cast<const uint4*>(gp + D_OUT + o0);
+          const uint4 pq = *reinterpret_cast<const uint4*>(gp + 2 * D_OUT + o0);
           const unsigned aw[4] = {av4.x, av4.y, av4.z, av4.w};
           unsigned mk[4];
 #pragma unroll
@@ -496,7 +574,7 @@ void cost_volume_bwd_kernel(
       } else {
 #pragma unroll
         for (int i = 0; i < D_OUT / 2; ++i) {
-          const float2 ga = gdam[2 * i + half];
+          const float2 ga = gdam(cu)[2 * i + half];
           gw1[i] = __builtin_fmaf(ga.x, T[__float_as_int(ga.y) * LD + l32], gw1[i]);
           if (i % 8 == 7) __builtin_amdgcn_sched_barrier(0);  // bound the hoisted LDS reads
         }
@@ -518,15 +596,21 @@ void cost_volume_bwd_kernel(
         }
         dz[e] = dacc[e] * sl;
       }
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- the next query's tables (its loads were issued before this query's MFMAs; nothing
+      // of this query's is stored yet)
+      tables(n + 1, cu ^ 1);
+      load_q(n + 2);
+      __builtin_amdgcn_sched_barrier(0);
       // ---- row pass: dP2 rows out, dP1, dWpos
       float dp1_acc = 0.f;
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int r = (e & 3) + 8 * (e >> 2) + 4 * half;
         const float v = dz[e];
-        const float4 dr = dirT[r];
-        const int slot = ranked ? __shfl(rkv, r, kWave) : (nbase + n) * k + r;
-        const unsigned off = (r < k && slot >= 0) ? ((unsigned)slot * D_IN + cg) * 4u : kOOB;
+        const float4 dr = dT[r];
+        const int slot = __float_as_int(dr.w);
+        const unsigned off = slot >= 0 ? ((unsigned)slot * D_IN + cg) * 4u : kOOB;
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rowr, (int)off, 0, 0);
         dp1_acc = __fadd_rn(dp1_acc, v);
         gwp0 = __builtin_fmaf(v, dr.x, gwp0);
@@ -534,7 +618,7 @@ void cost_volume_bwd_kernel(
         gwp2 = __builtin_fmaf(v, dr.z, gwp2);
         if (e % 4 == 3) __builtin_amdgcn_sched_barrier(0);
       }
-      dp1_acc = __fadd_rn(dp1_acc, __shfl_xor(dp1_acc, 32, kWave));
+      dp1_acc = __fadd_rn(dp1_acc, xor32(dp1_acc));
       if (half == 0) dp1[((long long)b * n1 + n) * D_IN + cg] = dp1_acc;
       gbp = __fadd_rn(gbp, dp1_acc);
       // ---- d(dir_r) = Wpos^T dz0[r]: dz0 through the LDS tile into row-per-lane
@@ -551,9 +635,9 @@ void cost_volume_bwd_kernel(
         g2 = __builtin_fmaf(wp.z, v, g2);
         if (i % 4 == 3) __builtin_amdgcn_sched_barrier(0);
       }
-      g0 = __fadd_rn(g0, __shfl_xor(g0, 32, kWave));
-      g1 = __fadd_rn(g1, __shfl_xor(g1, 32, kWave));
-      g2 = __fadd_rn(g2, __shfl_xor(g2, 32, kWave));
+      g0 = __fadd_rn(g0, xor32(g0));
+      g1 = __fadd_rn(g1, xor32(g1));
+      g2 = __fadd_rn(g2, xor32(g2));
       __builtin_amdgcn_wave_barrier();  // the tile is rewritten by the next query
     }  // act
     if constexpr (CS > 1) {  // the second channel half's d(dir) partials -> the first wave
@@ -579,13 +663,8 @@ void cost_volume_bwd_kernel(
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(g1), dirr, (int)(off == kOOB ? kOOB : off + 4u), 0, 0);
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(g2), dirr, (int)(off == kOOB ? kOOB : off + 8u), 0, 0);
       }
-      float s0 = row ? g0 : 0.f, s1 = row ? g1 : 0.f, s2 = row ? g2 : 0.f;
-#pragma unroll
-      for (int m = 16; m >= 1; m >>= 1) {
-        s0 = __fadd_rn(s0, __shfl_xor(s0, m, kWave));
-        s1 = __fadd_rn(s1, __shfl_xor(s1, m, kWave));
-        s2 = __fadd_rn(s2, __shfl_xor(s2, m, kWave));
-      }
+      const float s0 = sum32_lane0(row ? g0 : 0.f), s1 = sum32_lane0(row ? g1 : 0.f),
+                  s2 = sum32_lane0(row ? g2 : 0.f);
       if (lane == 0) {
         float* o = dx1 + ((long long)b * n1 + n) * 3;
         o[0] = -s0;
@@ -593,11 +672,18 @@ void cost_volume_bwd_kernel(
         o[2] = -s2;
       }
     }
+    // ---- the next query's h0: its gathers were issued before this query's stores, so the
+    // wait is counted (vmcnt) inside this iteration and lets the stores run on
+    if (act) {
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("" ::: "memory");
+      build_h0((it & 1) ^ 1);
+    }
   }
   // ---- workgroup partials: waves add their accumulators into one LDS slab in wave order
-  gwp0 = __fadd_rn(gwp0, __shfl_xor(gwp0, 32, kWave));
-  gwp1 = __fadd_rn(gwp1, __shfl_xor(gwp1, 32, kWave));
-  gwp2 = __fadd_rn(gwp2, __shfl_xor(gwp2, 32, kWave));
+  gwp0 = __fadd_rn(gwp0, xor32(gwp0));
+  gwp1 = __fadd_rn(gwp1, xor32(gwp1));
+  gwp2 = __fadd_rn(gwp2, xor32(gwp2));
   __syncthreads();  // every wave is done with its tiles (the buffer is reused)
   float* rw = lds_all;
   for (int w = 0; w < kWaves; ++w) {
