@@ -38,6 +38,7 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr float kSlope = 0.1f;
 constexpr int kRows = 32;        // MFMA M-tile = neighbour rows of one query
@@ -281,7 +282,7 @@ void cost_volume_bwd_kernel(
   // are written): directions + slots, (g', argmax), g' as three bf16 planes + the argmax row
   // as u16 (the A operand of dh0 = M W1 on mfma_x6: 8 outputs' planes masked per 16-bit half)
   constexpr int TABLES = 4 * 2 * kRows + 2 * D_OUT + 2 * D_OUT;
-  constexpr int PER_WAVE = TILE + 2 * TABLES;
+  constexpr int PER_WAVE = TILE + 2 * TABLES + 2 * kRows;  // + the neighbour-index row
   constexpr int SHARED = 4 * D_IN;                         // Wpos rows (x, y, z, 0)
   // dW1 on the VALU through the h0 tile (D_OUT = 32) or as M^T h0 on the matrix cores
   // (D_OUT = 64: the VALU update's 32 accumulators and hoisted reads spilled at 2 waves/SIMD)
@@ -308,8 +309,13 @@ void cost_volume_bwd_kernel(
   const int cg = hc * 32 + l32;                // the lane's channel
   float4* wposT = reinterpret_cast<float4*>(lds_all);
   float* T = lds_all + SHARED + wave * PER_WAVE;
-  // table buffer u: directions dirT(u), (g', argmax) gdam(u), planes gpl(u) [3][D_OUT], g16(u)
-  auto dirT = [&](int u) { return reinterpret_cast<float4*>(T + TILE + u * TABLES); };
+  // table buffer u: direction components dX(u), dY(u) = dX + 64, dZ(u) = dX + 128 and the
+  // rows' byte offsets dO(u) (structure of arrays: rows e .. e+3 of a lane are 4 consecutive
+  // entries, one 16-byte read, already register pairs for the packed math), (g', argmax)
+  // gdam(u), planes gpl(u) [3][D_OUT], g16(u)
+  auto dX = [&](int u) { return T + TILE + u * TABLES; };
+  auto dO = [&](int u) { return reinterpret_cast<unsigned*>(T + TILE + u * TABLES + 6 * kRows); };
+  int* jT = reinterpret_cast<int*>(T + TILE + 2 * TABLES);  // the next query's indices
   auto gdam = [&](int u) { return reinterpret_cast<float2*>(T + TILE + u * TABLES + 8 * kRows); };
   auto gpl = [&](int u) {
     return reinterpret_cast<__bf16*>(T + TILE + u * TABLES + 8 * kRows + 2 * D_OUT);
@@ -367,7 +373,11 @@ void cost_volume_bwd_kernel(
   float gb1[OT];  // db1[32 t + l32]: sum of g' (the same add chain as the previous kernel)
 #pragma unroll
   for (int t = 0; t < OT; ++t) gb1[t] = 0.f;
-  float gwp0 = 0.f, gwp1 = 0.f, gwp2 = 0.f, gbp = 0.f;
+  // dWpos partials per component, even and odd rows of the lane in the two halves of a packed
+  // pair (v_pk_fma_f32), folded at the end
+  f32x2 gpx = {0.f, 0.f}, gpy = {0.f, 0.f}, gpz = {0.f, 0.f};
+  float gbp = 0.f;
+  const f32x2 SL2 = {kSlope, kSlope};
 
   const int q0 = (bx * (kWaves / CS) + qw) * queries_per_wave;
   const int q1 = min(n1, q0 + queries_per_wave);
@@ -375,7 +385,8 @@ void cost_volume_bwd_kernel(
   // its MFMAs and its row stores, so they land under this query's work and -- vmcnt retiring
   // in issue order -- never wait behind this query's stores.  Query n+2's indices one further.
   int jn = (int)__builtin_amdgcn_raw_buffer_load_b32(ixr, (int)(((unsigned)q0 * (unsigned)k + lane) * 4u), 0, 0);
-  float pv[16], xv0, xv1, xv2, p1v, ovq[OT], dvq[OT];
+  f32x2 pv[8];  // the lane's gathered P2 values, rows e = 2 i, 2 i + 1 as a register pair
+  float xv0, xv1, xv2, p1v, ovq[OT], dvq[OT];
   // the query's own point, one query ahead in scalar registers (a load at its use waited out a
   // whole memory round trip per query)
   float qs0, qs1, qs2;
@@ -386,7 +397,14 @@ void cost_volume_bwd_kernel(
     qs2 = x1b[nq * 3 + 2];
   };
   int amq[OT], rkn;
-  auto issue = [&](int n) {  // loads of query n (jn = its indices)
+  auto load_idx = [&](int n) {
+    jn = (int)__builtin_amdgcn_raw_buffer_load_b32(ixr, (int)(((unsigned)n * (unsigned)k + lane) * 4u), 0, 0);
+  };
+  // loads of query n (jn = its indices) and of query n+1's indices: those go out before the
+  // P2 gathers, so every path into the loop head has the gathers issued after them (a wait for
+  // them at the next issue is then a partial vmcnt on the prologue path as well; issued last,
+  // the loop-head merge turned it into vmcnt(0), behind all of the previous query's stores)
+  auto issue = [&](int n) {
     // what its tables need first (written while the P2 gathers are still in flight: vmcnt
     // retires in issue order), then the gathers
     const unsigned xo = (unsigned)jn * 12u;
@@ -402,15 +420,22 @@ void cost_volume_bwd_kernel(
     }
     rkn = (int)__builtin_amdgcn_raw_buffer_load_b32(
         rkr, (int)(lane < k ? ((unsigned)n * (unsigned)k + lane) * 4u : kOOB), 0, 0);
+    // the indices of the lane's rows R_h(e) through LDS: rows 4 q + 4 h .. + 3 are four
+    // consecutive entries (one 16-byte read for e = 4 q .. 4 q + 3; a shuffle per row was 16
+    // ds_bpermute instructions)
+    jT[lane] = jn;
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    load_idx(n + 1);
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int j = __shfl(jn, (e & 3) + 8 * (e >> 2) + 4 * half, kWave);
-      pv[e] = bload(p2r, ((unsigned)j * D_IN + cg) * 4u);
+    for (int q = 0; q < 4; ++q) {
+      const int4 j4 = *reinterpret_cast<const int4*>(jT + 8 * q + 4 * half);
+      pv[2 * q][0] = bload(p2r, ((unsigned)j4.x * D_IN + cg) * 4u);
+      pv[2 * q][1] = bload(p2r, ((unsigned)j4.y * D_IN + cg) * 4u);
+      pv[2 * q + 1][0] = bload(p2r, ((unsigned)j4.z * D_IN + cg) * 4u);
+      pv[2 * q + 1][1] = bload(p2r, ((unsigned)j4.w * D_IN + cg) * 4u);
     }
     p1v = bload(p1r, ((unsigned)n * D_IN + cg) * 4u);
-  };
-  auto load_idx = [&](int n) {
-    jn = (int)__builtin_amdgcn_raw_buffer_load_b32(ixr, (int)(((unsigned)n * (unsigned)k + lane) * 4u), 0, 0);
   };
   // query m's tables into buffer u from its prefetched loads (issue(m), load_q(m)): g' and the
   // argmax rows (kept in registers for the dW1 / db1 updates), directions with the row's
@@ -430,7 +455,11 @@ void cost_volume_bwd_kernel(
     }
     rkm = rkn;
     const int slot = lane < k ? (ranked ? rkm : (nbase + m) * k + lane) : -1;
-    dirT(u)[lane] = make_float4(xv0 - qs0, xv1 - qs1, xv2 - qs2, __int_as_float(slot));
+    float* x = dX(u);
+    x[lane] = xv0 - qs0;
+    x[2 * kRows + lane] = xv1 - qs1;
+    x[4 * kRows + lane] = xv2 - qs2;
+    dO(u)[lane] = slot >= 0 ? (unsigned)slot * (unsigned)(D_IN * 4) : kOOB;
 #pragma unroll
     for (int t = 0; t < OT; ++t) {
       gdam(u)[32 * t + l32] = make_float2(gqn[t], __int_as_float(amn[t]));
@@ -442,25 +471,34 @@ void cost_volume_bwd_kernel(
       g16(u)[32 * t + l32] = (unsigned short)amn[t];
     }
   };
-  // h0 of query m in the accumulator layout (the forward's arithmetic; rows >= k are 0) from
-  // its tables (buffer u) and its gathered P2 rows: built at the end of query m-1 (a wait at
-  // the loop head for loads of the previous iteration came out as vmcnt(0): behind every row
-  // store of that iteration)
-  float h0[16];
+  // h0 of query m in the accumulator layout (the forward's arithmetic) from its tables (buffer
+  // u) and its gathered P2 rows: built at the end of query m-1 (a wait at the loop head for
+  // loads of the previous iteration came out as vmcnt(0): behind every row store of that
+  // iteration).  Rows e, e+1 as a register pair through the packed f32 ops (the same IEEE
+  // operations element by element); LeakyReLU as max(z, 0.1 z).  Rows >= k are left as they
+  // come (finite: out-of-range gathers read 0): they meet only zero routing (am < k), zero dz0
+  // and dropped stores.
+  f32x2 h0[8];
   auto build_h0 = [&](int u) {
-    const float4* dT = dirT(u);
+    const float* x = dX(u);
+    const f32x2 W0 = {w0, w0}, WY = {wy, wy}, WZ = {wz, wz}, BP = {bp, bp}, P1 = {p1v, p1v};
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int r = (e & 3) + 8 * (e >> 2) + 4 * half;
-      const float4 dr = dT[r];
-      const float pos = __fadd_rn(__builtin_fmaf(wz, dr.z, __builtin_fmaf(wy, dr.y, __fmul_rn(w0, dr.x))), bp);
-      const float h = lrelu(__fadd_rn(__fadd_rn(pv[e], p1v), pos));
-      h0[e] = r < k ? h : 0.f;
-      if (e % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // bound the hoisted LDS reads
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 X4 = *reinterpret_cast<const f32x4*>(x + 8 * q + 4 * half);
+      const f32x4 Y4 = *reinterpret_cast<const f32x4*>(x + 2 * kRows + 8 * q + 4 * half);
+      const f32x4 Z4 = *reinterpret_cast<const f32x4*>(x + 4 * kRows + 8 * q + 4 * half);
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const f32x2 X2 = {X4[2 * p], X4[2 * p + 1]}, Y2 = {Y4[2 * p], Y4[2 * p + 1]},
+                    Z2 = {Z4[2 * p], Z4[2 * p + 1]};
+        const f32x2 pos = __builtin_elementwise_fma(WZ, Z2, __builtin_elementwise_fma(WY, Y2, W0 * X2)) + BP;
+        const f32x2 z = (pv[2 * q + p] + P1) + pos;
+        h0[2 * q + p] = __builtin_elementwise_max(z, z * SL2);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // bound the hoisted LDS reads
     }
   };
   issue(q0);
-  load_idx(q0 + 1);
   load_q(q0);
   tables(q0, 0);
   load_q(q0 + 1);
@@ -482,7 +520,8 @@ void cost_volume_bwd_kernel(
       amc[t] = amn[t];
     }
     if (act) {
-      const float4* dT = dirT(cu);
+      const float* xc = dX(cu);
+      const unsigned* oc = dO(cu);
       const __bf16* gp = gpl(cu);
       const unsigned short* ga16 = g16(cu);
       // the tables are read back below through 16-byte (uint4) loads: a compiler memory barrier
@@ -491,12 +530,11 @@ void cost_volume_bwd_kernel(
       __builtin_amdgcn_wave_barrier();
       if constexpr (!DW1_MFMA) {  // the tile the dW1 update reads (h0 built by query n-1)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) T[((e & 3) + 8 * (e >> 2) + 4 * half) * LD + l32] = h0[e];
+        for (int e = 0; e < 16; ++e) T[((e & 3) + 8 * (e >> 2) + 4 * half) * LD + l32] = h0[e >> 1][e & 1];
       }
       __builtin_amdgcn_sched_barrier(0);
       // ---- the next query's loads, in flight during this query's MFMAs and stores
       issue(n + 1);
-      load_idx(n + 2);
       __builtin_amdgcn_sched_barrier(0);
       // ---- dh0 = M W1 on the bf16 matrix cores (mfma_x6), M[r][o] = g'[o] [am[o] == r]: K-step
       // ks, lane half h covers o = 16 ks + 8 h + j; the lane's A = the planes of g'[o] where
@@ -540,7 +578,7 @@ void cost_volume_bwd_kernel(
         for (int ks2 = 0; ks2 < 2; ++ks2) {
           float v[8];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = h0[8 * ks2 + j];
+          for (int j = 0; j < 8; ++j) v[j] = h0[4 * ks2 + (j >> 1)][j & 1];
           hp[ks2] = split8(v);
         }
 #pragma unroll
@@ -584,17 +622,22 @@ void cost_volume_bwd_kernel(
       __builtin_amdgcn_wave_barrier();  // the h0 tile is read before dz0 overwrites it
       __builtin_amdgcn_sched_barrier(0);
       // ---- dz0 = dh0 * LeakyReLU'(h0) (registers)
-      float dz[16];
+      f32x2 dz[8];
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        float sl = h0[e] > 0.f ? 1.f : kSlope;
-        if constexpr (OVR) {
-          const int r = (e & 3) + 8 * (e >> 2) + 4 * half;
-          const unsigned o = __builtin_amdgcn_raw_buffer_load_b8(
-              s0r, (int)((((unsigned)n * (unsigned)k + r) * D_IN + cg)), 0, 0);
-          sl = o == 1u ? 1.f : (o == 2u ? kSlope : sl);
+      for (int i = 0; i < 8; ++i) {
+        const f32x2 d2 = {dacc[2 * i], dacc[2 * i + 1]};
+        const f32x2 ds = d2 * SL2;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          bool pass = h0[i][p] > 0.f;
+          if constexpr (OVR) {
+            const int e = 2 * i + p, r = (e & 3) + 8 * (e >> 2) + 4 * half;
+            const unsigned o = __builtin_amdgcn_raw_buffer_load_b8(
+                s0r, (int)((((unsigned)n * (unsigned)k + r) * D_IN + cg)), 0, 0);
+            pass = o == 1u ? true : (o == 2u ? false : pass);
+          }
+          dz[i][p] = pass ? d2[p] : ds[p];
         }
-        dz[e] = dacc[e] * sl;
       }
       __builtin_amdgcn_sched_barrier(0);
       // ---- the next query's tables (its loads were issued before this query's MFMAs; nothing
@@ -603,28 +646,40 @@ void cost_volume_bwd_kernel(
       load_q(n + 2);
       __builtin_amdgcn_sched_barrier(0);
       // ---- row pass: dP2 rows out, dP1, dWpos
-      float dp1_acc = 0.f;
+      f32x2 dpp1 = {0.f, 0.f};  // dP1 partials of the even / odd rows
+      const unsigned cgo = (unsigned)cg * 4u;
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int r = (e & 3) + 8 * (e >> 2) + 4 * half;
-        const float v = dz[e];
-        const float4 dr = dT[r];
-        const int slot = __float_as_int(dr.w);
-        const unsigned off = slot >= 0 ? ((unsigned)slot * D_IN + cg) * 4u : kOOB;
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rowr, (int)off, 0, 0);
-        dp1_acc = __fadd_rn(dp1_acc, v);
-        gwp0 = __builtin_fmaf(v, dr.x, gwp0);
-        gwp1 = __builtin_fmaf(v, dr.y, gwp1);
-        gwp2 = __builtin_fmaf(v, dr.z, gwp2);
-        if (e % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+      for (int q = 0; q < 4; ++q) {
+        const uint4 O4 = *reinterpret_cast<const uint4*>(oc + 8 * q + 4 * half);
+        const f32x4 X4 = *reinterpret_cast<const f32x4*>(xc + 8 * q + 4 * half);
+        const f32x4 Y4 = *reinterpret_cast<const f32x4*>(xc + 2 * kRows + 8 * q + 4 * half);
+        const f32x4 Z4 = *reinterpret_cast<const f32x4*>(xc + 4 * kRows + 8 * q + 4 * half);
+        const unsigned o4[4] = {O4.x, O4.y, O4.z, O4.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)  // a dropped row's offset stays out of range (kOOB + cgo)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dz[2 * q + (i >> 1)][i & 1]), rowr,
+                                                (int)(o4[i] + cgo), 0, 0);
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const f32x2 v = dz[2 * q + p];
+          dpp1 = dpp1 + v;
+          gpx = __builtin_elementwise_fma(v, (f32x2){X4[2 * p], X4[2 * p + 1]}, gpx);
+          gpy = __builtin_elementwise_fma(v, (f32x2){Y4[2 * p], Y4[2 * p + 1]}, gpy);
+          gpz = __builtin_elementwise_fma(v, (f32x2){Z4[2 * p], Z4[2 * p + 1]}, gpz);
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
+      float dp1_acc = __fadd_rn(dpp1.x, dpp1.y);
       dp1_acc = __fadd_rn(dp1_acc, xor32(dp1_acc));
       if (half == 0) dp1[((long long)b * n1 + n) * D_IN + cg] = dp1_acc;
       gbp = __fadd_rn(gbp, dp1_acc);
       // ---- d(dir_r) = Wpos^T dz0[r]: dz0 through the LDS tile into row-per-lane
 #pragma unroll
-      for (int e = 0; e < 16; ++e) T[((e & 3) + 8 * (e >> 2) + 4 * half) * LD + l32] = dz[e];
+      for (int e = 0; e < 16; ++e) T[((e & 3) + 8 * (e >> 2) + 4 * half) * LD + l32] = dz[e >> 1][e & 1];
       __builtin_amdgcn_wave_barrier();
+      // scalar fmas: the packed form (v_pk_fma_f32 with the LDS value broadcast by op_sel)
+      // gave run-to-run different d(dir) on the MI355X at the model's sizes (tests/
+      // test_gpu_fused.py::test_cost_volume_bwd_deterministic_at_model_size)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int cc = half * 16 + i;
@@ -681,6 +736,8 @@ void cost_volume_bwd_kernel(
     }
   }
   // ---- workgroup partials: waves add their accumulators into one LDS slab in wave order
+  float gwp0 = __fadd_rn(gpx.x, gpx.y), gwp1 = __fadd_rn(gpy.x, gpy.y),
+        gwp2 = __fadd_rn(gpz.x, gpz.y);
   gwp0 = __fadd_rn(gwp0, xor32(gwp0));
   gwp1 = __fadd_rn(gwp1, xor32(gwp1));
   gwp2 = __fadd_rn(gwp2, xor32(gwp2));

@@ -93,6 +93,39 @@ def test_cost_volume_bwd_csr_bitwise(din, dout, n1, n2, bsz, k):
     assert torch.count_nonzero(r[1][:, -1]) == 0 and torch.count_nonzero(r[3][:, -1]) == 0
 
 
+@pytest.mark.parametrize("din,dout,n1", [(32, 32, 8192), (64, 64, 2048)])
+def test_cost_volume_bwd_deterministic_at_model_size(din, dout, n1):
+    """At the model's level-0/1 sizes (B=16 clouds, K=32: ~2000 waves, every SIMD busy) the
+    backward gives the same bits on every run, and the ranked and plain entry points agree.
+    (A packed-f32 d(dir) accumulation with a broadcast operand passed the small bitwise test
+    above and still gave run-to-run different dx1 / dx2 here.)"""
+    import kdpc_native as K
+    g = torch.Generator(device="cpu").manual_seed(din + n1)
+    bsz, k = 16, 32
+    x1 = torch.rand(bsz, n1, 3, generator=g).to(DEV)
+    x2 = torch.rand(bsz, n1, 3, generator=g).to(DEV)
+    idx = K.knn_point(k, x2, x1)
+    p1 = torch.randn(bsz, n1, din, generator=g).to(DEV)
+    p2 = torch.randn(bsz, n1, din, generator=g).to(DEV)
+    wpos = (torch.randn(din, 3, generator=g) * 0.3).to(DEV)
+    bpos = (torch.randn(din, generator=g) * 0.1).to(DEV)
+    w1 = (torch.randn(dout, din, generator=g) / din ** 0.5).to(DEV)
+    b1 = (torch.randn(dout, generator=g) * 0.1).to(DEV)
+    out, amax = K.cost_volume_fwd(x1, x2, idx, p1, p2, wpos, bpos, w1, b1)
+    gout = torch.randn(bsz, n1, dout, generator=g).to(DEV)
+    runs = [K.cost_volume_bwd_csr(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout)
+            for _ in range(3)]
+    dp1, dp2r, dx1, ddr, dpar = K.cost_volume_bwd(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax,
+                                                  gout)
+    csr = K.csr_of(idx, n1)
+    plain = [dp1, K.group_rows_grad(dp2r.view(bsz, n1 * k, din), csr, bsz, n1, din), dx1,
+             K.group_rows_grad(ddr.view(bsz, n1 * k, 3), csr, bsz, n1, 3), dpar]
+    for i, name in enumerate(["dp1", "dp2", "dx1", "dx2", "dparams"]):
+        for r in runs[1:]:
+            assert torch.equal(runs[0][i], r[i]), name
+        assert torch.equal(runs[0][i], plain[i]), name
+
+
 @pytest.mark.parametrize("din,dout,n1,n2,bsz,k", [
     (32, 32, 700, 800, 2, 32), (64, 64, 300, 500, 2, 32), (32, 64, 200, 300, 1, 17),
     (128, 128, 200, 250, 2, 32), (256, 256, 150, 200, 2, 20)])
