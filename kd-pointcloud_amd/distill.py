@@ -64,8 +64,13 @@ def _core(model):
     return model.module if isinstance(model, torch.nn.parallel.DistributedDataParallel) else model
 
 
-# False runs the frozen teacher's forward in line (the tests' reference)
-TEACHER_STREAM = True
+# True runs the frozen teacher's forward on a stream of its own, beside the student's forward
+# (round 3: 15.6 -> 13.8 ms per KD step).  Off since round 5: at the configs[3] slice (B=4,
+# N=8192) with the next batch's plan prefetched, the graphed and the eager KD steps then
+# disagreed in the last bits in about one process in three (tests/test_gpu_kd.py::
+# test_graphed_kd_step_b4_n8192; never with the teacher in line: DESIGN §5), and the cause is
+# not pinned down.  Bit-identical reproducibility comes first; the teacher runs in line.
+TEACHER_STREAM = False
 _teacher_streams = {}
 
 
