@@ -116,8 +116,7 @@ class _kd_student_streams:
 
     def __init__(self, student):
         core = _core(student)
-        self.core = core if (hasattr(core, "coord_fork") and TEACHER_STREAM
-                             and not KD_COORD_FORK) else None
+        self.core = core if (hasattr(core, "coord_fork") and not KD_COORD_FORK) else None
 
     def __enter__(self):
         if self.core is not None:
