@@ -65,12 +65,13 @@ def _core(model):
 
 
 # True runs the frozen teacher's forward on a stream of its own, beside the student's forward
-# (round 3: 15.6 -> 13.8 ms per KD step).  Off since round 5: at the configs[3] slice (B=4,
-# N=8192) with the next batch's plan prefetched, the graphed and the eager KD steps then
-# disagreed in the last bits in about one process in three (tests/test_gpu_kd.py::
-# test_graphed_kd_step_b4_n8192; never with the teacher in line: DESIGN §5), and the cause is
-# not pinned down.  Bit-identical reproducibility comes first; the teacher runs in line.
-TEACHER_STREAM = False
+# (round 3: 15.6 -> 13.8 ms per KD step).  The teacher reads its own copy of the coordinate
+# plan (_TEACHER_OWN_PLAN): reading the very plan tensors the student's forward reads, the
+# graphed and the eager KD steps disagreed in the last bits in about one process in three at
+# the configs[3] slice with the plan prefetched (round 5; never with a private copy
+# or with the teacher in line).
+TEACHER_STREAM = True
+_TEACHER_OWN_PLAN = True
 _teacher_streams = {}
 
 
@@ -90,6 +91,8 @@ class _TeacherFork:
                 self.side = _teacher_streams[dev.index] = torch.cuda.Stream(device=dev)
             self.side.wait_stream(self.cur)
             with torch.cuda.stream(self.side), torch.no_grad():
+                if _TEACHER_OWN_PLAN and kw.get("fps_idx") is not None:
+                    kw = dict(kw, fps_idx=[t.clone() for t in kw["fps_idx"]])
                 self.out = teacher(*args, **kw)
         else:
             with torch.no_grad():
