@@ -188,10 +188,17 @@ __global__ __launch_bounds__(256) void group_points_lds_kernel(int c, int n, int
     q[u] = pu + 3 < pend ? *reinterpret_cast<const int4*>(ib + pu) : make_int4(0, 0, 0, 0);
   }
   const float* pb = points + ((long long)bi * c + c0) * n;
-  if ((n & 3) == 0) {
-    const int n4 = n >> 2;
-    for (int e = threadIdx.x; e < cg * n4; e += 256)
-      reinterpret_cast<float4*>(rows)[e] = reinterpret_cast<const float4*>(pb)[e];
+  if ((n & 3) == 0) {  // straight from memory into LDS (as gather_points_lds_kernel)
+    const int tot4 = cg * (n >> 2), wbase = threadIdx.x & ~63;
+    const f32x4* src = reinterpret_cast<const f32x4*>(pb);
+    f32x4* dst = reinterpret_cast<f32x4*>(rows);
+    for (int base = 0; base < tot4; base += 256) {
+      if (base + (int)threadIdx.x < tot4)
+        __builtin_amdgcn_global_load_lds(static_cast<const void*>(src + base + threadIdx.x),
+                                         (__attribute__((address_space(3))) void*)(dst + base + wbase),
+                                         16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   } else {
     for (int e = threadIdx.x; e < cg * n; e += 256) rows[e] = pb[e];
   }
