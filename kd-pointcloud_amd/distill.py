@@ -65,12 +65,14 @@ def _core(model):
 
 
 # True runs the frozen teacher's forward on a stream of its own, beside the student's forward
-# (round 3: 15.6 -> 13.8 ms per KD step).  The teacher reads its own copy of the coordinate
-# plan (_TEACHER_OWN_PLAN): reading the very plan tensors the student's forward reads, the
-# graphed and the eager KD steps disagreed in the last bits in about one process in three at
-# the configs[3] slice with the plan prefetched (round 5; never with a private copy
-# or with the teacher in line).
-TEACHER_STREAM = True
+# (round 3: 15.6 -> 13.8 ms per KD step).  Off since round 5: with it on, the graphed and the
+# eager KD steps (and the world-2 graphed KD step against its eager average) disagreed now and
+# then -- in the last bits in about one process in three at the configs[3] slice, and once by
+# 8e-2 at world 2 -- and a private copy of the coordinate plan for the teacher
+# (_TEACHER_OWN_PLAN) made it rarer but did not remove it.  The cause is not
+# pinned down; with the teacher in line and the student's decoder fork off every KD test
+# passed in every run.  Bit-identical reproducibility comes first.
+TEACHER_STREAM = False
 _TEACHER_OWN_PLAN = True
 _teacher_streams = {}
 
