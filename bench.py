@@ -388,6 +388,40 @@ def _time_graph(fn, iters, warmup=3):
     return ms
 
 
+def _time_graph_rotated(fns, iters, warmup=1):
+    """ms per launch of `iters` launches cycling over `fns` (each on its own inputs), captured
+    in one HIP graph and replayed.  With the distinct inputs of the rotation totalling well
+    over the 256 MiB Infinity Cache (MALL) plus the 8 x 4 MB of L2, every launch reads its
+    inputs back from HBM: the cache-busting figure, where `_time_graph` on one
+    input set measures the cache-resident one."""
+    for f in fns:
+        for _ in range(warmup):
+            f()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.graph(g, stream=side):
+        for i in range(iters):
+            fns[i % len(fns)]()
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    times = []
+    for _ in range(7):
+        e0, e1 = _events(torch.cuda.current_stream())
+        g.replay()
+        e1.record(torch.cuda.current_stream())
+        e1.synchronize()
+        times.append(e0.elapsed_time(e1))
+    ms = sorted(times)[3] / iters
+    del g
+    return ms
+
+
+MALL_BYTES = 256 << 20  # MI355X Infinity Cache (MI355X_MICROARCH.md)
+
+
 def configs1_section(dev):
     """BASELINE configs[1]: FPS + ball_query + grouping_operation (+ gather_operation) at
     B=8, N=8192, S=2048, K=16, C=64; indices bit-exact (tests/test_gpu_kernels.py).  Each op
@@ -413,6 +447,23 @@ def configs1_section(dev):
     ga3_ms = _time_graph(lambda: K.gather_points(xyz_cn, fidx), 200)
     ga64_ms = _time_graph(lambda: K.gather_points(feats, fidx), 200)
     ga_bytes = lambda c: B * (4 * c * N + 4 * S + 4 * c * S)  # noqa: E731
+    # the same two ops rotated over distinct input sets (features + FPS / ball_query indices of
+    # other clouds) whose bytes between two uses of one set exceed 2x the MALL: HBM figures
+    nrot_g = 8   # 8 x 85 MB per grouping launch
+    nrot_a = 32  # 32 x 21 MB per gather launch
+    sets = []
+    for r in range(max(nrot_g, nrot_a)):
+        xr = torch.from_numpy(synthetic.ft3d_batch(B, N, seed=100 + r)[0]).to(dev)
+        fr = K.furthest_point_sampling(xr, S)
+        ir = K.ball_query(0.5, Kn, xr, K.group_rows(xr, fr)) if r < nrot_g else None
+        sets.append((torch.randn(B, C, N, device=dev), fr, ir))
+    gr_ms = _time_graph_rotated([lambda s=s: K.group_points(s[0], s[2]) for s in sets[:nrot_g]],
+                                64)
+    ar_ms = _time_graph_rotated([lambda s=s: K.gather_points(s[0], s[1]) for s in sets[:nrot_a]],
+                                128)
+    reuse_g = (nrot_g - 1) * g_bytes
+    reuse_a = (nrot_a - 1) * ga_bytes(64)
+    del sets
     return {
         "workload": "B=8 N=8192: FPS 8192->2048, ball_query r=0.5 K=16, grouping C=64 S=2048 "
                     "K=16, gather C=3 (the model's xyz) and C=64 (BASELINE configs[1])",
@@ -431,7 +482,22 @@ def configs1_section(dev):
                                                  "launches replayed from one HIP graph"),
         "gather_operation_c64": roofline_obj("kdpc_gather_points", "configs1_gather_c64",
                                              ga64_ms, 1, ga_bytes(64), 0, bound="hbm",
-                                             grid_workgroups=B * 64),
+                                             grid_workgroups=B * 64,
+                                             note="one input set replayed: cache-resident "
+                                                  "(16.8 MB < 256 MiB MALL); the HBM figure is "
+                                                  "gather_operation_c64_rotated"),
+        # cache-busting figures: distinct inputs per launch, each set
+        # re-read only after > 2x the MALL of other launches' traffic
+        "grouping_operation_rotated": roofline_obj(
+            "kdpc_group_points", wl + "_rot8", gr_ms, 1, g_bytes, 0, bound="hbm",
+            rotation_sets=nrot_g, bytes_between_reuse=reuse_g,
+            mall_bytes=MALL_BYTES, measured_hbm_ceiling_frac=0.79,
+            note="64 launches over 8 distinct (features, ball_query idx) sets, one HIP graph"),
+        "gather_operation_c64_rotated": roofline_obj(
+            "kdpc_gather_points", "configs1_gather_c64_rot32", ar_ms, 1, ga_bytes(64), 0,
+            bound="hbm", grid_workgroups=B * 64, rotation_sets=nrot_a,
+            bytes_between_reuse=reuse_a, mall_bytes=MALL_BYTES, measured_hbm_ceiling_frac=0.79,
+            note="128 launches over 32 distinct (features, FPS idx) sets, one HIP graph"),
     }
 
 
@@ -542,7 +608,8 @@ def main(argv=None):
         line["kd_step"] = sub_kd
     if cfg1 is not None:
         line["configs1"] = cfg1
-        line["roofline_gather"] = cfg1["grouping_operation"]  # the north star's gather target
+        # the north star's gather target, as an HBM figure (inputs rotated past the MALL)
+        line["roofline_gather"] = cfg1["grouping_operation_rotated"]
     if knn is not None:
         line["roofline_knn"] = knn
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -32,16 +32,20 @@ ARCH = os.environ.get("KDPC_ARCH", "gfx950")
 CFLAGS = [
     "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}",
     "-ffp-contract=off",            # every fma the parity contract needs is explicit
+    # no packed f32 VALU (v_pk_fma/mul/add_f32, which the SLP and loop vectorisers form from
+    # pairs of scalar ops): on the MI355X their results were occasionally wrong while another
+    # kernel's waves ran beside them (tools/knn_race.py);
+    # tests/test_native_lib.py checks the built library holds none
+    "-fno-slp-vectorize", "-fno-vectorize",
     "-fvisibility=hidden",          # only KDPC_API symbols are exported
     "-Wall", "-Wno-unused-result",
     "-I", os.path.join(ROOT, "include"), "-I", CSRC,
 ]
 
 
-# per-source extra flags.  cost_volume.hip: no SLP packing (v_pk_fma pairs of independent
-# accumulators force their LDS operands into adjacent registers, hoisted in bulk: the
-# backward kernel went from 182 to >256 VGPRs with it)
-EXTRA_FLAGS = {"cost_volume.hip": ["-fno-slp-vectorize"]}
+# per-source extra flags (none at present; SLP packing, off everywhere, also forced the
+# cost-volume backward's LDS operands into adjacent registers: 182 -> >256 VGPRs)
+EXTRA_FLAGS = {}
 
 
 def source_files(csrc=CSRC, root=ROOT):

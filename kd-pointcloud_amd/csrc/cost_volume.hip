@@ -38,7 +38,6 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr float kSlope = 0.1f;
 constexpr int kRows = 32;        // MFMA M-tile = neighbour rows of one query
@@ -373,11 +372,9 @@ void cost_volume_bwd_kernel(
   float gb1[OT];  // db1[32 t + l32]: sum of g' (the same add chain as the previous kernel)
 #pragma unroll
   for (int t = 0; t < OT; ++t) gb1[t] = 0.f;
-  // dWpos partials per component, even and odd rows of the lane in the two halves of a packed
-  // pair (v_pk_fma_f32), folded at the end
-  f32x2 gpx = {0.f, 0.f}, gpy = {0.f, 0.f}, gpz = {0.f, 0.f};
+  // dWpos partials per component, even and odd rows of the lane apart, folded at the end
+  float gpx[2] = {0.f, 0.f}, gpy[2] = {0.f, 0.f}, gpz[2] = {0.f, 0.f};
   float gbp = 0.f;
-  const f32x2 SL2 = {kSlope, kSlope};
 
   const int q0 = (bx * (kWaves / CS) + qw) * queries_per_wave;
   const int q1 = min(n1, q0 + queries_per_wave);
@@ -385,7 +382,7 @@ void cost_volume_bwd_kernel(
   // its MFMAs and its row stores, so they land under this query's work and -- vmcnt retiring
   // in issue order -- never wait behind this query's stores.  Query n+2's indices one further.
   int jn = (int)__builtin_amdgcn_raw_buffer_load_b32(ixr, (int)(((unsigned)q0 * (unsigned)k + lane) * 4u), 0, 0);
-  f32x2 pv[8];  // the lane's gathered P2 values, rows e = 2 i, 2 i + 1 as a register pair
+  float pv[8][2];  // the lane's gathered P2 values, rows e = 2 i, 2 i + 1
   float xv0, xv1, xv2, p1v, ovq[OT], dvq[OT];
   // the query's own point, one query ahead in scalar registers (a load at its use waited out a
   // whole memory round trip per query)
@@ -474,26 +471,23 @@ void cost_volume_bwd_kernel(
   // h0 of query m in the accumulator layout (the forward's arithmetic) from its tables (buffer
   // u) and its gathered P2 rows: built at the end of query m-1 (a wait at the loop head for
   // loads of the previous iteration came out as vmcnt(0): behind every row store of that
-  // iteration).  Rows e, e+1 as a register pair through the packed f32 ops (the same IEEE
-  // operations element by element); LeakyReLU as max(z, 0.1 z).  Rows >= k are left as they
-  // come (finite: out-of-range gathers read 0): they meet only zero routing (am < k), zero dz0
-  // and dropped stores.
-  f32x2 h0[8];
+  // iteration).  Scalar f32 ops only (kdpc_common.h: no packed f32); LeakyReLU as
+  // max(z, 0.1 z).  Rows >= k are left as they come (finite: out-of-range gathers read 0):
+  // they meet only zero routing (am < k), zero dz0 and dropped stores.
+  float h0[8][2];
   auto build_h0 = [&](int u) {
     const float* x = dX(u);
-    const f32x2 W0 = {w0, w0}, WY = {wy, wy}, WZ = {wz, wz}, BP = {bp, bp}, P1 = {p1v, p1v};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const f32x4 X4 = *reinterpret_cast<const f32x4*>(x + 8 * q + 4 * half);
       const f32x4 Y4 = *reinterpret_cast<const f32x4*>(x + 2 * kRows + 8 * q + 4 * half);
       const f32x4 Z4 = *reinterpret_cast<const f32x4*>(x + 4 * kRows + 8 * q + 4 * half);
 #pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        const f32x2 X2 = {X4[2 * p], X4[2 * p + 1]}, Y2 = {Y4[2 * p], Y4[2 * p + 1]},
-                    Z2 = {Z4[2 * p], Z4[2 * p + 1]};
-        const f32x2 pos = __builtin_elementwise_fma(WZ, Z2, __builtin_elementwise_fma(WY, Y2, W0 * X2)) + BP;
-        const f32x2 z = (pv[2 * q + p] + P1) + pos;
-        h0[2 * q + p] = __builtin_elementwise_max(z, z * SL2);
+      for (int e = 0; e < 4; ++e) {
+        const float pos = __fadd_rn(
+            __builtin_fmaf(wz, Z4[e], __builtin_fmaf(wy, Y4[e], __fmul_rn(w0, X4[e]))), bp);
+        const float z = __fadd_rn(__fadd_rn(pv[2 * q + (e >> 1)][e & 1], p1v), pos);
+        h0[2 * q + (e >> 1)][e & 1] = fmaxf(z, __fmul_rn(z, kSlope));
       }
       __builtin_amdgcn_sched_barrier(0);  // bound the hoisted LDS reads
     }
@@ -622,13 +616,12 @@ void cost_volume_bwd_kernel(
       __builtin_amdgcn_wave_barrier();  // the h0 tile is read before dz0 overwrites it
       __builtin_amdgcn_sched_barrier(0);
       // ---- dz0 = dh0 * LeakyReLU'(h0) (registers)
-      f32x2 dz[8];
+      float dz[8][2];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const f32x2 d2 = {dacc[2 * i], dacc[2 * i + 1]};
-        const f32x2 ds = d2 * SL2;
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
+          const float d2 = dacc[2 * i + p];
           bool pass = h0[i][p] > 0.f;
           if constexpr (OVR) {
             const int e = 2 * i + p, r = (e & 3) + 8 * (e >> 2) + 4 * half;
@@ -636,7 +629,7 @@ void cost_volume_bwd_kernel(
                 s0r, (int)((((unsigned)n * (unsigned)k + r) * D_IN + cg)), 0, 0);
             pass = o == 1u ? true : (o == 2u ? false : pass);
           }
-          dz[i][p] = pass ? d2[p] : ds[p];
+          dz[i][p] = pass ? d2 : __fmul_rn(d2, kSlope);
         }
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -646,7 +639,7 @@ void cost_volume_bwd_kernel(
       load_q(n + 2);
       __builtin_amdgcn_sched_barrier(0);
       // ---- row pass: dP2 rows out, dP1, dWpos
-      f32x2 dpp1 = {0.f, 0.f};  // dP1 partials of the even / odd rows
+      float dpp1[2] = {0.f, 0.f};  // dP1 partials of the even / odd rows
       const unsigned cgo = (unsigned)cg * 4u;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -660,16 +653,16 @@ void cost_volume_bwd_kernel(
           __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dz[2 * q + (i >> 1)][i & 1]), rowr,
                                                 (int)(o4[i] + cgo), 0, 0);
 #pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          const f32x2 v = dz[2 * q + p];
-          dpp1 = dpp1 + v;
-          gpx = __builtin_elementwise_fma(v, (f32x2){X4[2 * p], X4[2 * p + 1]}, gpx);
-          gpy = __builtin_elementwise_fma(v, (f32x2){Y4[2 * p], Y4[2 * p + 1]}, gpy);
-          gpz = __builtin_elementwise_fma(v, (f32x2){Z4[2 * p], Z4[2 * p + 1]}, gpz);
+        for (int e = 0; e < 4; ++e) {
+          const float v = dz[2 * q + (e >> 1)][e & 1];
+          dpp1[e & 1] = __fadd_rn(dpp1[e & 1], v);
+          gpx[e & 1] = __builtin_fmaf(v, X4[e], gpx[e & 1]);
+          gpy[e & 1] = __builtin_fmaf(v, Y4[e], gpy[e & 1]);
+          gpz[e & 1] = __builtin_fmaf(v, Z4[e], gpz[e & 1]);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
-      float dp1_acc = __fadd_rn(dpp1.x, dpp1.y);
+      float dp1_acc = __fadd_rn(dpp1[0], dpp1[1]);
       dp1_acc = __fadd_rn(dp1_acc, xor32(dp1_acc));
       if (half == 0) dp1[((long long)b * n1 + n) * D_IN + cg] = dp1_acc;
       gbp = __fadd_rn(gbp, dp1_acc);
@@ -677,9 +670,8 @@ void cost_volume_bwd_kernel(
 #pragma unroll
       for (int e = 0; e < 16; ++e) T[((e & 3) + 8 * (e >> 2) + 4 * half) * LD + l32] = dz[e >> 1][e & 1];
       __builtin_amdgcn_wave_barrier();
-      // scalar fmas: the packed form (v_pk_fma_f32 with the LDS value broadcast by op_sel)
-      // gave run-to-run different d(dir) on the MI355X at the model's sizes (tests/
-      // test_gpu_fused.py::test_cost_volume_bwd_deterministic_at_model_size)
+      // scalar fmas (kdpc_common.h: no packed f32; the packed form gave run-to-run different
+      // d(dir) here, tests/test_gpu_fused.py::test_cost_volume_bwd_deterministic_at_model_size)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int cc = half * 16 + i;
@@ -736,8 +728,8 @@ void cost_volume_bwd_kernel(
     }
   }
   // ---- workgroup partials: waves add their accumulators into one LDS slab in wave order
-  float gwp0 = __fadd_rn(gpx.x, gpx.y), gwp1 = __fadd_rn(gpy.x, gpy.y),
-        gwp2 = __fadd_rn(gpz.x, gpz.y);
+  float gwp0 = __fadd_rn(gpx[0], gpx[1]), gwp1 = __fadd_rn(gpy[0], gpy[1]),
+        gwp2 = __fadd_rn(gpz[0], gpz[1]);
   gwp0 = __fadd_rn(gwp0, xor32(gwp0));
   gwp1 = __fadd_rn(gwp1, xor32(gwp1));
   gwp2 = __fadd_rn(gwp2, xor32(gwp2));

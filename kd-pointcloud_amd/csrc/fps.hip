@@ -61,12 +61,8 @@ __device__ __forceinline__ unsigned long long wave_argmax_key(unsigned hi, unsig
   return ((unsigned long long)vmax << 32) | lbest;
 }
 
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
 // FULL: every thread owns exactly PPT points (N = T * PPT, T = BLOCK; the model's 8192 ->
-// 2048 case): no ownership selects, and the distance of two points at a time on packed f32
-// ops (v_pk_add / v_pk_mul / v_pk_fma: the same IEEE operations per element as dist3, so the
-// same bits).  The step is VALU-bound: ~11 -> ~7 instructions per point.
+// 2048 case): no ownership selects.  Scalar f32 only (kdpc_common.h: no packed f32).
 template <int BLOCK, int PPT, bool LDS_XYZ, bool FULL>
 __global__ __launch_bounds__(BLOCK) void fps_kernel(int n, int m, int T, int log2T,
                                                     const float* __restrict__ xyz,
@@ -116,23 +112,13 @@ __global__ __launch_bounds__(BLOCK) void fps_kernel(int n, int m, int T, int log
     float best = -1.f;
     int bestk = 0;
     if constexpr (FULL) {
-      const f32x2 X = {x1, x1}, Y = {y1, y1}, Z = {z1, z1};
 #pragma unroll
-      for (int q = 0; q < PPT / 2; ++q) {
-        const f32x2 dx = f32x2{px[2 * q], px[2 * q + 1]} - X;
-        const f32x2 dy = f32x2{py[2 * q], py[2 * q + 1]} - Y;
-        const f32x2 dz = f32x2{pz[2 * q], pz[2 * q + 1]} - Z;
-        const f32x2 d =
-            __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {  // points in the reference's scan order
-          const int p = 2 * q + e;
-          const float d2 = fminf(d[e], pt[p]);
-          pt[p] = d2;
-          const bool better = d2 > best;
-          bestk = better ? tid + p * T : bestk;
-          best = better ? d2 : best;
-        }
+      for (int p = 0; p < PPT; ++p) {  // points in the reference's scan order
+        const float d2 = fminf(dist3(x1, y1, z1, px[p], py[p], pz[p]), pt[p]);
+        pt[p] = d2;
+        const bool better = d2 > best;
+        bestk = better ? tid + p * T : bestk;
+        best = better ? d2 : best;
       }
     } else {
 #pragma unroll

@@ -1,5 +1,13 @@
 // Shared device helpers for the gfx950 kernels of kd-pointcloud_amd.
 // Wave64 only: every cross-lane helper below assumes 64 lanes (CDNA4).
+//
+// No packed f32 VALU anywhere (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32, from f32x2
+// arithmetic or from the SLP vectoriser): measured on the MI355X, their results were now and
+// then wrong while another kernel's waves (the KD teacher's forward on its own stream) ran
+// beside them -- the culled kNN's seed distances came out low, so whole neighbours went
+// missing -- and the same kernels built with scalar f32 ops never were (DESIGN.md section 5,
+// tools/knn_race.py).  Every source is built with -fno-slp-vectorize -fno-vectorize (build_native.py) and
+// tests/test_native_lib.py disassembles the library to check that none is left.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>

@@ -116,34 +116,29 @@ __device__ __forceinline__ float g_fetch(const Geo& g, const Srcs& s, int nb, in
   return 0.f;
 }
 
-// acc[c] = sum_k G[r,k,c] wk[k] over the tile's LDS gather (ascending k, one fma each).
-// Channel pairs go through packed f32 fmas (v_pk_fma_f32: the same IEEE fma per element, half
-// the VALU issue): the build is the VALU work both the forward and the weight kernel issue
-// beside their MFMAs, and VALU issue is what the co-resident wave's MFMA phase slows down.
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
+// acc[c] = sum_k G[r,k,c] wk[k] over the tile's LDS gather (ascending k, one fma each;
+// scalar fmas: kdpc_common.h, no packed f32).
 template <int KM>
 __device__ __forceinline__ void build_row(const float* gl, int r, int k_n, const float* wk,
                                           float (&a)[kCC]) {
-  f32x2 acc[kCC / 2];
 #pragma unroll
-  for (int c = 0; c < kCC / 2; ++c) acc[c] = f32x2{0.f, 0.f};
+  for (int c = 0; c < kCC; ++c) a[c] = 0.f;
 #pragma unroll
   for (int k = 0; k < KM; ++k) {
     if (k < k_n) {
       const float4 lo = *reinterpret_cast<const float4*>(gl + (r * k_n + k) * kCC);
       const float4 hi = *reinterpret_cast<const float4*>(gl + (r * k_n + k) * kCC + 4);
-      const f32x2 w = f32x2{wk[k], wk[k]};
-      acc[0] = __builtin_elementwise_fma(f32x2{lo.x, lo.y}, w, acc[0]);
-      acc[1] = __builtin_elementwise_fma(f32x2{lo.z, lo.w}, w, acc[1]);
-      acc[2] = __builtin_elementwise_fma(f32x2{hi.x, hi.y}, w, acc[2]);
-      acc[3] = __builtin_elementwise_fma(f32x2{hi.z, hi.w}, w, acc[3]);
+      const float w = wk[k];
+      a[0] = __builtin_fmaf(lo.x, w, a[0]);
+      a[1] = __builtin_fmaf(lo.y, w, a[1]);
+      a[2] = __builtin_fmaf(lo.z, w, a[2]);
+      a[3] = __builtin_fmaf(lo.w, w, a[3]);
+      a[4] = __builtin_fmaf(hi.x, w, a[4]);
+      a[5] = __builtin_fmaf(hi.y, w, a[5]);
+      a[6] = __builtin_fmaf(hi.z, w, a[6]);
+      a[7] = __builtin_fmaf(hi.w, w, a[7]);
     }
-  }
-#pragma unroll
-  for (int c = 0; c < kCC / 2; ++c) {
-    a[2 * c] = acc[c].x;
-    a[2 * c + 1] = acc[c].y;
+    if (k % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // bound the hoisted LDS reads
   }
 }
 

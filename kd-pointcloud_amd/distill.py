@@ -65,32 +65,52 @@ def _core(model):
 
 
 # True runs the frozen teacher's forward on a stream of its own, beside the student's forward
-# (round 3: 15.6 -> 13.8 ms per KD step).  Off since round 5: with it on, the graphed and the
-# eager KD steps (and the world-2 graphed KD step against its eager average) disagreed now and
-# then -- in the last bits in about one process in three at the configs[3] slice, and once by
-# 8e-2 at world 2 -- and a private copy of the coordinate plan for the teacher
-# (_TEACHER_OWN_PLAN) made it rarer but did not remove it.  The cause is not
-# pinned down; with the teacher in line and the student's decoder fork off every KD test
-# passed in every run.  Bit-identical reproducibility comes first.
-TEACHER_STREAM = False
-_TEACHER_OWN_PLAN = True
+# (round 3: 15.6 -> 13.8 ms per KD step): eagerly through _TeacherFork, and in the graphed step
+# as a HIP graph of its own (GraphedStep stages, TEACHER_GRAPH).  Round 5 switched it off
+# because graphed KD steps disagreed now and then; round 6 found why: a single
+# captured graph holding the teacher's and the student's forwards as two concurrent branches
+# computes wrong values now and then on this runtime (an out-of-range kNN index from inputs
+# that were intact), while the same forwards as two graphs on two streams are bit-reproducible
+# -- and the eager two-stream step is clean under torch's stream sanitizer.  The teacher and
+# the student share the coordinate plan (no private copy: nothing of it is written by either).
+TEACHER_STREAM = True
+# the graphed KD step: teacher forward = its own graph on the teacher stream (True), or in
+# line inside the student's graph (False)
+TEACHER_GRAPH = True
+_TEACHER_OWN_PLAN = False
 _teacher_streams = {}
+
+
+def _teacher_stream(dev):
+    s = _teacher_streams.get(dev.index)
+    if s is None:
+        s = _teacher_streams[dev.index] = torch.cuda.Stream(device=dev)
+    return s
+
+
+def _detached(x):
+    if isinstance(x, torch.Tensor):
+        return x.detach()
+    if isinstance(x, (list, tuple)):
+        return type(x)(_detached(t) for t in x)
+    return x
 
 
 class _TeacherFork:
     """The frozen teacher's forward (no_grad) on its own stream, beside the student's forward:
     the two share only their inputs, and at B=4 per GPU neither fills the chip.  join()
     makes the current stream wait before the teacher's outputs are read (the KD loss).  Same
-    kernels on the same inputs: bit-identical to running the teacher in line."""
+    kernels on the same inputs: bit-identical to running the teacher in line.  Inside a graph
+    capture the teacher runs in line: a second model forward as a concurrent branch of ONE
+    graph is what went wrong; the graphed step gives it a graph of its own
+    (GraphedStep stages)."""
 
     def __init__(self, teacher, args, kw):
         dev = args[0].device
         self.cur = self.side = None
-        if TEACHER_STREAM and dev.type == "cuda":
+        if TEACHER_STREAM and dev.type == "cuda" and not torch.cuda.is_current_stream_capturing():
             self.cur = torch.cuda.current_stream(dev)
-            self.side = _teacher_streams.get(dev.index)
-            if self.side is None:
-                self.side = _teacher_streams[dev.index] = torch.cuda.Stream(device=dev)
+            self.side = _teacher_stream(dev)
             self.side.wait_stream(self.cur)
             with torch.cuda.stream(self.side), torch.no_grad():
                 if _TEACHER_OWN_PLAN and kw.get("fps_idx") is not None:
@@ -349,11 +369,14 @@ class GraphedStep:
     bucket_bytes = 8 << 20  # all-reduce bucket size (world > 1)
 
     def __init__(self, loss_fn, params, optimizer, example_inputs, warmup=3, prefetch_fn=None,
-                 n_prefetch=2, overlap=None):
+                 n_prefetch=2, overlap=None, stages=None):
         if warmup < 1:
             raise ValueError("GraphedStep needs warmup >= 1: the last warm-up backward records "
                              "the gradient order the flat buffers are laid out in")
         self.loss_fn = loss_fn
+        # stages = (side_fn, forward_fn, loss_from): the step as three captured graphs (see
+        # _capture_stages); loss_fn stays the eager form, used by the warm-up iterations
+        self.stages = stages
         self.opt = optimizer
         self.params = [p for p in params if p.requires_grad]
         self.static = [t.detach().clone() for t in example_inputs]
@@ -402,18 +425,25 @@ class GraphedStep:
             kw["capture_error_mode"] = "thread_local"
         fork = torch.cuda.Stream() if prefetch_fn is not None else None
         self.comm = torch.cuda.Stream() if self.schedule == "overlap" else None
+        self.graph_t = self.graph_f = None
+        if self.stages is not None:
+            self._capture_stages(kw, fork)
         hooks = self._bucket_hooks() if self.schedule == "overlap" else []
-        with torch.cuda.graph(self.graph_a, **kw):
+        kw_a = dict(kw, pool=self.graph_f.pool()) if self.stages is not None else kw
+        with torch.cuda.graph(self.graph_a, **kw_a):
             cap = torch.cuda.current_stream()
             self._cap = cap
-            if fork is not None:
+            if fork is not None and self.stages is None:
                 # the previous replay's tail copied its fps_next into fps_cur
                 fork.wait_stream(cap)
                 with torch.cuda.stream(fork):
                     self.fps_next = list(prefetch_fn(*self.static_next))
-            self.loss = self.loss_fn(*self.static, **self._fps_kw(self.fps_cur))
+            if self.stages is None:
+                self.loss = self.loss_fn(*self.static, **self._fps_kw(self.fps_cur))
+            else:  # the loss of the captured forward stage and the teacher graph's outputs
+                self.loss = self.stages[2](self.s_out, self.t_out, *self.static)
             self.loss.backward()
-            if fork is not None:
+            if fork is not None and self.stages is None:
                 cap.wait_stream(fork)
             if self.schedule == "overlap":
                 cap.wait_stream(self.comm)  # every bucket's all-reduce
@@ -446,9 +476,60 @@ class GraphedStep:
         # to the capture stream) and torch warns of a stream mismatch (bench's eager
         # measurement steps after the timed region)
         self.loss = self.loss.detach()
+        if self.stages is not None:  # the forward stage's outputs, without its autograd graph
+            self.s_out = _detached(self.s_out)
         self._pending = None
 
+    def _capture_stages(self, kw, fork):
+        """stages = (side_fn, forward_fn, loss_from): side_fn (the KD step's frozen teacher
+        forward, no_grad) is captured as a graph of its own on the teacher stream, forward_fn
+        (the student forward, with the next batch's coordinate plan on the forked stream) as a
+        second graph on the capture stream; the caller then captures loss_from(forward out,
+        side out, *inputs) + backward + optimizer as graph_a in the forward graph's pool (it
+        reads the forward's saved tensors).  A replay runs the first two side by side on two
+        streams and joins them before graph_a.  One graph holding both forwards as two
+        concurrent branches computed wrong values now and then on this runtime (DESIGN §5:
+        kernels read inputs that were intact in stream order and wrote different results, and
+        some runs faulted); the same two forwards as two graphs on two streams are
+        bit-reproducible and no slower."""
+        side_fn, fwd_fn, _ = self.stages
+        cur = torch.cuda.current_stream()
+        ts = _teacher_stream(self.static[0].device)
+        self.graph_t = torch.cuda.CUDAGraph()
+        ts.wait_stream(cur)
+        kwt = {k: v for k, v in kw.items() if k != "stream"}
+        with torch.cuda.graph(self.graph_t, stream=ts, **kwt):
+            with torch.no_grad():
+                self.t_out = side_fn(*self.static, **self._fps_kw(self.fps_cur))
+        cur.wait_stream(ts)
+        self.graph_f = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph_f, **kw):
+            cap = torch.cuda.current_stream()
+            if fork is not None:
+                fork.wait_stream(cap)  # the previous replay's tail wrote fps_cur
+                with torch.cuda.stream(fork):
+                    self.fps_next = list(self.prefetch_fn(*self.static_next))
+            self.s_out = fwd_fn(*self.static, **self._fps_kw(self.fps_cur))
+            if fork is not None:
+                cap.wait_stream(fork)
+            _join_capture_streams(cap, (fork,))
+
+    def _replay(self):
+        if self.graph_t is not None:
+            cur = torch.cuda.current_stream()
+            ts = _teacher_stream(self.static[0].device)
+            ts.wait_stream(cur)  # the static inputs and the plan are written on `cur`
+            with torch.cuda.stream(ts):
+                self.graph_t.replay()
+            self.graph_f.replay()
+            cur.wait_stream(ts)
+        self.graph_a.replay()
+
     def schedule_name(self):
+        if self.graph_t is not None:
+            return (" (3 graphs: teacher fwd on its own stream beside the student fwd, then "
+                    "loss+bwd+flat Adam" + (", bucketed all-reduces" if self.schedule == "overlap"
+                                            else "") + ")")
         if self.schedule == "single":
             return " (1 graph: fwd+bwd+flat Adam)"
         if self.schedule == "overlap":
@@ -637,7 +718,7 @@ class GraphedStep:
                 s.copy_(t, non_blocking=True)
             self._pending = (self._key(nxt[:self.n_prefetch]) if next_batch is not None
                              else None)
-        self.graph_a.replay()
+        self._replay()
         if self.graph_b is not None:
             dist.all_reduce(self.G)
             self.graph_b.replay()
@@ -668,14 +749,29 @@ def graphed_kd_step(teacher, student, optimizer, example_inputs, gamma=0.3, beta
     teacher.eval()
     student.train()
 
-    def run(pos1, pos2, flow, fps=None):
-        kw = {} if fps is None else {"fps_idx": fps}
-        t_fork = _TeacherFork(teacher, (pos1, pos2, pos1, pos2), kw)
-        with _kd_student_streams(student):
-            flows, fps1, fps2, _, _, feat1s, feat2s, _ = student(pos1, pos2, pos1, pos2, **kw)
-        t_flows, t_fps1, t_fps2, _, _, t_feat1s, t_feat2s, _ = t_fork.join()
+    def loss_from(s_out, t_out, pos1, pos2, flow):
+        flows, fps1, fps2, _, _, feat1s, feat2s, _ = s_out
+        t_flows, t_fps1, t_fps2, _, _, t_feat1s, t_feat2s, _ = t_out
         return loss_functions.biDirection_loss_ht(
             flows, feat1s, feat2s, fps1, fps2, flow, t_flows, t_feat1s, t_feat2s, t_fps1, t_fps2,
             gamma, beta, layer=layer)
+
+    def teacher_fwd(pos1, pos2, flow, fps=None):
+        kw = {} if fps is None else {"fps_idx": fps}
+        with torch.no_grad():
+            return teacher(pos1, pos2, pos1, pos2, **kw)
+
+    def student_fwd(pos1, pos2, flow, fps=None):
+        kw = {} if fps is None else {"fps_idx": fps}
+        with _kd_student_streams(student):
+            return student(pos1, pos2, pos1, pos2, **kw)
+
+    def run(pos1, pos2, flow, fps=None):  # the eager form (warm-up; TEACHER_GRAPH = False)
+        kw = {} if fps is None else {"fps_idx": fps}
+        t_fork = _TeacherFork(teacher, (pos1, pos2, pos1, pos2), kw)
+        s_out = student_fwd(pos1, pos2, flow, fps)
+        return loss_from(s_out, t_fork.join(), pos1, pos2, flow)
+    stages = (teacher_fwd, student_fwd, loss_from) if TEACHER_GRAPH else None
     return GraphedStep(run, student.parameters(), optimizer, example_inputs, warmup,
-                       prefetch_fn=_plan_fn(student) if prefetch else None, overlap=overlap)
+                       prefetch_fn=_plan_fn(student) if prefetch else None, overlap=overlap,
+                       stages=stages)

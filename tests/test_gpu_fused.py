@@ -93,12 +93,16 @@ def test_cost_volume_bwd_csr_bitwise(din, dout, n1, n2, bsz, k):
     assert torch.count_nonzero(r[1][:, -1]) == 0 and torch.count_nonzero(r[3][:, -1]) == 0
 
 
-@pytest.mark.parametrize("din,dout,n1", [(32, 32, 8192), (64, 64, 2048)])
+@pytest.mark.parametrize("din,dout,n1", [(32, 32, 8192), (64, 64, 2048), (128, 128, 512),
+                                         (256, 256, 256)])
 def test_cost_volume_bwd_deterministic_at_model_size(din, dout, n1):
-    """At the model's level-0/1 sizes (B=16 clouds, K=32: ~2000 waves, every SIMD busy) the
-    backward gives the same bits on every run, and the ranked and plain entry points agree.
-    (A packed-f32 d(dir) accumulation with a broadcast operand passed the small bitwise test
-    above and still gave run-to-run different dx1 / dx2 here.)"""
+    """At the model's sizes of all four levels (B=16 clouds = both directions of the B=8 pair
+    batch, K=32; levels 0/1 on the narrow kernel, 2/3 on the fused wide one) the backward gives
+    the same bits on every run, the ranked and plain entry points agree, and an all-zero
+    slope0 (the OVR=true instantiation the model-level gradient parity tests run) is
+    bit-identical to no slope0 (the production instantiation).  (A packed-f32 d(dir)
+    accumulation with a broadcast operand passed the small bitwise test above and still gave
+    run-to-run different dx1 / dx2 here.)"""
     import kdpc_native as K
     g = torch.Generator(device="cpu").manual_seed(din + n1)
     bsz, k = 16, 32
@@ -120,10 +124,13 @@ def test_cost_volume_bwd_deterministic_at_model_size(din, dout, n1):
     csr = K.csr_of(idx, n1)
     plain = [dp1, K.group_rows_grad(dp2r.view(bsz, n1 * k, din), csr, bsz, n1, din), dx1,
              K.group_rows_grad(ddr.view(bsz, n1 * k, 3), csr, bsz, n1, 3), dpar]
+    zero = torch.zeros(bsz, n1, k, din, dtype=torch.uint8, device=DEV)
+    ovr = K.cost_volume_bwd_csr(x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout, zero)
     for i, name in enumerate(["dp1", "dp2", "dx1", "dx2", "dparams"]):
         for r in runs[1:]:
             assert torch.equal(runs[0][i], r[i]), name
         assert torch.equal(runs[0][i], plain[i]), name
+        assert torch.equal(runs[0][i], ovr[i]), name + " (zero slope0 vs none)"
 
 
 @pytest.mark.parametrize("din,dout,n1,n2,bsz,k", [

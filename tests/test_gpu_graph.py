@@ -15,12 +15,16 @@ def _batch(b, n, seed):
     return tuple(torch.from_numpy(a).to(DEV) for a in synthetic.ft3d_batch(b, n, seed=seed))
 
 
-@pytest.mark.parametrize("mode", ["train", "kd", "kd_fork", "kd_fork_own"])
+@pytest.mark.parametrize("mode", ["train", "kd", "kd_inline", "kd_fork", "kd_fork_own"])
 def test_graphed_step_equals_eager(mode, monkeypatch):
-    """kd_fork: the KD student keeps its decoder coordinate fork (models_bid_pointconv.
-    _CoordFork) on the parameter-gradient stream beside the teacher's stream; kd_fork_own:
-    on a stream of its own (five streams in the captured graph: capture, plan fork, teacher,
-    coordinate fork, parameter gradients) -- the round-3 capture_end segfault case."""
+    """kd: the KD step as three graphs (the teacher's forward as a graph of its own on the
+    teacher stream beside the student's forward graph, then loss + backward + Adam:
+    distill.GraphedStep stages) against the eager KDTrainStep with the teacher on its own
+    stream; kd_inline: the teacher in line inside one graph (TEACHER_GRAPH = False) against
+    the eager step with the teacher in line; kd_fork: the KD student keeps its decoder
+    coordinate fork (models_bid_pointconv._CoordFork) on the parameter-gradient stream inside
+    the student's forward graph; kd_fork_own: on a stream of its own (the round-3 capture_end
+    segfault case)."""
     import distill
     import models_bid_pointconv
     from distill import (FlowTrainStep, KDTrainStep, graphed_flow_step, graphed_kd_step,
@@ -29,6 +33,10 @@ def test_graphed_step_equals_eager(mode, monkeypatch):
     if mode.startswith("kd_fork"):
         monkeypatch.setattr(distill, "KD_COORD_FORK", True)
         monkeypatch.setattr(models_bid_pointconv, "SHARED_SIDE_STREAM", mode == "kd_fork")
+        mode = "kd"
+    if mode == "kd_inline":
+        monkeypatch.setattr(distill, "TEACHER_GRAPH", False)
+        monkeypatch.setattr(distill, "TEACHER_STREAM", False)
         mode = "kd"
     torch.manual_seed(0)
     base = PointConvBidirection().to(DEV)

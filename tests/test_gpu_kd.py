@@ -213,9 +213,10 @@ def test_coordinate_fork_is_bit_identical():
 
 
 def test_teacher_stream_is_bit_identical():
-    """The KD step's frozen-teacher forward on its own stream (distill._TeacherFork, beside the
-    student's forward) gives the same loss and parameters, bit for bit, as running it in
-    line, eagerly and from the captured graph."""
+    """The KD step's frozen-teacher forward on its own stream -- eagerly (distill._TeacherFork,
+    beside the student's forward) and graphed (a graph of its own on the teacher stream beside
+    the student's forward graph, distill.GraphedStep stages) -- gives the same losses and
+    parameters, bit for bit, as running it in line (one graph)."""
     import distill
     from distill import KDTrainStep, graphed_kd_step, make_optimizer
     from models_bid_pointconv import PointConvBidirection as Net
@@ -225,10 +226,10 @@ def test_teacher_stream_is_bit_identical():
     base = Net().to(DEV)
     batches = [_batch(2, 4096, s) for s in (61, 62)]
     runs = []
-    prev = distill.TEACHER_STREAM
+    prev = distill.TEACHER_STREAM, distill.TEACHER_GRAPH
     try:
         for on in (False, True):
-            distill.TEACHER_STREAM = on
+            distill.TEACHER_STREAM = distill.TEACHER_GRAPH = on
             m_e, m_g = copy.deepcopy(base), copy.deepcopy(base)
             eager = KDTrainStep(teacher, m_e, make_optimizer(m_e, capturable=True))
             graphed = graphed_kd_step(teacher, m_g, make_optimizer(m_g, capturable=True),
@@ -238,8 +239,38 @@ def test_teacher_stream_is_bit_identical():
             runs.append((losses, [p.detach().clone() for p in m_e.parameters()],
                          [p.detach().clone() for p in m_g.parameters()]))
     finally:
-        distill.TEACHER_STREAM = prev
+        distill.TEACHER_STREAM, distill.TEACHER_GRAPH = prev
     (l0, e0, g0), (l1, e1, g1) = runs
     assert l0 == l1, (l0, l1)
     for a, b in zip(e0 + g0, e1 + g1):
         assert torch.equal(a, b)
+
+
+def test_graphed_kd_steps_are_reproducible():
+    """Two graphed KD steps built from identical models and replayed side by side on the same
+    batches (configs[3]'s per-GPU slice, B=4, N=8192, the plan prefetched inside the graph)
+    give the same loss and the same packed student gradients at every replay.  Before round 6
+    they disagreed in about one replay in six and sometimes faulted: packed f32 instructions
+    in the culled kNN gave wrong seed distances while the teacher's PointConv kernels ran
+    beside them on the other stream (profiles/round06/race)."""
+    from distill import graphed_kd_step, make_optimizer
+    from models_bid_lighttoken_res import PointConvBidirection as Student
+    from models_bid_pointconv import PointConvBidirection as Teacher
+    torch.manual_seed(1)
+    teacher = Teacher().to(DEV)
+    torch.manual_seed(2)
+    base = Student().to(DEV)
+    batches = [_batch(4, 8192, s) for s in (81, 82, 83)]
+    m1, m2 = copy.deepcopy(base), copy.deepcopy(base)
+    g1 = graphed_kd_step(teacher, m1, make_optimizer(m1, capturable=True), batches[0], warmup=1)
+    g2 = graphed_kd_step(teacher, m2, make_optimizer(m2, capturable=True), batches[0], warmup=1)
+    assert g1.graph_t is not None  # the teacher's own graph
+    for i in range(12):
+        b, nxt = batches[i % 3], batches[(i + 1) % 3]
+        l1 = g1(*b, next_batch=nxt)
+        l2 = g2(*b, next_batch=nxt)
+        torch.cuda.synchronize()
+        assert torch.equal(l1, l2), (i, float(l1), float(l2))
+        assert torch.equal(g1.G, g2.G), i
+    for a, c in zip(m1.parameters(), m2.parameters()):
+        assert torch.equal(a, c)

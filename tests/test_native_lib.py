@@ -197,3 +197,32 @@ def test_torch_ops_reject_cpu_tensors():
     ops = kdpc_native.load_ops()
     with pytest.raises(NotImplementedError):  # no CPU kernel is registered
         ops.group_rows(torch.zeros(1, 4, 3), torch.zeros(1, 2, dtype=torch.int32))
+
+
+def test_library_holds_no_packed_f32_instructions(tmp_path):
+    """No v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 / v_pk_mov_b32 in any gfx950 code object
+    of the built library (kdpc_common.h: packed f32 results were wrong now and then beside
+    another kernel's waves on the MI355X).  Disassembles a copy of the
+    library (llvm-objdump --offloading writes the code objects next to its input)."""
+    import shutil
+    import subprocess
+    objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    if not os.path.exists(objdump):
+        pytest.skip("llvm-objdump not installed")
+    lib = tmp_path / "libkdpc_hip.so"
+    shutil.copy(kdpc_native.LIB_PATH, lib)
+    subprocess.run([objdump, "--offloading", str(lib)], check=True, capture_output=True)
+    objs = sorted(p for p in tmp_path.iterdir() if p.name.endswith("gfx950"))
+    assert objs, "no gfx950 code object in the library"
+    bad = {}
+    for p in objs:
+        text = subprocess.run([objdump, "-d", str(p)], check=True, capture_output=True,
+                              text=True).stdout
+        fn = None
+        for line in text.splitlines():
+            m = re.match(r"^[0-9a-f]+ <(.+)>:$", line)
+            if m:
+                fn = m.group(1)
+            elif re.search(r"\bv_pk_(fma|mul|add)_f32\b|\bv_pk_mov_b32\b", line):
+                bad[fn] = bad.get(fn, 0) + 1
+    assert not bad, f"packed f32 instructions in: {sorted(bad.items())[:8]}"

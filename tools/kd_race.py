@@ -1,0 +1,220 @@
+"""Diagnostics for the multi-stream KD step (DESIGN §5, round-5 "teacher stream" finding).
+
+  csan  : one eager KDTrainStep sequence (teacher on its own stream, shared plan, prefetched
+          plan for the next batch, parameter-gradient streams on) under torch's CUDA
+          sanitizer (torch.cuda._sanitizer): every unsynchronised cross-stream access to a
+          live tensor is collected (not raised) and printed with both stacks.
+  gg    : two graphed KD steps built from identical models, replayed side by side on the
+          same batches; after every replay the loss and every packed parameter gradient of
+          the two are compared (in gradient-ready order, so the first differing entry names
+          the layer where the backward starts to diverge), then the second step's state is
+          re-synchronised from the first (parameters, Adam moments, BN buffers) so one
+          process gives many independent samples.
+Options: teach=0|1 (teacher stream), own=0|1 (private plan copy), wgrad=0|1, steps=N, b=, n=.
+"""
+import copy
+import sys
+import os
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                "kd-pointcloud_amd"))
+import torch  # noqa: E402
+
+DEV = "cuda"
+
+
+def _opts():
+    o = {"mode": sys.argv[1] if len(sys.argv) > 1 else "gg"}
+    for a in sys.argv[2:]:
+        k, v = a.split("=")
+        o[k] = v
+    return o
+
+
+def _batch(b, n, seed):
+    import synthetic
+    return tuple(torch.from_numpy(a).to(DEV) for a in synthetic.ft3d_batch(b, n, seed=seed))
+
+
+def _setup(o):
+    import distill
+    import wgrad
+    distill.TEACHER_STREAM = o.get("teach", "1") == "1"
+    distill._TEACHER_OWN_PLAN = o.get("own", "0") == "1"
+    wgrad.enabled = o.get("wgrad", "1") == "1"
+    print("TEACHER_STREAM", distill.TEACHER_STREAM, "OWN_PLAN", distill._TEACHER_OWN_PLAN,
+          "wgrad", wgrad.enabled, flush=True)
+
+
+def run_csan(o):
+    from torch.cuda import _sanitizer as S
+    errors = []
+
+    orig = S.EventHandler._handle_kernel_launch
+
+    def collect(self, *a, **k):
+        errs = orig(self, *a, **k)
+        errors.extend(errs)
+        return []
+    S.EventHandler._handle_kernel_launch = collect
+    S.enable_cuda_sanitizer()
+    _setup(o)
+    from distill import KDTrainStep, make_optimizer
+    from models_bid_lighttoken_res import PointConvBidirection as Student
+    from models_bid_pointconv import PointConvBidirection as Teacher
+    b, n = int(o.get("b", 2)), int(o.get("n", 4096))
+    torch.manual_seed(1)
+    teacher = Teacher().to(DEV)
+    torch.manual_seed(2)
+    student = Student().to(DEV)
+    batches = [_batch(b, n, s) for s in (31, 32, 33)]
+    step = KDTrainStep(teacher, student, make_optimizer(student, capturable=True))
+    seq = [(batches[0], batches[1]), (batches[1], batches[2]), (batches[2], None)]
+    for i, (bt, nxt) in enumerate(seq):
+        step(*bt, next_batch=nxt)
+        print("step", i, "errors so far", len(errors), flush=True)
+    torch.cuda.synchronize()
+    import collections
+    groups = collections.OrderedDict()
+
+    def where(acc):
+        fr = [f for f in acc.stack_trace if "kd-pointcloud_amd" in f.filename]
+        fr = fr[-2:] if fr else list(acc.stack_trace)[-2:]
+        return " < ".join(f"{os.path.basename(f.filename)}:{f.lineno}:{f.name}"
+                          for f in reversed(fr))
+
+    for e in errors:
+        ca, pa = getattr(e, "current_access", None), getattr(e, "previous_access", None)
+        if ca is None:
+            key = str(e)[:300]
+        else:
+            key = (str(ca.operator).split("(")[0], ca.type.name, tuple(ca.aliases), where(ca),
+                   str(pa.operator).split("(")[0] if pa else None, pa.type.name if pa else None,
+                   tuple(pa.aliases) if pa else None, where(pa) if pa else None)
+        groups.setdefault(key, []).append(e)
+    print("CSAN errors:", len(errors), "distinct (op, access, previous op):", len(groups))
+    for key, es in groups.items():
+        print(f"  {len(es):4d} x {key}")
+    for i, (key, es) in enumerate(groups.items()):
+        if i >= int(o.get("full", 12)):
+            break
+        print("=" * 100)
+        print(es[0])
+    sys.stdout.flush()
+
+
+def _names(model):
+    return {id(p): n for n, p in model.named_parameters()}
+
+
+def _resync(dst, src, mdst, msrc):
+    with torch.no_grad():
+        fd = dst.flat_opt.param_groups[0]["params"][0]
+        fs = src.flat_opt.param_groups[0]["params"][0]
+        fd.copy_(fs)
+        sd, ss = dst.flat_opt.state[fd], src.flat_opt.state[fs]
+        for k in ("exp_avg", "exp_avg_sq", "step"):
+            sd[k].copy_(ss[k])
+        dst._steps.copy_(src._steps)
+        for bd, bs in zip(mdst.buffers(), msrc.buffers()):
+            bd.copy_(bs)
+
+
+def _kd_graph(teacher, student, opt, example, prefetch, stash):
+    """distill.graphed_kd_step with intermediate tensors stashed as graph outputs: the
+    teacher's and the student's flow0 and level-3 features, and the gradient reaching the
+    student's flow0 (every replay rewrites them, so two graphs can be compared stage by
+    stage)."""
+    import loss_functions
+    from distill import GraphedStep, _TeacherFork, _kd_student_streams, _plan_fn
+    for p in teacher.parameters():
+        p.requires_grad_(False)
+    teacher.eval()
+    student.train()
+
+    def run(pos1, pos2, flow, fps=None):
+        kw = {} if fps is None else {"fps_idx": fps}
+        t_fork = _TeacherFork(teacher, (pos1, pos2, pos1, pos2), kw)
+        with _kd_student_streams(student):
+            flows, fps1, fps2, _, _, feat1s, feat2s, _ = student(pos1, pos2, pos1, pos2, **kw)
+        t_flows, t_fps1, t_fps2, _, _, t_feat1s, t_feat2s, _ = t_fork.join()
+        stash["t_flow0"] = t_flows[0].detach().clone()
+        stash["t_feat1_3"] = t_feat1s[3].detach().clone()
+        stash["s_flow0"] = flows[0].detach().clone()
+        stash["s_flow3"] = flows[3].detach().clone()
+        stash["s_feat1_3"] = feat1s[3].detach().clone()
+        if flows[0].requires_grad:
+            flows[0].register_hook(lambda g: stash.__setitem__("d_flow0", g.detach().clone()))
+            feat1s[3].register_hook(lambda g: stash.__setitem__("d_feat1_3", g.detach().clone()))
+        return loss_functions.biDirection_loss_ht(
+            flows, feat1s, feat2s, fps1, fps2, flow, t_flows, t_feat1s, t_feat2s, t_fps1, t_fps2,
+            0.3, 0.8, layer=3)
+    return GraphedStep(run, student.parameters(), opt, example, 1,
+                       prefetch_fn=_plan_fn(student) if prefetch else None)
+
+
+def run_gg(o):
+    """Two product graphed steps (distill.graphed_kd_step / graphed_flow_step) from identical
+    models, replayed side by side; loss and packed gradients compared after every replay, the
+    second step re-synchronised from the first.  kind=kd|train, tgraph=0|1 (KD: teacher in its
+    own graph or in line), prefetch=0|1, wgrad=0|1, coord=0|1 (train: decoder coordinate fork),
+    b=, n=, steps=."""
+    _setup(o)
+    import distill
+    import models_bid_pointconv
+    from distill import graphed_flow_step, graphed_kd_step, make_optimizer
+    from models_bid_lighttoken_res import PointConvBidirection as Student
+    from models_bid_pointconv import PointConvBidirection as Teacher
+    kind = o.get("kind", "kd")
+    distill.TEACHER_GRAPH = o.get("tgraph", "1") == "1"
+    models_bid_pointconv.COORD_FORK = o.get("coord", "1") == "1"
+    b, n = int(o.get("b", 4 if kind == "kd" else 8)), int(o.get("n", 8192))
+    nsteps = int(o.get("steps", 24))
+    prefetch = o.get("prefetch", "1") == "1"
+    print(f"kind {kind} TEACHER_GRAPH {distill.TEACHER_GRAPH} prefetch {prefetch} "
+          f"coord_fork {models_bid_pointconv.COORD_FORK} b={b} n={n}", flush=True)
+    torch.manual_seed(1)
+    teacher = Teacher().to(DEV)
+    torch.manual_seed(2)
+    base = Student().to(DEV)
+    batches = [_batch(b, n, s) for s in (31, 32, 33)]
+    m1, m2 = copy.deepcopy(base), copy.deepcopy(base)
+
+    def build(m):
+        opt = make_optimizer(m, capturable=True)
+        if kind == "kd":
+            return graphed_kd_step(teacher, m, opt, batches[0], warmup=1, prefetch=prefetch)
+        return graphed_flow_step(m, opt, batches[0], warmup=1, prefetch=prefetch)
+    g1, g2 = build(m1), build(m2)
+    print("schedule:", g1.schedule_name(), flush=True)
+    names = _names(m1)
+    torch.cuda.synchronize()
+    _resync(g2, g1, m2, m1)
+    bad_steps = 0
+
+    def rel(a, c):
+        return float((a - c).abs().max()) / (float(a.abs().max()) + 1e-30)
+
+    for i in range(nsteps):
+        bt, nxt = batches[i % 3], batches[(i + 1) % 3]
+        kw = {"next_batch": nxt} if prefetch else {}
+        l1 = g1(*bt, **kw)
+        l2 = g2(*bt, **kw)
+        torch.cuda.synchronize()
+        diff = [j for j, (a, c) in enumerate(zip(g1._gviews, g2._gviews)) if not torch.equal(a, c)]
+        same_loss = torch.equal(l1, l2)
+        if diff or not same_loss:
+            bad_steps += 1
+            print(f"step {i}: loss {float(l1)!r} vs {float(l2)!r} same={same_loss}; "
+                  f"{len(diff)}/{len(g1._gviews)} gradients differ", flush=True)
+            for j in diff[:4]:
+                print(f"   [{j:3d}] rel {rel(g1._gviews[j], g2._gviews[j]):.2e} "
+                      f"{names.get(id(g1._used[j]), '?')}", flush=True)
+        _resync(g2, g1, m2, m1)
+        torch.cuda.synchronize()
+    print("RESULT kind", kind, "steps", nsteps, "differing", bad_steps, flush=True)
+
+
+if __name__ == "__main__":
+    o = _opts()
+    {"csan": run_csan, "gg": run_gg}[o["mode"]](o)
