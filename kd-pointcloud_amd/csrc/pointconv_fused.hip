@@ -1501,7 +1501,7 @@ void pc_bwd_weight_x6_kernel(Geo g, const float* __restrict__ wt, const float* _
   const Srcs src = srcs_of(g);
 
   const int h4 = t & 1;
-  float wr[2][KM], wc[2][KM];
+  float wc[2][KM];  // WeightNet weights of the row pair being built
   float4 gr[GS];
   float dr[DVI][2][8];
   int nbi[GS];
@@ -1530,8 +1530,9 @@ void pc_bwd_weight_x6_kernel(Geo g, const float* __restrict__ wt, const float* _
       nbi[i] = base + (int)__builtin_amdgcn_raw_buffer_load_b32(idx_rs, (int)off, 0, 0);
     }
   };
-  // WeightNet weights of rows 2 rp, 2 rp + 1 and the tile's gathered G (branch-free loads)
-  auto fetch_g = [&](int tile) {
+  // WeightNet weights of rows 2 rp, 2 rp + 1 of a tile, straight into wc: issued right after
+  // the build that last read wc, they land under the next MFMA phase (no second register set)
+  auto fetch_w = [&](int tile) {
     const int row0 = rbeg + tile * TR;
 #pragma unroll
     for (int p2 = 0; p2 < 2; ++p2) {
@@ -1540,10 +1541,14 @@ void pc_bwd_weight_x6_kernel(Geo g, const float* __restrict__ wt, const float* _
 #pragma unroll
       for (int k = 0; k < KM; ++k) {
         const unsigned off = k < kk ? base + (unsigned)(k * kW * 4) : kOOB;
-        wr[p2][k] = __builtin_bit_cast(
+        wc[p2][k] = __builtin_bit_cast(
             float, __builtin_amdgcn_raw_buffer_load_b32(wt_rs, (int)off, 0, 0));
       }
     }
+  };
+  // the tile's gathered G (branch-free loads)
+  auto fetch_g = [&](int tile) {
+    const int row0 = rbeg + tile * TR;
 #pragma unroll
     for (int i = 0; i < GS; ++i) {
       const int rk = (t >> 1) + (NT / 2) * i;
@@ -1600,10 +1605,6 @@ void pc_bwd_weight_x6_kernel(Geo g, const float* __restrict__ wt, const float* _
       const int rk = (t >> 1) + (NT / 2) * i;
       if (rk < tk) *reinterpret_cast<float4*>(gb + rk * kCC + 4 * h4) = gr[i];
     }
-#pragma unroll
-    for (int p2 = 0; p2 < 2; ++p2)
-#pragma unroll
-      for (int k = 0; k < KM; ++k) wc[p2][k] = wr[p2][k];
   };
   auto stage_dy = [&]() {
 #pragma unroll
@@ -1657,12 +1658,14 @@ void pc_bwd_weight_x6_kernel(Geo g, const float* __restrict__ wt, const float* _
   // prologue: tile 0 built (A planes), dy of tile 0 split, G of tile 1 in gl[1]
   fetch_idx(0);
   fetch_g(0);
+  fetch_w(0);
   fetch_dy(0);
   stage_g(gl[0]);
   stage_dy();
   fetch_g(1);
   __syncthreads();
   build(gl[0]);
+  fetch_w(1);
   stage_g(gl[1]);
   __syncthreads();
   const int col = wv * 32 + l32;  // this lane's A column (B operand) of the chunk
@@ -1681,9 +1684,12 @@ void pc_bwd_weight_x6_kernel(Geo g, const float* __restrict__ wt, const float* _
       }
     }
     __syncthreads();  // atp / dyp consumed
-    build(gl[(tile + 1) & 1]);  // tile + 1 (G staged one iteration ago, weights in wc)
+    // the prefetched dy (tile + 1) and G (tile + 2) go to LDS before the build, so their
+    // registers are free while it runs (no packed f32: the scalar build needs the room)
     stage_dy();                 // tile + 1
     stage_g(gl[tile & 1]);      // tile + 2 (G of tile: built last iteration)
+    build(gl[(tile + 1) & 1]);  // tile + 1 (G staged one iteration ago, weights in wc)
+    fetch_w(tile + 2);          // into wc, consumed by the next iteration's build
     __syncthreads();
   }
   const long long cc16 = (long long)c0 * kW + col;

@@ -17,6 +17,8 @@ The step is model-agnostic (any module returning the reference's 8-tuple), which
 multi-process path be tested on CPU with gloo.
 """
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -65,18 +67,17 @@ def _core(model):
 
 
 # True runs the frozen teacher's forward on a stream of its own, beside the student's forward
-# (round 3: 15.6 -> 13.8 ms per KD step): eagerly through _TeacherFork, and in the graphed step
-# as a HIP graph of its own (GraphedStep stages, TEACHER_GRAPH).  Round 5 switched it off
-# because graphed KD steps disagreed now and then; round 6 found why: a single
-# captured graph holding the teacher's and the student's forwards as two concurrent branches
-# computes wrong values now and then on this runtime (an out-of-range kNN index from inputs
-# that were intact), while the same forwards as two graphs on two streams are bit-reproducible
-# -- and the eager two-stream step is clean under torch's stream sanitizer.  The teacher and
-# the student share the coordinate plan (no private copy: nothing of it is written by either).
+# (round 3: 15.6 -> 13.8 ms per KD step), eagerly through _TeacherFork and in the graphed step.
+# Round 5 switched it off because graphed KD steps disagreed now and then; round 6 found why
+# (DESIGN §5): packed f32 instructions (v_pk_fma_f32 ...) gave wrong results now and then
+# while the other stream's kernels ran beside them.  The library holds none since, and the
+# two-stream step is bit-reproducible.  The teacher and the student share the coordinate
+# plan (no private copy: nothing of it is written by either).
 TEACHER_STREAM = True
-# the graphed KD step: teacher forward = its own graph on the teacher stream (True), or in
-# line inside the student's graph (False)
-TEACHER_GRAPH = True
+# the graphed KD step: the teacher's forward as a graph of its own on the teacher stream,
+# beside the student's forward graph (True), or as a concurrent branch of the one step graph
+# (False).  KDPC_TEACHER_GRAPH=0/1 overrides (A/B runs).
+TEACHER_GRAPH = os.environ.get("KDPC_TEACHER_GRAPH", "0") == "1"
 _TEACHER_OWN_PLAN = False
 _teacher_streams = {}
 
@@ -101,14 +102,12 @@ class _TeacherFork:
     the two share only their inputs, and at B=4 per GPU neither fills the chip.  join()
     makes the current stream wait before the teacher's outputs are read (the KD loss).  Same
     kernels on the same inputs: bit-identical to running the teacher in line.  Inside a graph
-    capture the teacher runs in line: a second model forward as a concurrent branch of ONE
-    graph is what went wrong; the graphed step gives it a graph of its own
-    (GraphedStep stages)."""
+    capture the fork becomes a concurrent branch of the captured graph."""
 
     def __init__(self, teacher, args, kw):
         dev = args[0].device
         self.cur = self.side = None
-        if TEACHER_STREAM and dev.type == "cuda" and not torch.cuda.is_current_stream_capturing():
+        if TEACHER_STREAM and dev.type == "cuda":
             self.cur = torch.cuda.current_stream(dev)
             self.side = _teacher_stream(dev)
             self.side.wait_stream(self.cur)

@@ -15,13 +15,15 @@ def _batch(b, n, seed):
     return tuple(torch.from_numpy(a).to(DEV) for a in synthetic.ft3d_batch(b, n, seed=seed))
 
 
-@pytest.mark.parametrize("mode", ["train", "kd", "kd_inline", "kd_fork", "kd_fork_own"])
+@pytest.mark.parametrize("mode", ["train", "kd", "kd_inline", "kd_tgraph", "kd_fork",
+                                  "kd_fork_own"])
 def test_graphed_step_equals_eager(mode, monkeypatch):
-    """kd: the KD step as three graphs (the teacher's forward as a graph of its own on the
-    teacher stream beside the student's forward graph, then loss + backward + Adam:
-    distill.GraphedStep stages) against the eager KDTrainStep with the teacher on its own
-    stream; kd_inline: the teacher in line inside one graph (TEACHER_GRAPH = False) against
-    the eager step with the teacher in line; kd_fork: the KD student keeps its decoder
+    """kd: the KD step as one graph with the teacher's forward a concurrent branch on the
+    teacher stream (the default) against the eager KDTrainStep with the teacher on its own
+    stream; kd_inline: the teacher in line (TEACHER_STREAM = False), graphed and eager;
+    kd_tgraph: the teacher's forward as a graph of its own beside the student's forward graph,
+    then loss + backward + Adam (TEACHER_GRAPH, distill.GraphedStep stages); kd_fork: the KD
+    student keeps its decoder
     coordinate fork (models_bid_pointconv._CoordFork) on the parameter-gradient stream inside
     the student's forward graph; kd_fork_own: on a stream of its own (the round-3 capture_end
     segfault case)."""
@@ -37,6 +39,10 @@ def test_graphed_step_equals_eager(mode, monkeypatch):
     if mode == "kd_inline":
         monkeypatch.setattr(distill, "TEACHER_GRAPH", False)
         monkeypatch.setattr(distill, "TEACHER_STREAM", False)
+        mode = "kd"
+    if mode == "kd_tgraph":
+        monkeypatch.setattr(distill, "TEACHER_GRAPH", True)
+        monkeypatch.setattr(distill, "TEACHER_STREAM", True)
         mode = "kd"
     torch.manual_seed(0)
     base = PointConvBidirection().to(DEV)
