@@ -88,8 +88,12 @@ void cost_volume_fwd_kernel(
     const float* __restrict__ p2, const float* __restrict__ wpos, const float* __restrict__ bpos,
     const float* __restrict__ w1, const float* __restrict__ b1, float* __restrict__ out,
     unsigned char* __restrict__ amax) {
-  constexpr int LD = D_IN + 1;
+  // the MLP on split-bf16 MFMAs (mfma_x6).  Round 5 reverted this form after the graphed train
+  // step disagreed and faulted; the cause was packed f32 elsewhere (the plan's kNN, DESIGN
+  // section 5), and with none left it is bit-reproducible (tools/kd_race.py gg kind=train)
+  constexpr int LD = D_IN + 4;  // 16-byte aligned rows: the A operand is read 8 channels at a time
   constexpr int TILES = D_OUT / 32;
+  constexpr int NKS = D_IN / 16;  // 16-deep K-steps (mfma_x6)
   constexpr int RPP = 64 / D_IN;  // layout-L rows per pass
   constexpr int RT = kRows / RPP;
   __shared__ float lds[kWaves][kRows * LD];
@@ -113,13 +117,17 @@ void cost_volume_fwd_kernel(
   unsigned char* amb = amax + (long long)b * n1 * D_OUT;
   const int q0 = (bx * kWaves + wave) * queries_per_wave;
   const int q1 = min(n1, q0 + queries_per_wave);
-  // B fragments of W1 (lane l: W1[t*32 + (l&31)][2s + (l>>5)]), reused for every query
-  float bw[TILES][D_IN / 2];
+  // B planes of W1 (lane l: W1[t*32 + (l&31)][16 ks + 8 (l>>5) + 0..7]), reused for every query
+  Planes bw[TILES][NKS];
 #pragma unroll
   for (int t = 0; t < TILES; ++t)
 #pragma unroll
-    for (int s = 0; s < D_IN / 2; ++s)
-      bw[t][s] = w1[(t * 32 + (lane & 31)) * D_IN + 2 * s + (lane >> 5)];
+    for (int ks = 0; ks < NKS; ++ks) {
+      const float4* src = reinterpret_cast<const float4*>(w1 + (t * 32 + (lane & 31)) * D_IN + 16 * ks + 8 * (lane >> 5));
+      const float4 lo = src[0], hi = src[1];
+      const float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      bw[t][ks] = split8(v);
+    }
   float bias[TILES];
 #pragma unroll
   for (int t = 0; t < TILES; ++t) bias[t] = b1[t * 32 + (lane & 31)];
@@ -189,12 +197,17 @@ void cost_volume_fwd_kernel(
     f32x16 acc[TILES];
 #pragma unroll
     for (int t = 0; t < TILES; ++t) acc[t] = f32x16{0};
+    // MLP on mfma_x6: the lane's A = row (lane & 31), channels 16 ks + 8 (lane >> 5) + 0..7,
+    // split into bf16 planes as read
 #pragma unroll
-    for (int s = 0; s < D_IN / 2; ++s) {
-      const float a = lds_h[(lane & 31) * LD + 2 * s + (lane >> 5)];
+    for (int ks = 0; ks < NKS; ++ks) {
+      const float4* ar = reinterpret_cast<const float4*>(lds_h + (lane & 31) * LD + 16 * ks + 8 * (lane >> 5));
+      const float4 lo = ar[0], hi = ar[1];
+      const float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      const Planes a = split8(v);
 #pragma unroll
       for (int t = 0; t < TILES; ++t)
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bw[t][s], acc[t], 0, 0, 0);
+        acc[t] = mfma_x6(a.h, a.m, a.l, bw[t][ks].h, bw[t][ks].m, bw[t][ks].l, acc[t]);
     }
     const int h = lane >> 5;
 #pragma unroll
