@@ -486,11 +486,10 @@ class GraphedStep:
         second graph on the capture stream; the caller then captures loss_from(forward out,
         side out, *inputs) + backward + optimizer as graph_a in the forward graph's pool (it
         reads the forward's saved tensors).  A replay runs the first two side by side on two
-        streams and joins them before graph_a.  One graph holding both forwards as two
-        concurrent branches computed wrong values now and then on this runtime (DESIGN §5:
-        kernels read inputs that were intact in stream order and wrote different results, and
-        some runs faulted); the same two forwards as two graphs on two streams are
-        bit-reproducible and no slower."""
+        streams and joins them before graph_a.  (Round 6 added this form while chasing the
+        multi-stream race, whose cause was packed f32 instructions; it is
+        bit-identical to the one-graph form and 0.3 ms slower, so it is the option
+        TEACHER_GRAPH, not the default.)"""
         side_fn, fwd_fn, _ = self.stages
         cur = torch.cuda.current_stream()
         ts = _teacher_stream(self.static[0].device)

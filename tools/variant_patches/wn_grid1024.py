@@ -1,0 +1,1 @@
+REPL = [("csrc/weightnet.hip", "constexpr int kBwdGrid = 512;", "constexpr int kBwdGrid = 1024;")]
