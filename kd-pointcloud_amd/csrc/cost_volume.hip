@@ -171,7 +171,7 @@ void cost_volume_fwd_kernel(
     // lane r's direction to its neighbour, broadcast to the row passes through LDS (one
     // 16-byte read per pass instead of 3-6 readlanes + selects; the same values)
     if (lane < kRows) dirT[lane] = make_float4(xv0 - qv0, xv1 - qv1, xv2 - qv2, 0.f);
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
     // all direction reads before the first h0 store (a store between them serialises the
     // reads: the compiler cannot move a read of dirT above a store to the same LDS array)
     float hv[RT];
@@ -193,7 +193,7 @@ void cost_volume_fwd_kernel(
       if (n + 2 < q1) load_idx(n + 2);
     }
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
     f32x16 acc[TILES];
 #pragma unroll
     for (int t = 0; t < TILES; ++t) acc[t] = f32x16{0};
@@ -234,7 +234,7 @@ void cost_volume_fwd_kernel(
         amb[(long long)n * D_OUT + t * 32 + lane] = (unsigned char)mr;
       }
     }
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
   }
 }
 
@@ -434,8 +434,7 @@ void cost_volume_bwd_kernel(
     // consecutive entries (one 16-byte read for e = 4 q .. 4 q + 3; a shuffle per row was 16
     // ds_bpermute instructions)
     jT[lane] = jn;
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
     load_idx(n + 1);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -509,8 +508,7 @@ void cost_volume_bwd_kernel(
   load_q(q0);
   tables(q0, 0);
   load_q(q0 + 1);
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
+  wave_lds_sync();
   build_h0(0);
   const int nit = CS > 1 ? queries_per_wave : q1 - q0;
   for (int it = 0; it < nit; ++it) {
@@ -531,10 +529,9 @@ void cost_volume_bwd_kernel(
       const unsigned* oc = dO(cu);
       const __bf16* gp = gpl(cu);
       const unsigned short* ga16 = g16(cu);
-      // the tables are read back below through 16-byte (uint4) loads: a compiler memory barrier
-      // so those loads are not moved above their 2-byte stores (wave_barrier orders no memory)
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
+      // the tables are read back below through 16-byte (uint4) loads: the compiler memory
+      // barrier keeps those loads below their 2-byte stores
+      wave_lds_sync();
       if constexpr (!DW1_MFMA) {  // the tile the dW1 update reads (h0 built by query n-1)
 #pragma unroll
         for (int e = 0; e < 16; ++e) T[((e & 3) + 8 * (e >> 2) + 4 * half) * LD + l32] = h0[e >> 1][e & 1];
@@ -626,7 +623,7 @@ void cost_volume_bwd_kernel(
       }
 #pragma unroll
       for (int t = 0; t < OT; ++t) gb1[t] += gq[t];
-      __builtin_amdgcn_wave_barrier();  // the h0 tile is read before dz0 overwrites it
+      wave_lds_sync();  // the h0 tile is read before dz0 overwrites it
       __builtin_amdgcn_sched_barrier(0);
       // ---- dz0 = dh0 * LeakyReLU'(h0) (registers)
       float dz[8][2];
@@ -682,7 +679,7 @@ void cost_volume_bwd_kernel(
       // ---- d(dir_r) = Wpos^T dz0[r]: dz0 through the LDS tile into row-per-lane
 #pragma unroll
       for (int e = 0; e < 16; ++e) T[((e & 3) + 8 * (e >> 2) + 4 * half) * LD + l32] = dz[e >> 1][e & 1];
-      __builtin_amdgcn_wave_barrier();
+      wave_lds_sync();
       // scalar fmas (kdpc_common.h: no packed f32; the packed form gave run-to-run different
       // d(dir) here, tests/test_gpu_fused.py::test_cost_volume_bwd_deterministic_at_model_size)
 #pragma unroll
@@ -698,7 +695,7 @@ void cost_volume_bwd_kernel(
       g0 = __fadd_rn(g0, xor32(g0));
       g1 = __fadd_rn(g1, xor32(g1));
       g2 = __fadd_rn(g2, xor32(g2));
-      __builtin_amdgcn_wave_barrier();  // the tile is rewritten by the next query
+      wave_lds_sync();  // the tile is rewritten by the next query
     }  // act
     if constexpr (CS > 1) {  // the second channel half's d(dir) partials -> the first wave
       float4* xch = reinterpret_cast<float4*>(lds_all + XCH_AT) +

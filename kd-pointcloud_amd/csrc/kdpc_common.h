@@ -46,6 +46,16 @@ __device__ __forceinline__ float sqdist_expanded(float qx, float qy, float qz, f
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
 
+// Intra-wave LDS hand-off (this wave's lanes wrote, other lanes of the same wave read next):
+// a compiler memory barrier -- no LDS access is moved across it, whatever the types or
+// addresses -- plus wave_barrier (which alone orders no memory).  The hardware keeps one
+// wave's LDS accesses in order, so no s_barrier is needed.
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // Full-wave butterfly reductions (every lane ends with the result).
 __device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
 #pragma unroll

@@ -484,9 +484,9 @@ __device__ __noinline__ void compact_buffer(float2* buf, int& cnt, float& thr, i
     ai = ri;
   }
   bitonic_merge64(ad, ai);
-  __builtin_amdgcn_wave_barrier();
+  wave_lds_sync();
   buf[lane] = make_float2(ad, __int_as_float(ai));
-  __builtin_amdgcn_wave_barrier();
+  wave_lds_sync();
   cnt = kWave;
   const float kth = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ad), k - 1));
   if (kth < INFINITY) thr = fminf(thr, from_ord_key(ord_key(kth) + 1u));
@@ -527,10 +527,10 @@ __device__ __noinline__ void shrink_buffer(float2* buf, int& cnt, float& thr, in
                                            __builtin_amdgcn_mbcnt_lo((unsigned)m0, 0u));
   const int p1 = __popcll(m0) + __builtin_amdgcn_mbcnt_hi((unsigned)(m1 >> 32),
                                                           __builtin_amdgcn_mbcnt_lo((unsigned)m1, 0u));
-  __builtin_amdgcn_wave_barrier();
+  wave_lds_sync();
   if (v0 && k0 <= tk) buf[p0] = e0;
   if (v1 && k1 <= tk) buf[p1] = e1;
-  __builtin_amdgcn_wave_barrier();
+  wave_lds_sync();
   cnt = __popcll(m0) + __popcll(m1);
   if (tk < ord_key(INFINITY)) thr = fminf(thr, from_ord_key(tk + 1u));
 }
@@ -669,7 +669,7 @@ __global__ __launch_bounds__(256) void knn_cull_kernel(
     if (live > 0)
       atomicAdd(evals, (unsigned long long)visits * kWave * QW + (unsigned long long)kWin * live);
   }
-  __builtin_amdgcn_wave_barrier();
+  wave_lds_sync();
 #pragma unroll
   for (int q = 0; q < QW; ++q) {
     if (cnt[q] > kWave) shrink_buffer(cand_buf[wave][q], cnt[q], thr[q], k);
