@@ -78,7 +78,6 @@ TEACHER_STREAM = True
 # beside the student's forward graph (True), or as a concurrent branch of the one step graph
 # (False).  KDPC_TEACHER_GRAPH=0/1 overrides (A/B runs).
 TEACHER_GRAPH = os.environ.get("KDPC_TEACHER_GRAPH", "0") == "1"
-_TEACHER_OWN_PLAN = False
 _teacher_streams = {}
 
 
@@ -112,8 +111,6 @@ class _TeacherFork:
             self.side = _teacher_stream(dev)
             self.side.wait_stream(self.cur)
             with torch.cuda.stream(self.side), torch.no_grad():
-                if _TEACHER_OWN_PLAN and kw.get("fps_idx") is not None:
-                    kw = dict(kw, fps_idx=[t.clone() for t in kw["fps_idx"]])
                 self.out = teacher(*args, **kw)
         else:
             with torch.no_grad():

@@ -10,7 +10,7 @@
           the layer where the backward starts to diverge), then the second step's state is
           re-synchronised from the first (parameters, Adam moments, BN buffers) so one
           process gives many independent samples.
-Options: teach=0|1 (teacher stream), own=0|1 (private plan copy), wgrad=0|1, steps=N, b=, n=.
+Options: teach=0|1 (teacher stream), wgrad=0|1, steps=N, b=, n=.
 """
 import copy
 import sys
@@ -40,9 +40,8 @@ def _setup(o):
     import distill
     import wgrad
     distill.TEACHER_STREAM = o.get("teach", "1") == "1"
-    distill._TEACHER_OWN_PLAN = o.get("own", "0") == "1"
     wgrad.enabled = o.get("wgrad", "1") == "1"
-    print("TEACHER_STREAM", distill.TEACHER_STREAM, "OWN_PLAN", distill._TEACHER_OWN_PLAN,
+    print("TEACHER_STREAM", distill.TEACHER_STREAM,
           "wgrad", wgrad.enabled, flush=True)
 
 
