@@ -467,8 +467,11 @@ __device__ __forceinline__ void sort64_multi(float (&d)[QW], int (&i)[QW]) {
 }
 
 // Reduce a query's candidate buffer (cnt > 64 entries) to its 64 smallest, sorted, in
-// slots 0..63; tighten thr to the K-th of them.
-__device__ __noinline__ void compact_buffer(float2* buf, int& cnt, float& thr, int k) {
+// slots 0..63; tighten thr to the K-th of them.  (This and shrink_buffer are inlined: as
+// called functions (__noinline__ until round 6) their by-reference cnt / thr lived in
+// scratch and every call saved registers there -- 48 B per lane; inlined the kernel needs
+// no scratch and configs[4] runs 1222 -> 838 us.)
+__device__ __forceinline__ void compact_buffer(float2* buf, int& cnt, float& thr, int k) {
   const int lane = lane_id();
   const float2 a = lane < cnt ? buf[lane] : make_float2(INFINITY, __int_as_float(0x7fffffff));
   const float2 c = lane + kWave < cnt ? buf[kWave + lane]
@@ -508,7 +511,7 @@ __device__ __noinline__ void compact_buffer(float2* buf, int& cnt, float& thr, i
 // among them (16-bit radix select over the <= 128 entries, two per lane: ballot popcounts,
 // no cross-lane data movement), compacted in place; tighten thr to d <= T.  Everything
 // dropped is farther than K buffered candidates, so it is not among the K nearest.
-__device__ __noinline__ void shrink_buffer(float2* buf, int& cnt, float& thr, int k) {
+__device__ __forceinline__ void shrink_buffer(float2* buf, int& cnt, float& thr, int k) {
   const int lane = lane_id();
   const bool v0 = lane < cnt, v1 = lane + kWave < cnt;
   const float2 e0 = v0 ? buf[lane] : make_float2(INFINITY, 0.f);
