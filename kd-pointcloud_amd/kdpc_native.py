@@ -469,6 +469,8 @@ TILED_PC = True
 BIAS_IN_WEIGHT = True
 # the forward through the same row tiles (bit-identical)
 TILED_FWD = True
+# K = 16 (the encoder layers) through the tiles measured slower: 13.60-13.80 -> 14.28-14.36 ms
+# per train step (round 6, profiles/round06/rejected/tiled_max_k_*)
 TILED_MAX_K = 9
 
 
