@@ -513,13 +513,6 @@ size_t kdpc_colsum_workspace_bytes(int nrows, int len);
 int kdpc_colsum(int nrows, int len, const float *src, float *dst, void *workspace,
                 size_t workspace_bytes, void *stream);
 
-/* dst (rows, width) dense = rows of `width` floats taken `src_ld` floats apart in src (internal:
- * the gradient slice the backward of a feature concatenation hands each part --
- * pointconv_util.py `torch.cat([feats, cost_volume], -1)` and the IDW blend's values -- made
- * dense; replaces torch's strided copy of it). */
-int kdpc_copy_rows(size_t rows, int width, const float *src, size_t src_ld, float *dst,
-                   void *stream);
-
 /* out (m, c) = -sum_{j<k} in (m, k, c) in ascending j: the center gradient -sum_k drel of the
  * grouped relative offsets (replaces the torch reduction of pointconv_util.py's WeightNet
  * backward: `-drel.sum(2)`). */

@@ -87,7 +87,6 @@ _SIGNATURES = {
     "kdpc_colsum": [_c_int, _c_int, _vp, _vp, _vp, _c_size, _vp],
     "kdpc_neg_sum_k": [_c_int, _c_int, _c_int, _vp, _vp, _vp],
     "kdpc_copy_segments": [_c_int, _vp, _vp, _vp, _vp],
-    "kdpc_copy_rows": [_c_size, _c_int, _vp, _c_size, _vp, _vp],
     "kdpc_weightnet_param_count": [],
     "kdpc_weightnet_fwd": [_c_int] * 4 + [_vp] * 11,
     "kdpc_weightnet_bwd_workspace_bytes": [],
@@ -805,14 +804,14 @@ def idw_blend_fwd(ref, qry, vals, idx, warp=False):
 
 def idw_blend_bwd_vals(dout, w, csr, S, warp=False):
     """-> dvals (B,S,C) through the CSR of the blend's idx (B,N,3)."""
-    return _op("kdpc_idw_blend_bwd_vals", "idw_blend_bwd_vals", dense_rows(_gpu(dout, "dout")),
+    return _op("kdpc_idw_blend_bwd_vals", "idw_blend_bwd_vals", _gpu(dout, "dout").contiguous(),
                w, csr.offsets, csr.perm, S, bool(warp))
 
 
 def idw_blend_bwd_coords(ref, qry, vals, idx, dout, warp=False):
     """-> (drow (B,3N,3) per-neighbour rows of d/d ref, dqry (B,N,3))."""
     return _op("kdpc_idw_blend_bwd_coords", "idw_blend_bwd_coords", _gpu(ref, "ref"), qry,
-               vals, idx, dense_rows(dout), bool(warp))
+               vals, idx, dout.contiguous(), bool(warp))
 
 
 # ------------------------------------------------------------------- fused WeightNet
@@ -853,7 +852,7 @@ def wn_wsum_fwd(dir_, idx, v, params):
 def wn_wsum_bwd(dir_, idx, v, params, dout):
     """-> dv_rows (B,N,K,C) = w * dout, ddir (B,N,K,3), dparams (104 + 9C)."""
     return _op("kdpc_wn_wsum_bwd", "wn_wsum_bwd", _gpu(dir_, "dir"), idx, v, *params,
-               dense_rows(dout))
+               dout.contiguous())
 
 
 # ------------------------------------------------------- BatchNorm1d + LeakyReLU (rows)
@@ -915,20 +914,6 @@ def copy_segments(dst, src):
     dst, src = list(dst), list(src)
     _op("kdpc_copy_segments", "copy_segments", dst, src,
         work=(2.0 * sum(s.numel() * s.element_size() for s in src), 0.0))
-
-
-def dense_rows(x):
-    """A contiguous copy of x; a slice of the last dim of a contiguous tensor (the gradient a
-    concatenation's backward hands each part) goes through kdpc_copy_rows instead of torch's
-    strided copy.  Other layouts: torch's .contiguous()."""
-    if x.is_contiguous():
-        return x
-    if x.dim() >= 2 and x.stride(-1) == 1 and all(
-            x.size(d) == 1 or x.stride(d) == x.stride(d + 1) * x.size(d + 1)
-            for d in range(x.dim() - 2)):
-        return _op("kdpc_copy_rows", "dense_rows", _gpu(x, "x"),
-                   work=(2.0 * x.numel() * x.element_size(), 0.0))
-    return x.contiguous()
 
 
 def colsum(x2):

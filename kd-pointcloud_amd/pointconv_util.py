@@ -107,7 +107,7 @@ class _BnLReLU(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x2, weight, mean, invstd, y = ctx.saved_tensors
-        dx, dw, db = _nat.batchnorm_lrelu_bwd(_nat.dense_rows(dy), y, x2, weight, mean, invstd,
+        dx, dw, db = _nat.batchnorm_lrelu_bwd(dy.contiguous(), y, x2, weight, mean, invstd,
                                               ctx.slope)
         return dx, dw, db, None, None, None, None, None
 
@@ -326,7 +326,7 @@ class _WeightNetFn(torch.autograd.Function):
     def backward(ctx, dwt):
         xyz, center, idx, *params = ctx.saved_tensors
         need_rel = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
-        dwt = _nat.dense_rows(dwt)
+        dwt = dwt.contiguous()
         if wgrad.active() and xyz.is_cuda:
             # drel (what the upstream layers wait for) here, the 248-parameter reduction on
             # the parameter-gradient stream (same kernels' arithmetic: bit-identical)
@@ -363,7 +363,7 @@ class _PointConvContract(torch.autograd.Function):
         S, K = idx.shape[1], idx.shape[2]
         C = 3 + feats.shape[2]
         dg_rows, dwt, dcenter = _nat.pointconv_contract_bwd(xyz, center, feats, idx, wt,
-                                                             _nat.dense_rows(gout))
+                                                             gout.contiguous())
         dsum = _nat.group_rows_grad(dg_rows.view(B, S * K, C), _nat.csr_of(idx, N), B, N, C)
         return dsum[..., :3], dcenter, dsum[..., 3:], None, dwt
 
@@ -385,7 +385,7 @@ class _PointConvLayer(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         xyz, center, feats, idx, wt, wl, bias = ctx.saved_tensors
-        gy = _nat.dense_rows(gy)
+        gy = gy.contiguous()
         # K <= 9 (the estimators): dG summed per (Morton-ordered row tile, destination) in
         # the data kernel (kdpc_native.tile_plan_of); else one dG row per pair + the kNN CSR
         tp = (_nat.tile_plan_of(idx, center, xyz.shape[1])
@@ -552,7 +552,7 @@ class _CostVolume(torch.autograd.Function):
         x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, slope0 = ctx.saved_tensors
         din, dout = p1.shape[2], w1.shape[0]
         dp1, dp2, dx1, dx2, dpar = _nat.cost_volume_bwd_csr(
-            x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, _nat.dense_rows(gout), slope0)
+            x1, x2, idx, p1, p2, wpos, bpos, w1, out, amax, gout.contiguous(), slope0)
         o = dout * din
         dw1 = dpar[:o].view(dout, din)
         db1 = dpar[o:o + dout]
@@ -584,7 +584,7 @@ class _CostVolumeWide(torch.autograd.Function):
         x1, x2, idx, wpos, w1, h0, out, amax, bpos, b1 = ctx.saved_tensors
         B, N1, K = idx.shape
         N2, din = x2.shape[1], h0.shape[-1]
-        dz1, gsc = _nat.cost_volume_wide_max_bwd(_nat.dense_rows(gout), out, amax, K)
+        dz1, gsc = _nat.cost_volume_wide_max_bwd(gout.contiguous(), out, amax, K)
         h0f = h0.view(-1, din)
         # parameter gradients on the parameter-gradient stream (wgrad.py); split-K because
         # one 262144-deep GEMM ran ~10x below the MFMA rate

@@ -884,22 +884,6 @@ void copy_segments(at::TensorList dst, at::TensorList src) {
         "copy_segments");
 }
 
-// x (..., W) whose leading dims are one uniform run of rows src_ld floats apart (a slice of
-// the last dim of a contiguous tensor) -> a dense copy
-Tensor dense_rows(Tensor x) {
-  TORCH_CHECK(x.is_cuda() && x.scalar_type() == kF, "kdpc: dense_rows expects a GPU f32 tensor");
-  TORCH_CHECK(x.dim() >= 2 && x.stride(-1) == 1, "kdpc: dense_rows expects unit last stride");
-  const int64_t w = x.size(-1), ld = x.stride(-2);
-  for (int64_t d = 0; d + 2 < x.dim(); ++d)
-    TORCH_CHECK(x.size(d) == 1 || x.stride(d) == x.stride(d + 1) * x.size(d + 1),
-                "kdpc: dense_rows expects rows a uniform stride apart");
-  GUARD(x);
-  Tensor out = at::empty(x.sizes(), x.options().memory_format(at::MemoryFormat::Contiguous));
-  const int64_t rows = w == 0 ? 0 : x.numel() / w;
-  check(kdpc_copy_rows(rows, (int)w, F(x), ld, F(out), stream_of(x)), "dense_rows");
-  return out;
-}
-
 Tensor colsum(Tensor x) {
   dev(x, kF, "src");
   TORCH_CHECK(x.dim() == 2, "kdpc: colsum expects a (rows, len) tensor");
@@ -1127,7 +1111,6 @@ TORCH_LIBRARY(kdpc, m) {
   m.def("batchnorm_lrelu_bwd(Tensor dy, Tensor y, Tensor x, Tensor weight, Tensor mean, "
         "Tensor invstd, float slope) -> (Tensor, Tensor, Tensor)");
   m.def("colsum(Tensor x) -> Tensor");
-  m.def("dense_rows(Tensor x) -> Tensor");
   m.def("idw_blend_fwd(Tensor ref, Tensor qry, Tensor vals, Tensor idx, bool warp) "
         "-> (Tensor, Tensor)");
   m.def("idw_blend_bwd_vals(Tensor dout, Tensor w, Tensor offsets, Tensor perm, int s, "
@@ -1194,7 +1177,6 @@ TORCH_LIBRARY_IMPL(kdpc, CUDA, m) {
   m.impl("batchnorm_lrelu_apply", batchnorm_lrelu_apply);
   m.impl("batchnorm_lrelu_bwd", batchnorm_lrelu_bwd);
   m.impl("colsum", colsum);
-  m.impl("dense_rows", dense_rows);
   m.impl("idw_blend_fwd", idw_blend_fwd);
   m.impl("idw_blend_bwd_vals", idw_blend_bwd_vals);
   m.impl("idw_blend_bwd_coords", idw_blend_bwd_coords);

@@ -513,21 +513,3 @@ def test_copy_segments(nat, count):
     assert (dst_buf.cpu()[mask] == -7.0).all()
     with pytest.raises(RuntimeError):
         nat.copy_segments([dst_buf[:4]], [src[0][:3] if sizes[0] >= 3 else torch.zeros(3, device=DEV)])
-
-
-@pytest.mark.parametrize("shape,cut", [((8, 8192, 128), (96, 128)), ((8, 2048, 192), (128, 192)),
-                                       ((4, 100, 7), (2, 7)), ((3, 5, 6, 10), (1, 9)),
-                                       ((16, 33, 8), (0, 5))])
-def test_dense_rows_equals_contiguous(shape, cut):
-    """kdpc_copy_rows (kdpc_native.dense_rows): a slice of the last dim of a contiguous tensor
-    -- the gradient a concatenation's backward hands each part -- copied dense, bit for bit
-    as torch's .contiguous(); 16-byte and scalar paths, leading dims of any rank."""
-    import kdpc_native as K
-    g = torch.Generator(device="cpu").manual_seed(sum(shape))
-    full = torch.randn(*shape, generator=g).to(DEV)
-    x = full[..., cut[0]:cut[1]]
-    assert not x.is_contiguous()
-    y = K.dense_rows(x)
-    assert y.is_contiguous() and torch.equal(y, x.contiguous())
-    z = full.transpose(0, 1)  # not a uniform run of rows: torch's copy
-    assert torch.equal(K.dense_rows(z), z.contiguous())

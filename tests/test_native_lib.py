@@ -160,7 +160,7 @@ TORCH_OPS = {
     "idw_blend_bwd_coords": "kdpc_idw_blend_bwd_coords",
     "dense_tn_small": "kdpc_dense_tn_small", "dense_small": "kdpc_dense_small",
     "neg_sum_k": "kdpc_neg_sum_k",
-    "copy_segments": "kdpc_copy_segments", "dense_rows": "kdpc_copy_rows",
+    "copy_segments": "kdpc_copy_segments",
     "morton_order": "kdpc_morton_order", "pc_tile_plan": "kdpc_pc_tile_plan",
     "pointconv_bwd_tiled": "kdpc_pointconv_bwd_tiled",
     "pointconv_fwd_tiled": "kdpc_pointconv_fwd_tiled",
