@@ -4,7 +4,7 @@ A layer's backward produces two kinds of output: the gradients of its inputs, wh
 next (upstream) backward op waits for, and the gradients of its parameters, which only the
 optimizer reads.  The second kind -- the PointConv weight-gradient kernel (pc_bwd_weight,
 ~1.8 ms of a B=8 training step), the dense layers' split-K weight GEMMs and every bias column
-sum -- is issued here on side HIP streams (two, round-robin), forked from the backward's
+sum -- is issued here on a side HIP stream (_NSTREAMS, round-robin), forked from the backward's
 stream at that point, so it runs beside the rest of the backward instead of in front of it.  Same kernels on
 the same inputs: the gradients are bit-identical to issuing them in line.
 
@@ -44,11 +44,12 @@ import torch
 
 # False issues every parameter gradient in line (the tests' bit-identity reference)
 enabled = True
-# parameter-gradient streams per device, used round-robin by run(): two, so that the
-# parameter-gradient kernels of consecutive layers can run beside each other as well as beside
-# the backward (round-4 A/B, tools/gpu_r4aa.sh, three runs each: 1 stream 16.07-16.21 ms,
-# 2 streams 15.89-16.04, 3 streams 16.01-16.29; KD 12.83-12.89 / 12.67-12.72 / 12.82-12.97).
-_NSTREAMS = 2
+# parameter-gradient streams per device, used round-robin by run().  Round 4 measured two
+# best (tools/gpu_r4aa.sh: 1 stream 16.07-16.21 ms, 2 streams 15.89-16.04, 3 streams
+# 16.01-16.29).  With round 6's kernels one is: train 13.97 -> 13.55 ms, KD 11.13-11.19 ->
+# 11.09 (tools/ab_step.py, two runs each, profiles/round06/ab_streams.txt).  The second stream's
+# weight kernels competed with the backward for the CUs more than they overlapped each other.
+_NSTREAMS = 1
 _side = {}      # device index -> the first side stream (the decoder coordinate fork's)
 _pool = {}      # device index -> [side streams]
 _turn = {}      # device index -> next pool entry
