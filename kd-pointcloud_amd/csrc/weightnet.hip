@@ -27,6 +27,8 @@ using namespace kdpc;
 
 namespace {
 
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
 constexpr int kIn = 3, kH0 = 8, kH1 = 8, kOut = 16;
 // packed parameter layout (floats): W0 8x3 | b0 8 | W1 8x8 | b1 8 | W2 16x8 | b2 16
 constexpr int oW0 = 0, oB0 = oW0 + kH0 * kIn, oW1 = oB0 + kH0, oB1 = oW1 + kH1 * kH0,
@@ -92,16 +94,6 @@ __global__ __launch_bounds__(kBlock) void wn_fwd_kernel(int rows, int s, int k, 
     dst[v] = make_float4(o[4 * v], o[4 * v + 1], o[4 * v + 2], o[4 * v + 3]);
 }
 
-// Backward.  Fixed grid of kBwdGrid workgroups walking tiles of 256 rows (grid-stride).
-// Per tile: each thread back-propagates one row and stores the row's factors
-// [d2(16) h1(8) d1(8) h0(8) d0(8) rel(3)] in LDS; then thread i < 248 adds parameter i's
-// contribution of the 256 rows (ascending row) to its accumulator.  The workgroup's 248
-// partials form one slab row; wn_slab_sum_kernel adds the slabs in slab order.
-constexpr int kF = kOut + kH1 + kH1 + kH0 + kH0 + kIn;  // 51 factors per row
-constexpr int kFS = kF + 1;                              // LDS row stride
-constexpr int fD2 = 0, fH1 = fD2 + kOut, fD1 = fH1 + kH1, fH0 = fD1 + kH1, fD0 = fH0 + kH0,
-              fRel = fD0 + kH0;
-
 // One row's forward recomputed and back-propagated through the three ReLUs: the factors
 // both backward kernels start from (one definition, so their drel rows are bit-identical).
 struct RowGrad {
@@ -156,7 +148,7 @@ __device__ __forceinline__ void store_drel(int r, const Params& sp, const RowGra
 }
 
 // drel only (one thread per row): the half of the backward the upstream layers wait for;
-// the parameter half (wn_bwd_kernel with drel = nullptr) can then run on another stream.
+// the parameter half (wn_bwd_mfma_kernel<false>) can then run on another stream.
 __global__ __launch_bounds__(kBlock) void wn_bwd_rel_kernel(int rows, int s, int k, int n,
                                                             const float* __restrict__ xyz,
                                                             const float* __restrict__ center,
@@ -171,63 +163,112 @@ __global__ __launch_bounds__(kBlock) void wn_bwd_rel_kernel(int rows, int s, int
   store_drel(r, sp, t, drel);
 }
 
-__global__ __launch_bounds__(kBlock) void wn_bwd_kernel(int rows, int s, int k, int n,
-                                                        const float* __restrict__ xyz,
-                                                        const float* __restrict__ center,
-                                                        const int* __restrict__ idx,
-                                                        Params sp,
-                                                        const float* __restrict__ dwt,
-                                                        float* __restrict__ drel,
-                                                        float* __restrict__ slab) {
-  __shared__ float fac[kBlock * kFS];
-  // parameter handled by this thread in the reduction phase: (factor a, factor b) pair or a
-  // bias (factor a alone)
-  const int pi = threadIdx.x;
-  int fa = -1, fb = -1;
-  if (pi < oB0) { fa = fD0 + (pi - oW0) / kIn; fb = fRel + (pi - oW0) % kIn; }
-  else if (pi < oW1) { fa = fD0 + (pi - oB0); }
-  else if (pi < oB1) { fa = fD1 + (pi - oW1) / kH0; fb = fH0 + (pi - oW1) % kH0; }
-  else if (pi < oW2) { fa = fD1 + (pi - oB1); }
-  else if (pi < oB2) { fa = fD2 + (pi - oW2) / kH1; fb = fH1 + (pi - oW2) % kH1; }
-  else if (pi < kNP) { fa = fD2 + (pi - oB2); }
-  float acc = 0.f;
-  for (int t0 = blockIdx.x * kBlock; t0 < rows; t0 += gridDim.x * kBlock) {
-    const int r = t0 + threadIdx.x;
-    float* f = fac + threadIdx.x * kFS;
+// Parameter half on the f32 matrix cores (round 6; replaces round 5's wn_bwd_kernel, which
+// summed per-row factor products from an LDS tile one parameter per thread).  Every parameter gradient is one entry of
+//   P = sum_r D_r H_r^T,  D_r = [d0 (8) | d1 (8) | d2 (16)],  H_r = [rel (3) | h0 (8) | h1 (8) | 1]
+// (dW0 = the d0 x rel block, db0 = d0 x 1, dW1 = d1 x h0, db1 = d1 x 1, dW2 = d2 x h1,
+// db2 = d2 x 1), i.e. a 32 x 32 x rows product: a wave takes 64 rows (one per lane: the
+// row's forward and backward as row_grad), transposes D and H through its own LDS tile and
+// runs 32 v_mfma_f32_32x32x2_f32 (exact f32 products, f32 accumulation in the matrix core's
+// fixed order) per 64 rows.  A workgroup's 4 waves take 4 consecutive 64-row tiles per
+// grid-stride step; at the end their 4 accumulators are summed in wave order into the block's
+// slab row, and the kBwdGrid slab rows are summed in slab order by colsum.  Deterministic: the
+// result depends only on the problem size.  Product alone (tools/bench_wn.py, 589,824 rows):
+// 39.6 us against 54.8 us for round 5's kernel.
+constexpr int kWaveTile = 64;
+constexpr int kBwdWaves = kBwdGrid;  // slab rows: one per workgroup
+constexpr int kDS = 33, kHS = 21;  // LDS row strides of the D / H tiles (bank spread)
+
+// REL: also store drel (kdpc_weightnet_bwd with drel)
+template <bool REL>
+__global__ __launch_bounds__(kBlock) void wn_bwd_mfma_kernel(int rows, int s, int k, int n,
+                                                            const float* __restrict__ xyz,
+                                                            const float* __restrict__ center,
+                                                            const int* __restrict__ idx,
+                                                            Params sp,
+                                                            const float* __restrict__ dwt,
+                                                            float* __restrict__ drel,
+                                                            float* __restrict__ slab) {
+  __shared__ float tiles[kBlock / 64][kWaveTile * (kDS + kHS)];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float* Dt = tiles[wv];
+  float* Ht = Dt + kWaveTile * kDS;
+    f32x16 acc;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+  // block-uniform trip count (the block's 4 waves take 4 consecutive 64-row tiles per step),
+  // so the loop can hold a workgroup barrier: with it the 248 weights are re-read per step
+  // with scalar loads (SGPR operands) instead of being hoisted out of the loop into VGPRs
+  for (long long tb = (long long)blockIdx.x * kBlock; tb < rows; tb += (long long)kBwdGrid * kBlock) {
+    __syncthreads();
+    const long long r = tb + wv * kWaveTile + lane;
+    float* dl = Dt + lane * kDS;
+    float* hl = Ht + lane * kHS;
     if (r < rows) {
       RowGrad t;
-      row_grad(r, s, k, n, xyz, center, idx, sp, dwt, t);
-      if (drel) store_drel(r, sp, t, drel);
-      const float (&d2)[kOut] = t.d2;
-      const float (&h1)[kH1] = t.h1;
-      const float (&d1)[kH1] = t.d1;
-      const float (&h0)[kH0] = t.h0;
-      const float (&d0)[kH0] = t.d0;
-      const float (&rel)[3] = t.rel;
+      row_grad((int)r, s, k, n, xyz, center, idx, sp, dwt, t);
+      if (REL) store_drel((int)r, sp, t, drel);
 #pragma unroll
-      for (int q = 0; q < kOut; ++q) f[fD2 + q] = d2[q];
+      for (int q = 0; q < kH0; ++q) dl[q] = t.d0[q];
 #pragma unroll
-      for (int q = 0; q < kH1; ++q) { f[fH1 + q] = h1[q]; f[fD1 + q] = d1[q]; }
+      for (int q = 0; q < kH1; ++q) dl[kH0 + q] = t.d1[q];
 #pragma unroll
-      for (int q = 0; q < kH0; ++q) { f[fH0 + q] = h0[q]; f[fD0 + q] = d0[q]; }
+      for (int q = 0; q < kOut; ++q) dl[kH0 + kH1 + q] = t.d2[q];
 #pragma unroll
-      for (int q = 0; q < kIn; ++q) f[fRel + q] = rel[q];
-    } else {
+      for (int q = 0; q < kIn; ++q) hl[q] = t.rel[q];
 #pragma unroll
-      for (int q = 0; q < kF; ++q) f[q] = 0.f;
+      for (int q = 0; q < kH0; ++q) hl[kIn + q] = t.h0[q];
+#pragma unroll
+      for (int q = 0; q < kH1; ++q) hl[kIn + kH0 + q] = t.h1[q];
+      hl[19] = 1.f;
+    } else {  // rows past the end add nothing
+#pragma unroll
+      for (int q = 0; q < 32; ++q) dl[q] = 0.f;
+#pragma unroll
+      for (int q = 0; q < 20; ++q) hl[q] = 0.f;
     }
-    __syncthreads();
-    const int nr = min(kBlock, rows - t0);
-    if (fa >= 0) {
-      if (fb >= 0) {
-        for (int j = 0; j < nr; ++j) acc = __builtin_fmaf(fac[j * kFS + fa], fac[j * kFS + fb], acc);
-      } else {
-        for (int j = 0; j < nr; ++j) acc = __fadd_rn(acc, fac[j * kFS + fa]);
-      }
+    __syncthreads();  // (not wave_lds_sync: its asm memory clobber turns the weights' scalar
+                      // loads into vector loads held in VGPRs)
+    // K-step st: rows 2 st (lanes 0-31) and 2 st + 1 (lanes 32-63); A[i][.] = D[row][i],
+    // B[.][j] = H[row][j] (0 past column 20)
+    const int i = lane & 31, rr = lane >> 5;
+#pragma unroll 4
+    for (int st = 0; st < kWaveTile / 2; ++st) {
+      const int row = 2 * st + rr;
+      const float a = Dt[row * kDS + i];
+      const float bv = i < 20 ? Ht[row * kHS + i] : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv, acc, 0, 0, 0);
     }
-    __syncthreads();
+    // (the next step's __syncthreads orders these reads before the tile is rewritten)
   }
-  if (pi < kNP) slab[(long long)blockIdx.x * kNP + pi] = acc;
+  // acc register e of lane l = P[(e & 3) + 8 (e >> 2) + 4 (l >> 5)][l & 31]; the block's 4
+  // waves leave their parameter vectors in LDS and are summed in wave order into one slab row
+  __syncthreads();  // every wave is done reading its tiles
+  float* red = &tiles[0][0];  // [kBlock / 64][kNP]
+  const int j = lane & 31;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int i = (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+    int pi = -1;
+    if (i < kH0) {
+      if (j < kIn) pi = oW0 + i * kIn + j;
+      else if (j == 19) pi = oB0 + i;
+    } else if (i < kH0 + kH1) {
+      if (j >= kIn && j < kIn + kH0) pi = oW1 + (i - kH0) * kH0 + (j - kIn);
+      else if (j == 19) pi = oB1 + (i - kH0);
+    } else {
+      if (j >= kIn + kH0 && j < kIn + kH0 + kH1) pi = oW2 + (i - kH0 - kH1) * kH1 + (j - kIn - kH0);
+      else if (j == 19) pi = oB2 + (i - kH0 - kH1);
+    }
+    if (pi >= 0) red[wv * kNP + pi] = acc[e];
+  }
+  __syncthreads();
+  if (threadIdx.x < kNP) {
+    float v = red[threadIdx.x];
+#pragma unroll
+    for (int w = 1; w < kBlock / 64; ++w) v += red[w * kNP + threadIdx.x];
+    slab[(long long)blockIdx.x * kNP + threadIdx.x] = v;
+  }
 }
 
 }  // namespace
@@ -235,7 +276,7 @@ __global__ __launch_bounds__(kBlock) void wn_bwd_kernel(int rows, int s, int k, 
 KDPC_API int kdpc_weightnet_param_count(void) { return kNP; }
 
 KDPC_API size_t kdpc_weightnet_bwd_workspace_bytes(void) {
-  return ((size_t)kBwdGrid * kNP + colsum_scratch_floats(kBwdGrid, kNP)) * sizeof(float);
+  return ((size_t)kBwdWaves * kNP + colsum_scratch_floats(kBwdWaves, kNP)) * sizeof(float);
 }
 
 KDPC_API int kdpc_weightnet_fwd(int b, int n, int s, int k, const float* xyz, const float* center,
@@ -285,9 +326,13 @@ KDPC_API int kdpc_weightnet_bwd(int b, int n, int s, int k, const float* xyz,
   const Params p{w0, b0, w1, b1, w2, b2};
   float* slab = reinterpret_cast<float*>(workspace);
   // every slab row is written (rows == 0 -> all-zero partials)
-  hipLaunchKernelGGL(wn_bwd_kernel, dim3(kBwdGrid), dim3(kBlock), 0, st, (int)rows, s, k, n, xyz,
-                     center, idx, p, dwt, drel, slab);
+  if (drel)
+    hipLaunchKernelGGL(wn_bwd_mfma_kernel<true>, dim3(kBwdGrid), dim3(kBlock), 0, st, (int)rows, s,
+                       k, n, xyz, center, idx, p, dwt, drel, slab);
+  else
+    hipLaunchKernelGGL(wn_bwd_mfma_kernel<false>, dim3(kBwdGrid), dim3(kBlock), 0, st, (int)rows, s,
+                       k, n, xyz, center, idx, p, dwt, drel, slab);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  return (int)colsum(kBwdGrid, kNP, slab, dparams, slab + (size_t)kBwdGrid * kNP, st);
+  return (int)colsum(kBwdWaves, kNP, slab, dparams, slab + (size_t)kBwdWaves * kNP, st);
 }
