@@ -525,6 +525,18 @@ int kdpc_neg_sum_k(int m, int k, int c, const float *in, float *out, void *strea
 int kdpc_copy_segments(int n, const void *const *src, void *const *dst, const long long *bytes,
                        void *stream);
 
+/* One Adam step (L2 weight decay, no amsgrad) over flat float buffers of n elements (n a
+ * multiple of 4, 16-byte aligned): param, exp_avg, exp_avg_sq updated in place from grad; lr and
+ * step (already incremented) are device scalars, read by the kernel (graph replays see their
+ * current values).  The same update as torch's fused Adam (ATen fused_adam_utils.cuh adam_math)
+ * operation for operation; mode bit 0: the double expressions contracted as clang does by
+ * default, bit 1: fast (not correctly rounded) f32 division and square root.  Replaces the multi-tensor fused Adam
+ * in the graphed training step; the reference steps torch.optim.Adam (distilTrain.py:134-135). */
+int kdpc_adam_step(long long n, float *param, const float *grad, float *exp_avg,
+                   float *exp_avg_sq, const float *lr, const float *step, double beta1,
+                   double beta2, double eps, double weight_decay, int maximize, int mode,
+                   void *stream);
+
 #ifdef __cplusplus
 }
 #endif

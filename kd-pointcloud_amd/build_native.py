@@ -45,7 +45,13 @@ CFLAGS = [
 
 # per-source extra flags (none at present; SLP packing, off everywhere, also forced the
 # cost-volume backward's LDS operands into adjacent registers: 182 -> >256 VGPRs)
-EXTRA_FLAGS = {}
+# Adam's update is compiled the way torch compiles its fused Adam (clang's default HIP
+# contraction; adam_fastdiv.hip also with fast f32 division / sqrt), see csrc/adam_math.h
+EXTRA_FLAGS = {
+    "adam.hip": ["-ffp-contract=fast-honor-pragmas"],
+    "adam_fastdiv.hip": ["-ffp-contract=fast-honor-pragmas",
+                         "-fno-hip-fp32-correctly-rounded-divide-sqrt"],
+}
 
 
 def source_files(csrc=CSRC, root=ROOT):

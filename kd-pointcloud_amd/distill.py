@@ -62,6 +62,11 @@ def make_optimizer(model, lr=1e-3, weight_decay=1e-4, capturable=False):
                             fused=True if fused else None)
 
 
+# the graphed step's flat Adam on csrc/adam.hip (one launch) rather than torch's fused Adam
+# (multi-tensor, 7 launches); both give the same bits (tests/test_gpu_adam.py)
+HIP_ADAM = True
+
+
 def _core(model):
     return model.module if isinstance(model, torch.nn.parallel.DistributedDataParallel) else model
 
@@ -605,6 +610,14 @@ class GraphedStep:
         fo.state[flat] = {"step": steps[0].clone(), "exp_avg": M, "exp_avg_sq": V}
         self.flat_opt = fo
         self._flat_step = fo.state[flat]["step"]
+        # the update itself runs as one full-chip HIP launch (csrc/adam.hip) instead of
+        # torch's multi-tensor fused Adam (7 launches of 40-57 workgroups over ~20 M floats:
+        # 308 us per step); same elementwise arithmetic, same bits (tests/test_gpu_adam.py)
+        if grp.get("amsgrad", False) or grp.get("differentiable", False):
+            raise ValueError("GraphedStep: amsgrad / differentiable Adam is not supported")
+        self._pmv = (P, M, V)
+        self._adam_hp = (grp["betas"][0], grp["betas"][1], grp["eps"], grp["weight_decay"],
+                         bool(grp["maximize"]))
         # gradient buckets (world > 1): consecutive runs of `used` of about bucket_bytes
         self.buckets = []
         if self.schedule == "overlap":
@@ -656,7 +669,12 @@ class GraphedStep:
             self._pack()
         # an eager optimizer step in between advanced the per-parameter counters
         self._flat_step.copy_(self._steps[0])
-        self.flat_opt.step()
+        if HIP_ADAM:
+            self._flat_step.add_(1)  # as torch's fused Adam: the counter advances, then the update
+            P, M, V = self._pmv
+            _nat.adam_step(P, self.G, M, V, self._lr, self._flat_step, *self._adam_hp)
+        else:
+            self.flat_opt.step()
         self._steps.copy_(self._flat_step.reshape(1).expand_as(self._steps))
         if fork is not None:
             _nat.copy_segments(self.fps_cur, [t.contiguous() for t in self.fps_next])

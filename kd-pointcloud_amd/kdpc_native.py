@@ -20,6 +20,7 @@ LIB_PATH = os.environ.get("KDPC_LIB", os.path.join(_HERE, "lib", "libkdpc_hip.so
 OPS_PATH = os.path.join(os.path.dirname(LIB_PATH), "libkdpc_torch.so")
 
 _c_int, _c_float, _c_size, _vp = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
+_c_double, _c_longlong = ctypes.c_double, ctypes.c_longlong
 
 # name -> argtypes (all return int hipError_t, except where noted)
 _SIGNATURES = {
@@ -87,6 +88,8 @@ _SIGNATURES = {
     "kdpc_colsum": [_c_int, _c_int, _vp, _vp, _vp, _c_size, _vp],
     "kdpc_neg_sum_k": [_c_int, _c_int, _c_int, _vp, _vp, _vp],
     "kdpc_copy_segments": [_c_int, _vp, _vp, _vp, _vp],
+    "kdpc_adam_step": [_c_longlong, _vp, _vp, _vp, _vp, _vp, _vp, _c_double, _c_double,
+                       _c_double, _c_double, _c_int, _c_int, _vp],
     "kdpc_weightnet_param_count": [],
     "kdpc_weightnet_fwd": [_c_int] * 4 + [_vp] * 11,
     "kdpc_weightnet_bwd_workspace_bytes": [],
@@ -907,6 +910,24 @@ def dense_small_out(x2, m, bias, y2):
 def neg_sum_k(x):
     """x (..., K, C) -> -x.sum(-2) (..., C), ascending-K order, one launch."""
     return _op("kdpc_neg_sum_k", "neg_sum_k", _gpu(x, "x").contiguous())
+
+
+# torch's fused Adam over the flat buffers of distill.GraphedStep, as one full-chip launch
+# (csrc/adam.hip); ADAM_MODE: how the update is evaluated (bit 0 contracted double expressions,
+# bit 1 fast f32 division / sqrt): the form tests/test_gpu_adam.py finds bit-identical to
+# torch's fused Adam
+ADAM_MODE = 1
+
+
+def adam_step(param, grad, exp_avg, exp_avg_sq, lr, step, beta1, beta2, eps, weight_decay,
+              maximize=False, mode=None):
+    """In-place Adam on flat f32 buffers (n % 4 == 0, 16-byte aligned); lr / step: device
+    scalars, step already incremented."""
+    c = ADAM_MODE if mode is None else int(mode)
+    n = _gpu(param, "param").numel()
+    _op("kdpc_adam_step", "adam_step", param, grad, exp_avg, exp_avg_sq, lr, step,
+        float(beta1), float(beta2), float(eps), float(weight_decay), bool(maximize), c,
+        work=(28.0 * n, 0.0))
 
 
 def copy_segments(dst, src):

@@ -860,6 +860,27 @@ Tensor neg_sum_k(Tensor x) {
   return out;
 }
 
+// Adam over flat buffers (kdpc_adam_step): param / exp_avg / exp_avg_sq in place
+void adam_step(Tensor param, Tensor grad, Tensor exp_avg, Tensor exp_avg_sq, Tensor lr,
+               Tensor step, double beta1, double beta2, double eps, double weight_decay,
+               bool maximize, int64_t mode) {
+  dev(param, kF, "param");
+  dev(grad, kF, "grad");
+  dev(exp_avg, kF, "exp_avg");
+  dev(exp_avg_sq, kF, "exp_avg_sq");
+  dev(lr, kF, "lr");
+  dev(step, kF, "step");
+  const int64_t n = param.numel();
+  TORCH_CHECK(grad.numel() == n && exp_avg.numel() == n && exp_avg_sq.numel() == n,
+              "kdpc: adam_step: buffers of different sizes");
+  TORCH_CHECK(lr.numel() == 1 && step.numel() == 1, "kdpc: adam_step: lr / step must be scalars");
+  GUARD(param);
+  check(kdpc_adam_step(n, F(param), F(grad), F(exp_avg), F(exp_avg_sq), F(lr), F(step), beta1,
+                       beta2, eps, weight_decay, maximize ? 1 : 0, (int)mode,
+                       stream_of(param)),
+        "adam_step");
+}
+
 // dst[i] <- src[i] for same-size contiguous tensors on one device, one launch per 128 pairs
 void copy_segments(at::TensorList dst, at::TensorList src) {
   TORCH_CHECK(dst.size() == src.size(), "kdpc: copy_segments: ", dst.size(), " destinations, ",
@@ -1120,6 +1141,9 @@ TORCH_LIBRARY(kdpc, m) {
   m.def("dense_tn_small(Tensor a, Tensor b) -> Tensor");
   m.def("neg_sum_k(Tensor x) -> Tensor");
   m.def("copy_segments(Tensor(a!)[] dst, Tensor[] src) -> ()");
+  m.def("adam_step(Tensor(a!) param, Tensor grad, Tensor(b!) exp_avg, Tensor(c!) exp_avg_sq, "
+        "Tensor lr, Tensor step, float beta1, float beta2, float eps, float weight_decay, "
+        "bool maximize, int mode) -> ()");
   m.def("dense_small(Tensor x, Tensor m, Tensor? bias) -> Tensor");
   m.def("dense_small_out(Tensor x, Tensor m, Tensor? bias, Tensor(a!) y) -> ()");
 }
@@ -1183,6 +1207,7 @@ TORCH_LIBRARY_IMPL(kdpc, CUDA, m) {
   m.impl("dense_tn_small", dense_tn_small);
   m.impl("neg_sum_k", neg_sum_k);
   m.impl("copy_segments", copy_segments);
+  m.impl("adam_step", adam_step);
   m.impl("dense_small", dense_small);
   m.impl("dense_small_out", dense_small_out);
 }

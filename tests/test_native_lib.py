@@ -66,7 +66,7 @@ def _declared_arity():
 
 def test_ctypes_signatures_match_header():
     """Every ctypes binding passes exactly the header's parameters, with matching kinds
-    (pointer / size_t / float / int)."""
+    (pointer / size_t / float / double / long long / int)."""
     decl = _declared_arity()
     for name, argtypes in kdpc_native._SIGNATURES.items():
         params = decl[name]
@@ -79,6 +79,10 @@ def test_ctypes_signatures_match_header():
                 assert t is ctypes.c_size_t, (name, p)
             elif p.startswith("float"):
                 assert t is ctypes.c_float, (name, p)
+            elif p.startswith("double"):
+                assert t is ctypes.c_double, (name, p)
+            elif p.startswith("long long"):
+                assert t is ctypes.c_longlong, (name, p)
             else:
                 assert t is ctypes.c_int, (name, p)
 
@@ -161,6 +165,7 @@ TORCH_OPS = {
     "dense_tn_small": "kdpc_dense_tn_small", "dense_small": "kdpc_dense_small",
     "neg_sum_k": "kdpc_neg_sum_k",
     "copy_segments": "kdpc_copy_segments",
+    "adam_step": "kdpc_adam_step",
     "morton_order": "kdpc_morton_order", "pc_tile_plan": "kdpc_pc_tile_plan",
     "pointconv_bwd_tiled": "kdpc_pointconv_bwd_tiled",
     "pointconv_fwd_tiled": "kdpc_pointconv_fwd_tiled",
