@@ -94,7 +94,7 @@ def test_cost_volume_bwd_csr_bitwise(din, dout, n1, n2, bsz, k):
 
 
 @pytest.mark.parametrize("din,dout,n1", [(32, 32, 8192), (64, 64, 2048), (128, 128, 512),
-                                         (256, 256, 256)])
+                                         (256, 256, 256), (32, 64, 4096), (64, 32, 4096)])
 def test_cost_volume_bwd_deterministic_at_model_size(din, dout, n1):
     """At the model's sizes of all four levels (B=16 clouds = both directions of the B=8 pair
     batch, K=32; levels 0/1 on the narrow kernel, 2/3 on the fused wide one) the backward gives
